@@ -1,0 +1,189 @@
+/*
+ * rt_abi.h — the drop-in boundary: a C ABI (plain pointers and sizes) over the
+ * MI355X path tracer. Every entry point returns RT_OK (0) or a negative RT_ERR_*
+ * code; nothing aborts and no C++ exception crosses it.
+ *
+ * What it replaces in the reference (paths relative to /root/reference/src):
+ *
+ *   rt_render                 the per-(pixel, sample) driver loop main.rs:497-551
+ *                             = Camera::get_ray (camera.rs:58-66) followed by
+ *                             ray_color (main.rs:19-38) per sample, summed per
+ *                             pixel and divided by spp (math.rs:119-126)
+ *   rt_camera_new             Camera::new (camera.rs:18-56)
+ *   rt_world_*                World + register_material (main.rs:40-50) and the
+ *                             Hittable / Material / Texture constructors
+ *                             (hittable.rs:77-207, material.rs:6-12, texture.rs:4-22,
+ *                             perlin.rs:13-30)
+ *   rt_world_build_scene      the scene builders main.rs:52-289
+ *   rt_scene_preset           the per-scene camera/background table main.rs:314-464
+ *   rt_world_flatten          (new) lowers the Hittable tree to rt_scene_soa
+ *   rt_ctx_upload_*           (new) copies the SoA tables into HBM
+ *   rt_write_ppm              write_color + the P3 writer (math.rs:119-132,
+ *                             main.rs:472, 591-596)
+ *
+ * Threading: a context is bound to one device and is used by one host thread at
+ * a time. Worlds are plain host objects.
+ */
+#ifndef RT_ABI_H
+#define RT_ABI_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "rt_scene.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RT_ABI_VERSION 1
+
+enum {
+    RT_OK = 0,
+    RT_ERR_INVALID = -1,      /* bad argument / handle */
+    RT_ERR_HIP = -2,          /* a HIP runtime call failed (see rt_last_error) */
+    RT_ERR_UNSUPPORTED = -3,  /* a Hittable nesting the flattener does not lower */
+    RT_ERR_OOM = -4,
+    RT_ERR_NO_DEVICE = -5,
+    RT_ERR_NO_SCENE = -6      /* render before upload */
+};
+
+typedef struct rt_ctx rt_ctx;
+typedef struct rt_world rt_world;
+
+int rt_abi_version(void);
+/* Text of the last error on this thread ("" if none). */
+const char* rt_last_error(void);
+
+/* ---- device context --------------------------------------------------------- */
+int rt_device_count(int* count);
+int rt_ctx_create(int device, rt_ctx** out);
+void rt_ctx_destroy(rt_ctx* ctx);
+
+/* ---- host scene model (the reference's World / Hittable surface) --------------- */
+/* A world owns a seeded construction stream (Philox, rt_numerics.h) that replaces
+ * thread_rng() during scene building (random_double in main.rs:191,233,256-268,
+ * perlin.rs:16-22,123-124, hittable.rs:82). */
+int rt_world_create(uint64_t scene_seed, rt_world** out);
+void rt_world_destroy(rt_world* w);
+
+/* Textures (texture.rs:4-22) -> texture id >= 0. */
+int rt_world_texture_solid(rt_world* w, double r, double g, double b, int* tex_out);
+int rt_world_texture_checker(rt_world* w, const double even[3], const double odd[3], int* tex_out);
+/* Perlin::new() draws from the world's stream (perlin.rs:13-30). */
+int rt_world_texture_noise(rt_world* w, double scale, int* tex_out);
+/* RGB8 texels as stb_image returns them; the world copies them. */
+int rt_world_texture_image(rt_world* w, const uint8_t* rgb, int width, int height, int* tex_out);
+
+/* Materials (material.rs:6-12) -> 1-based MaterialHandle (main.rs:46-49). */
+int rt_world_material_lambertian(rt_world* w, int tex, int* handle_out);
+int rt_world_material_metal(rt_world* w, const double albedo[3], double fuzz, int* handle_out);
+int rt_world_material_dielectric(rt_world* w, double ir, int* handle_out);
+int rt_world_material_diffuse_light(rt_world* w, int tex, int* handle_out);
+int rt_world_material_isotropic(rt_world* w, int tex, int* handle_out);
+
+/* Hittables (hittable.rs:30-41, constructors :77-207) -> hittable id >= 0. */
+int rt_world_sphere(rt_world* w, int mat, const double center[3], double radius, int* id_out);
+int rt_world_moving_sphere(rt_world* w, int mat, const double c0[3], const double c1[3], double t0, double t1,
+                           double radius, int* id_out);
+/* axis: 0 XYRect (k on z), 1 XZRect (k on y), 2 YZRect (k on x). */
+int rt_world_rect(rt_world* w, int axis, int mat, double a0, double a1, double b0, double b1, double k,
+                  int* id_out);
+int rt_world_box(rt_world* w, const double mn[3], const double mx[3], int mat, int* id_out);
+int rt_world_translate(rt_world* w, int child, const double offset[3], int* id_out);
+int rt_world_rotate_y(rt_world* w, int child, double angle_degrees, int* id_out);
+int rt_world_constant_medium(rt_world* w, int boundary, double density, int phase_mat, int* id_out);
+/* new_bvh_node(list, 0, n, t0, t1): random axis + median split, draws from the stream. */
+int rt_world_bvh(rt_world* w, const int* ids, int n, double t0, double t1, int* id_out);
+/* world.hittables.push(id) */
+int rt_world_push(rt_world* w, int id);
+
+/* Built-in scene builders, ids as the reference's match arms (main.rs:314-464):
+ * 0 random, 1 two_spheres, 2 two_perlin, 3 earth, 4 simple_light, 5 cornell,
+ * 6 cornell_smoke, 7 final. Scenes 3 and 7 need the earth texture (RGB8). */
+int rt_world_build_scene(rt_world* w, int scene_id, const uint8_t* image_rgb, int image_w, int image_h);
+
+typedef struct rt_world_info {
+    int32_t n_hittables;     /* top-level list length */
+    int32_t n_materials;
+    int32_t n_leaf_prims;    /* leaves reachable from the list */
+    int32_t n_media;
+    double checksum;         /* same probe as the oracle's orc_scene_info */
+} rt_world_info;
+int rt_world_info_get(const rt_world* w, rt_world_info* out);
+
+/* ---- camera ----------------------------------------------------------------------- */
+int rt_camera_new(const double look_from[3], const double look_at[3], const double vup[3], double vfov,
+                  double aspect_ratio, double aperture, double focus_dist, double time0, double time1,
+                  rt_camera* out);
+
+typedef struct rt_scene_preset {
+    double look_from[3], look_at[3], background[3];
+    double vfov, aperture, focus_dist, time0, time1;
+    int32_t default_width, default_spp;   /* the reference's own image_width / samples_per_pixel */
+    double default_aspect;
+} rt_scene_preset;
+int rt_scene_preset_get(int scene_id, rt_scene_preset* out);
+/* Preset camera for an explicit width x height (aspect = width/height). */
+int rt_scene_camera(int scene_id, int width, int height, rt_camera* cam_out, double background_out[3]);
+
+/* ---- lowering + upload ---------------------------------------------------------------- */
+/* Flattens the world into SoA tables owned by the world (valid until the next
+ * flatten or rt_world_destroy). accel: RT_ACCEL_SAH. */
+int rt_world_flatten(rt_world* w, int accel, const rt_scene_soa** soa_out);
+int rt_ctx_upload_soa(rt_ctx* ctx, const rt_scene_soa* soa);
+int rt_ctx_upload_world(rt_ctx* ctx, rt_world* w, int accel);
+
+/* ---- render ----------------------------------------------------------------------------- */
+enum { RT_OUT_F32 = 0, RT_OUT_F64 = 1 };
+
+typedef struct rt_render_params {
+    int32_t width, height;       /* full image */
+    int32_t spp, max_depth;
+    int32_t spp_chunk;           /* samples a lane sums before its partial is written; 0 = auto */
+    int32_t row_begin, row_stride; /* rows rendered: y = row_begin + k*row_stride < height (y = 0 bottom) */
+    int32_t out_format;          /* RT_OUT_F32 / RT_OUT_F64 */
+    int32_t out_on_device;       /* 0: out is host memory (copied back); 1: out is a device pointer */
+    int32_t count_work;          /* 1: also count casts / node visits / prim tests (slower) */
+    double background[3];
+    uint64_t render_seed;
+    void* stream;                /* hipStream_t to launch on (NULL = the context's stream) */
+} rt_render_params;
+
+/* Renders the selected rows into out (rows_local x width x 3, row k = the k-th
+ * selected row) as the per-pixel mean radiance sum * (1/spp). Synchronous unless
+ * out_on_device is set, in which case the work is only enqueued on `stream`. */
+int rt_render(rt_ctx* ctx, const rt_camera* cam, const rt_render_params* p, void* out);
+
+/* Rows rendered for (height, row_begin, row_stride). */
+int rt_rows_in_shard(int height, int row_begin, int row_stride);
+
+typedef struct rt_stats {
+    double kernel_ms;            /* last rt_render: trace kernel time (HIP events) */
+    double reduce_ms;            /* last rt_render: chunk-reduction kernel time */
+    uint64_t samples;
+    uint64_t casts;              /* count_work only */
+    uint64_t node_visits;        /* count_work only: BVH nodes fetched */
+    uint64_t prim_tests;         /* count_work only */
+    uint64_t n_items;            /* work items (pixel, chunk) */
+    int32_t n_chunks, spp_chunk;
+    int64_t scene_bytes;         /* device bytes of the uploaded scene */
+    int32_t node_bytes, prim_bytes, material_bytes, pad;
+} rt_stats;
+int rt_last_stats(rt_ctx* ctx, rt_stats* out);
+
+/* ---- output ------------------------------------------------------------------------------ */
+/* P3 PPM exactly as the reference writes it: header "P3\nW H\n255\n\n", rows top to
+ * bottom, each channel (int)(256 * clamp(sqrt(mean), 0, 0.999)) with NaN -> 0.
+ * mean_rgb is height x width x 3 f32 with row 0 = bottom (y = 0). */
+int rt_write_ppm(const float* mean_rgb, int width, int height, const char* path);
+
+/* ---- self test ------------------------------------------------------------------------------ */
+/* Evaluates rt_numerics.h functions on the device (same fn ids as the oracle's
+ * orc_eval) so tests can check host/device bit equality. */
+int rt_device_eval(rt_ctx* ctx, int fn, const double* x, const double* y, const double* z, double* out, int n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,626 @@
+// abi.cpp — the extern "C" boundary (include/rt/rt_abi.h). No exception and no
+// C++ type crosses it; every entry point returns RT_OK or a negative RT_ERR_*.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "rt/rt_abi.h"
+#include "scene_model.hpp"
+#include "trace_kernel.hpp"
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const std::string& msg)
+{
+    g_last_error = msg;
+    return code;
+}
+
+int hip_fail(hipError_t e, const char* what)
+{
+    return fail(RT_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+#define HIP_TRY(expr)                                   \
+    do {                                                \
+        hipError_t e_ = (expr);                         \
+        if (e_ != hipSuccess) return hip_fail(e_, #expr); \
+    } while (0)
+
+size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+}  // namespace
+
+struct rt_world {
+    explicit rt_world(uint64_t seed) : w(seed) {}
+    rtw::World w;
+};
+
+struct rt_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    void* scene_buf = nullptr;
+    size_t scene_bytes = 0;
+    rtk::SceneDev S{};
+    bool has_scene = false;
+    double* partial = nullptr;
+    size_t partial_cap = 0;
+    void* out_buf = nullptr;
+    size_t out_cap = 0;
+    unsigned long long* counters = nullptr;
+    hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+    bool pending_stats = false;
+    bool pending_counts = false;
+    rt_stats stats{};
+};
+
+extern "C" {
+
+int rt_abi_version(void) { return RT_ABI_VERSION; }
+const char* rt_last_error(void) { return g_last_error.c_str(); }
+
+int rt_device_count(int* count)
+{
+    if (!count) return fail(RT_ERR_INVALID, "null count");
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess) {
+        *count = 0;
+        return hip_fail(e, "hipGetDeviceCount");
+    }
+    *count = n;
+    return RT_OK;
+}
+
+int rt_ctx_create(int device, rt_ctx** out)
+{
+    if (!out) return fail(RT_ERR_INVALID, "null out");
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return fail(RT_ERR_NO_DEVICE, "no HIP device visible");
+    if (device < 0 || device >= n) return fail(RT_ERR_INVALID, "device index out of range");
+    HIP_TRY(hipSetDevice(device));
+    rt_ctx* c = new (std::nothrow) rt_ctx();
+    if (!c) return fail(RT_ERR_OOM, "rt_ctx");
+    c->device = device;
+    hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    for (int i = 0; i < 3 && e == hipSuccess; ++i) e = hipEventCreate(&c->ev[i]);
+    if (e == hipSuccess) e = hipMalloc((void**)&c->counters, 4 * sizeof(unsigned long long));
+    if (e != hipSuccess) {
+        rt_ctx_destroy(c);
+        return hip_fail(e, "rt_ctx_create");
+    }
+    *out = c;
+    return RT_OK;
+}
+
+void rt_ctx_destroy(rt_ctx* c)
+{
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    (void)hipFree(c->scene_buf);
+    (void)hipFree(c->partial);
+    (void)hipFree(c->out_buf);
+    (void)hipFree(c->counters);
+    for (auto& e : c->ev)
+        if (e) (void)hipEventDestroy(e);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+// ---- world -------------------------------------------------------------------
+int rt_world_create(uint64_t scene_seed, rt_world** out)
+{
+    if (!out) return fail(RT_ERR_INVALID, "null out");
+    *out = new (std::nothrow) rt_world(scene_seed);
+    return *out ? RT_OK : fail(RT_ERR_OOM, "rt_world");
+}
+void rt_world_destroy(rt_world* w) { delete w; }
+
+#define CHECK_WORLD(w, o)                                              \
+    do {                                                               \
+        if (!(w) || !(o)) return fail(RT_ERR_INVALID, "null argument"); \
+    } while (0)
+
+static rtw::V3 vec(const double* a) { return rtw::v3(a[0], a[1], a[2]); }
+
+int rt_world_texture_solid(rt_world* w, double r, double g, double b, int* o)
+{
+    CHECK_WORLD(w, o);
+    *o = w->w.texture_solid(rtw::v3(r, g, b));
+    return RT_OK;
+}
+int rt_world_texture_checker(rt_world* w, const double even[3], const double odd[3], int* o)
+{
+    CHECK_WORLD(w, o);
+    if (!even || !odd) return fail(RT_ERR_INVALID, "null color");
+    *o = w->w.texture_checker(vec(even), vec(odd));
+    return RT_OK;
+}
+int rt_world_texture_noise(rt_world* w, double scale, int* o)
+{
+    CHECK_WORLD(w, o);
+    *o = w->w.texture_noise(scale);
+    return RT_OK;
+}
+int rt_world_texture_image(rt_world* w, const uint8_t* rgb, int width, int height, int* o)
+{
+    CHECK_WORLD(w, o);
+    if (width < 0 || height < 0 || (!rgb && width * height > 0)) return fail(RT_ERR_INVALID, "bad image");
+    *o = w->w.texture_image(rgb, width, height);
+    return RT_OK;
+}
+
+int rt_world_material_lambertian(rt_world* w, int tex, int* o)
+{
+    CHECK_WORLD(w, o);
+    if (!w->w.valid_texture(tex)) return fail(RT_ERR_INVALID, "bad texture id");
+    *o = w->w.lambertian(tex);
+    return RT_OK;
+}
+int rt_world_material_metal(rt_world* w, const double albedo[3], double fuzz, int* o)
+{
+    CHECK_WORLD(w, o);
+    if (!albedo) return fail(RT_ERR_INVALID, "null albedo");
+    *o = w->w.metal(vec(albedo), fuzz);
+    return RT_OK;
+}
+int rt_world_material_dielectric(rt_world* w, double ir, int* o)
+{
+    CHECK_WORLD(w, o);
+    *o = w->w.dielectric(ir);
+    return RT_OK;
+}
+int rt_world_material_diffuse_light(rt_world* w, int tex, int* o)
+{
+    CHECK_WORLD(w, o);
+    if (!w->w.valid_texture(tex)) return fail(RT_ERR_INVALID, "bad texture id");
+    *o = w->w.diffuse_light(tex);
+    return RT_OK;
+}
+int rt_world_material_isotropic(rt_world* w, int tex, int* o)
+{
+    CHECK_WORLD(w, o);
+    if (!w->w.valid_texture(tex)) return fail(RT_ERR_INVALID, "bad texture id");
+    *o = w->w.isotropic(tex);
+    return RT_OK;
+}
+
+int rt_world_sphere(rt_world* w, int mat, const double c[3], double r, int* o)
+{
+    CHECK_WORLD(w, o);
+    if (!c || !w->w.valid_material(mat)) return fail(RT_ERR_INVALID, "bad sphere");
+    *o = w->w.sphere(mat, vec(c), r);
+    return RT_OK;
+}
+int rt_world_moving_sphere(rt_world* w, int mat, const double c0[3], const double c1[3], double t0, double t1,
+                           double r, int* o)
+{
+    CHECK_WORLD(w, o);
+    if (!c0 || !c1 || !w->w.valid_material(mat)) return fail(RT_ERR_INVALID, "bad moving sphere");
+    *o = w->w.moving_sphere(mat, vec(c0), vec(c1), t0, t1, r);
+    return RT_OK;
+}
+int rt_world_rect(rt_world* w, int axis, int mat, double a0, double a1, double b0, double b1, double k, int* o)
+{
+    CHECK_WORLD(w, o);
+    if (axis < 0 || axis > 2 || !w->w.valid_material(mat)) return fail(RT_ERR_INVALID, "bad rect");
+    rtw::HKind kind = axis == 0 ? rtw::HKind::XYRect : axis == 1 ? rtw::HKind::XZRect : rtw::HKind::YZRect;
+    *o = w->w.rect(kind, mat, a0, a1, b0, b1, k);
+    return RT_OK;
+}
+int rt_world_box(rt_world* w, const double mn[3], const double mx[3], int mat, int* o)
+{
+    CHECK_WORLD(w, o);
+    if (!mn || !mx || !w->w.valid_material(mat)) return fail(RT_ERR_INVALID, "bad box");
+    *o = w->w.box(vec(mn), vec(mx), mat);
+    return RT_OK;
+}
+int rt_world_translate(rt_world* w, int child, const double off[3], int* o)
+{
+    CHECK_WORLD(w, o);
+    if (!off || !w->w.valid_hittable(child)) return fail(RT_ERR_INVALID, "bad translate");
+    *o = w->w.translate(child, vec(off));
+    return RT_OK;
+}
+int rt_world_rotate_y(rt_world* w, int child, double angle, int* o)
+{
+    CHECK_WORLD(w, o);
+    if (!w->w.valid_hittable(child)) return fail(RT_ERR_INVALID, "bad rotate_y");
+    *o = w->w.rotate_y(child, angle);
+    return RT_OK;
+}
+int rt_world_constant_medium(rt_world* w, int boundary, double density, int phase, int* o)
+{
+    CHECK_WORLD(w, o);
+    if (!w->w.valid_hittable(boundary) || !w->w.valid_material(phase)) return fail(RT_ERR_INVALID, "bad medium");
+    *o = w->w.constant_medium(boundary, density, phase);
+    return RT_OK;
+}
+int rt_world_bvh(rt_world* w, const int* ids, int n, double t0, double t1, int* o)
+{
+    CHECK_WORLD(w, o);
+    if (!ids || n <= 0) return fail(RT_ERR_INVALID, "empty bvh list");
+    std::vector<int> list(ids, ids + n);
+    for (int id : list)
+        if (!w->w.valid_hittable(id)) return fail(RT_ERR_INVALID, "bad id in bvh list");
+    *o = w->w.bvh(list, 0, n, t0, t1);
+    return RT_OK;
+}
+int rt_world_push(rt_world* w, int id)
+{
+    if (!w || !w->w.valid_hittable(id)) return fail(RT_ERR_INVALID, "bad hittable id");
+    w->w.push(id);
+    return RT_OK;
+}
+
+int rt_world_build_scene(rt_world* w, int scene_id, const uint8_t* img, int iw, int ih)
+{
+    if (!w) return fail(RT_ERR_INVALID, "null world");
+    int rc = rtw::build_scene(w->w, scene_id, img, iw, ih);
+    if (rc) return fail(rc, "unknown scene id or missing image texture");
+    return RT_OK;
+}
+
+// Same structure probe as the oracle's orc_scene_info (leaves through BVHs,
+// instances and media; span-1 duplicates counted once).
+static void count_leaves(const rtw::World& w, int id, int& n, double& cs)
+{
+    const rtw::HNode& h = w.nodes[id];
+    switch (h.kind) {
+    case rtw::HKind::BvhNode:
+        count_leaves(w, h.left, n, cs);
+        if (h.right != h.left) count_leaves(w, h.right, n, cs);
+        return;
+    case rtw::HKind::Translate: case rtw::HKind::RotateY: case rtw::HKind::ConstantMedium:
+        count_leaves(w, h.ptr, n, cs);
+        return;
+    default: {
+        n++;
+        double cy1 = h.kind == rtw::HKind::MovingSphere ? h.c1.y : 0.0;
+        double rad = (h.kind == rtw::HKind::Sphere || h.kind == rtw::HKind::MovingSphere) ? h.radius : 0.0;
+        double k = (h.kind == rtw::HKind::XYRect || h.kind == rtw::HKind::XZRect || h.kind == rtw::HKind::YZRect) ? h.k : 0.0;
+        double by = h.kind == rtw::HKind::Box ? h.bmax.y : 0.0;
+        double c0x = (h.kind == rtw::HKind::Sphere || h.kind == rtw::HKind::MovingSphere) ? h.c0.x : 0.0;
+        double c0y = (h.kind == rtw::HKind::Sphere || h.kind == rtw::HKind::MovingSphere) ? h.c0.y : 0.0;
+        double c0z = (h.kind == rtw::HKind::Sphere || h.kind == rtw::HKind::MovingSphere) ? h.c0.z : 0.0;
+        cs += c0x + 2.0 * c0y + 3.0 * c0z + rad + k + by + cy1;
+        return;
+    }
+    }
+}
+
+int rt_world_info_get(const rt_world* w, rt_world_info* out)
+{
+    if (!w || !out) return fail(RT_ERR_INVALID, "null argument");
+    int n = 0;
+    double cs = 0.0;
+    for (int id : w->w.hittables) count_leaves(w->w, id, n, cs);
+    for (const rtw::Material& m : w->w.materials) {
+        double tex_c0y = m.tex >= 0 ? w->w.textures[m.tex].c0.y : 0.0;
+        double albedo_x = m.kind == RT_MAT_METAL ? m.albedo.x : 0.0;
+        cs += 0.5 * (albedo_x + tex_c0y + m.fuzz + m.ir);
+    }
+    out->n_hittables = (int32_t)w->w.hittables.size();
+    out->n_materials = (int32_t)w->w.materials.size();
+    out->n_leaf_prims = n;
+    out->n_media = w->w.n_media;
+    out->checksum = cs;
+    return RT_OK;
+}
+
+// ---- camera -----------------------------------------------------------------------
+int rt_camera_new(const double look_from[3], const double look_at[3], const double vup[3], double vfov,
+                  double aspect, double aperture, double focus_dist, double t0, double t1, rt_camera* out)
+{
+    if (!look_from || !look_at || !vup || !out) return fail(RT_ERR_INVALID, "null argument");
+    *out = rtw::camera_new(vec(look_from), vec(look_at), vec(vup), vfov, aspect, aperture, focus_dist, t0, t1);
+    return RT_OK;
+}
+
+int rt_scene_preset_get(int scene_id, rt_scene_preset* out)
+{
+    if (!out) return fail(RT_ERR_INVALID, "null out");
+    rtw::Preset p;
+    if (!rtw::scene_preset(scene_id, p)) return fail(RT_ERR_INVALID, "unknown scene id");
+    auto put = [](double* d, rtw::V3 a) { d[0] = a.x; d[1] = a.y; d[2] = a.z; };
+    put(out->look_from, p.look_from);
+    put(out->look_at, p.look_at);
+    put(out->background, p.background);
+    out->vfov = p.vfov;
+    out->aperture = 0.1;     // main.rs:469
+    out->focus_dist = 10.0;  // main.rs:312
+    out->time0 = 0.0;
+    out->time1 = 1.0;
+    out->default_width = p.width;
+    out->default_spp = p.spp;
+    out->default_aspect = p.aspect;
+    return RT_OK;
+}
+
+int rt_scene_camera(int scene_id, int width, int height, rt_camera* cam, double bg[3])
+{
+    if (!cam || width < 1 || height < 1) return fail(RT_ERR_INVALID, "bad argument");
+    rtw::Preset p;
+    if (!rtw::scene_preset(scene_id, p)) return fail(RT_ERR_INVALID, "unknown scene id");
+    *cam = rtw::camera_new(p.look_from, p.look_at, rtw::v3(0.0, 1.0, 0.0), p.vfov, (double)width / (double)height,
+                           0.1, 10.0, 0.0, 1.0);
+    if (bg) {
+        bg[0] = p.background.x;
+        bg[1] = p.background.y;
+        bg[2] = p.background.z;
+    }
+    return RT_OK;
+}
+
+// ---- lowering + upload ---------------------------------------------------------------
+int rt_world_flatten(rt_world* w, int accel, const rt_scene_soa** soa_out)
+{
+    if (!w || !soa_out) return fail(RT_ERR_INVALID, "null argument");
+    std::string err;
+    int rc = rtw::flatten(w->w, accel, err);
+    if (rc) return fail(rc, err);
+    *soa_out = &w->w.flat.soa;
+    return RT_OK;
+}
+
+int rt_ctx_upload_soa(rt_ctx* c, const rt_scene_soa* s)
+{
+    if (!c || !s) return fail(RT_ERR_INVALID, "null argument");
+    if (s->n_prims < 0 || s->n_prim_refs < 0 || s->n_nodes < 0 || s->n_instances < 0 || s->n_materials < 0 ||
+        s->n_textures < 0 || s->n_perlin < 0 || s->image_bytes < 0)
+        return fail(RT_ERR_INVALID, "negative table size");
+    // validate references so the kernel never indexes out of bounds
+    for (int i = 0; i < s->n_prims; ++i) {
+        const rt_prim& p = s->prims[i];
+        if (p.kind < RT_PRIM_SPHERE || p.kind > RT_PRIM_MEDIUM) return fail(RT_ERR_INVALID, "bad prim kind");
+        if (p.kind == RT_PRIM_INSTANCE && (p.a < 0 || p.a >= s->n_instances)) return fail(RT_ERR_INVALID, "bad instance");
+        if (p.kind == RT_PRIM_MEDIUM && (p.a < 0 || p.a >= s->n_prims)) return fail(RT_ERR_INVALID, "bad boundary");
+        if (p.kind != RT_PRIM_INSTANCE && (p.mat < 0 || p.mat >= s->n_materials)) return fail(RT_ERR_INVALID, "bad material");
+    }
+    for (int i = 0; i < s->n_materials; ++i) {
+        const rt_material& m = s->materials[i];
+        bool needs_tex = m.kind == RT_MAT_LAMBERTIAN || m.kind == RT_MAT_DIFFUSE_LIGHT || m.kind == RT_MAT_ISOTROPIC;
+        if (needs_tex && (m.tex < 0 || m.tex >= s->n_textures)) return fail(RT_ERR_INVALID, "bad texture ref");
+    }
+    for (int i = 0; i < s->n_textures; ++i) {
+        const rt_texture& t = s->textures[i];
+        if (t.kind == RT_TEX_NOISE && (t.perlin < 0 || t.perlin >= s->n_perlin)) return fail(RT_ERR_INVALID, "bad perlin");
+        if (t.kind == RT_TEX_IMAGE && t.img_w > 0 &&
+            t.img_offset + t.img_bps * (int64_t)(t.img_h - 1) + 3 * (int64_t)t.img_w > s->image_bytes)
+            return fail(RT_ERR_INVALID, "image texture out of range");
+    }
+    for (int i = 0; i < s->n_prim_refs; ++i)
+        if (s->prim_refs[i] < 0 || s->prim_refs[i] >= s->n_prims) return fail(RT_ERR_INVALID, "bad prim ref");
+    auto check_ref = [&](int ref) {
+        if (ref >= 0) return ref < s->n_nodes;
+        int code = ~ref;
+        return (code >> 5) + (code & 31) <= s->n_prim_refs;
+    };
+    for (int i = 0; i < s->n_nodes; ++i)
+        if (!check_ref(s->nodes[i].child[0]) || !check_ref(s->nodes[i].child[1])) return fail(RT_ERR_INVALID, "bad node");
+    if (!check_ref(s->tlas_root)) return fail(RT_ERR_INVALID, "bad tlas root");
+    for (int i = 0; i < s->n_instances; ++i) {
+        const rt_instance& in = s->instances[i];
+        if (in.n_ops < 0 || in.n_ops > 4) return fail(RT_ERR_INVALID, "bad instance ops");
+        if (in.child_kind == RT_CHILD_PRIM ? (in.child < 0 || in.child >= s->n_prims) : !check_ref(in.child))
+            return fail(RT_ERR_INVALID, "bad instance child");
+    }
+
+    size_t off[9], bytes[9] = {
+        (size_t)s->n_nodes * sizeof(rt_bvh_node), (size_t)s->n_prim_refs * 4, (size_t)s->n_prims * sizeof(rt_prim),
+        (size_t)s->n_instances * sizeof(rt_instance), (size_t)s->n_materials * sizeof(rt_material),
+        (size_t)s->n_textures * sizeof(rt_texture), (size_t)s->n_perlin * 768 * 8, (size_t)s->n_perlin * 768 * 4,
+        (size_t)s->image_bytes};
+    const void* src[9] = {s->nodes, s->prim_refs, s->prims, s->instances, s->materials, s->textures,
+                          s->perlin_ranvec, s->perlin_perm, s->image_data};
+    size_t total = 0;
+    for (int i = 0; i < 9; ++i) {
+        off[i] = total;
+        total = align_up(total + bytes[i], 256);
+    }
+    total = std::max<size_t>(total, 256);
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (total > c->scene_bytes) {
+        (void)hipFree(c->scene_buf);
+        c->scene_buf = nullptr;
+        c->scene_bytes = 0;
+        HIP_TRY(hipMalloc(&c->scene_buf, total));
+        c->scene_bytes = total;
+    }
+    char* base = (char*)c->scene_buf;
+    for (int i = 0; i < 9; ++i)
+        if (bytes[i]) HIP_TRY(hipMemcpy(base + off[i], src[i], bytes[i], hipMemcpyHostToDevice));
+    c->S.nodes = (const rt_bvh_node*)(base + off[0]);
+    c->S.prim_refs = (const int32_t*)(base + off[1]);
+    c->S.prims = (const rt_prim*)(base + off[2]);
+    c->S.instances = (const rt_instance*)(base + off[3]);
+    c->S.materials = (const rt_material*)(base + off[4]);
+    c->S.textures = (const rt_texture*)(base + off[5]);
+    c->S.perlin_ranvec = (const double*)(base + off[6]);
+    c->S.perlin_perm = (const int32_t*)(base + off[7]);
+    c->S.image = (const uint8_t*)(base + off[8]);
+    c->S.tlas_root = s->tlas_root;
+    c->has_scene = true;
+    c->stats.scene_bytes = (int64_t)total;
+    return RT_OK;
+}
+
+int rt_ctx_upload_world(rt_ctx* c, rt_world* w, int accel)
+{
+    const rt_scene_soa* soa = nullptr;
+    int rc = rt_world_flatten(w, accel, &soa);
+    if (rc) return rc;
+    return rt_ctx_upload_soa(c, soa);
+}
+
+// ---- render ----------------------------------------------------------------------------
+int rt_rows_in_shard(int height, int row_begin, int row_stride)
+{
+    if (height <= 0 || row_stride <= 0 || row_begin < 0 || row_begin >= height) return 0;
+    return (height - row_begin + row_stride - 1) / row_stride;
+}
+
+static int auto_chunk(int spp) { return std::max(1, (spp + 15) / 16); }
+
+int rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, void* out)
+{
+    if (!c || !cam || !p || !out) return fail(RT_ERR_INVALID, "null argument");
+    if (!c->has_scene) return fail(RT_ERR_NO_SCENE, "no scene uploaded");
+    if (p->width < 2 || p->height < 2 || p->spp < 1 || p->max_depth < 0 || p->row_stride < 1 || p->row_begin < 0 ||
+        p->spp_chunk < 0 || (p->out_format != RT_OUT_F32 && p->out_format != RT_OUT_F64))
+        return fail(RT_ERR_INVALID, "bad render params");
+    if ((long long)p->width * p->height > 0xffffffffLL) return fail(RT_ERR_INVALID, "image too large for 32-bit pixel keys");
+    const int n_rows = rt_rows_in_shard(p->height, p->row_begin, p->row_stride);
+    const int chunk = p->spp_chunk > 0 ? std::min(p->spp_chunk, p->spp) : auto_chunk(p->spp);
+    const int n_chunks = (p->spp + chunk - 1) / chunk;
+    const long long n_px = (long long)n_rows * p->width;
+
+    rtk::KParams K;
+    std::memset(&K, 0, sizeof K);
+    K.cam = *cam;
+    for (int i = 0; i < 3; ++i) K.bg[i] = p->background[i];
+    K.scale_m11 = rt_uniform_incl_scale(-1.0, 1.0);
+    K.scale_time = rt_uniform_incl_scale(cam->time0, cam->time1);
+    K.seed = p->render_seed;
+    K.width = p->width;
+    K.height = p->height;
+    K.spp = p->spp;
+    K.max_depth = p->max_depth;
+    K.spp_chunk = chunk;
+    K.n_chunks = n_chunks;
+    K.row_begin = p->row_begin;
+    K.row_stride = p->row_stride;
+    K.n_rows = n_rows;
+    K.tiles_x = (p->width + 7) / 8;
+    K.tiles_y = (n_rows + 7) / 8;
+
+    HIP_TRY(hipSetDevice(c->device));
+    hipStream_t stream = p->stream ? (hipStream_t)p->stream : c->stream;
+    const size_t need = (size_t)n_chunks * (size_t)std::max<long long>(n_px, 1) * 3 * sizeof(double);
+    if (need > c->partial_cap) {
+        HIP_TRY(hipStreamSynchronize(stream));
+        (void)hipFree(c->partial);
+        c->partial = nullptr;
+        c->partial_cap = 0;
+        HIP_TRY(hipMalloc((void**)&c->partial, need));
+        c->partial_cap = need;
+    }
+    const size_t out_bytes = (size_t)n_px * 3 * (p->out_format == RT_OUT_F64 ? 8 : 4);
+    void* dev_out = out;
+    if (!p->out_on_device) {
+        if (out_bytes > c->out_cap) {
+            (void)hipFree(c->out_buf);
+            c->out_buf = nullptr;
+            c->out_cap = 0;
+            HIP_TRY(hipMalloc(&c->out_buf, std::max<size_t>(out_bytes, 16)));
+            c->out_cap = std::max<size_t>(out_bytes, 16);
+        }
+        dev_out = c->out_buf;
+    }
+    const bool count = p->count_work != 0;
+    if (count) HIP_TRY(hipMemsetAsync(c->counters, 0, 4 * sizeof(unsigned long long), stream));
+    HIP_TRY(hipEventRecord(c->ev[0], stream));
+    HIP_TRY(rtk::launch_trace(c->S, K, c->partial, c->counters, count, stream));
+    HIP_TRY(hipEventRecord(c->ev[1], stream));
+    HIP_TRY(rtk::launch_reduce(c->partial, dev_out, p->out_format == RT_OUT_F64, n_px, n_chunks,
+                               1.0 / (double)p->spp, stream));
+    HIP_TRY(hipEventRecord(c->ev[2], stream));
+
+    c->stats.samples = (uint64_t)n_px * (uint64_t)p->spp;
+    c->stats.n_items = (uint64_t)n_px * (uint64_t)n_chunks;
+    c->stats.n_chunks = n_chunks;
+    c->stats.spp_chunk = chunk;
+    c->stats.node_bytes = (int32_t)sizeof(rt_bvh_node);
+    c->stats.prim_bytes = (int32_t)sizeof(rt_prim);
+    c->stats.material_bytes = (int32_t)sizeof(rt_material);
+    c->pending_stats = true;
+    c->pending_counts = count;
+    if (!c->stats.samples) {
+        c->stats.casts = c->stats.node_visits = c->stats.prim_tests = 0;
+    }
+    if (!p->out_on_device) {
+        HIP_TRY(hipMemcpyAsync(out, dev_out, out_bytes, hipMemcpyDeviceToHost, stream));
+        HIP_TRY(hipStreamSynchronize(stream));
+    }
+    return RT_OK;
+}
+
+int rt_last_stats(rt_ctx* c, rt_stats* out)
+{
+    if (!c || !out) return fail(RT_ERR_INVALID, "null argument");
+    if (c->pending_stats) {
+        HIP_TRY(hipSetDevice(c->device));
+        HIP_TRY(hipEventSynchronize(c->ev[2]));
+        float a = 0, b = 0;
+        HIP_TRY(hipEventElapsedTime(&a, c->ev[0], c->ev[1]));
+        HIP_TRY(hipEventElapsedTime(&b, c->ev[1], c->ev[2]));
+        c->stats.kernel_ms = a;
+        c->stats.reduce_ms = b;
+        if (c->pending_counts) {
+            unsigned long long h[4];
+            HIP_TRY(hipMemcpy(h, c->counters, sizeof h, hipMemcpyDeviceToHost));
+            c->stats.casts = h[0];
+            c->stats.node_visits = h[1];
+            c->stats.prim_tests = h[2];
+        } else {
+            c->stats.casts = c->stats.node_visits = c->stats.prim_tests = 0;
+        }
+        c->pending_stats = false;
+    }
+    *out = c->stats;
+    return RT_OK;
+}
+
+// ---- output ---------------------------------------------------------------------------------
+int rt_write_ppm(const float* mean, int width, int height, const char* path)
+{
+    if (!mean || !path || width < 1 || height < 1) return fail(RT_ERR_INVALID, "bad argument");
+    FILE* f = std::fopen(path, "wb");
+    if (!f) return fail(RT_ERR_INVALID, std::string("cannot open ") + path);
+    std::fprintf(f, "P3\n%d %d\n255\n\n", width, height);  // main.rs:472 (println! adds the blank line)
+    auto to_byte = [](double x) {                           // math.rs:119-131
+        double r = std::sqrt(x);
+        double c = r < 0.0 ? 0.0 : r > 0.999 ? 0.999 : r;   // clamp (NaN passes through)
+        return (int)rt_sat_i32(256.0 * c);                  // `as i32`: NaN -> 0
+    };
+    for (int j = height - 1; j >= 0; --j)                   // main.rs:591-596
+        for (int i = 0; i < width; ++i) {
+            const float* px = mean + ((size_t)j * width + i) * 3;
+            std::fprintf(f, "%d %d %d\n", to_byte(px[0]), to_byte(px[1]), to_byte(px[2]));
+        }
+    std::fclose(f);
+    return RT_OK;
+}
+
+// ---- self test ----------------------------------------------------------------------------------
+int rt_device_eval(rt_ctx* c, int fn, const double* x, const double* y, const double* z, double* out, int n)
+{
+    if (!c || !x || !out || n < 0 || fn < 0 || fn > 11) return fail(RT_ERR_INVALID, "bad argument");
+    if (n == 0) return RT_OK;
+    HIP_TRY(hipSetDevice(c->device));
+    double* d = nullptr;
+    const size_t b = (size_t)n * sizeof(double);
+    HIP_TRY(hipMalloc((void**)&d, 4 * b));
+    hipError_t e = hipMemcpy(d, x, b, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(d + n, y ? y : x, b, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(d + 2 * n, z ? z : x, b, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = rtk::launch_eval(fn, d, d + n, d + 2 * n, d + 3 * n, n, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e == hipSuccess) e = hipMemcpy(out, d + 3 * n, b, hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    if (e != hipSuccess) return hip_fail(e, "rt_device_eval");
+    return RT_OK;
+}
+
+}  // extern "C"

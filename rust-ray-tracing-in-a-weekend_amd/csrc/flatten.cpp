@@ -1,0 +1,408 @@
+// flatten.cpp — lowers the World's Hittable tree into the SoA tables of
+// rt_scene.h and builds the SAH BVHs the megakernel traverses.
+//
+// Lowering rules (hittable.rs:30-41):
+//   Sphere / MovingSphere / XY,XZ,YZ rects / Box   -> one rt_prim each
+//   BvhNode (reference median BVH, :77-130)        -> dissolved; its leaves join the
+//                                                     enclosing SAH BVH (closest-hit is
+//                                                     independent of the hierarchy)
+//   Translate / RotateY chains (:232-244, :386-415) -> rt_instance (<= 4 ops) whose child
+//                                                     is a single prim or its own BLAS
+//   ConstantMedium (:417-473)                       -> RT_PRIM_MEDIUM whose boundary is a
+//                                                     hidden prim (sphere / box / instance)
+// The top-level list becomes the TLAS. A medium or an instance below an instance is
+// not lowered (RT_ERR_UNSUPPORTED); none of the reference scenes builds one.
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <numeric>
+
+#include "rt/rt_abi.h"
+#include "scene_model.hpp"
+
+namespace rtw {
+
+namespace {
+
+struct Item {
+    int prim;
+    double lo[3], hi[3];
+    double c[3];
+};
+
+struct Builder {
+    World& w;
+    FlatScene& f;
+    std::string& err;
+
+    int add_prim(const rt_prim& p)
+    {
+        f.prims.push_back(p);
+        return (int)f.prims.size() - 1;
+    }
+
+    static rt_prim blank(int kind, int mat)
+    {
+        rt_prim p;
+        std::memset(&p, 0, sizeof p);
+        p.kind = kind;
+        p.mat = mat;
+        return p;
+    }
+
+    bool is_simple(HKind k) const
+    {
+        return k == HKind::Sphere || k == HKind::MovingSphere || k == HKind::XYRect || k == HKind::XZRect ||
+               k == HKind::YZRect || k == HKind::Box;
+    }
+
+    int lower_simple(int id)
+    {
+        const HNode& h = w.nodes[id];
+        rt_prim p = blank(0, h.mat - 1);
+        switch (h.kind) {
+        case HKind::Sphere:
+            p.kind = RT_PRIM_SPHERE;
+            p.p[0] = h.c0.x; p.p[1] = h.c0.y; p.p[2] = h.c0.z;
+            p.p[3] = h.radius;
+            p.p[4] = 1.0 / h.radius;  // the reference's Div: (1/r) * v (math.rs:260-266)
+            break;
+        case HKind::MovingSphere:
+            p.kind = RT_PRIM_MOVING_SPHERE;
+            p.p[0] = h.c0.x; p.p[1] = h.c0.y; p.p[2] = h.c0.z;
+            p.p[3] = h.radius;
+            p.p[4] = 1.0 / h.radius;
+            p.p[5] = h.c1.x - h.c0.x; p.p[6] = h.c1.y - h.c0.y; p.p[7] = h.c1.z - h.c0.z;  // hittable.rs:557
+            p.p[8] = h.t0; p.p[9] = h.t1;
+            p.a = (h.t0 == 0.0 && h.t1 == 1.0) ? 1 : 0;  // (time - 0) / (1 - 0) == time exactly
+            break;
+        case HKind::XYRect: case HKind::XZRect: case HKind::YZRect:
+            p.kind = h.kind == HKind::XYRect ? RT_PRIM_XY_RECT : h.kind == HKind::XZRect ? RT_PRIM_XZ_RECT
+                                                                                         : RT_PRIM_YZ_RECT;
+            p.p[0] = h.a0; p.p[1] = h.a1; p.p[2] = h.b0; p.p[3] = h.b1; p.p[4] = h.k;
+            break;
+        case HKind::Box:
+            p.kind = RT_PRIM_BOX;
+            p.p[0] = h.bmin.x; p.p[1] = h.bmin.y; p.p[2] = h.bmin.z;
+            p.p[3] = h.bmax.x; p.p[4] = h.bmax.y; p.p[5] = h.bmax.z;
+            break;
+        default: break;
+        }
+        return add_prim(p);
+    }
+
+    // Collects the simple leaves under id (through BvhNodes). Returns false on an
+    // instance or medium inside.
+    bool collect_simple(int id, std::vector<int>& out)
+    {
+        const HNode& h = w.nodes[id];
+        if (h.kind == HKind::BvhNode) {
+            if (!collect_simple(h.left, out)) return false;
+            if (h.right != h.left && !collect_simple(h.right, out)) return false;  // span-1 duplicate
+            return true;
+        }
+        if (!is_simple(h.kind)) return false;
+        out.push_back(id);
+        return true;
+    }
+
+    Item item_of(int prim, int hid)
+    {
+        Item it;
+        it.prim = prim;
+        AABB b;
+        w.bounding_box(hid, 0.0, 1.0, b);
+        it.lo[0] = b.minimum.x; it.lo[1] = b.minimum.y; it.lo[2] = b.minimum.z;
+        it.hi[0] = b.maximum.x; it.hi[1] = b.maximum.y; it.hi[2] = b.maximum.z;
+        for (int a = 0; a < 3; ++a) it.c[a] = 0.5 * (it.lo[a] + it.hi[a]);
+        return it;
+    }
+
+    int lower_instance(int id, int& prim_out)
+    {
+        rt_instance in;
+        std::memset(&in, 0, sizeof in);
+        int cur = id;
+        while (w.nodes[cur].kind == HKind::Translate || w.nodes[cur].kind == HKind::RotateY) {
+            if (in.n_ops == 4) { err = "instance chain longer than 4 Translate/RotateY ops"; return RT_ERR_UNSUPPORTED; }
+            const HNode& h = w.nodes[cur];
+            if (h.kind == HKind::Translate) {
+                in.op_kind[in.n_ops] = RT_OP_TRANSLATE;
+                in.op[in.n_ops][0] = h.offset.x; in.op[in.n_ops][1] = h.offset.y; in.op[in.n_ops][2] = h.offset.z;
+            } else {
+                in.op_kind[in.n_ops] = RT_OP_ROTATE_Y;
+                in.op[in.n_ops][0] = h.sin_theta; in.op[in.n_ops][1] = h.cos_theta;
+            }
+            in.n_ops++;
+            cur = h.ptr;
+        }
+        const HNode& child = w.nodes[cur];
+        if (is_simple(child.kind)) {
+            in.child_kind = RT_CHILD_PRIM;
+            in.child = lower_simple(cur);
+        } else if (child.kind == HKind::BvhNode) {
+            std::vector<int> leaves;
+            if (!collect_simple(cur, leaves)) {
+                err = "instance over a BVH that contains an instance or a medium";
+                return RT_ERR_UNSUPPORTED;
+            }
+            std::vector<Item> items;
+            for (int hid : leaves) items.push_back(item_of(lower_simple(hid), hid));
+            in.child_kind = RT_CHILD_BVH;
+            in.child = build_bvh(items);
+        } else {
+            err = "instance over an instance or a medium";
+            return RT_ERR_UNSUPPORTED;
+        }
+        f.instances.push_back(in);
+        rt_prim p = blank(RT_PRIM_INSTANCE, -1);
+        p.a = (int)f.instances.size() - 1;
+        prim_out = add_prim(p);
+        return RT_OK;
+    }
+
+    int lower_boundary(int id, int& prim_out)
+    {
+        const HNode& h = w.nodes[id];
+        if (h.kind == HKind::Sphere || h.kind == HKind::MovingSphere || h.kind == HKind::Box ||
+            h.kind == HKind::XYRect || h.kind == HKind::XZRect || h.kind == HKind::YZRect) {
+            prim_out = lower_simple(id);
+            return RT_OK;
+        }
+        if (h.kind == HKind::Translate || h.kind == HKind::RotateY) return lower_instance(id, prim_out);
+        err = "constant medium boundary must be a primitive or a Translate/RotateY chain";
+        return RT_ERR_UNSUPPORTED;
+    }
+
+    int lower_top(int id, std::vector<Item>& items)
+    {
+        const HNode& h = w.nodes[id];
+        switch (h.kind) {
+        case HKind::BvhNode: {
+            int rc = lower_top(h.left, items);
+            if (rc) return rc;
+            if (h.right != h.left) return lower_top(h.right, items);
+            return RT_OK;
+        }
+        case HKind::Translate: case HKind::RotateY: {
+            int prim;
+            int rc = lower_instance(id, prim);
+            if (rc) return rc;
+            items.push_back(item_of(prim, id));
+            return RT_OK;
+        }
+        case HKind::ConstantMedium: {
+            int bprim;
+            int rc = lower_boundary(h.ptr, bprim);
+            if (rc) return rc;
+            rt_prim p = blank(RT_PRIM_MEDIUM, h.mat - 1);
+            p.a = bprim;
+            p.b = h.medium_id;
+            p.p[0] = h.neg_inv_density;
+            items.push_back(item_of(add_prim(p), id));
+            return RT_OK;
+        }
+        default:
+            items.push_back(item_of(lower_simple(id), id));
+            return RT_OK;
+        }
+    }
+
+    // ---- SAH BVH ---------------------------------------------------------------
+    static double area(const double lo[3], const double hi[3])
+    {
+        double dx = std::max(0.0, hi[0] - lo[0]), dy = std::max(0.0, hi[1] - lo[1]), dz = std::max(0.0, hi[2] - lo[2]);
+        return 2.0 * (dx * dy + dy * dz + dz * dx);
+    }
+
+    static void bounds(const std::vector<Item>& items, int b, int e, double lo[3], double hi[3])
+    {
+        for (int a = 0; a < 3; ++a) { lo[a] = INFINITY; hi[a] = -INFINITY; }
+        for (int i = b; i < e; ++i)
+            for (int a = 0; a < 3; ++a) {
+                lo[a] = std::min(lo[a], items[i].lo[a]);
+                hi[a] = std::max(hi[a], items[i].hi[a]);
+            }
+    }
+
+    // Pads and rounds a box outward to f32 so the f64 slab test on it never culls
+    // a primitive the exact test would hit (the box only gates traversal).
+    static void to_f32_box(const double lo[3], const double hi[3], float flo[3], float fhi[3])
+    {
+        for (int a = 0; a < 3; ++a) {
+            double mag = std::max(std::fabs(lo[a]), std::fabs(hi[a]));
+            double pad = 1e-6 * (1.0 + mag);
+            double l = lo[a] - pad, h = hi[a] + pad;
+            float fl = (float)l, fh = (float)h;
+            if ((double)fl > l) fl = std::nextafter(fl, -INFINITY);
+            if ((double)fh < h) fh = std::nextafter(fh, INFINITY);
+            flo[a] = fl;
+            fhi[a] = fh;
+        }
+    }
+
+    int make_leaf(std::vector<Item>& items, int b, int e)
+    {
+        int first = (int)f.prim_refs.size();
+        for (int i = b; i < e; ++i) f.prim_refs.push_back(items[i].prim);
+        return RT_LEAF_CODE(first, e - b);
+    }
+
+    int build_rec(std::vector<Item>& items, int b, int e)
+    {
+        const int n = e - b;
+        const double c_trav = 1.0, c_isect = 1.5;
+        double plo[3], phi[3];
+        bounds(items, b, e, plo, phi);
+        double parea = area(plo, phi);
+        if (n <= 2) return make_leaf(items, b, e);
+        // full-sweep SAH over the three axes (centroid order; ties by prim index)
+        double best_cost = INFINITY;
+        int best_axis = -1, best_split = -1;
+        std::vector<double> right_area(n);
+        for (int axis = 0; axis < 3; ++axis) {
+            std::sort(items.begin() + b, items.begin() + e, [axis](const Item& x, const Item& y) {
+                return x.c[axis] < y.c[axis] || (x.c[axis] == y.c[axis] && x.prim < y.prim);
+            });
+            double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+            for (int i = n - 1; i >= 1; --i) {
+                for (int a = 0; a < 3; ++a) {
+                    lo[a] = std::min(lo[a], items[b + i].lo[a]);
+                    hi[a] = std::max(hi[a], items[b + i].hi[a]);
+                }
+                right_area[i] = area(lo, hi);
+            }
+            for (int a = 0; a < 3; ++a) { lo[a] = INFINITY; hi[a] = -INFINITY; }
+            for (int i = 1; i < n; ++i) {
+                for (int a = 0; a < 3; ++a) {
+                    lo[a] = std::min(lo[a], items[b + i - 1].lo[a]);
+                    hi[a] = std::max(hi[a], items[b + i - 1].hi[a]);
+                }
+                double cost = c_trav + c_isect * (area(lo, hi) * i + right_area[i] * (n - i)) / std::max(parea, 1e-300);
+                if (cost < best_cost) {
+                    best_cost = cost;
+                    best_axis = axis;
+                    best_split = i;
+                }
+            }
+        }
+        double leaf_cost = c_isect * n;
+        if (n <= 4 && leaf_cost <= best_cost) return make_leaf(items, b, e);
+        if (best_axis < 0) best_axis = 0, best_split = n / 2;
+        std::sort(items.begin() + b, items.begin() + e, [best_axis](const Item& x, const Item& y) {
+            return x.c[best_axis] < y.c[best_axis] || (x.c[best_axis] == y.c[best_axis] && x.prim < y.prim);
+        });
+        int mid = b + best_split;
+        int node = (int)f.nodes.size();
+        f.nodes.emplace_back();
+        double llo[3], lhi[3], rlo[3], rhi[3];
+        bounds(items, b, mid, llo, lhi);
+        bounds(items, mid, e, rlo, rhi);
+        int lc = build_rec(items, b, mid);
+        int rc = build_rec(items, mid, e);
+        rt_bvh_node& nd = f.nodes[node];
+        std::memset(&nd, 0, sizeof nd);
+        to_f32_box(llo, lhi, nd.lo0, nd.hi0);
+        to_f32_box(rlo, rhi, nd.lo1, nd.hi1);
+        nd.child[0] = lc;
+        nd.child[1] = rc;
+        return node;
+    }
+
+    int build_bvh(std::vector<Item>& items)
+    {
+        if (items.empty()) return RT_LEAF_CODE((int)f.prim_refs.size(), 0);
+        return build_rec(items, 0, (int)items.size());
+    }
+};
+
+}  // namespace
+
+int flatten(World& w, int accel, std::string& err)
+{
+    if (accel != RT_ACCEL_SAH) {
+        err = "unknown accel mode";
+        return RT_ERR_INVALID;
+    }
+    FlatScene f;
+    Builder bld{w, f, err};
+    std::vector<Item> top;
+    for (int id : w.hittables) {
+        if (!w.valid_hittable(id)) {
+            err = "invalid hittable id in world list";
+            return RT_ERR_INVALID;
+        }
+        int rc = bld.lower_top(id, top);
+        if (rc) return rc;
+    }
+    f.tlas_root = bld.build_bvh(top);
+    f.media = w.n_media;
+
+    for (const Material& m : w.materials) {
+        rt_material rm;
+        std::memset(&rm, 0, sizeof rm);
+        rm.kind = m.kind;
+        rm.tex = m.tex;
+        rm.albedo[0] = m.albedo.x; rm.albedo[1] = m.albedo.y; rm.albedo[2] = m.albedo.z;
+        rm.fuzz = m.fuzz;
+        rm.ir = m.ir;
+        f.materials.push_back(rm);
+    }
+    for (const PerlinTables& p : w.perlins) {
+        for (int i = 0; i < 256; ++i)
+            for (int a = 0; a < 3; ++a) f.perlin_ranvec.push_back(p.ranvec[i][a]);
+        for (int a = 0; a < 3; ++a)
+            for (int i = 0; i < 256; ++i) f.perlin_perm.push_back(p.perm[a][i]);
+    }
+    std::vector<int64_t> img_off;
+    for (const Image& im : w.images) {
+        img_off.push_back((int64_t)f.image.size());
+        f.image.insert(f.image.end(), im.rgb.begin(), im.rgb.end());
+    }
+    for (const Texture& t : w.textures) {
+        rt_texture rt;
+        std::memset(&rt, 0, sizeof rt);
+        rt.kind = t.kind;
+        rt.perlin = t.perlin;
+        rt.c0[0] = t.c0.x; rt.c0[1] = t.c0.y; rt.c0[2] = t.c0.z;
+        rt.c1[0] = t.c1.x; rt.c1[1] = t.c1.y; rt.c1[2] = t.c1.z;
+        rt.scale = t.scale;
+        if (t.kind == RT_TEX_IMAGE) {
+            const Image& im = w.images[t.image];
+            rt.img_w = im.rgb.empty() ? 0 : im.w;
+            rt.img_h = im.rgb.empty() ? 0 : im.h;
+            rt.img_offset = img_off[t.image];
+            rt.img_bps = 3 * (int64_t)im.w;
+        }
+        f.textures.push_back(rt);
+    }
+
+    rt_scene_soa& s = f.soa;
+    std::memset(&s, 0, sizeof s);
+    s.n_prims = (int32_t)f.prims.size();
+    s.n_prim_refs = (int32_t)f.prim_refs.size();
+    s.n_nodes = (int32_t)f.nodes.size();
+    s.n_instances = (int32_t)f.instances.size();
+    s.n_materials = (int32_t)f.materials.size();
+    s.n_textures = (int32_t)f.textures.size();
+    s.n_perlin = (int32_t)w.perlins.size();
+    s.n_media = f.media;
+    s.tlas_root = f.tlas_root;
+    s.accel = accel;
+    s.image_bytes = (int64_t)f.image.size();
+    w.flat = std::move(f);
+    FlatScene& g = w.flat;
+    rt_scene_soa& t = g.soa;
+    t.prims = g.prims.data();
+    t.prim_refs = g.prim_refs.data();
+    t.nodes = g.nodes.data();
+    t.instances = g.instances.data();
+    t.materials = g.materials.data();
+    t.textures = g.textures.data();
+    t.perlin_ranvec = g.perlin_ranvec.data();
+    t.perlin_perm = g.perlin_perm.data();
+    t.image_data = g.image.data();
+    return RT_OK;
+}
+
+}  // namespace rtw

@@ -1,0 +1,748 @@
+// trace_kernel.hip — the MI355X megakernel for the reference's per-(pixel, sample)
+// hot path: Camera::get_ray (camera.rs:58-66) + ray_color (main.rs:19-38) and
+// everything below it (hittable.rs, material.rs, texture.rs, perlin.rs), in f64
+// like the reference (math.rs:13-17).
+//
+// Execution model:
+//   * one work item = (pixel, chunk of spp_chunk samples); a wave64 owns an 8x8
+//     pixel tile of one chunk, so neighbouring lanes trace coherent rays;
+//   * the depth-50 recursion is an iterative bounce loop; a lane whose path ends
+//     starts its next sample in the same loop iteration (path regeneration), so a
+//     wave stays busy until every lane has finished its chunk;
+//   * the lane sums its chunk's samples in sample order (deterministic), writes
+//     one f64x3 partial; a second kernel adds the partials in chunk order and
+//     scales by 1/spp (math.rs:119-126), so the image does not depend on the
+//     launch geometry or on how rows are sharded over GPUs;
+//   * RNG: Philox4x32-10 keyed by (pixel, sample) (rt_numerics.h), the medium's
+//     in-hit draw keyed by (pixel, sample, bounce, medium id).
+// Built with -ffp-contract=off: bit-for-bit the operation order of the reference.
+#include <hip/hip_runtime.h>
+
+#include "rt/rt_numerics.h"
+#include "rt/rt_scene.h"
+#include "trace_kernel.hpp"
+
+namespace rtk {
+
+struct Ray {
+    double ox, oy, oz;
+    double dx, dy, dz;
+    double time;
+    double a;                 // length_squared(direction)
+    double ix, iy, iz;        // 1 / direction (slab tests only)
+};
+
+struct Hit {
+    double t, px, py, pz, nx, ny, nz;
+    double uv0, uv1, uv2, uv3;  // uvkind 1: object-space outward normal; 2: (x-a0, a1-a0, y-b0, b1-b0)
+    int front, mat, uvkind;
+};
+
+struct Keyed {                 // coordinates of the medium's keyed draw
+    uint64_t seed;
+    uint32_t pixel, sample, bounce;
+};
+
+struct Count {
+    uint32_t casts, nodes, prims;
+};
+
+__device__ __forceinline__ void finish_ray(Ray& r)
+{
+    r.a = r.dx * r.dx + r.dy * r.dy + r.dz * r.dz;
+    r.ix = 1.0 / r.dx;
+    r.iy = 1.0 / r.dy;
+    r.iz = 1.0 / r.dz;
+}
+
+// hittable.rs:23-26
+__device__ __forceinline__ void set_face_normal(Hit& h, double dx, double dy, double dz, double nx, double ny,
+                                                double nz)
+{
+    const bool front = dx * nx + dy * ny + dz * nz < 0.0;
+    h.front = front;
+    h.nx = front ? nx : -nx;
+    h.ny = front ? ny : -ny;
+    h.nz = front ? nz : -nz;
+}
+
+// hittable.rs:254-288 (sphere_uv deferred: the outward normal is kept in uv0..2)
+__device__ __forceinline__ bool hit_sphere(double cx, double cy, double cz, double radius, double inv_r,
+                                           const Ray& r, double t_min, double t_max, int mat, Hit& h)
+{
+    const double ocx = r.ox - cx, ocy = r.oy - cy, ocz = r.oz - cz;
+    const double half_b = ocx * r.dx + ocy * r.dy + ocz * r.dz;
+    const double c = (ocx * ocx + ocy * ocy + ocz * ocz) - radius * radius;
+    const double disc = half_b * half_b - r.a * c;
+    if (disc < 0.0) return false;
+    const double sqrtd = __builtin_sqrt(disc);
+    double root = (-half_b - sqrtd) / r.a;
+    if (root < t_min || t_max < root) {
+        root = (-half_b + sqrtd) / r.a;
+        if (root < t_min || t_max < root) return false;
+    }
+    h.t = root;
+    h.px = r.ox + r.dx * root;
+    h.py = r.oy + r.dy * root;
+    h.pz = r.oz + r.dz * root;
+    const double onx = (h.px - cx) * inv_r, ony = (h.py - cy) * inv_r, onz = (h.pz - cz) * inv_r;
+    set_face_normal(h, r.dx, r.dy, r.dz, onx, ony, onz);
+    h.mat = mat;
+    h.uvkind = 1;
+    h.uv0 = onx;
+    h.uv1 = ony;
+    h.uv2 = onz;
+    return true;
+}
+
+// hittable.rs:308-384. axis: 0 XY (k on z), 1 XZ (k on y), 2 YZ (k on x).
+__device__ __forceinline__ bool hit_rect(int axis, double a0, double a1, double b0, double b1, double k,
+                                         const Ray& r, double t_min, double t_max, int mat, Hit& h)
+{
+    double ok, dk, oa, da, ob, db;
+    if (axis == 0) { ok = r.oz; dk = r.dz; oa = r.ox; da = r.dx; ob = r.oy; db = r.dy; }
+    else if (axis == 1) { ok = r.oy; dk = r.dy; oa = r.ox; da = r.dx; ob = r.oz; db = r.dz; }
+    else { ok = r.ox; dk = r.dx; oa = r.oy; da = r.dy; ob = r.oz; db = r.dz; }
+    const double t = (k - ok) / dk;
+    if (t < t_min || t > t_max) return false;
+    const double x = oa + t * da;
+    const double y = ob + t * db;
+    if (x < a0 || x > a1 || y < b0 || y > b1) return false;
+    h.uvkind = 2;
+    h.uv0 = x - a0;
+    h.uv1 = a1 - a0;
+    h.uv2 = y - b0;
+    h.uv3 = b1 - b0;
+    h.t = t;
+    set_face_normal(h, r.dx, r.dy, r.dz, axis == 2 ? 1.0 : 0.0, axis == 1 ? 1.0 : 0.0, axis == 0 ? 1.0 : 0.0);
+    h.mat = mat;
+    h.px = r.ox + r.dx * t;
+    h.py = r.oy + r.dy * t;
+    h.pz = r.oz + r.dz * t;
+    return true;
+}
+
+// Sphere, MovingSphere, rects, Box (hittable.rs:211-231).
+template <bool COUNT>
+__device__ __forceinline__ bool hit_simple(const rt_prim& p, const Ray& r, double t_min, double t_max, Hit& h,
+                                           Count& cnt)
+{
+    if (COUNT) cnt.prims++;
+    switch (p.kind) {
+    case RT_PRIM_SPHERE: return hit_sphere(p.p[0], p.p[1], p.p[2], p.p[3], p.p[4], r, t_min, t_max, p.mat, h);
+    case RT_PRIM_MOVING_SPHERE: {
+        // center_0 + ((time - time_0) / (time_1 - time_0)) * (center_1 - center_0)
+        const double s = p.a ? r.time : (r.time - p.p[8]) / (p.p[9] - p.p[8]);
+        return hit_sphere(p.p[0] + p.p[5] * s, p.p[1] + p.p[6] * s, p.p[2] + p.p[7] * s, p.p[3], p.p[4], r, t_min,
+                          t_max, p.mat, h);
+    }
+    case RT_PRIM_XY_RECT: return hit_rect(0, p.p[0], p.p[1], p.p[2], p.p[3], p.p[4], r, t_min, t_max, p.mat, h);
+    case RT_PRIM_XZ_RECT: return hit_rect(1, p.p[0], p.p[1], p.p[2], p.p[3], p.p[4], r, t_min, t_max, p.mat, h);
+    case RT_PRIM_YZ_RECT: return hit_rect(2, p.p[0], p.p[1], p.p[2], p.p[3], p.p[4], r, t_min, t_max, p.mat, h);
+    case RT_PRIM_BOX: {  // hit_hittables over the 6 sides in new_box order (hittable.rs:135-142)
+        const double mnx = p.p[0], mny = p.p[1], mnz = p.p[2], mxx = p.p[3], mxy = p.p[4], mxz = p.p[5];
+        double closest = t_max;
+        bool any = false;
+        if (hit_rect(0, mnx, mxx, mny, mxy, mxz, r, t_min, closest, p.mat, h)) { closest = h.t; any = true; }
+        if (hit_rect(0, mnx, mxx, mny, mxy, mnz, r, t_min, closest, p.mat, h)) { closest = h.t; any = true; }
+        if (hit_rect(1, mnx, mxx, mnz, mxz, mxy, r, t_min, closest, p.mat, h)) { closest = h.t; any = true; }
+        if (hit_rect(1, mnx, mxx, mnz, mxz, mny, r, t_min, closest, p.mat, h)) { closest = h.t; any = true; }
+        if (hit_rect(2, mny, mxy, mnz, mxz, mxx, r, t_min, closest, p.mat, h)) { closest = h.t; any = true; }
+        if (hit_rect(2, mny, mxy, mnz, mxz, mnx, r, t_min, closest, p.mat, h)) { closest = h.t; any = true; }
+        return any;
+    }
+    default: return false;
+    }
+}
+
+// Conservative slab test against an f32 box (rounded outward and padded on the
+// host), in f64. NaN products (0 * inf) are ignored by fmin/fmax.
+__device__ __forceinline__ bool slab(const float* lo, const float* hi, const Ray& r, double t_min, double t_max,
+                                     double& t_near)
+{
+    const double x0 = ((double)lo[0] - r.ox) * r.ix, x1 = ((double)hi[0] - r.ox) * r.ix;
+    const double y0 = ((double)lo[1] - r.oy) * r.iy, y1 = ((double)hi[1] - r.oy) * r.iy;
+    const double z0 = ((double)lo[2] - r.oz) * r.iz, z1 = ((double)hi[2] - r.oz) * r.iz;
+    const double tn = fmax(fmax(fmin(x0, x1), fmin(y0, y1)), fmax(fmin(z0, z1), t_min));
+    const double tf = fmin(fmin(fmax(x0, x1), fmax(y0, y1)), fmin(fmax(z0, z1), t_max));
+    t_near = tn;
+    return tn <= tf;
+}
+
+// Closest hit in a BVH whose leaves hold simple prims (a BLAS).
+template <bool COUNT>
+__device__ bool trace_blas(const SceneDev& S, int root, const Ray& r, double t_min, double t_max, Hit& h,
+                           int* stack, int sp0, Count& cnt)
+{
+    bool any = false;
+    int sp = sp0;
+    int cur = root;
+    for (;;) {
+        if (cur < 0) {
+            const int code = ~cur;
+            const int first = code >> 5, count = code & 31;
+            for (int i = 0; i < count; ++i) {
+                const rt_prim& p = S.prims[S.prim_refs[first + i]];
+                if (hit_simple<COUNT>(p, r, t_min, t_max, h, cnt)) { t_max = h.t; any = true; }
+            }
+            if (sp == sp0) break;
+            cur = stack[--sp];
+        } else {
+            if (COUNT) cnt.nodes++;
+            const rt_bvh_node& nd = S.nodes[cur];
+            double tn0, tn1;
+            const bool h0 = slab(nd.lo0, nd.hi0, r, t_min, t_max, tn0);
+            const bool h1 = slab(nd.lo1, nd.hi1, r, t_min, t_max, tn1);
+            if (h0 && h1) {
+                const bool first_left = tn0 <= tn1;
+                stack[sp++] = first_left ? nd.child[1] : nd.child[0];
+                cur = first_left ? nd.child[0] : nd.child[1];
+            } else if (h0) {
+                cur = nd.child[0];
+            } else if (h1) {
+                cur = nd.child[1];
+            } else {
+                if (sp == sp0) break;
+                cur = stack[--sp];
+            }
+        }
+    }
+    return any;
+}
+
+// Translate / RotateY chain (hittable.rs:232-244, 386-415), outermost op first.
+template <bool COUNT>
+__device__ bool hit_instance(const SceneDev& S, const rt_instance& in, const Ray& ray, double t_min, double t_max,
+                             Hit& h, int* stack, int sp0, Count& cnt)
+{
+    Ray r = ray;
+    double dirx[4], diry[4], dirz[4];
+    const int n = in.n_ops;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        if (i < n) {
+            if (in.op_kind[i] == RT_OP_TRANSLATE) {  // moved_ray = (o - offset, d, time)
+                r.ox = r.ox - in.op[i][0];
+                r.oy = r.oy - in.op[i][1];
+                r.oz = r.oz - in.op[i][2];
+            } else {                                  // rotated_ray
+                const double s = in.op[i][0], c = in.op[i][1];
+                const double ox = c * r.ox - s * r.oz, oz = s * r.ox + c * r.oz;
+                const double dx = c * r.dx - s * r.dz, dz = s * r.dx + c * r.dz;
+                r.ox = ox; r.oz = oz; r.dx = dx; r.dz = dz;
+            }
+            dirx[i] = r.dx; diry[i] = r.dy; dirz[i] = r.dz;
+        }
+    }
+    finish_ray(r);
+    bool hit;
+    if (in.child_kind == RT_CHILD_PRIM) hit = hit_simple<COUNT>(S.prims[in.child], r, t_min, t_max, h, cnt);
+    else hit = trace_blas<COUNT>(S, in.child, r, t_min, t_max, h, stack, sp0, cnt);
+    if (!hit) return false;
+#pragma unroll
+    for (int i = 3; i >= 0; --i) {
+        if (i < n) {
+            if (in.op_kind[i] == RT_OP_TRANSLATE) {  // rec.point += offset; set_face_normal(moved_ray, normal)
+                h.px = h.px + in.op[i][0];
+                h.py = h.py + in.op[i][1];
+                h.pz = h.pz + in.op[i][2];
+                set_face_normal(h, dirx[i], diry[i], dirz[i], h.nx, h.ny, h.nz);
+            } else {                                  // rotate back; set_face_normal(rotated_ray, normal)
+                const double s = in.op[i][0], c = in.op[i][1];
+                const double px = c * h.px + s * h.pz, pz = -s * h.px + c * h.pz;
+                const double nx = c * h.nx + s * h.nz, nz = -s * h.nx + c * h.nz;
+                h.px = px; h.pz = pz;
+                set_face_normal(h, dirx[i], diry[i], dirz[i], nx, h.ny, nz);
+            }
+        }
+    }
+    return true;
+}
+
+template <bool COUNT>
+__device__ __forceinline__ bool hit_boundary(const SceneDev& S, int prim, const Ray& r, double t_min, double t_max,
+                                             Hit& h, int* stack, int sp0, Count& cnt)
+{
+    const rt_prim& p = S.prims[prim];
+    if (p.kind == RT_PRIM_INSTANCE) return hit_instance<COUNT>(S, S.instances[p.a], r, t_min, t_max, h, stack, sp0, cnt);
+    return hit_simple<COUNT>(p, r, t_min, t_max, h, cnt);
+}
+
+// ConstantMedium (hittable.rs:417-473), keyed draw instead of the in-hit thread_rng().
+template <bool COUNT>
+__device__ bool hit_medium(const SceneDev& S, const rt_prim& m, const Ray& r, double t_min, double t_max, Hit& h,
+                           int* stack, int sp0, const Keyed& key, Count& cnt)
+{
+    Hit h1, h2;
+    if (!hit_boundary<COUNT>(S, m.a, r, -RT_INF, RT_INF, h1, stack, sp0, cnt)) return false;
+    if (!hit_boundary<COUNT>(S, m.a, r, h1.t + 0.0001, RT_INF, h2, stack, sp0, cnt)) return false;
+    double t1 = h1.t, t2 = h2.t;
+    if (t1 < t_min) t1 = t_min;
+    if (t2 > t_max) t2 = t_max;
+    if (t1 >= t2) return false;
+    if (t1 < 0.0) t1 = 0.0;
+    const double ray_length = __builtin_sqrt(r.a);
+    const double distance_inside = (t2 - t1) * ray_length;
+    const double xi = rt_unit53(rt_keyed_u64(key.seed, key.pixel, key.sample, key.bounce,
+                                             RT_STREAM_MEDIUM + (uint32_t)m.b));
+    const double hit_distance = m.p[0] * rt_log(xi);
+    if (hit_distance > distance_inside) return false;
+    h.t = t1 + hit_distance / ray_length;
+    h.px = r.ox + r.dx * h.t;
+    h.py = r.oy + r.dy * h.t;
+    h.pz = r.oz + r.dz * h.t;
+    h.nx = 1.0; h.ny = 0.0; h.nz = 0.0;
+    h.front = 1;
+    h.mat = m.mat;
+    h.uvkind = 0;
+    return true;
+}
+
+// hit_hittables(world, ray, 0.001, inf) (hittable.rs:43-55) over the TLAS.
+template <bool COUNT>
+__device__ bool trace_world(const SceneDev& S, const Ray& r, Hit& h, int* stack, const Keyed& key, Count& cnt)
+{
+    double t_min = 0.001, t_max = RT_INF;
+    bool any = false;
+    int sp = 0;
+    int cur = S.tlas_root;
+    for (;;) {
+        if (cur < 0) {
+            const int code = ~cur;
+            const int first = code >> 5, count = code & 31;
+            for (int i = 0; i < count; ++i) {
+                const rt_prim& p = S.prims[S.prim_refs[first + i]];
+                bool hit;
+                if (p.kind == RT_PRIM_INSTANCE)
+                    hit = hit_instance<COUNT>(S, S.instances[p.a], r, t_min, t_max, h, stack, sp, cnt);
+                else if (p.kind == RT_PRIM_MEDIUM)
+                    hit = hit_medium<COUNT>(S, p, r, t_min, t_max, h, stack, sp, key, cnt);
+                else
+                    hit = hit_simple<COUNT>(p, r, t_min, t_max, h, cnt);
+                if (hit) { t_max = h.t; any = true; }
+            }
+            if (sp == 0) break;
+            cur = stack[--sp];
+        } else {
+            if (COUNT) cnt.nodes++;
+            const rt_bvh_node& nd = S.nodes[cur];
+            double tn0, tn1;
+            const bool h0 = slab(nd.lo0, nd.hi0, r, t_min, t_max, tn0);
+            const bool h1 = slab(nd.lo1, nd.hi1, r, t_min, t_max, tn1);
+            if (h0 && h1) {
+                const bool first_left = tn0 <= tn1;
+                stack[sp++] = first_left ? nd.child[1] : nd.child[0];
+                cur = first_left ? nd.child[0] : nd.child[1];
+            } else if (h0) {
+                cur = nd.child[0];
+            } else if (h1) {
+                cur = nd.child[1];
+            } else {
+                if (sp == 0) break;
+                cur = stack[--sp];
+            }
+        }
+    }
+    return any;
+}
+
+// ---------------------------------------------------------------------------
+// appearance: texture.rs:30-75, perlin.rs:32-108, material.rs:15-94
+// ---------------------------------------------------------------------------
+__device__ double perlin_noise(const double* ranvec, const int32_t* perm, double px, double py, double pz)
+{
+    const double fx = __builtin_floor(px), fy = __builtin_floor(py), fz = __builtin_floor(pz);
+    double u = px - fx, v = py - fy, w = pz - fz;
+    u = u * u * (3.0 - 2.0 * u);
+    v = v * v * (3.0 - 2.0 * v);
+    w = w * w * (3.0 - 2.0 * w);
+    const int32_t i = rt_sat_i32(fx), j = rt_sat_i32(fy), k = rt_sat_i32(fz);
+    const double uu = u * u * (3.0 - 2.0 * u);
+    const double vv = v * v * (3.0 - 2.0 * v);
+    const double ww = w * w * (3.0 - 2.0 * w);
+    double accum = 0.0;
+#pragma unroll
+    for (int di = 0; di < 2; ++di)
+#pragma unroll
+        for (int dj = 0; dj < 2; ++dj)
+#pragma unroll
+            for (int dk = 0; dk < 2; ++dk) {
+                const uint32_t xi = ((uint32_t)i + (uint32_t)di) & 255u;
+                const uint32_t yi = ((uint32_t)j + (uint32_t)dj) & 255u;
+                const uint32_t zi = ((uint32_t)k + (uint32_t)dk) & 255u;
+                const uint32_t idx = (uint32_t)(perm[xi] ^ perm[256 + yi] ^ perm[512 + zi]) & 255u;
+                const double cx = ranvec[3 * idx], cy = ranvec[3 * idx + 1], cz = ranvec[3 * idx + 2];
+                const double fi = (double)di, fj = (double)dj, fk = (double)dk;
+                const double wx = u - fi, wy = v - fj, wz = w - fk;
+                accum += (fi * uu + (1.0 - fi) * (1.0 - uu)) * (fj * vv + (1.0 - fj) * (1.0 - vv)) *
+                         (fk * ww + (1.0 - fk) * (1.0 - ww)) * (cx * wx + cy * wy + cz * wz);
+            }
+    return accum;
+}
+
+__device__ double perlin_turb(const double* ranvec, const int32_t* perm, double px, double py, double pz)
+{
+    double accum = 0.0, weight = 1.0;
+    for (int i = 0; i < 7; ++i) {
+        accum += weight * perlin_noise(ranvec, perm, px, py, pz);
+        weight *= 0.5;
+        px = px * 2.0;
+        py = py * 2.0;
+        pz = pz * 2.0;
+    }
+    return __builtin_fabs(accum);
+}
+
+__device__ __forceinline__ double clampd(double x, double mn, double mx)
+{
+    if (x < mn) return mn;
+    if (x > mx) return mx;
+    return x;
+}
+
+__device__ void hit_uv(const Hit& h, double& u, double& v)
+{
+    if (h.uvkind == 1) {  // sphere_uv (math.rs:288-300)
+        const double theta = rt_acos(-h.uv1);
+        const double phi = rt_atan2(-h.uv2, h.uv0) + RT_PI;
+        u = phi / (2.0 * RT_PI);
+        v = theta / RT_PI;
+    } else if (h.uvkind == 2) {
+        u = h.uv0 / h.uv1;
+        v = h.uv2 / h.uv3;
+    } else {
+        u = 0.0;
+        v = 0.0;
+    }
+}
+
+__device__ void tex_value(const SceneDev& S, int ti, const Hit& h, double& cr, double& cg, double& cb)
+{
+    const rt_texture& t = S.textures[ti];
+    switch (t.kind) {
+    case RT_TEX_SOLID: cr = t.c0[0]; cg = t.c0[1]; cb = t.c0[2]; return;
+    case RT_TEX_CHECKER: {
+        const double sines = rt_sin(10.0 * h.px) * rt_sin(10.0 * h.py) * rt_sin(10.0 * h.pz);
+        if (sines < 0.0) { cr = t.c1[0]; cg = t.c1[1]; cb = t.c1[2]; }
+        else { cr = t.c0[0]; cg = t.c0[1]; cb = t.c0[2]; }
+        return;
+    }
+    case RT_TEX_NOISE: {
+        const double* rv = S.perlin_ranvec + (size_t)t.perlin * 768;
+        const int32_t* pm = S.perlin_perm + (size_t)t.perlin * 768;
+        const double s = 1.0 + rt_sin(t.scale * h.pz + 10.0 * perlin_turb(rv, pm, h.px, h.py, h.pz));
+        const double c = 1.0 * 0.5 * s;
+        cr = c; cg = c; cb = c;
+        return;
+    }
+    default: {
+        if (t.img_w <= 0 || t.img_h <= 0) { cr = 0.0; cg = 1.0; cb = 1.0; return; }
+        double u, v;
+        hit_uv(h, u, v);
+        u = clampd(u, 0.0, 1.0);
+        v = 1.0 - clampd(v, 0.0, 1.0);
+        uint64_t i = rt_sat_u64(u * (double)t.img_w);
+        uint64_t j = rt_sat_u64(v * (double)t.img_h);
+        if (i >= (uint64_t)t.img_w) i = (uint64_t)t.img_w - 1;
+        if (j >= (uint64_t)t.img_h) j = (uint64_t)t.img_h - 1;
+        const uint8_t* px = S.image + t.img_offset + j * (uint64_t)t.img_bps + i * 3;
+        const double color_scale = 1.0 / 255.0;
+        cr = color_scale * (double)px[0];
+        cg = color_scale * (double)px[1];
+        cb = color_scale * (double)px[2];
+        return;
+    }
+    }
+}
+
+__device__ __forceinline__ double rnd01(rt_stream& st) { return rt_unit53(rt_stream_next_u64(&st)); }
+__device__ __forceinline__ double rnd_m11(rt_stream& st, double scale_m11)
+{
+    return rt_uniform_sample(rt_stream_next_u64(&st), -1.0, scale_m11);
+}
+
+// math.rs:51-58
+__device__ __forceinline__ void random_in_unit_sphere(rt_stream& st, double scale_m11, double& x, double& y,
+                                                      double& z, double& len2)
+{
+    for (;;) {
+        x = rnd_m11(st, scale_m11);
+        y = rnd_m11(st, scale_m11);
+        z = rnd_m11(st, scale_m11);
+        len2 = x * x + y * y + z * z;
+        if (len2 < 1.0) return;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// the integrator
+// ---------------------------------------------------------------------------
+template <bool COUNT>
+__global__ void __launch_bounds__(256) trace_chunks(SceneDev S, KParams P, double* __restrict__ partial,
+                                                    unsigned long long* __restrict__ counters)
+{
+    const int lane = threadIdx.x & 63;
+    const long long wave = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const long long n_tiles = (long long)P.tiles_x * P.tiles_y;
+    if (wave >= n_tiles * P.n_chunks) return;
+    const int chunk = (int)(wave / n_tiles);
+    const int tile = (int)(wave % n_tiles);
+    const int x = (tile % P.tiles_x) * 8 + (lane & 7);
+    const int k = (tile / P.tiles_x) * 8 + (lane >> 3);
+    if (x >= P.width || k >= P.n_rows) return;
+    const int y = P.row_begin + k * P.row_stride;
+    const uint32_t pixel = (uint32_t)y * (uint32_t)P.width + (uint32_t)x;
+    const int s_begin = chunk * P.spp_chunk;
+    const int s_end = min(P.spp, s_begin + P.spp_chunk);
+
+    int stack[64];
+    Count cnt{0, 0, 0};
+    double sum_r = 0.0, sum_g = 0.0, sum_b = 0.0;
+    Keyed key{P.seed, pixel, 0, 0};
+    rt_stream st;
+    Ray r;
+    double Lr = 0, Lg = 0, Lb = 0, Tr = 1, Tg = 1, Tb = 1;
+    int depth = 0;
+    int s = s_begin;
+    bool new_sample = true;
+    while (s < s_end) {
+        if (new_sample) {  // main.rs:517-520 + camera.rs:58-66
+            new_sample = false;
+            rt_stream_init(&st, P.seed, pixel, (uint32_t)s, RT_STREAM_MAIN);
+            key.sample = (uint32_t)s;
+            const double u = ((double)x + rnd01(st)) / ((double)P.width - 1.0);
+            const double v = ((double)y + rnd01(st)) / ((double)P.height - 1.0);
+            double dxl, dyl;
+            for (;;) {
+                dxl = rnd_m11(st, P.scale_m11);
+                dyl = rnd_m11(st, P.scale_m11);
+                if (dxl * dxl + dyl * dyl + 0.0 * 0.0 < 1.0) break;
+            }
+            const double rdx = dxl * P.cam.lens_radius, rdy = dyl * P.cam.lens_radius;
+            const double offx = P.cam.u[0] * rdx + P.cam.v[0] * rdy;
+            const double offy = P.cam.u[1] * rdx + P.cam.v[1] * rdy;
+            const double offz = P.cam.u[2] * rdx + P.cam.v[2] * rdy;
+            r.ox = P.cam.origin[0] + offx;
+            r.oy = P.cam.origin[1] + offy;
+            r.oz = P.cam.origin[2] + offz;
+            r.dx = P.cam.lower_left_corner[0] + P.cam.horizontal[0] * u + P.cam.vertical[0] * v - P.cam.origin[0] - offx;
+            r.dy = P.cam.lower_left_corner[1] + P.cam.horizontal[1] * u + P.cam.vertical[1] * v - P.cam.origin[1] - offy;
+            r.dz = P.cam.lower_left_corner[2] + P.cam.horizontal[2] * u + P.cam.vertical[2] * v - P.cam.origin[2] - offz;
+            r.time = rt_uniform_sample(rt_stream_next_u64(&st), P.cam.time0, P.scale_time);
+            finish_ray(r);
+            Lr = Lg = Lb = 0.0;
+            Tr = Tg = Tb = 1.0;
+            depth = P.max_depth;
+        }
+        bool done = false;
+        if (depth <= 0) {  // main.rs:21-23
+            done = true;
+        } else {
+            key.bounce = (uint32_t)(P.max_depth - depth);
+            if (COUNT) cnt.casts++;
+            Hit h;
+            if (!trace_world<COUNT>(S, r, h, stack, key, cnt)) {  // main.rs:37
+                Lr = Lr + Tr * P.bg[0];
+                Lg = Lg + Tg * P.bg[1];
+                Lb = Lb + Tb * P.bg[2];
+                done = true;
+            } else {
+                const rt_material& m = S.materials[h.mat];
+                if (m.kind == RT_MAT_DIFFUSE_LIGHT) {  // material.rs:25-34
+                    double er, eg, eb;
+                    tex_value(S, m.tex, h, er, eg, eb);
+                    Lr = Lr + Tr * er;
+                    Lg = Lg + Tg * eg;
+                    Lb = Lb + Tb * eb;
+                    done = true;  // DiffuseLight never scatters
+                } else {
+                    double sdx, sdy, sdz, ar = 1.0, ag = 1.0, ab = 1.0;
+                    bool scattered = true;
+                    switch (m.kind) {
+                    case RT_MAT_LAMBERTIAN: {  // material.rs:36-48
+                        double qx, qy, qz, l2;
+                        random_in_unit_sphere(st, P.scale_m11, qx, qy, qz, l2);
+                        const double inv = 1.0 / __builtin_sqrt(l2);
+                        sdx = h.nx + qx * inv;
+                        sdy = h.ny + qy * inv;
+                        sdz = h.nz + qz * inv;
+                        if (__builtin_fabs(sdx) < 1e-8 && __builtin_fabs(sdy) < 1e-8 && __builtin_fabs(sdz) < 1e-8) {
+                            sdx = h.nx; sdy = h.ny; sdz = h.nz;
+                        }
+                        tex_value(S, m.tex, h, ar, ag, ab);
+                        break;
+                    }
+                    case RT_MAT_METAL: {  // material.rs:50-60
+                        const double inv = 1.0 / __builtin_sqrt(r.a);
+                        const double ux = r.dx * inv, uy = r.dy * inv, uz = r.dz * inv;
+                        const double k2 = 2.0 * (ux * h.nx + uy * h.ny + uz * h.nz);
+                        double qx, qy, qz, l2;
+                        random_in_unit_sphere(st, P.scale_m11, qx, qy, qz, l2);
+                        sdx = (ux - h.nx * k2) + qx * m.fuzz;
+                        sdy = (uy - h.ny * k2) + qy * m.fuzz;
+                        sdz = (uz - h.nz * k2) + qz * m.fuzz;
+                        scattered = sdx * h.nx + sdy * h.ny + sdz * h.nz > 0.0;
+                        ar = m.albedo[0]; ag = m.albedo[1]; ab = m.albedo[2];
+                        break;
+                    }
+                    case RT_MAT_DIELECTRIC: {  // material.rs:62-82, 89-94
+                        const double ratio = h.front ? (1.0 / m.ir) : m.ir;
+                        const double inv = 1.0 / __builtin_sqrt(r.a);
+                        const double ux = r.dx * inv, uy = r.dy * inv, uz = r.dz * inv;
+                        const double cos_theta = fmin((-ux) * h.nx + (-uy) * h.ny + (-uz) * h.nz, 1.0);
+                        const double sin_theta = __builtin_sqrt(1.0 - cos_theta * cos_theta);
+                        const bool cannot_refract = ratio * sin_theta > 1.0;
+                        bool reflect = cannot_refract;
+                        if (!reflect) {
+                            double r0 = (1.0 - ratio) / (1.0 + ratio);
+                            r0 = r0 * r0;
+                            const double refl = r0 + (1.0 - r0) * rt_pow5(1.0 - cos_theta);
+                            reflect = refl > rnd01(st);
+                        }
+                        if (reflect) {
+                            const double k2 = 2.0 * (ux * h.nx + uy * h.ny + uz * h.nz);
+                            sdx = ux - h.nx * k2;
+                            sdy = uy - h.ny * k2;
+                            sdz = uz - h.nz * k2;
+                        } else {  // math.rs:110-117
+                            const double ct = fmin((-ux) * h.nx + (-uy) * h.ny + (-uz) * h.nz, 1.0);
+                            const double px = (ux + h.nx * ct) * ratio;
+                            const double py = (uy + h.ny * ct) * ratio;
+                            const double pz = (uz + h.nz * ct) * ratio;
+                            const double pl = px * px + py * py + pz * pz;
+                            const double kk = -__builtin_sqrt(__builtin_fabs(1.0 - pl));
+                            sdx = px + h.nx * kk;
+                            sdy = py + h.ny * kk;
+                            sdz = pz + h.nz * kk;
+                        }
+                        break;
+                    }
+                    default: {  // isotropic, material.rs:84-87
+                        double l2;
+                        random_in_unit_sphere(st, P.scale_m11, sdx, sdy, sdz, l2);
+                        tex_value(S, m.tex, h, ar, ag, ab);
+                        break;
+                    }
+                    }
+                    if (!scattered) {
+                        done = true;  // emitted (0) only
+                    } else {
+                        Tr = Tr * ar;
+                        Tg = Tg * ag;
+                        Tb = Tb * ab;
+                        r.ox = h.px; r.oy = h.py; r.oz = h.pz;
+                        r.dx = sdx; r.dy = sdy; r.dz = sdz;
+                        finish_ray(r);
+                        depth -= 1;
+                    }
+                }
+            }
+        }
+        if (done) {
+            sum_r = sum_r + Lr;
+            sum_g = sum_g + Lg;
+            sum_b = sum_b + Lb;
+            s += 1;
+            new_sample = true;
+        }
+    }
+    double* o = partial + (((size_t)chunk * P.n_rows + k) * P.width + x) * 3;
+    o[0] = sum_r;
+    o[1] = sum_g;
+    o[2] = sum_b;
+    if (COUNT) {
+        atomicAdd(&counters[0], (unsigned long long)cnt.casts);
+        atomicAdd(&counters[1], (unsigned long long)cnt.nodes);
+        atomicAdd(&counters[2], (unsigned long long)cnt.prims);
+    }
+}
+
+// sum of partials in chunk order, times 1/spp (math.rs:120-125 before sqrt).
+template <typename T>
+__global__ void __launch_bounds__(256) reduce_chunks(const double* __restrict__ partial, T* __restrict__ out,
+                                                     long long n_px, int n_chunks, double scale)
+{
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n_px) return;
+    double r = 0.0, g = 0.0, b = 0.0;
+    for (int c = 0; c < n_chunks; ++c) {
+        const double* p = partial + ((size_t)c * n_px + i) * 3;
+        r = r + p[0];
+        g = g + p[1];
+        b = b + p[2];
+    }
+    out[3 * i + 0] = (T)(r * scale);
+    out[3 * i + 1] = (T)(g * scale);
+    out[3 * i + 2] = (T)(b * scale);
+}
+
+__global__ void eval_numerics(int fn, const double* x, const double* y, const double* z, double* out, int n)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    double r = 0.0;
+    switch (fn) {
+    case 0: r = rt_sin(x[i]); break;
+    case 1: r = rt_cos(x[i]); break;
+    case 2: r = rt_log(x[i]); break;
+    case 3: r = rt_atan2(x[i], y[i]); break;
+    case 4: r = rt_acos(x[i]); break;
+    case 5: case 6: {
+        Hit h;
+        h.uvkind = 1;
+        h.uv0 = x[i]; h.uv1 = y[i]; h.uv2 = z[i];
+        double u, v;
+        hit_uv(h, u, v);
+        r = fn == 5 ? u : v;
+        break;
+    }
+    case 7: r = rt_pow5(x[i]); break;
+    case 8: r = __builtin_sqrt(x[i]); break;
+    case 9: r = x[i] / y[i]; break;
+    case 10: r = rt_unit53(rt_f64_bits(x[i])); break;
+    case 11: r = rt_uniform_sample(rt_f64_bits(x[i]), -1.0, rt_uniform_incl_scale(-1.0, 1.0)); break;
+    default: break;
+    }
+    out[i] = r;
+}
+
+// ---------------------------------------------------------------------------
+// host-side launchers
+// ---------------------------------------------------------------------------
+hipError_t launch_trace(const SceneDev& S, const KParams& P, double* partial, unsigned long long* counters,
+                        bool count, hipStream_t stream)
+{
+    const long long waves = (long long)P.tiles_x * P.tiles_y * P.n_chunks;
+    const long long blocks = (waves + 3) / 4;
+    if (blocks <= 0) return hipSuccess;
+    if (blocks > 0x7fffffffLL) return hipErrorInvalidValue;
+    if (count)
+        hipLaunchKernelGGL(trace_chunks<true>, dim3((unsigned)blocks), dim3(256), 0, stream, S, P, partial, counters);
+    else
+        hipLaunchKernelGGL(trace_chunks<false>, dim3((unsigned)blocks), dim3(256), 0, stream, S, P, partial, counters);
+    return hipGetLastError();
+}
+
+hipError_t launch_reduce(const double* partial, void* out, bool f64, long long n_px, int n_chunks, double scale,
+                         hipStream_t stream)
+{
+    const long long blocks = (n_px + 255) / 256;
+    if (blocks <= 0) return hipSuccess;
+    if (f64)
+        hipLaunchKernelGGL(reduce_chunks<double>, dim3((unsigned)blocks), dim3(256), 0, stream, partial, (double*)out,
+                           n_px, n_chunks, scale);
+    else
+        hipLaunchKernelGGL(reduce_chunks<float>, dim3((unsigned)blocks), dim3(256), 0, stream, partial, (float*)out,
+                           n_px, n_chunks, scale);
+    return hipGetLastError();
+}
+
+hipError_t launch_eval(int fn, const double* x, const double* y, const double* z, double* out, int n,
+                       hipStream_t stream)
+{
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(eval_numerics, dim3((n + 255) / 256), dim3(256), 0, stream, fn, x, y, z, out, n);
+    return hipGetLastError();
+}
+
+}  // namespace rtk

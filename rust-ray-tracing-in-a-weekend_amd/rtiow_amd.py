@@ -1,0 +1,380 @@
+"""rtiow_amd — Python host binding over the C ABI (include/rt/rt_abi.h).
+
+This mirrors the reference's host surface (themeshpotato/rust-ray-tracing-in-a-weekend):
+``World`` + ``register_material`` (main.rs:40-50), the Hittable / Material / Texture
+constructors (hittable.rs:77-207, material.rs:6-12, texture.rs:4-22), the scene
+builders (main.rs:52-289), ``Camera::new`` (camera.rs:18-56) and the render loop
+(main.rs:497-551, ray_color main.rs:19-38), which here runs as the HIP megakernel in
+``lib/librtiow_amd.so``.
+
+There is no CPU fallback: if the shared library is missing or no GPU is visible,
+``Renderer`` raises. (The CPU oracle under oracle/ is test infrastructure only.)
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Optional, Sequence
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "librtiow_amd.so")
+REPO = os.path.dirname(HERE)
+EARTH_JPG = os.path.join(REPO, "assets", "earthmap.jpg")
+
+RT_OK = 0
+ERRORS = {-1: "RT_ERR_INVALID", -2: "RT_ERR_HIP", -3: "RT_ERR_UNSUPPORTED", -4: "RT_ERR_OOM",
+          -5: "RT_ERR_NO_DEVICE", -6: "RT_ERR_NO_SCENE"}
+
+SCENES = {"random": 0, "two_spheres": 1, "two_perlin": 2, "earth": 3, "simple_light": 4,
+          "cornell": 5, "cornell_smoke": 6, "final": 7}
+SCENES_NEEDING_IMAGE = (3, 7)
+
+RT_OUT_F32, RT_OUT_F64 = 0, 1
+RT_ACCEL_SAH = 0
+
+# every symbol include/rt/rt_abi.h declares
+EXPORTED = [
+    "rt_abi_version", "rt_last_error", "rt_device_count", "rt_ctx_create", "rt_ctx_destroy",
+    "rt_world_create", "rt_world_destroy", "rt_world_texture_solid", "rt_world_texture_checker",
+    "rt_world_texture_noise", "rt_world_texture_image", "rt_world_material_lambertian",
+    "rt_world_material_metal", "rt_world_material_dielectric", "rt_world_material_diffuse_light",
+    "rt_world_material_isotropic", "rt_world_sphere", "rt_world_moving_sphere", "rt_world_rect",
+    "rt_world_box", "rt_world_translate", "rt_world_rotate_y", "rt_world_constant_medium",
+    "rt_world_bvh", "rt_world_push", "rt_world_build_scene", "rt_world_info_get", "rt_camera_new",
+    "rt_scene_preset_get", "rt_scene_camera", "rt_world_flatten", "rt_ctx_upload_soa",
+    "rt_ctx_upload_world", "rt_render", "rt_rows_in_shard", "rt_last_stats", "rt_write_ppm",
+    "rt_device_eval",
+]
+
+
+class RTError(RuntimeError):
+    pass
+
+
+class Camera(ctypes.Structure):
+    """rt_camera == the reference's Camera struct (camera.rs:4-15)."""
+    _fields_ = [("origin", ctypes.c_double * 3), ("lower_left_corner", ctypes.c_double * 3),
+                ("horizontal", ctypes.c_double * 3), ("vertical", ctypes.c_double * 3),
+                ("u", ctypes.c_double * 3), ("v", ctypes.c_double * 3), ("w", ctypes.c_double * 3),
+                ("lens_radius", ctypes.c_double), ("time0", ctypes.c_double), ("time1", ctypes.c_double)]
+
+
+class ScenePreset(ctypes.Structure):
+    _fields_ = [("look_from", ctypes.c_double * 3), ("look_at", ctypes.c_double * 3),
+                ("background", ctypes.c_double * 3), ("vfov", ctypes.c_double),
+                ("aperture", ctypes.c_double), ("focus_dist", ctypes.c_double),
+                ("time0", ctypes.c_double), ("time1", ctypes.c_double),
+                ("default_width", ctypes.c_int32), ("default_spp", ctypes.c_int32),
+                ("default_aspect", ctypes.c_double)]
+
+
+class WorldInfo(ctypes.Structure):
+    _fields_ = [("n_hittables", ctypes.c_int32), ("n_materials", ctypes.c_int32),
+                ("n_leaf_prims", ctypes.c_int32), ("n_media", ctypes.c_int32), ("checksum", ctypes.c_double)]
+
+
+class SceneSoA(ctypes.Structure):
+    _fields_ = [("n_prims", ctypes.c_int32), ("n_prim_refs", ctypes.c_int32), ("n_nodes", ctypes.c_int32),
+                ("n_instances", ctypes.c_int32), ("n_materials", ctypes.c_int32), ("n_textures", ctypes.c_int32),
+                ("n_perlin", ctypes.c_int32), ("n_media", ctypes.c_int32), ("tlas_root", ctypes.c_int32),
+                ("accel", ctypes.c_int32), ("image_bytes", ctypes.c_int64),
+                ("prims", ctypes.c_void_p), ("prim_refs", ctypes.c_void_p), ("nodes", ctypes.c_void_p),
+                ("instances", ctypes.c_void_p), ("materials", ctypes.c_void_p), ("textures", ctypes.c_void_p),
+                ("perlin_ranvec", ctypes.c_void_p), ("perlin_perm", ctypes.c_void_p),
+                ("image_data", ctypes.c_void_p)]
+
+
+class RenderParams(ctypes.Structure):
+    _fields_ = [("width", ctypes.c_int32), ("height", ctypes.c_int32), ("spp", ctypes.c_int32),
+                ("max_depth", ctypes.c_int32), ("spp_chunk", ctypes.c_int32), ("row_begin", ctypes.c_int32),
+                ("row_stride", ctypes.c_int32), ("out_format", ctypes.c_int32),
+                ("out_on_device", ctypes.c_int32), ("count_work", ctypes.c_int32),
+                ("background", ctypes.c_double * 3), ("render_seed", ctypes.c_uint64),
+                ("stream", ctypes.c_void_p)]
+
+
+class Stats(ctypes.Structure):
+    _fields_ = [("kernel_ms", ctypes.c_double), ("reduce_ms", ctypes.c_double), ("samples", ctypes.c_uint64),
+                ("casts", ctypes.c_uint64), ("node_visits", ctypes.c_uint64), ("prim_tests", ctypes.c_uint64),
+                ("n_items", ctypes.c_uint64), ("n_chunks", ctypes.c_int32), ("spp_chunk", ctypes.c_int32),
+                ("scene_bytes", ctypes.c_int64), ("node_bytes", ctypes.c_int32), ("prim_bytes", ctypes.c_int32),
+                ("material_bytes", ctypes.c_int32), ("pad", ctypes.c_int32)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_ if k != "pad"}
+
+
+_lib = None
+
+
+def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
+    """Loads lib/librtiow_amd.so (built by __graft_entry__.build()); raises if absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise RTError(f"HIP library not built: {path} (run __graft_entry__.build())")
+    lib = ctypes.CDLL(path)
+    P, I, D, U64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_double, ctypes.c_uint64
+    PI = ctypes.POINTER(ctypes.c_int)
+    PD = ctypes.POINTER(ctypes.c_double)
+    sigs = {
+        "rt_abi_version": ([], I), "rt_last_error": ([], ctypes.c_char_p),
+        "rt_device_count": ([PI], I), "rt_ctx_create": ([I, ctypes.POINTER(P)], I),
+        "rt_ctx_destroy": ([P], None), "rt_world_create": ([U64, ctypes.POINTER(P)], I),
+        "rt_world_destroy": ([P], None), "rt_world_texture_solid": ([P, D, D, D, PI], I),
+        "rt_world_texture_checker": ([P, PD, PD, PI], I), "rt_world_texture_noise": ([P, D, PI], I),
+        "rt_world_texture_image": ([P, P, I, I, PI], I),
+        "rt_world_material_lambertian": ([P, I, PI], I), "rt_world_material_metal": ([P, PD, D, PI], I),
+        "rt_world_material_dielectric": ([P, D, PI], I), "rt_world_material_diffuse_light": ([P, I, PI], I),
+        "rt_world_material_isotropic": ([P, I, PI], I), "rt_world_sphere": ([P, I, PD, D, PI], I),
+        "rt_world_moving_sphere": ([P, I, PD, PD, D, D, D, PI], I),
+        "rt_world_rect": ([P, I, I, D, D, D, D, D, PI], I), "rt_world_box": ([P, PD, PD, I, PI], I),
+        "rt_world_translate": ([P, I, PD, PI], I), "rt_world_rotate_y": ([P, I, D, PI], I),
+        "rt_world_constant_medium": ([P, I, D, I, PI], I), "rt_world_bvh": ([P, PI, I, D, D, PI], I),
+        "rt_world_push": ([P, I], I), "rt_world_build_scene": ([P, I, P, I, I], I),
+        "rt_world_info_get": ([P, ctypes.POINTER(WorldInfo)], I),
+        "rt_camera_new": ([PD, PD, PD, D, D, D, D, D, D, ctypes.POINTER(Camera)], I),
+        "rt_scene_preset_get": ([I, ctypes.POINTER(ScenePreset)], I),
+        "rt_scene_camera": ([I, I, I, ctypes.POINTER(Camera), PD], I),
+        "rt_world_flatten": ([P, I, ctypes.POINTER(ctypes.POINTER(SceneSoA))], I),
+        "rt_ctx_upload_soa": ([P, ctypes.POINTER(SceneSoA)], I), "rt_ctx_upload_world": ([P, P, I], I),
+        "rt_render": ([P, ctypes.POINTER(Camera), ctypes.POINTER(RenderParams), P], I),
+        "rt_rows_in_shard": ([I, I, I], I), "rt_last_stats": ([P, ctypes.POINTER(Stats)], I),
+        "rt_write_ppm": ([P, I, I, ctypes.c_char_p], I),
+        "rt_device_eval": ([P, I, P, P, P, P, I], I),
+    }
+    for name, (args, res) in sigs.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = res
+    _lib = lib
+    return lib
+
+
+def _check(rc: int, what: str) -> None:
+    if rc != RT_OK:
+        msg = _lib.rt_last_error().decode() if _lib is not None else ""
+        raise RTError(f"{what} failed: {ERRORS.get(rc, rc)} {msg}")
+
+
+def _d3(v: Sequence[float]):
+    return (ctypes.c_double * 3)(*[float(x) for x in v])
+
+
+def load_earth_texture(path: str = EARTH_JPG) -> np.ndarray:
+    """RGB8 texels of textures/earthmap.jpg (texture.rs:12-22; decoded with PIL instead of stb_image)."""
+    from PIL import Image
+    return np.ascontiguousarray(np.asarray(Image.open(path).convert("RGB"), dtype=np.uint8))
+
+
+class World:
+    """The reference's World (main.rs:40-50) with its Hittable / Material / Texture constructors."""
+
+    def __init__(self, scene_seed: int = 1):
+        self.lib = load_library()
+        h = ctypes.c_void_p()
+        _check(self.lib.rt_world_create(ctypes.c_uint64(scene_seed), ctypes.byref(h)), "rt_world_create")
+        self.h = h
+        self._keep = []
+
+    def close(self):
+        if self.h:
+            self.lib.rt_world_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _id(self, fn, *args) -> int:
+        out = ctypes.c_int()
+        _check(fn(self.h, *args, ctypes.byref(out)), fn.__name__)
+        return out.value
+
+    # textures (texture.rs:4-22)
+    def solid(self, r, g, b): return self._id(self.lib.rt_world_texture_solid, r, g, b)
+    def checker(self, even, odd): return self._id(self.lib.rt_world_texture_checker, _d3(even), _d3(odd))
+    def noise(self, scale): return self._id(self.lib.rt_world_texture_noise, scale)
+
+    def image(self, rgb: np.ndarray):
+        rgb = np.ascontiguousarray(rgb, dtype=np.uint8)
+        return self._id(self.lib.rt_world_texture_image, rgb.ctypes.data, rgb.shape[1], rgb.shape[0])
+
+    # materials (material.rs:6-12) -> 1-based handles
+    def lambertian(self, tex): return self._id(self.lib.rt_world_material_lambertian, tex)
+    def metal(self, albedo, fuzz): return self._id(self.lib.rt_world_material_metal, _d3(albedo), fuzz)
+    def dielectric(self, ir): return self._id(self.lib.rt_world_material_dielectric, ir)
+    def diffuse_light(self, tex): return self._id(self.lib.rt_world_material_diffuse_light, tex)
+    def isotropic(self, tex): return self._id(self.lib.rt_world_material_isotropic, tex)
+
+    # hittables (hittable.rs:30-41)
+    def sphere(self, mat, center, radius): return self._id(self.lib.rt_world_sphere, mat, _d3(center), radius)
+
+    def moving_sphere(self, mat, c0, c1, t0, t1, radius):
+        return self._id(self.lib.rt_world_moving_sphere, mat, _d3(c0), _d3(c1), t0, t1, radius)
+
+    def xy_rect(self, mat, x0, x1, y0, y1, k): return self._id(self.lib.rt_world_rect, 0, mat, x0, x1, y0, y1, k)
+    def xz_rect(self, mat, x0, x1, z0, z1, k): return self._id(self.lib.rt_world_rect, 1, mat, x0, x1, z0, z1, k)
+    def yz_rect(self, mat, y0, y1, z0, z1, k): return self._id(self.lib.rt_world_rect, 2, mat, y0, y1, z0, z1, k)
+    def box(self, mn, mx, mat): return self._id(self.lib.rt_world_box, _d3(mn), _d3(mx), mat)
+    def translate(self, child, offset): return self._id(self.lib.rt_world_translate, child, _d3(offset))
+    def rotate_y(self, child, angle): return self._id(self.lib.rt_world_rotate_y, child, angle)
+
+    def constant_medium(self, boundary, density, phase):
+        return self._id(self.lib.rt_world_constant_medium, boundary, density, phase)
+
+    def bvh(self, ids, t0=0.0, t1=1.0):
+        arr = (ctypes.c_int * len(ids))(*ids)
+        return self._id(self.lib.rt_world_bvh, arr, len(ids), t0, t1)
+
+    def push(self, hid):
+        _check(self.lib.rt_world_push(self.h, hid), "rt_world_push")
+
+    def build_scene(self, scene_id: int, image: Optional[np.ndarray] = None):
+        """The reference's scene builders (main.rs:52-289)."""
+        if scene_id in SCENES_NEEDING_IMAGE and image is None:
+            image = load_earth_texture()
+        if image is not None:
+            image = np.ascontiguousarray(image, dtype=np.uint8)
+            self._keep.append(image)
+            ptr, w, h = image.ctypes.data, image.shape[1], image.shape[0]
+        else:
+            ptr, w, h = None, 0, 0
+        _check(self.lib.rt_world_build_scene(self.h, scene_id, ptr, w, h), "rt_world_build_scene")
+        return self
+
+    def info(self) -> WorldInfo:
+        out = WorldInfo()
+        _check(self.lib.rt_world_info_get(self.h, ctypes.byref(out)), "rt_world_info_get")
+        return out
+
+    def flatten(self, accel: int = RT_ACCEL_SAH) -> SceneSoA:
+        p = ctypes.POINTER(SceneSoA)()
+        _check(self.lib.rt_world_flatten(self.h, accel, ctypes.byref(p)), "rt_world_flatten")
+        return p.contents
+
+
+def camera_new(look_from, look_at, vup, vfov, aspect_ratio, aperture, focus_dist, time0, time1) -> Camera:
+    lib = load_library()
+    cam = Camera()
+    _check(lib.rt_camera_new(_d3(look_from), _d3(look_at), _d3(vup), vfov, aspect_ratio, aperture, focus_dist,
+                             time0, time1, ctypes.byref(cam)), "rt_camera_new")
+    return cam
+
+
+def scene_preset(scene_id: int) -> ScenePreset:
+    lib = load_library()
+    out = ScenePreset()
+    _check(lib.rt_scene_preset_get(scene_id, ctypes.byref(out)), "rt_scene_preset_get")
+    return out
+
+
+def scene_camera(scene_id: int, width: int, height: int):
+    """(Camera, background) of a preset scene at width x height (aspect = width/height)."""
+    lib = load_library()
+    cam = Camera()
+    bg = (ctypes.c_double * 3)()
+    _check(lib.rt_scene_camera(scene_id, width, height, ctypes.byref(cam), bg), "rt_scene_camera")
+    return cam, tuple(bg)
+
+
+def rows_in_shard(height: int, row_begin: int, row_stride: int) -> int:
+    return load_library().rt_rows_in_shard(height, row_begin, row_stride)
+
+
+def write_ppm(mean_rgb: np.ndarray, path: str) -> None:
+    """P3 writer with the reference's write_color semantics (math.rs:119-132)."""
+    lib = load_library()
+    a = np.ascontiguousarray(mean_rgb, dtype=np.float32)
+    _check(lib.rt_write_ppm(a.ctypes.data, a.shape[1], a.shape[0], str(path).encode()), "rt_write_ppm")
+
+
+class Renderer:
+    """One device context: upload a world, render row shards through the megakernel."""
+
+    def __init__(self, device: int = 0):
+        self.lib = load_library()
+        n = ctypes.c_int()
+        _check(self.lib.rt_device_count(ctypes.byref(n)), "rt_device_count")
+        if n.value <= 0:
+            raise RTError("no HIP device visible")
+        h = ctypes.c_void_p()
+        _check(self.lib.rt_ctx_create(device, ctypes.byref(h)), "rt_ctx_create")
+        self.h = h
+
+    def close(self):
+        if self.h:
+            self.lib.rt_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def upload(self, world: World, accel: int = RT_ACCEL_SAH):
+        _check(self.lib.rt_ctx_upload_world(self.h, world.h, accel), "rt_ctx_upload_world")
+
+    @staticmethod
+    def params(width, height, spp, max_depth=50, background=(0.0, 0.0, 0.0), render_seed=1, row_begin=0,
+               row_stride=1, spp_chunk=0, out_format=RT_OUT_F32, out_on_device=0, count_work=0, stream=None):
+        p = RenderParams()
+        p.width, p.height, p.spp, p.max_depth = width, height, spp, max_depth
+        p.spp_chunk, p.row_begin, p.row_stride = spp_chunk, row_begin, row_stride
+        p.out_format, p.out_on_device, p.count_work = out_format, out_on_device, count_work
+        p.background = _d3(background)
+        p.render_seed = render_seed
+        p.stream = stream
+        return p
+
+    def render(self, camera: Camera, params: RenderParams, out=None) -> np.ndarray:
+        """Host-output render: returns rows_local x width x 3 mean radiance (row k = k-th selected row)."""
+        n_rows = rows_in_shard(params.height, params.row_begin, params.row_stride)
+        dt = np.float64 if params.out_format == RT_OUT_F64 else np.float32
+        if out is None:
+            out = np.empty((n_rows, params.width, 3), dtype=dt)
+        params.out_on_device = 0
+        _check(self.lib.rt_render(self.h, ctypes.byref(camera), ctypes.byref(params), out.ctypes.data), "rt_render")
+        return out
+
+    def render_device(self, camera: Camera, params: RenderParams, dev_ptr: int, stream: Optional[int] = None):
+        """Enqueues a render into a device buffer (e.g. a torch tensor's data_ptr()) on `stream`."""
+        params.out_on_device = 1
+        params.stream = stream
+        _check(self.lib.rt_render(self.h, ctypes.byref(camera), ctypes.byref(params), ctypes.c_void_p(dev_ptr)),
+               "rt_render")
+
+    def stats(self) -> Stats:
+        s = Stats()
+        _check(self.lib.rt_last_stats(self.h, ctypes.byref(s)), "rt_last_stats")
+        return s
+
+    def device_eval(self, fn: int, x, y=None, z=None) -> np.ndarray:
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        y = np.ascontiguousarray(x if y is None else y, dtype=np.float64)
+        z = np.ascontiguousarray(x if z is None else z, dtype=np.float64)
+        out = np.empty_like(x)
+        _check(self.lib.rt_device_eval(self.h, fn, x.ctypes.data, y.ctypes.data, z.ctypes.data, out.ctypes.data,
+                                       x.size), "rt_device_eval")
+        return out
+
+
+def render_scene(scene_id: int, width: int, height: int, spp: int, max_depth: int = 50, scene_seed: int = 1,
+                 render_seed: int = 1, row_begin: int = 0, row_stride: int = 1, out_format: int = RT_OUT_F32,
+                 spp_chunk: int = 0, device: int = 0, renderer: Optional[Renderer] = None,
+                 image: Optional[np.ndarray] = None):
+    """One-call path: build the preset scene, upload, render the row shard. Returns (image, stats)."""
+    world = World(scene_seed).build_scene(scene_id, image)
+    cam, bg = scene_camera(scene_id, width, height)
+    r = renderer or Renderer(device)
+    r.upload(world)
+    p = Renderer.params(width, height, spp, max_depth, bg, render_seed, row_begin, row_stride, spp_chunk,
+                        out_format)
+    img = r.render(cam, p)
+    return img, r.stats()
