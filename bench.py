@@ -1,0 +1,206 @@
+#!/usr/bin/env python3
+"""Headline benchmark: Msamples/s (pixels x spp per second) on the 1200x800 random-spheres
+scene, 500 spp, max depth 50 (BASELINE.json configs[1] = SURVEY C2), at N GPUs.
+
+One step = one full render of the frame: every rank traces its interleaved row shard
+(rows y = rank + k*N) through the HIP megakernel (C ABI, librtiow_amd.so); for N > 1
+the shards are gathered to rank 0 over RCCL (torch.distributed "nccl") and put back
+in row order — inside the timed region. The scene is built and uploaded before timing.
+
+Prints ONE JSON line (rank 0). Besides the contract fields it carries
+  roofline:     algorithmic bytes per launch (BVH nodes + primitives + materials +
+                partial writes, counted by the kernel's count_work pass) / kernel time,
+                against the 8 TB/s HBM peak; `traffic` from a rocprofv3 PMC pass if
+                RT_PMC_TRAFFIC_JSON points at one (else null);
+  cpu_baseline: the CPU oracle (reference-faithful C restatement, linear list scan like
+                hittable.rs:43-55) on this host's cores, rank 0 at N=1 only, on a bounded
+                row subset of the same workload.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+CPU_BASELINE_CORES = 16        # the GPU box's CPU share per GPU
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--scene", type=int, default=0)
+    ap.add_argument("--width", type=int, default=1200)
+    ap.add_argument("--height", type=int, default=800)
+    ap.add_argument("--spp", type=int, default=500)
+    ap.add_argument("--depth", type=int, default=50)
+    ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--count-spp", type=int, default=16, help="spp of the untimed count_work pass")
+    ap.add_argument("--ppm", default="", help="write the rendered frame (rank 0) as a P3 PPM")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run (one rank per GPU)")
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(local)
+    device = torch.device("cuda", local)
+
+    import __graft_entry__ as ge
+    rt = ge.import_binding()          # after torch: one HIP runtime in the process
+
+    W, H, spp, depth = args.width, args.height, args.spp, args.depth
+    t_build = time.perf_counter()
+    scene = rt.World(args.seed).build_scene(args.scene)
+    cam, bg = rt.scene_camera(args.scene, W, H)
+    renderer = rt.Renderer(local)
+    renderer.upload(scene)
+    t_build = time.perf_counter() - t_build
+
+    rows = rt.rows_in_shard(H, rank, world)
+    rows_max = (H + world - 1) // world
+    slab = torch.zeros((rows_max, W, 3), dtype=torch.float32, device=device)
+    gathered = [torch.empty_like(slab) for _ in range(world)] if (world > 1 and rank == 0) else None
+    frame = torch.empty((H, W, 3), dtype=torch.float32, device=device) if rank == 0 else None
+    stream = torch.cuda.current_stream(device)
+    params = rt.Renderer.params(W, H, spp, depth, bg, args.seed, row_begin=rank, row_stride=world,
+                                out_format=rt.RT_OUT_F32)
+    kernel_ms = []
+
+    def step():
+        renderer.render_device(cam, params, slab.data_ptr(), stream.cuda_stream)
+        if world > 1:
+            dist.gather(slab, gathered if rank == 0 else None, dst=0)
+            if rank == 0:
+                for r in range(world):   # rows y = r + k*world
+                    n = rt.rows_in_shard(H, r, world)
+                    frame[r::world] = gathered[r][:n]
+        else:
+            frame[:] = slab[:H]
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(device)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+        kernel_ms.append(renderer.stats().kernel_ms)   # HIP events around the trace kernel on `stream`
+    torch.cuda.synchronize(device)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(device)
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    last = renderer.stats()
+
+    samples_per_step = W * H * spp
+    value = samples_per_step * args.steps / elapsed / 1e6
+    ms_per_step = elapsed / args.steps * 1e3
+
+    # ---- algorithmic bytes per sample from an untimed count_work pass (same scene/camera)
+    count_spp = min(args.count_spp, spp)
+    cp = rt.Renderer.params(W, H, count_spp, depth, bg, args.seed, row_begin=rank, row_stride=world,
+                            out_format=rt.RT_OUT_F32, count_work=1)
+    renderer.render(cam, cp)
+    cs = renderer.stats()
+    bytes_per_sample = (cs.node_visits * cs.node_bytes + cs.prim_tests * cs.prim_bytes +
+                        cs.casts * cs.material_bytes) / max(cs.samples, 1)
+    samples_per_launch = rows * W * spp
+    items_per_launch = last.n_items
+    alg_bytes_launch = bytes_per_sample * samples_per_launch + items_per_launch * 24
+    k_ms = float(np.mean(kernel_ms)) if kernel_ms else float("nan")
+    achieved = alg_bytes_launch / (k_ms * 1e-3) / 1e9
+    traffic = None
+    pmc = os.environ.get("RT_PMC_TRAFFIC_JSON")
+    if pmc and os.path.exists(pmc):
+        traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
+
+    if args.ppm and rank == 0:
+        rt.write_ppm(frame.cpu().numpy(), args.ppm)
+
+    # ---- CPU baseline (rank 0, N = 1 only)
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        from tests import oracle_binding as ob
+        cores = min(CPU_BASELINE_CORES, os.cpu_count() or 1)
+        # calibrate on `cores` interleaved rows at low spp, then take an interleaved row
+        # subset of the real workload worth ~cpu_seconds (a multiple of `cores` rows)
+        cal_stride = max(1, H // cores)
+        _, st1 = ob.render(args.scene, W, H, min(spp, 16), depth, args.seed, args.seed, row_begin=0,
+                           row_stride=cal_stride, threads=cores, return_stats=True)
+        rate = st1.samples / max(st1.seconds, 1e-9)
+        n_rows = int(args.cpu_seconds * rate / (W * spp))
+        n_rows = max(cores, min(H, n_rows // cores * cores))
+        stride = max(1, H // n_rows)
+        _, st = ob.render(args.scene, W, H, spp, depth, args.seed, args.seed, row_begin=0, row_stride=stride,
+                          threads=cores, return_stats=True)
+        cpu = {"value": st.samples / st.seconds / 1e6, "unit": "Msamples/s", "cores": cores, "kind": "port",
+               "sample": f"oracle (C, f64, recursive ray_color, linear hit_hittables scan) on rows y % {stride} == 0 "
+                         f"of the same {W}x{H}x{spp} depth-{depth} frame: {st.samples} samples in {st.seconds:.1f} s "
+                         f"on {cores} threads"}
+
+    if rank == 0:
+        out = {
+            "metric": "Msamples/s (pixels x spp) for 1200x800 random-spheres scene",
+            "value": round(value, 3),
+            "unit": "Msamples/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 3),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (seeded scene builders, scene_seed=render_seed=%d)" % args.seed,
+            "config": {"workload": "random_scene (main.rs:245-289) %dx%d, %d spp, max depth %d, row-sharded over %d GPU"
+                                   % (W, H, spp, depth, world),
+                       "scene": args.scene, "width": W, "height": H, "spp": spp, "max_depth": depth,
+                       "parallelism": "rows interleaved over %d rank(s), RCCL gather" % world},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic},
+            "cpu_baseline": cpu,
+            "detail": {"kernel_ms_mean": round(k_ms, 3), "reduce_ms": round(last.reduce_ms, 3),
+                       "bytes_per_sample": round(bytes_per_sample, 1),
+                       "casts_per_sample": round(cs.casts / max(cs.samples, 1), 4),
+                       "nodes_per_cast": round(cs.node_visits / max(cs.casts, 1), 3),
+                       "prims_per_cast": round(cs.prim_tests / max(cs.casts, 1), 3),
+                       "alg_bytes_per_launch": int(alg_bytes_launch), "n_items": int(items_per_launch),
+                       "spp_chunk": last.spp_chunk, "scene_bytes": int(last.scene_bytes),
+                       "scene_build_upload_s": round(t_build, 3)},
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,29 @@
+import os
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if REPO not in sys.path:
+    sys.path.insert(0, REPO)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (runs the HIP megakernel through the C ABI)")
+
+
+@pytest.fixture(scope="session")
+def rt():
+    """The Python binding of the C ABI (builds the library first if it is missing)."""
+    import __graft_entry__ as ge
+    lib = os.path.join(ge.PKG, "lib", "librtiow_amd.so")
+    if not os.path.exists(lib):
+        ge.build_library()
+    return ge.import_binding()
+
+
+@pytest.fixture(scope="session")
+def renderer(rt):
+    r = rt.Renderer(0)
+    yield r
+    r.close()

@@ -1,0 +1,146 @@
+"""CPU-side checks of the product library: it loads, exports every symbol the header
+declares, and its host scene model reproduces the oracle's scenes and cameras exactly
+(no GPU needed — no compute calls)."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+from tests import oracle_binding as ob
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(REPO, "include", "rt", "rt_abi.h")
+
+
+def header_symbols():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(rt_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_library_exports_every_header_symbol(rt):
+    lib = rt.load_library()
+    declared = header_symbols()
+    assert len(declared) >= 30
+    missing = [s for s in declared if not hasattr(lib, s)]
+    assert not missing, missing
+    assert sorted(declared) == sorted(rt.EXPORTED)
+    assert lib.rt_abi_version() == 1
+
+
+@pytest.mark.parametrize("scene_id", range(8))
+def test_scene_builders_match_oracle(rt, scene_id):
+    """Same draw order as the reference builders (main.rs:52-289, incl. BVH axis draws and Perlin tables)."""
+    w = rt.World(7).build_scene(scene_id)
+    info = w.info()
+    o = ob.scene_info(scene_id, 7)
+    assert info.n_hittables == o["n_hittables"]
+    assert info.n_materials == o["n_materials"]
+    assert info.n_leaf_prims == o["n_leaf_prims"]
+    assert info.checksum == o["checksum"]
+
+
+def test_random_scene_composition(rt):
+    """main.rs:254-287: 1 ground + kept small spheres + 3 big; ~485 objects."""
+    counts = [rt.World(s).build_scene(0).info().n_hittables for s in range(1, 21)]
+    assert all(470 <= c <= 489 for c in counts)
+    assert len(set(counts)) > 1          # the layout really depends on the seed
+
+
+@pytest.mark.parametrize("scene_id", range(8))
+def test_flatten_all_scenes(rt, scene_id):
+    w = rt.World(1).build_scene(scene_id)
+    soa = w.flatten()
+    assert soa.n_prims >= 1 and soa.n_materials == w.info().n_materials
+    if scene_id == 7:
+        assert soa.n_instances == 1 and soa.n_media == 2 and soa.image_bytes == 1024 * 512 * 3
+    if scene_id == 6:
+        assert soa.n_media == 2 and soa.n_instances == 2
+
+
+@pytest.mark.parametrize("scene_id,w,h", [(0, 1200, 800), (5, 800, 800), (7, 1920, 1080), (4, 64, 36)])
+def test_camera_matches_oracle_bitwise(rt, scene_id, w, h):
+    cam, _ = rt.scene_camera(scene_id, w, h)
+    mine = np.array(list(cam.origin) + list(cam.lower_left_corner) + list(cam.horizontal) + list(cam.vertical) +
+                    list(cam.u) + list(cam.v) + list(cam.w) + [cam.lens_radius, cam.time0, cam.time1])
+    assert np.array_equal(mine, ob.camera(scene_id, w, h))
+
+
+def test_camera_new_book_values(rt):
+    cam = rt.camera_new((13, 2, 3), (0, 0, 0), (0, 1, 0), 20.0, 1.5, 0.1, 10.0, 0.0, 1.0)
+    assert cam.lens_radius == 0.05
+    w = np.array(cam.w)
+    assert np.allclose(w, np.array([13, 2, 3]) / np.linalg.norm([13, 2, 3]))
+    # viewport height 2*tan(10deg)*focus, width = aspect * height
+    assert np.linalg.norm(cam.vertical) == pytest.approx(20 * np.tan(np.radians(10)), rel=1e-14)
+    assert np.linalg.norm(cam.horizontal) == pytest.approx(1.5 * 20 * np.tan(np.radians(10)), rel=1e-14)
+
+
+def test_presets_match_reference_table(rt):
+    p = rt.scene_preset(7)   # main.rs:442-459
+    assert tuple(p.look_from) == (478.0, 278.0, -600.0) and p.vfov == 40.0
+    assert p.default_width == 800 and p.default_spp == 2000 and p.aperture == 0.1 and p.focus_dist == 10.0
+    p0 = rt.scene_preset(0)  # main.rs:316-333
+    assert tuple(p0.background) == (0.7, 0.8, 1.0) and p0.default_spp == 100
+    with pytest.raises(rt.RTError):
+        rt.scene_preset(8)   # main.rs:461-463 panics
+
+
+def test_errors_do_not_abort(rt):
+    w = rt.World(1)
+    with pytest.raises(rt.RTError):
+        w.sphere(1, (0, 0, 0), 1.0)         # no material 1 yet
+    m = w.lambertian(w.solid(0.5, 0.5, 0.5))
+    assert m == 1                            # 1-based handles (main.rs:46-49)
+    with pytest.raises(rt.RTError):
+        w.push(12345)
+    with pytest.raises(rt.RTError):
+        w.build_scene(42)
+    lib = rt.load_library()
+    assert lib.rt_ctx_create(0, None) == -1
+    assert lib.rt_render(None, None, None, None) == -1
+    assert lib.rt_rows_in_shard(800, 3, 8) == 100
+    assert lib.rt_rows_in_shard(7, 3, 8) == 1
+    assert lib.rt_rows_in_shard(7, 7, 8) == 0
+
+
+def test_unsupported_nesting_reported(rt):
+    w = rt.World(1)
+    m = w.lambertian(w.solid(1, 1, 1))
+    s = w.sphere(m, (0, 0, 0), 1.0)
+    med = w.constant_medium(s, 0.5, w.isotropic(w.solid(1, 1, 1)))
+    inst = w.translate(med, (1, 0, 0))       # a medium under an instance is not lowered
+    w.push(inst)
+    with pytest.raises(rt.RTError, match="UNSUPPORTED"):
+        w.flatten()
+
+
+def test_custom_world_flattens(rt):
+    """The reference's constructor surface composes: BVH over boxes, instances, media."""
+    w = rt.World(3)
+    white = w.lambertian(w.solid(0.73, 0.73, 0.73))
+    boxes = [w.box((i, 0, 0), (i + 0.5, 1, 1), white) for i in range(10)]
+    w.push(w.bvh(boxes))
+    inst = w.translate(w.rotate_y(w.bvh([w.sphere(white, (0, j, 0), 0.3) for j in range(5)]), 30.0), (0, 0, 5))
+    w.push(inst)
+    w.push(w.constant_medium(w.sphere(white, (0, 0, 0), 50.0), 0.01, w.isotropic(w.solid(1, 1, 1))))
+    w.push(w.xy_rect(w.diffuse_light(w.solid(4, 4, 4)), 0, 1, 0, 1, -2))
+    soa = w.flatten()
+    assert soa.n_instances == 1 and soa.n_media == 1
+    assert w.info().n_leaf_prims == 10 + 5 + 1 + 1
+
+
+def test_ppm_writer_reference_format(rt, tmp_path):
+    """math.rs:119-132 + main.rs:472,591-596: P3, blank line after 255, rows top to bottom, NaN -> 0."""
+    img = np.zeros((2, 3, 3), np.float32)
+    img[1, 0] = [1.0, 0.25, 0.0]    # top-left pixel (row 1 = top since y = 0 is the bottom)
+    img[0, 2] = [np.nan, 4.0, 0.5]  # bottom-right
+    path = tmp_path / "x.ppm"
+    rt.write_ppm(img, str(path))
+    lines = path.read_text().split("\n")
+    assert lines[:4] == ["P3", "3 2", "255", ""]
+    assert lines[4] == "255 128 0"           # (int)(256 * clamp(sqrt(x), 0, .999))
+    assert lines[4 + 5] == "0 255 181"       # NaN -> 0, clamp to .999 -> 255, sqrt(.5)*256 = 181.02
+    assert len([l for l in lines[4:] if l]) == 6

@@ -1,0 +1,157 @@
+"""GPU parity: the HIP megakernel (through the C ABI) against the CPU oracle.
+
+Bar (BASELINE.json north_star): per-pixel L_inf <= 1e-3 on the linear mean radiance.
+The kernel and the oracle follow the same paths (same seeded draws, same f64
+operation order), so we also require a relative agreement of 1e-9: a single
+diverged sample would move a pixel by ~1e-2, so this checks path identity; what is
+left is only the summation order of the bounce loop (iterative on the GPU, recursive
+in the reference).
+"""
+import numpy as np
+import pytest
+
+from tests import oracle_binding as ob
+
+pytestmark = pytest.mark.gpu
+
+LINF = 1e-3          # north_star tolerance
+REL = 1e-9           # path identity (f64 output)
+
+
+def gpu_render(rt, renderer, scene_id, W, H, spp, depth=50, scene_seed=1, render_seed=1, row_begin=0,
+               row_stride=1, spp_chunk=0, out_format=None):
+    fmt = rt.RT_OUT_F64 if out_format is None else out_format
+    img, _ = rt.render_scene(scene_id, W, H, spp, depth, scene_seed, render_seed, row_begin, row_stride, fmt,
+                             spp_chunk, renderer=renderer)
+    return img
+
+
+def assert_parity(got, ref, label):
+    assert got.shape == ref.shape, label
+    assert np.all(np.isfinite(got)), label
+    diff = np.abs(got - ref)
+    linf = float(diff.max())
+    assert linf <= LINF, f"{label}: L_inf {linf}"
+    bad = diff > REL * np.maximum(1.0, np.abs(ref))
+    assert not bad.any(), f"{label}: {int(bad.sum())} px differ beyond {REL} (max {linf})"
+
+
+def test_device_numerics_bit_equal_host(rt, renderer):
+    rng = np.random.default_rng(11)
+    x = np.concatenate([rng.uniform(-50, 50, 4000), rng.uniform(-2e4, 2e4, 2000), [0.0, -0.0, np.inf, np.nan]])
+    pos = np.concatenate([rng.uniform(0, 1, 4000), 2.0 ** -rng.uniform(0, 53, 2000), [0.0, 1.0, 5e-324, np.inf]])
+    y = rng.normal(size=x.size)
+    n = rng.normal(size=(3, 3000))
+    n /= np.linalg.norm(n, axis=0)
+    bits = rng.integers(0, 2 ** 63, size=5000, dtype=np.int64).astype(np.uint64).view(np.float64)
+    cases = {0: (x,), 1: (x,), 2: (pos,), 3: (x, y), 4: (np.clip(y / 3, -1, 1),), 5: tuple(n), 6: tuple(n),
+             7: (pos,), 8: (np.abs(x),), 9: (x, y), 10: (bits,), 11: (bits,)}
+    for fn, args in cases.items():
+        host = ob.evaluate(fn, *args)
+        dev = renderer.device_eval(fn, *args)
+        same = (host.view(np.uint64) == dev.view(np.uint64)) | (np.isnan(host) & np.isnan(dev))
+        assert same.all(), f"fn {fn}: {int((~same).sum())} mismatches, e.g. {args[0][~same][:3]}"
+
+
+@pytest.mark.parametrize("scene_id,W,H,spp", [
+    (0, 64, 48, 8),      # random spheres (C1/C2/C5 scene)
+    (1, 48, 27, 4),      # two checker spheres
+    (2, 48, 27, 4),      # perlin
+    (3, 48, 27, 4),      # earth (image texture, sphere_uv)
+    (4, 48, 27, 8),      # simple light
+    (5, 40, 40, 8),      # cornell (C3 scene)
+    (6, 40, 40, 8),      # cornell smoke (media with instanced box boundary)
+    (7, 48, 27, 8),      # final scene (C4 scene)
+])
+def test_scene_parity(rt, renderer, scene_id, W, H, spp):
+    got = gpu_render(rt, renderer, scene_id, W, H, spp)
+    ref = ob.render(scene_id, W, H, spp)
+    assert_parity(got, ref, f"scene {scene_id}")
+
+
+def test_parity_other_seeds_and_depths(rt, renderer):
+    for scene_seed, render_seed, depth in [(2, 9, 50), (3, 4, 8), (5, 77, 1), (1, 1, 2)]:
+        got = gpu_render(rt, renderer, 0, 40, 24, 4, depth, scene_seed, render_seed)
+        ref = ob.render(0, 40, 24, 4, depth, scene_seed, render_seed)
+        assert_parity(got, ref, f"seeds {scene_seed}/{render_seed} depth {depth}")
+
+
+def test_depth_zero_is_black(rt, renderer):
+    got = gpu_render(rt, renderer, 0, 16, 8, 2, depth=0)
+    assert np.all(got == 0.0)   # main.rs:21-23
+
+
+def test_tiny_and_ragged_images(rt, renderer):
+    for W, H, spp in [(2, 2, 1), (9, 7, 3), (67, 5, 2), (3, 65, 1)]:
+        got = gpu_render(rt, renderer, 5, W, H, spp)
+        ref = ob.render(5, W, H, spp)
+        assert_parity(got, ref, f"{W}x{H}x{spp}")
+
+
+def test_row_shards_reassemble_bit_exactly(rt, renderer):
+    """Row sharding (the multi-GPU partition) does not change any pixel (keys are per pixel/sample)."""
+    W, H, spp, G = 40, 30, 4, 4
+    full = gpu_render(rt, renderer, 7, W, H, spp)
+    for r in range(G):
+        shard = gpu_render(rt, renderer, 7, W, H, spp, row_begin=r, row_stride=G)
+        assert np.array_equal(shard, full[r::G]), r
+
+
+def test_chunking_only_changes_rounding(rt, renderer):
+    a = gpu_render(rt, renderer, 0, 32, 16, 12, spp_chunk=12)
+    b = gpu_render(rt, renderer, 0, 32, 16, 12, spp_chunk=1)
+    c = gpu_render(rt, renderer, 0, 32, 16, 12, spp_chunk=5)
+    assert np.allclose(a, b, rtol=1e-12, atol=1e-14) and np.allclose(a, c, rtol=1e-12, atol=1e-14)
+    ref = ob.render(0, 32, 16, 12, spp_chunk=5)
+    assert np.array_equal(c, ref) or np.allclose(c, ref, rtol=REL, atol=0)
+
+
+def test_f32_output_matches(rt, renderer):
+    got = gpu_render(rt, renderer, 5, 32, 32, 4, out_format=rt.RT_OUT_F32)
+    ref = ob.render(5, 32, 32, 4)
+    assert got.dtype == np.float32
+    assert np.max(np.abs(got - ref)) <= 1e-5 * max(1.0, float(np.abs(ref).max()))
+
+
+def test_full_width_rows_c2_geometry(rt, renderer):
+    """BASELINE config C2 geometry (1200x800, depth 50) on a bounded row subset at 2 spp."""
+    W, H = 1200, 800
+    got = gpu_render(rt, renderer, 0, W, H, 2, row_begin=5, row_stride=40)
+    ref = ob.render(0, W, H, 2, row_begin=5, row_stride=40)
+    assert_parity(got, ref, "C2 rows")
+
+
+def test_count_work_mode(rt, renderer):
+    world = rt.World(1).build_scene(0)
+    cam, bg = rt.scene_camera(0, 120, 80)
+    renderer.upload(world)
+    p = rt.Renderer.params(120, 80, 8, 50, bg, 1, count_work=1, out_format=rt.RT_OUT_F64)
+    counted = renderer.render(cam, p)
+    st = renderer.stats()
+    _, ost = ob.render(0, 120, 80, 8, return_stats=True)
+    assert st.samples == 120 * 80 * 8
+    assert st.casts == ost.casts            # same paths -> same number of hit_hittables calls
+    assert st.node_visits > st.casts and st.prim_tests > st.casts
+    p2 = rt.Renderer.params(120, 80, 8, 50, bg, 1, out_format=rt.RT_OUT_F64)
+    assert np.array_equal(renderer.render(cam, p2), counted)
+
+
+def test_custom_world_parity_against_preset(rt, renderer):
+    """A world built through the constructor ABI renders like the same preset scene."""
+    w = rt.World(1)
+    red = w.lambertian(w.solid(0.65, 0.05, 0.05))
+    white = w.lambertian(w.solid(0.73, 0.73, 0.73))
+    green = w.lambertian(w.solid(0.12, 0.45, 0.15))
+    light = w.diffuse_light(w.solid(15.0, 15.0, 15.0))
+    w.push(w.yz_rect(green, 0, 555, 0, 555, 555))
+    w.push(w.yz_rect(red, 0, 555, 0, 555, 0))
+    w.push(w.xz_rect(light, 213, 343, 227, 332, 554))
+    w.push(w.xz_rect(white, 0, 555, 0, 555, 0))
+    w.push(w.xz_rect(white, 0, 555, 0, 555, 555))
+    w.push(w.xy_rect(white, 0, 555, 0, 555, 555))
+    w.push(w.translate(w.rotate_y(w.box((0, 0, 0), (165, 330, 165), white), 15.0), (265, 0, 295)))
+    w.push(w.translate(w.rotate_y(w.box((0, 0, 0), (165, 165, 165), white), -18.0), (130, 0, 65)))
+    cam, bg = rt.scene_camera(5, 32, 32)
+    renderer.upload(w)
+    got = renderer.render(cam, rt.Renderer.params(32, 32, 4, 50, bg, 1, out_format=rt.RT_OUT_F64))
+    assert_parity(got, ob.render(5, 32, 32, 4), "custom cornell")
