@@ -248,14 +248,25 @@ struct Builder {
         return RT_LEAF_CODE(first, e - b);
     }
 
-    int build_rec(std::vector<Item>& items, int b, int e)
+    int max_depth_seen = 0;
+
+    int build_rec(std::vector<Item>& items, int b, int e, int depth)
     {
+        max_depth_seen = std::max(max_depth_seen, depth);
         const int n = e - b;
         const double c_trav = 1.0, c_isect = 1.5;
         double plo[3], phi[3];
         bounds(items, b, e, plo, phi);
         double parea = area(plo, phi);
         if (n <= 2) return make_leaf(items, b, e);
+        if (depth >= 20) {  // bound the traversal stack: median split on the widest centroid axis
+            double clo[3] = {INFINITY, INFINITY, INFINITY}, chi[3] = {-INFINITY, -INFINITY, -INFINITY};
+            for (int i = b; i < e; ++i)
+                for (int a = 0; a < 3; ++a) { clo[a] = std::min(clo[a], items[i].c[a]); chi[a] = std::max(chi[a], items[i].c[a]); }
+            int ax = 0;
+            for (int a = 1; a < 3; ++a) if (chi[a] - clo[a] > chi[ax] - clo[ax]) ax = a;
+            return split_at(items, b, e, ax, n / 2, depth);
+        }
         // full-sweep SAH over the three axes (centroid order; ties by prim index)
         double best_cost = INFINITY;
         int best_axis = -1, best_split = -1;
@@ -289,17 +300,22 @@ struct Builder {
         double leaf_cost = c_isect * n;
         if (n <= 4 && leaf_cost <= best_cost) return make_leaf(items, b, e);
         if (best_axis < 0) best_axis = 0, best_split = n / 2;
-        std::sort(items.begin() + b, items.begin() + e, [best_axis](const Item& x, const Item& y) {
-            return x.c[best_axis] < y.c[best_axis] || (x.c[best_axis] == y.c[best_axis] && x.prim < y.prim);
+        return split_at(items, b, e, best_axis, best_split, depth);
+    }
+
+    int split_at(std::vector<Item>& items, int b, int e, int axis, int split, int depth)
+    {
+        std::sort(items.begin() + b, items.begin() + e, [axis](const Item& x, const Item& y) {
+            return x.c[axis] < y.c[axis] || (x.c[axis] == y.c[axis] && x.prim < y.prim);
         });
-        int mid = b + best_split;
+        int mid = b + split;
         int node = (int)f.nodes.size();
         f.nodes.emplace_back();
         double llo[3], lhi[3], rlo[3], rhi[3];
         bounds(items, b, mid, llo, lhi);
         bounds(items, mid, e, rlo, rhi);
-        int lc = build_rec(items, b, mid);
-        int rc = build_rec(items, mid, e);
+        int lc = build_rec(items, b, mid, depth + 1);
+        int rc = build_rec(items, mid, e, depth + 1);
         rt_bvh_node& nd = f.nodes[node];
         std::memset(&nd, 0, sizeof nd);
         to_f32_box(llo, lhi, nd.lo0, nd.hi0);
@@ -312,7 +328,7 @@ struct Builder {
     int build_bvh(std::vector<Item>& items)
     {
         if (items.empty()) return RT_LEAF_CODE((int)f.prim_refs.size(), 0);
-        return build_rec(items, 0, (int)items.size());
+        return build_rec(items, 0, (int)items.size(), 0);
     }
 };
 
@@ -337,6 +353,11 @@ int flatten(World& w, int accel, std::string& err)
     }
     f.tlas_root = bld.build_bvh(top);
     f.media = w.n_media;
+    // the kernel's traversal stack holds 64 entries shared by a TLAS walk and a nested BLAS walk
+    if (2 * bld.max_depth_seen > 62) {
+        err = "BVH too deep for the kernel's 64-entry traversal stack";
+        return RT_ERR_UNSUPPORTED;
+    }
 
     for (const Material& m : w.materials) {
         rt_material rm;
