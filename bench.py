@@ -45,6 +45,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--count-spp", type=int, default=16, help="spp of the untimed count_work pass")
+    ap.add_argument("--no-count", action="store_true", help="skip the count_work pass (profiling runs)")
     ap.add_argument("--ppm", default="", help="write the rendered frame (rank 0) as a P3 PPM")
     return ap.parse_args()
 
@@ -127,9 +128,10 @@ def main():
 
     # ---- algorithmic bytes per sample from an untimed count_work pass (same scene/camera)
     count_spp = min(args.count_spp, spp)
-    cp = rt.Renderer.params(W, H, count_spp, depth, bg, args.seed, row_begin=rank, row_stride=world,
-                            out_format=rt.RT_OUT_F32, count_work=1)
-    renderer.render(cam, cp)
+    cp = rt.Renderer.params(W, H, count_spp if not args.no_count else 1, depth, bg, args.seed, row_begin=rank,
+                            row_stride=world, out_format=rt.RT_OUT_F32, count_work=0 if args.no_count else 1)
+    if not args.no_count:
+        renderer.render(cam, cp)
     cs = renderer.stats()
     bytes_per_sample = (cs.node_visits * cs.node_bytes + cs.prim_tests * cs.prim_bytes +
                         cs.casts * cs.material_bytes) / max(cs.samples, 1)
@@ -138,10 +140,14 @@ def main():
     alg_bytes_launch = bytes_per_sample * samples_per_launch + items_per_launch * 24
     k_ms = float(np.mean(kernel_ms)) if kernel_ms else float("nan")
     achieved = alg_bytes_launch / (k_ms * 1e-3) / 1e9
-    traffic = None
-    pmc = os.environ.get("RT_PMC_TRAFFIC_JSON")
-    if pmc and os.path.exists(pmc):
-        traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
+    # HBM traffic per launch from the committed rocprofv3 PMC pass of this workload
+    # (scripts/profile.sh + scripts/prof_summary.py); null if none matches.
+    traffic, traffic_src = None, None
+    pmc = os.environ.get("RT_PMC_TRAFFIC_JSON", os.path.join(REPO, "profiles", "pmc_traffic.json"))
+    if os.path.exists(pmc):
+        pj = json.load(open(pmc))
+        if pj.get("workload") == [args.scene, W, H, spp, depth, world]:
+            traffic, traffic_src = pj.get("hbm_bytes_per_launch"), pj.get("tag")
 
     if args.ppm and rank == 0:
         rt.write_ppm(frame.cpu().numpy(), args.ppm)
@@ -186,7 +192,8 @@ def main():
                        "scene": args.scene, "width": W, "height": H, "spp": spp, "max_depth": depth,
                        "parallelism": "rows interleaved over %d rank(s), RCCL gather" % world},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic},
+                         "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": None if traffic is None else int(traffic)},
             "cpu_baseline": cpu,
             "detail": {"kernel_ms_mean": round(k_ms, 3), "reduce_ms": round(last.reduce_ms, 3),
                        "bytes_per_sample": round(bytes_per_sample, 1),
@@ -195,7 +202,9 @@ def main():
                        "prims_per_cast": round(cs.prim_tests / max(cs.casts, 1), 3),
                        "alg_bytes_per_launch": int(alg_bytes_launch), "n_items": int(items_per_launch),
                        "spp_chunk": last.spp_chunk, "scene_bytes": int(last.scene_bytes),
-                       "scene_build_upload_s": round(t_build, 3)},
+                       "scene_build_upload_s": round(t_build, 3),
+                       "traffic_source": traffic_src,
+                       "traffic_gbs": None if traffic is None else round(traffic / (k_ms * 1e-3) / 1e9, 2)},
         }
         print(json.dumps(out), flush=True)
     if world > 1:
