@@ -168,7 +168,10 @@ typedef struct rt_stats {
     uint64_t n_items;            /* work items (pixel, chunk) */
     int32_t n_chunks, spp_chunk;
     int64_t scene_bytes;         /* device bytes of the uploaded scene */
-    int32_t node_bytes, prim_bytes, material_bytes, pad;
+    int32_t node_bytes, prim_bytes, material_bytes;
+    int32_t variant_features;    /* feature set of the kernel variant launched */
+    int32_t slab32;              /* 1 if the conservative f32 slab test was used */
+    int32_t loop;                /* traversal loop form (0 if-if, 1 while-while) */
 } rt_stats;
 int rt_last_stats(rt_ctx* ctx, rt_stats* out);
 
@@ -177,6 +180,10 @@ int rt_last_stats(rt_ctx* ctx, rt_stats* out);
  * bottom, each channel (int)(256 * clamp(sqrt(mean), 0, 0.999)) with NaN -> 0.
  * mean_rgb is height x width x 3 f32 with row 0 = bottom (y = 0). */
 int rt_write_ppm(const float* mean_rgb, int width, int height, const char* path);
+
+/* Kernel variant knobs of a context (defaults: slab32 = 1, loop = 0, or the RT_SLAB32 /
+ * RT_LOOP environment variables). Results do not depend on them (tests check this). */
+int rt_ctx_set_variant(rt_ctx* ctx, int slab32, int loop);
 
 /* ---- self test ------------------------------------------------------------------------------ */
 /* Evaluates rt_numerics.h functions on the device (same fn ids as the oracle's

@@ -102,6 +102,10 @@ typedef struct rt_scene_soa {
     int32_t tlas_root;       /* BVH root reference of the top level */
     int32_t accel;           /* RT_ACCEL_* the tables were built with */
     int64_t image_bytes;
+    /* M such that every node box is padded by >= 2^-18 * M (plus BLAS offsets); the
+     * kernel uses its conservative f32 slab test only when ray origins stay within 2M.
+     * 0: boxes not padded, f64 slab tests only. */
+    double pad_extent;
     const rt_prim* prims;
     const int32_t* prim_refs;
     const rt_bvh_node* nodes;

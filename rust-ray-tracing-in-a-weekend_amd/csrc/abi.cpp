@@ -5,6 +5,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -60,6 +61,10 @@ struct rt_ctx {
     bool pending_stats = false;
     bool pending_counts = false;
     rt_stats stats{};
+    uint32_t features = rtk::FEAT_ALL;  // of the uploaded scene
+    double pad_extent = 0.0;
+    int opt_slab32 = 1;                 // rt_ctx_set_variant / RT_SLAB32
+    int opt_loop = 1;                   // rt_ctx_set_variant / RT_LOOP
 };
 
 extern "C" {
@@ -91,6 +96,8 @@ int rt_ctx_create(int device, rt_ctx** out)
     rt_ctx* c = new (std::nothrow) rt_ctx();
     if (!c) return fail(RT_ERR_OOM, "rt_ctx");
     c->device = device;
+    if (const char* e = std::getenv("RT_SLAB32")) c->opt_slab32 = std::atoi(e) != 0;
+    if (const char* e = std::getenv("RT_LOOP")) c->opt_loop = std::atoi(e) != 0;
     hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     for (int i = 0; i < 3 && e == hipSuccess; ++i) e = hipEventCreate(&c->ev[i]);
     if (e == hipSuccess) e = hipMalloc((void**)&c->counters, 4 * sizeof(unsigned long long));
@@ -376,6 +383,7 @@ int rt_world_flatten(rt_world* w, int accel, const rt_scene_soa** soa_out)
 int rt_ctx_upload_soa(rt_ctx* c, const rt_scene_soa* s)
 {
     if (!c || !s) return fail(RT_ERR_INVALID, "null argument");
+    if (s->n_prim_refs >= (1 << 26) - 64) return fail(RT_ERR_UNSUPPORTED, "too many primitive references");
     if (s->n_prims < 0 || s->n_prim_refs < 0 || s->n_nodes < 0 || s->n_instances < 0 || s->n_materials < 0 ||
         s->n_textures < 0 || s->n_perlin < 0 || s->image_bytes < 0)
         return fail(RT_ERR_INVALID, "negative table size");
@@ -452,6 +460,19 @@ int rt_ctx_upload_soa(rt_ctx* c, const rt_scene_soa* s)
     c->S.image = (const uint8_t*)(base + off[8]);
     c->S.tlas_root = s->tlas_root;
     c->has_scene = true;
+    uint32_t feat = 0;
+    for (int i = 0; i < s->n_prims; ++i) {
+        const int k = s->prims[i].kind;
+        if (k == RT_PRIM_XY_RECT || k == RT_PRIM_XZ_RECT || k == RT_PRIM_YZ_RECT || k == RT_PRIM_BOX) feat |= rtk::FEAT_RECT;
+        if (k == RT_PRIM_INSTANCE) feat |= rtk::FEAT_INST;
+        if (k == RT_PRIM_MEDIUM) feat |= rtk::FEAT_MEDIUM;
+    }
+    for (int i = 0; i < s->n_textures; ++i) {
+        if (s->textures[i].kind == RT_TEX_NOISE) feat |= rtk::FEAT_NOISE;
+        if (s->textures[i].kind == RT_TEX_IMAGE) feat |= rtk::FEAT_IMAGE;
+    }
+    c->features = feat;
+    c->pad_extent = s->pad_extent > 0.0 && std::isfinite(s->pad_extent) ? s->pad_extent : 0.0;
     c->stats.scene_bytes = (int64_t)total;
     return RT_OK;
 }
@@ -529,9 +550,23 @@ int rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, void* 
         dev_out = c->out_buf;
     }
     const bool count = p->count_work != 0;
+    // conservative f32 slab tests need every ray origin within 2M of the origin (flatten.cpp):
+    // hit points are inside the scene bounds; check the camera (+ lens) here
+    const double cam_mag = std::sqrt(cam->origin[0] * cam->origin[0] + cam->origin[1] * cam->origin[1] +
+                                     cam->origin[2] * cam->origin[2]) + std::fabs(cam->lens_radius) *
+                           (1.0 + std::sqrt(cam->u[0] * cam->u[0] + cam->u[1] * cam->u[1] + cam->u[2] * cam->u[2]) +
+                            std::sqrt(cam->v[0] * cam->v[0] + cam->v[1] * cam->v[1] + cam->v[2] * cam->v[2]));
+    rtk::LaunchOpts o;
+    o.features = c->features;
+    o.slab32 = c->opt_slab32 && c->pad_extent > 0.0 && cam_mag <= 2.0 * c->pad_extent;
+    o.loop = c->opt_loop;
+    o.count = count;
     if (count) HIP_TRY(hipMemsetAsync(c->counters, 0, 4 * sizeof(unsigned long long), stream));
     HIP_TRY(hipEventRecord(c->ev[0], stream));
-    HIP_TRY(rtk::launch_trace(c->S, K, c->partial, c->counters, count, stream));
+    HIP_TRY(rtk::launch_trace(c->S, K, c->partial, c->counters, o, stream));
+    c->stats.variant_features = (int32_t)rtk::variant_features(o.features);
+    c->stats.slab32 = o.slab32;
+    c->stats.loop = o.loop;
     HIP_TRY(hipEventRecord(c->ev[1], stream));
     HIP_TRY(rtk::launch_reduce(c->partial, dev_out, p->out_format == RT_OUT_F64, n_px, n_chunks,
                                1.0 / (double)p->spp, stream));
@@ -604,6 +639,14 @@ int rt_write_ppm(const float* mean, int width, int height, const char* path)
 }
 
 // ---- self test ----------------------------------------------------------------------------------
+int rt_ctx_set_variant(rt_ctx* c, int slab32, int loop)
+{
+    if (!c || slab32 < 0 || slab32 > 1 || loop < 0 || loop > 1) return fail(RT_ERR_INVALID, "bad variant");
+    c->opt_slab32 = slab32;
+    c->opt_loop = loop;
+    return RT_OK;
+}
+
 int rt_device_eval(rt_ctx* c, int fn, const double* x, const double* y, const double* z, double* out, int n)
 {
     if (!c || !x || !out || n < 0 || fn < 0 || fn > 11) return fail(RT_ERR_INVALID, "bad argument");

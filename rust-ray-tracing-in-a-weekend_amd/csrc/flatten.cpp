@@ -149,7 +149,14 @@ struct Builder {
             std::vector<Item> items;
             for (int hid : leaves) items.push_back(item_of(lower_simple(hid), hid));
             in.child_kind = RT_CHILD_BVH;
+            double off = 0.0;  // object-space origins: |o_obj| <= |o_world| + sum |offsets|
+            for (int i = 0; i < in.n_ops; ++i)
+                if (in.op_kind[i] == RT_OP_TRANSLATE)
+                    off += std::sqrt(in.op[i][0] * in.op[i][0] + in.op[i][1] * in.op[i][1] + in.op[i][2] * in.op[i][2]);
+            const double saved = pad_abs;
+            pad_abs = 0x1.0p-18 * (world_extent + off);
             in.child = build_bvh(items);
+            pad_abs = saved;
         } else {
             err = "instance over an instance or a medium";
             return RT_ERR_UNSUPPORTED;
@@ -225,13 +232,17 @@ struct Builder {
             }
     }
 
-    // Pads and rounds a box outward to f32 so the f64 slab test on it never culls
-    // a primitive the exact test would hit (the box only gates traversal).
-    static void to_f32_box(const double lo[3], const double hi[3], float flo[3], float fhi[3])
+    // Pads and rounds a box outward to f32 so that neither the f64 slab test nor the
+    // conservative f32 one ever culls a primitive the exact test would hit (the box only
+    // gates traversal). pad_abs = 2^-18 * M covers the f32 rounding of ray origins with
+    // |o| <= 2M and of the slab products (DESIGN.md §Traversal precision).
+    double pad_abs = 0.0;
+
+    void to_f32_box(const double lo[3], const double hi[3], float flo[3], float fhi[3]) const
     {
         for (int a = 0; a < 3; ++a) {
             double mag = std::max(std::fabs(lo[a]), std::fabs(hi[a]));
-            double pad = 1e-6 * (1.0 + mag);
+            double pad = 1e-6 * (1.0 + mag) + pad_abs;
             double l = lo[a] - pad, h = hi[a] + pad;
             float fl = (float)l, fh = (float)h;
             if ((double)fl > l) fl = std::nextafter(fl, -INFINITY);
@@ -249,6 +260,7 @@ struct Builder {
     }
 
     int max_depth_seen = 0;
+    double world_extent = 0.0;  // M: max |coordinate| over the top-level items' boxes
 
     int build_rec(std::vector<Item>& items, int b, int e, int depth)
     {
@@ -343,6 +355,15 @@ int flatten(World& w, int accel, std::string& err)
     FlatScene f;
     Builder bld{w, f, err};
     std::vector<Item> top;
+    for (int id : w.hittables) {  // M for the f32-slab padding (see to_f32_box)
+        AABB b;
+        if (w.valid_hittable(id) && w.bounding_box(id, 0.0, 1.0, b)) {
+            const double c[6] = {b.minimum.x, b.minimum.y, b.minimum.z, b.maximum.x, b.maximum.y, b.maximum.z};
+            for (double v : c)
+                if (std::isfinite(v)) bld.world_extent = std::max(bld.world_extent, std::fabs(v));
+        }
+    }
+    bld.pad_abs = 0x1.0p-18 * bld.world_extent;
     for (int id : w.hittables) {
         if (!w.valid_hittable(id)) {
             err = "invalid hittable id in world list";
@@ -351,6 +372,7 @@ int flatten(World& w, int accel, std::string& err)
         int rc = bld.lower_top(id, top);
         if (rc) return rc;
     }
+    // instances build their BLAS while being lowered, so take M from the world's boxes first
     f.tlas_root = bld.build_bvh(top);
     f.media = w.n_media;
     // the kernel's traversal stack holds 64 entries shared by a TLAS walk and a nested BLAS walk
@@ -411,6 +433,7 @@ int flatten(World& w, int accel, std::string& err)
     s.tlas_root = f.tlas_root;
     s.accel = accel;
     s.image_bytes = (int64_t)f.image.size();
+    s.pad_extent = bld.world_extent;
     w.flat = std::move(f);
     FlatScene& g = w.flat;
     rt_scene_soa& t = g.soa;

@@ -9,6 +9,9 @@
 //   * the depth-50 recursion is an iterative bounce loop; a lane whose path ends
 //     starts its next sample in the same loop iteration (path regeneration), so a
 //     wave stays busy until every lane has finished its chunk;
+//   * traversal carries only (t, primitive ids); the full HitRecord (point, normal,
+//     face, uv; hittable.rs:6-27) is rebuilt once per cast for the winning primitive
+//     by re-running its test with t_max = t — same inputs, same arithmetic, same bits;
 //   * the lane sums its chunk's samples in sample order (deterministic), writes
 //     one f64x3 partial; a second kernel adds the partials in chunk order and
 //     scales by 1/spp (math.rs:119-126), so the image does not depend on the
@@ -29,13 +32,25 @@ struct Ray {
     double dx, dy, dz;
     double time;
     double a;                 // length_squared(direction)
-    double ix, iy, iz;        // 1 / direction (slab tests only)
+    double ix, iy, iz;        // 1 / direction (f64 slab tests only)
+    float fix, fiy, fiz;      // f32 1 / direction (f32 slab tests only)
+    float fox, foy, foz;      // -origin * (1 / direction) in f32
 };
 
+// The HitRecord of hittable.rs:6-27 (uv deferred to texture lookup: uvkind 1 keeps the
+// object-space outward normal for sphere_uv, 2 keeps (x-a0, a1-a0, y-b0, b1-b0)).
 struct Hit {
     double t, px, py, pz, nx, ny, nz;
-    double uv0, uv1, uv2, uv3;  // uvkind 1: object-space outward normal; 2: (x-a0, a1-a0, y-b0, b1-b0)
+    double uv0, uv1, uv2, uv3;
     int front, mat, uvkind;
+};
+
+// What traversal keeps per candidate: the parameter and which primitive produced it.
+struct HitRef {
+    double t;
+    int prim;   // prim index (top level)
+    int sub;    // instance: BLAS prim index; box: winning side (0..5)
+    int side;   // box inside an instance: winning side
 };
 
 struct Keyed {                 // coordinates of the medium's keyed draw
@@ -47,12 +62,45 @@ struct Count {
     uint32_t casts, nodes, prims;
 };
 
+// Compile-time kernel configuration (one instantiation per variant):
+//   F      scene features the variant handles (trace_kernel.hpp FEAT_*); code for the
+//          others is not emitted, which keeps register pressure and code size down
+//   S32    conservative f32 slab tests (boxes padded on the host, see flatten.cpp)
+//   LOOP   0: one node-or-leaf step per iteration; 1: while-while (Aila & Laine 2009)
+//   COUNT  also count casts / node visits / primitive tests
+template <uint32_t F_, bool S32_, int LOOP_, bool COUNT_>
+struct Cfg {
+    static constexpr uint32_t F = F_;
+    static constexpr bool S32 = S32_;
+    static constexpr int LOOP = LOOP_;
+    static constexpr bool COUNT = COUNT_;
+};
+
+__device__ __forceinline__ float f32_inv_dir(double d)
+{
+    // an exact 0 would give inf * 0 = NaN in the slab products; a 1e-30 component keeps the
+    // interval of a ray parallel to a slab finite and correct (inside: huge, outside: empty)
+    float f = (float)d;
+    if (__builtin_fabsf(f) < 1e-30f) f = __builtin_copysignf(1e-30f, f);
+    return __builtin_amdgcn_rcpf(f);
+}
+
+template <class C>
 __device__ __forceinline__ void finish_ray(Ray& r)
 {
     r.a = r.dx * r.dx + r.dy * r.dy + r.dz * r.dz;
-    r.ix = 1.0 / r.dx;
-    r.iy = 1.0 / r.dy;
-    r.iz = 1.0 / r.dz;
+    if constexpr (C::S32) {
+        r.fix = f32_inv_dir(r.dx);
+        r.fiy = f32_inv_dir(r.dy);
+        r.fiz = f32_inv_dir(r.dz);
+        r.fox = -(float)r.ox * r.fix;
+        r.foy = -(float)r.oy * r.fiy;
+        r.foz = -(float)r.oz * r.fiz;
+    } else {
+        r.ix = 1.0 / r.dx;
+        r.iy = 1.0 / r.dy;
+        r.iz = 1.0 / r.dz;
+    }
 }
 
 // hittable.rs:23-26
@@ -66,9 +114,13 @@ __device__ __forceinline__ void set_face_normal(Hit& h, double dx, double dy, do
     h.nz = front ? nz : -nz;
 }
 
-// hittable.rs:254-288 (sphere_uv deferred: the outward normal is kept in uv0..2)
-__device__ __forceinline__ bool hit_sphere(double cx, double cy, double cz, double radius, double inv_r,
-                                           const Ray& r, double t_min, double t_max, int mat, Hit& h)
+// ---------------------------------------------------------------------------
+// primitives: a t-only test (traversal) and a finisher (once per cast)
+// ---------------------------------------------------------------------------
+
+// hittable.rs:254-273: the root in [t_min, t_max]
+__device__ __forceinline__ bool sphere_t(double cx, double cy, double cz, double radius, const Ray& r, double t_min,
+                                         double t_max, double& t)
 {
     const double ocx = r.ox - cx, ocy = r.oy - cy, ocz = r.oz - cz;
     const double half_b = ocx * r.dx + ocy * r.dy + ocz * r.dz;
@@ -81,78 +133,194 @@ __device__ __forceinline__ bool hit_sphere(double cx, double cy, double cz, doub
         root = (-half_b + sqrtd) / r.a;
         if (root < t_min || t_max < root) return false;
     }
-    h.t = root;
-    h.px = r.ox + r.dx * root;
-    h.py = r.oy + r.dy * root;
-    h.pz = r.oz + r.dz * root;
+    t = root;
+    return true;
+}
+
+// hittable.rs:275-287
+template <class C>
+__device__ __forceinline__ void sphere_finish(double cx, double cy, double cz, double inv_r, const Ray& r, double t,
+                                              int mat, Hit& h)
+{
+    h.t = t;
+    h.px = r.ox + r.dx * t;
+    h.py = r.oy + r.dy * t;
+    h.pz = r.oz + r.dz * t;
     const double onx = (h.px - cx) * inv_r, ony = (h.py - cy) * inv_r, onz = (h.pz - cz) * inv_r;
     set_face_normal(h, r.dx, r.dy, r.dz, onx, ony, onz);
     h.mat = mat;
     h.uvkind = 1;
-    h.uv0 = onx;
-    h.uv1 = ony;
-    h.uv2 = onz;
-    return true;
+    if constexpr ((C::F & FEAT_IMAGE) != 0) {
+        h.uv0 = onx;
+        h.uv1 = ony;
+        h.uv2 = onz;
+    }
 }
 
-// hittable.rs:308-384. axis: 0 XY (k on z), 1 XZ (k on y), 2 YZ (k on x).
-__device__ __forceinline__ bool hit_rect(int axis, double a0, double a1, double b0, double b1, double k,
-                                         const Ray& r, double t_min, double t_max, int mat, Hit& h)
+// hittable.rs:308-320 (axis 0: XY, k on z; 1: XZ, k on y; 2: YZ, k on x)
+__device__ __forceinline__ void rect_axes(int axis, const Ray& r, double& ok, double& dk, double& oa, double& da,
+                                          double& ob, double& db)
 {
-    double ok, dk, oa, da, ob, db;
     if (axis == 0) { ok = r.oz; dk = r.dz; oa = r.ox; da = r.dx; ob = r.oy; db = r.dy; }
     else if (axis == 1) { ok = r.oy; dk = r.dy; oa = r.ox; da = r.dx; ob = r.oz; db = r.dz; }
     else { ok = r.ox; dk = r.dx; oa = r.oy; da = r.dy; ob = r.oz; db = r.dz; }
+}
+
+__device__ __forceinline__ bool rect_t(int axis, double a0, double a1, double b0, double b1, double k, const Ray& r,
+                                       double t_min, double t_max, double& t_out)
+{
+    double ok, dk, oa, da, ob, db;
+    rect_axes(axis, r, ok, dk, oa, da, ob, db);
     const double t = (k - ok) / dk;
     if (t < t_min || t > t_max) return false;
     const double x = oa + t * da;
     const double y = ob + t * db;
     if (x < a0 || x > a1 || y < b0 || y > b1) return false;
+    t_out = t;
+    return true;
+}
+
+// hittable.rs:322-331
+template <class C>
+__device__ __forceinline__ void rect_finish(int axis, double a0, double a1, double b0, double b1, const Ray& r,
+                                            double t, int mat, Hit& h)
+{
+    double ok, dk, oa, da, ob, db;
+    rect_axes(axis, r, ok, dk, oa, da, ob, db);
     h.uvkind = 2;
-    h.uv0 = x - a0;
-    h.uv1 = a1 - a0;
-    h.uv2 = y - b0;
-    h.uv3 = b1 - b0;
+    if constexpr ((C::F & FEAT_IMAGE) != 0) {
+        const double x = oa + t * da;
+        const double y = ob + t * db;
+        h.uv0 = x - a0;
+        h.uv1 = a1 - a0;
+        h.uv2 = y - b0;
+        h.uv3 = b1 - b0;
+    }
     h.t = t;
     set_face_normal(h, r.dx, r.dy, r.dz, axis == 2 ? 1.0 : 0.0, axis == 1 ? 1.0 : 0.0, axis == 0 ? 1.0 : 0.0);
     h.mat = mat;
     h.px = r.ox + r.dx * t;
     h.py = r.oy + r.dy * t;
     h.pz = r.oz + r.dz * t;
-    return true;
 }
 
-// Sphere, MovingSphere, rects, Box (hittable.rs:211-231).
-template <bool COUNT>
-__device__ __forceinline__ bool hit_simple(const rt_prim& p, const Ray& r, double t_min, double t_max, Hit& h,
-                                           Count& cnt)
+// the six sides of new_box (hittable.rs:135-142): side -> axis, (a0 a1 b0 b1 k) from min/max
+__device__ __forceinline__ void box_side(const rt_prim& p, int side, int& axis, double& a0, double& a1, double& b0,
+                                         double& b1, double& k)
 {
-    if (COUNT) cnt.prims++;
-    switch (p.kind) {
-    case RT_PRIM_SPHERE: return hit_sphere(p.p[0], p.p[1], p.p[2], p.p[3], p.p[4], r, t_min, t_max, p.mat, h);
-    case RT_PRIM_MOVING_SPHERE: {
-        // center_0 + ((time - time_0) / (time_1 - time_0)) * (center_1 - center_0)
-        const double s = p.a ? r.time : (r.time - p.p[8]) / (p.p[9] - p.p[8]);
-        return hit_sphere(p.p[0] + p.p[5] * s, p.p[1] + p.p[6] * s, p.p[2] + p.p[7] * s, p.p[3], p.p[4], r, t_min,
-                          t_max, p.mat, h);
+    const double mnx = p.p[0], mny = p.p[1], mnz = p.p[2], mxx = p.p[3], mxy = p.p[4], mxz = p.p[5];
+    if (side < 2) { axis = 0; a0 = mnx; a1 = mxx; b0 = mny; b1 = mxy; k = side == 0 ? mxz : mnz; }
+    else if (side < 4) { axis = 1; a0 = mnx; a1 = mxx; b0 = mnz; b1 = mxz; k = side == 2 ? mxy : mny; }
+    else { axis = 2; a0 = mny; a1 = mxy; b0 = mnz; b1 = mxz; k = side == 4 ? mxx : mnx; }
+}
+
+// Box::hit = hit_hittables over its sides (hittable.rs:229-231): closest, ties to the later side.
+__device__ __forceinline__ bool box_t(const rt_prim& p, const Ray& r, double t_min, double t_max, double& t,
+                                      int& side)
+{
+    bool any = false;
+#pragma unroll
+    for (int s = 0; s < 6; ++s) {
+        int axis;
+        double a0, a1, b0, b1, k, ts;
+        box_side(p, s, axis, a0, a1, b0, b1, k);
+        if (rect_t(axis, a0, a1, b0, b1, k, r, t_min, t_max, ts)) {
+            t_max = ts;
+            t = ts;
+            side = s;
+            any = true;
+        }
     }
-    case RT_PRIM_XY_RECT: return hit_rect(0, p.p[0], p.p[1], p.p[2], p.p[3], p.p[4], r, t_min, t_max, p.mat, h);
-    case RT_PRIM_XZ_RECT: return hit_rect(1, p.p[0], p.p[1], p.p[2], p.p[3], p.p[4], r, t_min, t_max, p.mat, h);
-    case RT_PRIM_YZ_RECT: return hit_rect(2, p.p[0], p.p[1], p.p[2], p.p[3], p.p[4], r, t_min, t_max, p.mat, h);
-    case RT_PRIM_BOX: {  // hit_hittables over the 6 sides in new_box order (hittable.rs:135-142)
-        const double mnx = p.p[0], mny = p.p[1], mnz = p.p[2], mxx = p.p[3], mxy = p.p[4], mxz = p.p[5];
-        double closest = t_max;
-        bool any = false;
-        if (hit_rect(0, mnx, mxx, mny, mxy, mxz, r, t_min, closest, p.mat, h)) { closest = h.t; any = true; }
-        if (hit_rect(0, mnx, mxx, mny, mxy, mnz, r, t_min, closest, p.mat, h)) { closest = h.t; any = true; }
-        if (hit_rect(1, mnx, mxx, mnz, mxz, mxy, r, t_min, closest, p.mat, h)) { closest = h.t; any = true; }
-        if (hit_rect(1, mnx, mxx, mnz, mxz, mny, r, t_min, closest, p.mat, h)) { closest = h.t; any = true; }
-        if (hit_rect(2, mny, mxy, mnz, mxz, mxx, r, t_min, closest, p.mat, h)) { closest = h.t; any = true; }
-        if (hit_rect(2, mny, mxy, mnz, mxz, mnx, r, t_min, closest, p.mat, h)) { closest = h.t; any = true; }
-        return any;
+    return any;
+}
+
+// center_0 + ((time - time_0) / (time_1 - time_0)) * (center_1 - center_0)   (hittable.rs:556-558)
+__device__ __forceinline__ void moving_center(const rt_prim& p, const Ray& r, double& cx, double& cy, double& cz)
+{
+    const double s = p.a ? r.time : (r.time - p.p[8]) / (p.p[9] - p.p[8]);
+    cx = p.p[0] + p.p[5] * s;
+    cy = p.p[1] + p.p[6] * s;
+    cz = p.p[2] + p.p[7] * s;
+}
+
+// Sphere, MovingSphere, rects, Box: t-only (hittable.rs:211-231).
+template <class C>
+__device__ __forceinline__ bool simple_t(const rt_prim& p, const Ray& r, double t_min, double t_max, double& t,
+                                         int& side, Count& cnt)
+{
+    if (C::COUNT) cnt.prims++;
+    if constexpr (!(C::F & FEAT_RECT)) {
+        if (p.kind == RT_PRIM_SPHERE) return sphere_t(p.p[0], p.p[1], p.p[2], p.p[3], r, t_min, t_max, t);
+        double cx, cy, cz;
+        moving_center(p, r, cx, cy, cz);
+        return sphere_t(cx, cy, cz, p.p[3], r, t_min, t_max, t);
+    } else {
+        switch (p.kind) {
+        case RT_PRIM_SPHERE: return sphere_t(p.p[0], p.p[1], p.p[2], p.p[3], r, t_min, t_max, t);
+        case RT_PRIM_MOVING_SPHERE: {
+            double cx, cy, cz;
+            moving_center(p, r, cx, cy, cz);
+            return sphere_t(cx, cy, cz, p.p[3], r, t_min, t_max, t);
+        }
+        case RT_PRIM_XY_RECT: return rect_t(0, p.p[0], p.p[1], p.p[2], p.p[3], p.p[4], r, t_min, t_max, t);
+        case RT_PRIM_XZ_RECT: return rect_t(1, p.p[0], p.p[1], p.p[2], p.p[3], p.p[4], r, t_min, t_max, t);
+        case RT_PRIM_YZ_RECT: return rect_t(2, p.p[0], p.p[1], p.p[2], p.p[3], p.p[4], r, t_min, t_max, t);
+        case RT_PRIM_BOX: return box_t(p, r, t_min, t_max, t, side);
+        default: return false;
+        }
     }
-    default: return false;
+}
+
+template <class C>
+__device__ __forceinline__ void simple_finish(const rt_prim& p, const Ray& r, double t, int side, Hit& h)
+{
+    if constexpr ((C::F & FEAT_RECT) != 0) {
+        if (p.kind >= RT_PRIM_XY_RECT && p.kind <= RT_PRIM_YZ_RECT) {
+            rect_finish<C>(p.kind - RT_PRIM_XY_RECT, p.p[0], p.p[1], p.p[2], p.p[3], r, t, p.mat, h);
+            return;
+        }
+        if (p.kind == RT_PRIM_BOX) {
+            int axis;
+            double a0, a1, b0, b1, k;
+            box_side(p, side, axis, a0, a1, b0, b1, k);
+            rect_finish<C>(axis, a0, a1, b0, b1, r, t, p.mat, h);
+            return;
+        }
     }
+    if (p.kind == RT_PRIM_SPHERE) {
+        sphere_finish<C>(p.p[0], p.p[1], p.p[2], p.p[4], r, t, p.mat, h);
+    } else {
+        double cx, cy, cz;
+        moving_center(p, r, cx, cy, cz);
+        sphere_finish<C>(cx, cy, cz, p.p[4], r, t, p.mat, h);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// BVH traversal
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ bool slab32(const float* lo, const float* hi, const Ray& r, float t_min, float t_max,
+                                       float& t_near)
+{
+    const float x0 = __builtin_fmaf(lo[0], r.fix, r.fox), x1 = __builtin_fmaf(hi[0], r.fix, r.fox);
+    const float y0 = __builtin_fmaf(lo[1], r.fiy, r.foy), y1 = __builtin_fmaf(hi[1], r.fiy, r.foy);
+    const float z0 = __builtin_fmaf(lo[2], r.fiz, r.foz), z1 = __builtin_fmaf(hi[2], r.fiz, r.foz);
+    const float tn = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fmaxf(fminf(z0, z1), t_min));
+    const float tf = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fminf(fmaxf(z0, z1), t_max));
+    t_near = tn;
+    return tn <= tf;
+}
+
+// f32 bounds of a double t range, rounded outward
+__device__ __forceinline__ float f32_down(double t)
+{
+    const float f = (float)t;
+    return f > 0.0f ? f * (1.0f - 0x1.0p-20f) : f * (1.0f + 0x1.0p-20f);
+}
+__device__ __forceinline__ float f32_up(double t)
+{
+    const float f = (float)t;
+    return f > 0.0f ? f * (1.0f + 0x1.0p-20f) : f * (1.0f - 0x1.0p-20f);
 }
 
 // Conservative slab test against an f32 box (rounded outward and padded on the
@@ -169,54 +337,84 @@ __device__ __forceinline__ bool slab(const float* lo, const float* hi, const Ray
     return tn <= tf;
 }
 
-// Closest hit in a BVH whose leaves hold simple prims (a BLAS).
-template <bool COUNT>
-__device__ bool trace_blas(const SceneDev& S, int root, const Ray& r, double t_min, double t_max, Hit& h,
-                           int* stack, int sp0, Count& cnt)
+constexpr int RT_DONE = (int)0x80000000;
+
+// Closest hit in a BVH (nodes + leaf ranges of prim_refs). `leaf(prim, t_max, best)`
+// tests one primitive; on a closer hit it fills best (t and sub ids) and returns true.
+template <class C, class LeafFn>
+__device__ __forceinline__ bool traverse(const SceneDev& S, int root, const Ray& r, double t_min, double t_max,
+                                         HitRef& best, int* stack, int sp0, Count& cnt, LeafFn&& leaf)
 {
     bool any = false;
     int sp = sp0;
     int cur = root;
-    for (;;) {
-        if (cur < 0) {
-            const int code = ~cur;
-            const int first = code >> 5, count = code & 31;
-            for (int i = 0; i < count; ++i) {
-                const rt_prim& p = S.prims[S.prim_refs[first + i]];
-                if (hit_simple<COUNT>(p, r, t_min, t_max, h, cnt)) { t_max = h.t; any = true; }
-            }
-            if (sp == sp0) break;
-            cur = stack[--sp];
+    float tmin_f = 0.0f, tmax_f = 0.0f;
+    if constexpr (C::S32) {
+        tmin_f = f32_down(t_min);
+        tmax_f = f32_up(t_max);
+    }
+    // one node visit: test both children, continue with the nearer, push the farther
+    auto visit = [&](int node) -> int {
+        if (C::COUNT) cnt.nodes++;
+        const rt_bvh_node& nd = S.nodes[node];
+        bool h0, h1, near0;
+        if constexpr (C::S32) {
+            float tn0, tn1;
+            h0 = slab32(nd.lo0, nd.hi0, r, tmin_f, tmax_f, tn0);
+            h1 = slab32(nd.lo1, nd.hi1, r, tmin_f, tmax_f, tn1);
+            near0 = tn0 <= tn1;
         } else {
-            if (COUNT) cnt.nodes++;
-            const rt_bvh_node& nd = S.nodes[cur];
             double tn0, tn1;
-            const bool h0 = slab(nd.lo0, nd.hi0, r, t_min, t_max, tn0);
-            const bool h1 = slab(nd.lo1, nd.hi1, r, t_min, t_max, tn1);
-            if (h0 && h1) {
-                const bool first_left = tn0 <= tn1;
-                stack[sp++] = first_left ? nd.child[1] : nd.child[0];
-                cur = first_left ? nd.child[0] : nd.child[1];
-            } else if (h0) {
-                cur = nd.child[0];
-            } else if (h1) {
-                cur = nd.child[1];
-            } else {
-                if (sp == sp0) break;
-                cur = stack[--sp];
+            h0 = slab(nd.lo0, nd.hi0, r, t_min, t_max, tn0);
+            h1 = slab(nd.lo1, nd.hi1, r, t_min, t_max, tn1);
+            near0 = tn0 <= tn1;
+        }
+        if (h0 && h1) {
+            stack[sp++] = near0 ? nd.child[1] : nd.child[0];
+            return near0 ? nd.child[0] : nd.child[1];
+        }
+        if (h0) return nd.child[0];
+        if (h1) return nd.child[1];
+        return sp == sp0 ? RT_DONE : stack[--sp];
+    };
+    auto do_leaf = [&](int code) {
+        code = ~code;
+        const int first = code >> 5, count = code & 31;
+        for (int i = 0; i < count; ++i) {
+            const int prim = S.prim_refs[first + i];
+            if (leaf(prim, t_max, best)) {
+                best.prim = prim;
+                t_max = best.t;
+                any = true;
+                if constexpr (C::S32) tmax_f = f32_up(t_max);
             }
+        }
+    };
+    if constexpr (C::LOOP == 0) {
+        while (cur != RT_DONE) {
+            if (cur < 0) {
+                do_leaf(cur);
+                cur = sp == sp0 ? RT_DONE : stack[--sp];
+            } else {
+                cur = visit(cur);
+            }
+        }
+    } else {
+        while (cur != RT_DONE) {
+            while (cur >= 0) cur = visit(cur);
+            if (cur == RT_DONE) break;
+            do_leaf(cur);
+            cur = sp == sp0 ? RT_DONE : stack[--sp];
         }
     }
     return any;
 }
 
-// Translate / RotateY chain (hittable.rs:232-244, 386-415), outermost op first.
-template <bool COUNT>
-__device__ bool hit_instance(const SceneDev& S, const rt_instance& in, const Ray& ray, double t_min, double t_max,
-                             Hit& h, int* stack, int sp0, Count& cnt)
+// ---------------------------------------------------------------------------
+// Translate / RotateY instances (hittable.rs:232-244, 386-415), outermost op first
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void instance_ray(const rt_instance& in, Ray& r, double* dirx, double* diry, double* dirz)
 {
-    Ray r = ray;
-    double dirx[4], diry[4], dirz[4];
     const int n = in.n_ops;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -231,14 +429,47 @@ __device__ bool hit_instance(const SceneDev& S, const rt_instance& in, const Ray
                 const double dx = c * r.dx - s * r.dz, dz = s * r.dx + c * r.dz;
                 r.ox = ox; r.oz = oz; r.dx = dx; r.dz = dz;
             }
-            dirx[i] = r.dx; diry[i] = r.dy; dirz[i] = r.dz;
+            if (dirx) { dirx[i] = r.dx; diry[i] = r.dy; dirz[i] = r.dz; }
         }
     }
-    finish_ray(r);
-    bool hit;
-    if (in.child_kind == RT_CHILD_PRIM) hit = hit_simple<COUNT>(S.prims[in.child], r, t_min, t_max, h, cnt);
-    else hit = trace_blas<COUNT>(S, in.child, r, t_min, t_max, h, stack, sp0, cnt);
-    if (!hit) return false;
+}
+
+// t-only: the closest hit of the instance's child; sub = BLAS prim (or the child prim),
+// side = winning box side.
+template <class C>
+__device__ bool instance_t(const SceneDev& S, const rt_instance& in, const Ray& ray, double t_min, double t_max,
+                           HitRef& ref, int* stack, int sp0, Count& cnt)
+{
+    Ray r = ray;
+    instance_ray(in, r, nullptr, nullptr, nullptr);
+    finish_ray<C>(r);
+    if (in.child_kind == RT_CHILD_PRIM) {
+        int side = 0;
+        if (!simple_t<C>(S.prims[in.child], r, t_min, t_max, ref.t, side, cnt)) return false;
+        ref.sub = in.child;
+        ref.side = side;
+        return true;
+    }
+    HitRef inner;
+    if (!traverse<C>(S, in.child, r, t_min, t_max, inner, stack, sp0, cnt,
+                     [&](int prim, double tmax, HitRef& b) {
+                         return simple_t<C>(S.prims[prim], r, t_min, tmax, b.t, b.side, cnt);
+                     }))
+        return false;
+    ref.t = inner.t;
+    ref.sub = inner.prim;
+    ref.side = inner.side;
+    return true;
+}
+
+template <class C>
+__device__ void instance_finish(const SceneDev& S, const rt_instance& in, const Ray& ray, const HitRef& ref, Hit& h)
+{
+    Ray r = ray;
+    double dirx[4], diry[4], dirz[4];
+    instance_ray(in, r, dirx, diry, dirz);
+    simple_finish<C>(S.prims[ref.sub], r, ref.t, ref.side, h);
+    const int n = in.n_ops;
 #pragma unroll
     for (int i = 3; i >= 0; --i) {
         if (i < n) {
@@ -256,27 +487,34 @@ __device__ bool hit_instance(const SceneDev& S, const rt_instance& in, const Ray
             }
         }
     }
-    return true;
 }
 
-template <bool COUNT>
-__device__ __forceinline__ bool hit_boundary(const SceneDev& S, int prim, const Ray& r, double t_min, double t_max,
-                                             Hit& h, int* stack, int sp0, Count& cnt)
+// t of a medium boundary (a simple prim or an instance).
+template <class C>
+__device__ __forceinline__ bool boundary_t(const SceneDev& S, int prim, const Ray& r, double t_min, double t_max,
+                                           double& t, int* stack, int sp0, Count& cnt)
 {
     const rt_prim& p = S.prims[prim];
-    if (p.kind == RT_PRIM_INSTANCE) return hit_instance<COUNT>(S, S.instances[p.a], r, t_min, t_max, h, stack, sp0, cnt);
-    return hit_simple<COUNT>(p, r, t_min, t_max, h, cnt);
+    if constexpr ((C::F & FEAT_INST) != 0) {
+        if (p.kind == RT_PRIM_INSTANCE) {
+            HitRef ref;
+            if (!instance_t<C>(S, S.instances[p.a], r, t_min, t_max, ref, stack, sp0, cnt)) return false;
+            t = ref.t;
+            return true;
+        }
+    }
+    int side = 0;
+    return simple_t<C>(p, r, t_min, t_max, t, side, cnt);
 }
 
 // ConstantMedium (hittable.rs:417-473), keyed draw instead of the in-hit thread_rng().
-template <bool COUNT>
-__device__ bool hit_medium(const SceneDev& S, const rt_prim& m, const Ray& r, double t_min, double t_max, Hit& h,
-                           int* stack, int sp0, const Keyed& key, Count& cnt)
+template <class C>
+__device__ bool medium_t(const SceneDev& S, const rt_prim& m, const Ray& r, double t_min, double t_max, double& t,
+                         int* stack, int sp0, const Keyed& key, Count& cnt)
 {
-    Hit h1, h2;
-    if (!hit_boundary<COUNT>(S, m.a, r, -RT_INF, RT_INF, h1, stack, sp0, cnt)) return false;
-    if (!hit_boundary<COUNT>(S, m.a, r, h1.t + 0.0001, RT_INF, h2, stack, sp0, cnt)) return false;
-    double t1 = h1.t, t2 = h2.t;
+    double t1, t2;
+    if (!boundary_t<C>(S, m.a, r, -RT_INF, RT_INF, t1, stack, sp0, cnt)) return false;
+    if (!boundary_t<C>(S, m.a, r, t1 + 0.0001, RT_INF, t2, stack, sp0, cnt)) return false;
     if (t1 < t_min) t1 = t_min;
     if (t2 > t_max) t2 = t_max;
     if (t1 >= t2) return false;
@@ -287,63 +525,58 @@ __device__ bool hit_medium(const SceneDev& S, const rt_prim& m, const Ray& r, do
                                              RT_STREAM_MEDIUM + (uint32_t)m.b));
     const double hit_distance = m.p[0] * rt_log(xi);
     if (hit_distance > distance_inside) return false;
-    h.t = t1 + hit_distance / ray_length;
-    h.px = r.ox + r.dx * h.t;
-    h.py = r.oy + r.dy * h.t;
-    h.pz = r.oz + r.dz * h.t;
+    t = t1 + hit_distance / ray_length;
+    return true;
+}
+
+// hittable.rs:452-463
+__device__ __forceinline__ void medium_finish(const rt_prim& m, const Ray& r, double t, Hit& h)
+{
+    h.t = t;
+    h.px = r.ox + r.dx * t;
+    h.py = r.oy + r.dy * t;
+    h.pz = r.oz + r.dz * t;
     h.nx = 1.0; h.ny = 0.0; h.nz = 0.0;
     h.front = 1;
     h.mat = m.mat;
     h.uvkind = 0;
-    return true;
 }
 
-// hit_hittables(world, ray, 0.001, inf) (hittable.rs:43-55) over the TLAS.
-template <bool COUNT>
+// hit_hittables(world, ray, 0.001, inf) (hittable.rs:43-55) over the TLAS, then the
+// HitRecord of the closest primitive.
+template <class C>
 __device__ bool trace_world(const SceneDev& S, const Ray& r, Hit& h, int* stack, const Keyed& key, Count& cnt)
 {
-    double t_min = 0.001, t_max = RT_INF;
-    bool any = false;
-    int sp = 0;
-    int cur = S.tlas_root;
-    for (;;) {
-        if (cur < 0) {
-            const int code = ~cur;
-            const int first = code >> 5, count = code & 31;
-            for (int i = 0; i < count; ++i) {
-                const rt_prim& p = S.prims[S.prim_refs[first + i]];
-                bool hit;
-                if (p.kind == RT_PRIM_INSTANCE)
-                    hit = hit_instance<COUNT>(S, S.instances[p.a], r, t_min, t_max, h, stack, sp, cnt);
-                else if (p.kind == RT_PRIM_MEDIUM)
-                    hit = hit_medium<COUNT>(S, p, r, t_min, t_max, h, stack, sp, key, cnt);
-                else
-                    hit = hit_simple<COUNT>(p, r, t_min, t_max, h, cnt);
-                if (hit) { t_max = h.t; any = true; }
-            }
-            if (sp == 0) break;
-            cur = stack[--sp];
-        } else {
-            if (COUNT) cnt.nodes++;
-            const rt_bvh_node& nd = S.nodes[cur];
-            double tn0, tn1;
-            const bool h0 = slab(nd.lo0, nd.hi0, r, t_min, t_max, tn0);
-            const bool h1 = slab(nd.lo1, nd.hi1, r, t_min, t_max, tn1);
-            if (h0 && h1) {
-                const bool first_left = tn0 <= tn1;
-                stack[sp++] = first_left ? nd.child[1] : nd.child[0];
-                cur = first_left ? nd.child[0] : nd.child[1];
-            } else if (h0) {
-                cur = nd.child[0];
-            } else if (h1) {
-                cur = nd.child[1];
-            } else {
-                if (sp == 0) break;
-                cur = stack[--sp];
-            }
+    const double t_min = 0.001;
+    HitRef best;
+    best.sub = 0;
+    best.side = 0;
+    const bool hit = traverse<C>(S, S.tlas_root, r, t_min, RT_INF, best, stack, 0, cnt,
+                                 [&](int prim, double tmax, HitRef& b) {
+        const rt_prim& p = S.prims[prim];
+        if constexpr ((C::F & FEAT_INST) != 0)
+            if (p.kind == RT_PRIM_INSTANCE)
+                return instance_t<C>(S, S.instances[p.a], r, t_min, tmax, b, stack, 32, cnt);
+        if constexpr ((C::F & FEAT_MEDIUM) != 0)
+            if (p.kind == RT_PRIM_MEDIUM) return medium_t<C>(S, p, r, t_min, tmax, b.t, stack, 32, key, cnt);
+        return simple_t<C>(p, r, t_min, tmax, b.t, b.side, cnt);
+    });
+    if (!hit) return false;
+    const rt_prim& p = S.prims[best.prim];
+    if constexpr ((C::F & FEAT_INST) != 0) {
+        if (p.kind == RT_PRIM_INSTANCE) {
+            instance_finish<C>(S, S.instances[p.a], r, best, h);
+            return true;
         }
     }
-    return any;
+    if constexpr ((C::F & FEAT_MEDIUM) != 0) {
+        if (p.kind == RT_PRIM_MEDIUM) {
+            medium_finish(p, r, best.t, h);
+            return true;
+        }
+    }
+    simple_finish<C>(p, r, best.t, best.side, h);
+    return true;
 }
 
 // ---------------------------------------------------------------------------
@@ -416,9 +649,20 @@ __device__ void hit_uv(const Hit& h, double& u, double& v)
     }
 }
 
+template <class C>
 __device__ void tex_value(const SceneDev& S, int ti, const Hit& h, double& cr, double& cg, double& cb)
 {
     const rt_texture& t = S.textures[ti];
+    if constexpr (!(C::F & (FEAT_NOISE | FEAT_IMAGE))) {
+        if (t.kind == RT_TEX_CHECKER) {
+            const double sines = rt_sin(10.0 * h.px) * rt_sin(10.0 * h.py) * rt_sin(10.0 * h.pz);
+            const double* c = sines < 0.0 ? t.c1 : t.c0;
+            cr = c[0]; cg = c[1]; cb = c[2];
+        } else {
+            cr = t.c0[0]; cg = t.c0[1]; cb = t.c0[2];
+        }
+        return;
+    }
     switch (t.kind) {
     case RT_TEX_SOLID: cr = t.c0[0]; cg = t.c0[1]; cb = t.c0[2]; return;
     case RT_TEX_CHECKER: {
@@ -477,10 +721,11 @@ __device__ __forceinline__ void random_in_unit_sphere(rt_stream& st, double scal
 // ---------------------------------------------------------------------------
 // the integrator
 // ---------------------------------------------------------------------------
-template <bool COUNT>
+template <class C>
 __global__ void __launch_bounds__(256) trace_chunks(SceneDev S, KParams P, double* __restrict__ partial,
                                                     unsigned long long* __restrict__ counters)
 {
+    constexpr bool COUNT = C::COUNT;
     const int lane = threadIdx.x & 63;
     const long long wave = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const long long n_tiles = (long long)P.tiles_x * P.tiles_y;
@@ -529,7 +774,7 @@ __global__ void __launch_bounds__(256) trace_chunks(SceneDev S, KParams P, doubl
             r.dy = P.cam.lower_left_corner[1] + P.cam.horizontal[1] * u + P.cam.vertical[1] * v - P.cam.origin[1] - offy;
             r.dz = P.cam.lower_left_corner[2] + P.cam.horizontal[2] * u + P.cam.vertical[2] * v - P.cam.origin[2] - offz;
             r.time = rt_uniform_sample(rt_stream_next_u64(&st), P.cam.time0, P.scale_time);
-            finish_ray(r);
+            finish_ray<C>(r);
             Lr = Lg = Lb = 0.0;
             Tr = Tg = Tb = 1.0;
             depth = P.max_depth;
@@ -541,7 +786,7 @@ __global__ void __launch_bounds__(256) trace_chunks(SceneDev S, KParams P, doubl
             key.bounce = (uint32_t)(P.max_depth - depth);
             if (COUNT) cnt.casts++;
             Hit h;
-            if (!trace_world<COUNT>(S, r, h, stack, key, cnt)) {  // main.rs:37
+            if (!trace_world<C>(S, r, h, stack, key, cnt)) {  // main.rs:37
                 Lr = Lr + Tr * P.bg[0];
                 Lg = Lg + Tg * P.bg[1];
                 Lb = Lb + Tb * P.bg[2];
@@ -550,7 +795,7 @@ __global__ void __launch_bounds__(256) trace_chunks(SceneDev S, KParams P, doubl
                 const rt_material& m = S.materials[h.mat];
                 if (m.kind == RT_MAT_DIFFUSE_LIGHT) {  // material.rs:25-34
                     double er, eg, eb;
-                    tex_value(S, m.tex, h, er, eg, eb);
+                    tex_value<C>(S, m.tex, h, er, eg, eb);
                     Lr = Lr + Tr * er;
                     Lg = Lg + Tg * eg;
                     Lb = Lb + Tb * eb;
@@ -569,7 +814,7 @@ __global__ void __launch_bounds__(256) trace_chunks(SceneDev S, KParams P, doubl
                         if (__builtin_fabs(sdx) < 1e-8 && __builtin_fabs(sdy) < 1e-8 && __builtin_fabs(sdz) < 1e-8) {
                             sdx = h.nx; sdy = h.ny; sdz = h.nz;
                         }
-                        tex_value(S, m.tex, h, ar, ag, ab);
+                        tex_value<C>(S, m.tex, h, ar, ag, ab);
                         break;
                     }
                     case RT_MAT_METAL: {  // material.rs:50-60
@@ -620,7 +865,7 @@ __global__ void __launch_bounds__(256) trace_chunks(SceneDev S, KParams P, doubl
                     default: {  // isotropic, material.rs:84-87
                         double l2;
                         random_in_unit_sphere(st, P.scale_m11, sdx, sdy, sdz, l2);
-                        tex_value(S, m.tex, h, ar, ag, ab);
+                        tex_value<C>(S, m.tex, h, ar, ag, ab);
                         break;
                     }
                     }
@@ -632,7 +877,7 @@ __global__ void __launch_bounds__(256) trace_chunks(SceneDev S, KParams P, doubl
                         Tb = Tb * ab;
                         r.ox = h.px; r.oy = h.py; r.oz = h.pz;
                         r.dx = sdx; r.dy = sdy; r.dz = sdz;
-                        finish_ray(r);
+                        finish_ray<C>(r);
                         depth -= 1;
                     }
                 }
@@ -709,17 +954,54 @@ __global__ void eval_numerics(int fn, const double* x, const double* y, const do
 // ---------------------------------------------------------------------------
 // host-side launchers
 // ---------------------------------------------------------------------------
+template <uint32_t F, bool S32, int LOOP, bool COUNT>
+static void launch_one(unsigned blocks, hipStream_t stream, const SceneDev& S, const KParams& P, double* partial,
+                       unsigned long long* counters)
+{
+    hipLaunchKernelGGL((trace_chunks<Cfg<F, S32, LOOP, COUNT>>), dim3(blocks), dim3(256), 0, stream, S, P, partial,
+                       counters);
+}
+
+// Variant table: feature set x slab precision x loop form. The launcher takes the
+// smallest feature set covering the scene.
+template <uint32_t F, bool COUNT>
+static void launch_f(int slab32, int loop, unsigned blocks, hipStream_t stream, const SceneDev& S, const KParams& P,
+                     double* partial, unsigned long long* counters)
+{
+    if (slab32) {
+        if (loop) launch_one<F, true, 1, COUNT>(blocks, stream, S, P, partial, counters);
+        else launch_one<F, true, 0, COUNT>(blocks, stream, S, P, partial, counters);
+    } else {
+        if (loop) launch_one<F, false, 1, COUNT>(blocks, stream, S, P, partial, counters);
+        else launch_one<F, false, 0, COUNT>(blocks, stream, S, P, partial, counters);
+    }
+}
+
+uint32_t variant_features(uint32_t scene_features)
+{
+    if ((scene_features & ~FEAT_SET_SPHERES) == 0) return FEAT_SET_SPHERES;
+    if ((scene_features & ~FEAT_SET_RECTINST) == 0) return FEAT_SET_RECTINST;
+    return FEAT_ALL;
+}
+
 hipError_t launch_trace(const SceneDev& S, const KParams& P, double* partial, unsigned long long* counters,
-                        bool count, hipStream_t stream)
+                        const LaunchOpts& o, hipStream_t stream)
 {
     const long long waves = (long long)P.tiles_x * P.tiles_y * P.n_chunks;
     const long long blocks = (waves + 3) / 4;
     if (blocks <= 0) return hipSuccess;
     if (blocks > 0x7fffffffLL) return hipErrorInvalidValue;
-    if (count)
-        hipLaunchKernelGGL(trace_chunks<true>, dim3((unsigned)blocks), dim3(256), 0, stream, S, P, partial, counters);
-    else
-        hipLaunchKernelGGL(trace_chunks<false>, dim3((unsigned)blocks), dim3(256), 0, stream, S, P, partial, counters);
+    const unsigned nb = (unsigned)blocks;
+    const uint32_t f = variant_features(o.features);
+    if (o.count) {
+        if (f == FEAT_SET_SPHERES) launch_f<FEAT_SET_SPHERES, true>(o.slab32, o.loop, nb, stream, S, P, partial, counters);
+        else if (f == FEAT_SET_RECTINST) launch_f<FEAT_SET_RECTINST, true>(o.slab32, o.loop, nb, stream, S, P, partial, counters);
+        else launch_f<FEAT_ALL, true>(o.slab32, o.loop, nb, stream, S, P, partial, counters);
+    } else {
+        if (f == FEAT_SET_SPHERES) launch_f<FEAT_SET_SPHERES, false>(o.slab32, o.loop, nb, stream, S, P, partial, counters);
+        else if (f == FEAT_SET_RECTINST) launch_f<FEAT_SET_RECTINST, false>(o.slab32, o.loop, nb, stream, S, P, partial, counters);
+        else launch_f<FEAT_ALL, false>(o.slab32, o.loop, nb, stream, S, P, partial, counters);
+    }
     return hipGetLastError();
 }
 

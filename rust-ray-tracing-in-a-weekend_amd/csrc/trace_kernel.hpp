@@ -35,8 +35,28 @@ struct KParams {
     int32_t pad;
 };
 
+// Scene features (which code a kernel variant must contain).
+enum : uint32_t {
+    FEAT_RECT = 1,      // XY/XZ/YZ rects and boxes
+    FEAT_INST = 2,      // Translate / RotateY instances
+    FEAT_MEDIUM = 4,    // ConstantMedium
+    FEAT_NOISE = 8,     // Perlin noise texture
+    FEAT_IMAGE = 16,    // image texture
+    FEAT_ALL = 31,
+    FEAT_SET_SPHERES = 0,                      // compiled variant: spheres + solid/checker
+    FEAT_SET_RECTINST = FEAT_RECT | FEAT_INST  // compiled variant: + rects, boxes, instances
+};
+
+struct LaunchOpts {
+    uint32_t features;  // scene features (FEAT_*)
+    int slab32;         // conservative f32 slab tests
+    int loop;           // 0 if-if, 1 while-while traversal
+    int count;          // count_work variant
+};
+
+uint32_t variant_features(uint32_t scene_features);
 hipError_t launch_trace(const SceneDev& S, const KParams& P, double* partial, unsigned long long* counters,
-                        bool count, hipStream_t stream);
+                        const LaunchOpts& o, hipStream_t stream);
 hipError_t launch_reduce(const double* partial, void* out, bool f64, long long n_px, int n_chunks, double scale,
                          hipStream_t stream);
 hipError_t launch_eval(int fn, const double* x, const double* y, const double* z, double* out, int n,

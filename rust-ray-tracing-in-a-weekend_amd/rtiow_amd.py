@@ -45,7 +45,7 @@ EXPORTED = [
     "rt_world_bvh", "rt_world_push", "rt_world_build_scene", "rt_world_info_get", "rt_camera_new",
     "rt_scene_preset_get", "rt_scene_camera", "rt_world_flatten", "rt_ctx_upload_soa",
     "rt_ctx_upload_world", "rt_render", "rt_rows_in_shard", "rt_last_stats", "rt_write_ppm",
-    "rt_device_eval",
+    "rt_ctx_set_variant", "rt_device_eval",
 ]
 
 
@@ -79,7 +79,7 @@ class SceneSoA(ctypes.Structure):
     _fields_ = [("n_prims", ctypes.c_int32), ("n_prim_refs", ctypes.c_int32), ("n_nodes", ctypes.c_int32),
                 ("n_instances", ctypes.c_int32), ("n_materials", ctypes.c_int32), ("n_textures", ctypes.c_int32),
                 ("n_perlin", ctypes.c_int32), ("n_media", ctypes.c_int32), ("tlas_root", ctypes.c_int32),
-                ("accel", ctypes.c_int32), ("image_bytes", ctypes.c_int64),
+                ("accel", ctypes.c_int32), ("image_bytes", ctypes.c_int64), ("pad_extent", ctypes.c_double),
                 ("prims", ctypes.c_void_p), ("prim_refs", ctypes.c_void_p), ("nodes", ctypes.c_void_p),
                 ("instances", ctypes.c_void_p), ("materials", ctypes.c_void_p), ("textures", ctypes.c_void_p),
                 ("perlin_ranvec", ctypes.c_void_p), ("perlin_perm", ctypes.c_void_p),
@@ -100,10 +100,11 @@ class Stats(ctypes.Structure):
                 ("casts", ctypes.c_uint64), ("node_visits", ctypes.c_uint64), ("prim_tests", ctypes.c_uint64),
                 ("n_items", ctypes.c_uint64), ("n_chunks", ctypes.c_int32), ("spp_chunk", ctypes.c_int32),
                 ("scene_bytes", ctypes.c_int64), ("node_bytes", ctypes.c_int32), ("prim_bytes", ctypes.c_int32),
-                ("material_bytes", ctypes.c_int32), ("pad", ctypes.c_int32)]
+                ("material_bytes", ctypes.c_int32), ("variant_features", ctypes.c_int32),
+                ("slab32", ctypes.c_int32), ("loop", ctypes.c_int32)]
 
     def as_dict(self):
-        return {k: getattr(self, k) for k, _ in self._fields_ if k != "pad"}
+        return {k: getattr(self, k) for k, _ in self._fields_}
 
 
 _lib = None
@@ -144,7 +145,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "rt_render": ([P, ctypes.POINTER(Camera), ctypes.POINTER(RenderParams), P], I),
         "rt_rows_in_shard": ([I, I, I], I), "rt_last_stats": ([P, ctypes.POINTER(Stats)], I),
         "rt_write_ppm": ([P, I, I, ctypes.c_char_p], I),
-        "rt_device_eval": ([P, I, P, P, P, P, I], I),
+        "rt_device_eval": ([P, I, P, P, P, P, I], I), "rt_ctx_set_variant": ([P, I, I], I),
     }
     for name, (args, res) in sigs.items():
         fn = getattr(lib, name)
@@ -349,6 +350,9 @@ class Renderer:
         params.stream = stream
         _check(self.lib.rt_render(self.h, ctypes.byref(camera), ctypes.byref(params), ctypes.c_void_p(dev_ptr)),
                "rt_render")
+
+    def set_variant(self, slab32: int = 1, loop: int = 0):
+        _check(self.lib.rt_ctx_set_variant(self.h, slab32, loop), "rt_ctx_set_variant")
 
     def stats(self) -> Stats:
         s = Stats()

@@ -1,0 +1,67 @@
+#!/usr/bin/env python3
+"""A/B the megakernel's variant knobs in ONE process (interleaved rounds), on a bench config.
+
+usage: python scripts/ab_variants.py [--scene 0] [--width 1200] [--height 800] [--spp 500] [--rounds 3]
+Prints per-variant kernel ms (median, min) and checks the variants render identical images.
+"""
+import argparse
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--scene", type=int, default=0)
+    ap.add_argument("--width", type=int, default=1200)
+    ap.add_argument("--height", type=int, default=800)
+    ap.add_argument("--spp", type=int, default=500)
+    ap.add_argument("--depth", type=int, default=50)
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--variants", default="0:0,1:0,0:1,1:1", help="slab32:loop pairs")
+    args = ap.parse_args()
+    import numpy as np
+    import torch  # noqa: F401  (same HIP runtime as bench.py)
+    import __graft_entry__ as ge
+    rt = ge.import_binding()
+
+    W, H = args.width, args.height
+    world = rt.World(1).build_scene(args.scene)
+    cam, bg = rt.scene_camera(args.scene, W, H)
+    r = rt.Renderer(0)
+    r.upload(world)
+    variants = [tuple(int(x) for x in v.split(":")) for v in args.variants.split(",")]
+    # identity check on a small f64 render
+    imgs = {}
+    for v in variants:
+        r.set_variant(*v)
+        imgs[v] = r.render(cam, rt.Renderer.params(W, H, 2, args.depth, bg, 1, row_stride=8, out_format=rt.RT_OUT_F64))
+    base = imgs[variants[0]]
+    for v in variants[1:]:
+        same = np.array_equal(imgs[v], base)
+        print(f"variant {v} identical to {variants[0]}: {same}" +
+              ("" if same else f" (max diff {np.max(np.abs(imgs[v] - base)):.3e}, "
+                               f"{int(np.sum(np.any(imgs[v] != base, axis=2)))} px)"))
+    times = {v: [] for v in variants}
+    p = rt.Renderer.params(W, H, args.spp, args.depth, bg, 1, out_format=rt.RT_OUT_F32)
+    out = np.empty((H, W, 3), np.float32)
+    for rnd in range(args.rounds + 1):
+        for v in variants:
+            r.set_variant(*v)
+            r.render(cam, p, out)
+            st = r.stats()
+            if rnd > 0:
+                times[v].append(st.kernel_ms)
+            used = (st.variant_features, st.slab32, st.loop)
+    for v in variants:
+        t = times[v]
+        ms = float(np.median(t))
+        print(f"slab32={v[0]} loop={v[1]}: median {ms:.2f} ms  min {min(t):.2f} ms  "
+              f"-> {W * H * args.spp / ms / 1e3:.1f} Msamples/s")
+    print("last variant features/slab32/loop:", used)
+
+
+if __name__ == "__main__":
+    main()
