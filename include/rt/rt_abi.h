@@ -171,7 +171,10 @@ typedef struct rt_stats {
     int32_t node_bytes, prim_bytes, material_bytes;
     int32_t variant_features;    /* feature set of the kernel variant launched */
     int32_t slab32;              /* 1 if the conservative f32 slab test was used */
-    int32_t loop;                /* traversal loop form (0 if-if, 1 while-while) */
+    int32_t lds_stack;           /* 1 if the traversal stack lived in LDS */
+    uint64_t cycles_camera;      /* count_work only: wave-cycles in camera-ray generation */
+    uint64_t cycles_trace;       /* count_work only: wave-cycles in traversal + hit records */
+    uint64_t cycles_shade;       /* count_work only: wave-cycles in materials / textures */
 } rt_stats;
 int rt_last_stats(rt_ctx* ctx, rt_stats* out);
 
@@ -181,9 +184,10 @@ int rt_last_stats(rt_ctx* ctx, rt_stats* out);
  * mean_rgb is height x width x 3 f32 with row 0 = bottom (y = 0). */
 int rt_write_ppm(const float* mean_rgb, int width, int height, const char* path);
 
-/* Kernel variant knobs of a context (defaults: slab32 = 1, loop = 0, or the RT_SLAB32 /
- * RT_LOOP environment variables). Results do not depend on them (tests check this). */
-int rt_ctx_set_variant(rt_ctx* ctx, int slab32, int loop);
+/* Kernel variant knobs of a context: slab32 (conservative f32 BVH slab tests) and
+ * lds_stack (traversal stack in LDS instead of scratch). Defaults, or the RT_SLAB32 /
+ * RT_LDS_STACK environment variables. Results do not depend on them (tests check this). */
+int rt_ctx_set_variant(rt_ctx* ctx, int slab32, int lds_stack);
 
 /* ---- self test ------------------------------------------------------------------------------ */
 /* Evaluates rt_numerics.h functions on the device (same fn ids as the oracle's

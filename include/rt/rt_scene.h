@@ -106,6 +106,9 @@ typedef struct rt_scene_soa {
      * kernel uses its conservative f32 slab test only when ray origins stay within 2M.
      * 0: boxes not padded, f64 slab tests only. */
     double pad_extent;
+    /* stack entries a walk of the TLAS / of the deepest instance BLAS needs (<= 32 each);
+     * 0: unknown (the kernel then uses a 64-entry scratch stack) */
+    int32_t tlas_depth, blas_depth;
     const rt_prim* prims;
     const int32_t* prim_refs;
     const rt_bvh_node* nodes;

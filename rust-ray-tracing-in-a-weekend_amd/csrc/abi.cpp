@@ -38,6 +38,9 @@ int hip_fail(hipError_t e, const char* what)
 
 size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
+// LDS stack entries per lane above which the scratch stack is used (48 KB per block)
+constexpr int kMaxLdsStack = 48;
+
 }  // namespace
 
 struct rt_world {
@@ -64,7 +67,7 @@ struct rt_ctx {
     uint32_t features = rtk::FEAT_ALL;  // of the uploaded scene
     double pad_extent = 0.0;
     int opt_slab32 = 1;                 // rt_ctx_set_variant / RT_SLAB32
-    int opt_loop = 1;                   // rt_ctx_set_variant / RT_LOOP
+    int opt_lds = 1;                    // rt_ctx_set_variant / RT_LDS_STACK
 };
 
 extern "C" {
@@ -97,10 +100,10 @@ int rt_ctx_create(int device, rt_ctx** out)
     if (!c) return fail(RT_ERR_OOM, "rt_ctx");
     c->device = device;
     if (const char* e = std::getenv("RT_SLAB32")) c->opt_slab32 = std::atoi(e) != 0;
-    if (const char* e = std::getenv("RT_LOOP")) c->opt_loop = std::atoi(e) != 0;
+    if (const char* e = std::getenv("RT_LDS_STACK")) c->opt_lds = std::atoi(e) != 0;
     hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     for (int i = 0; i < 3 && e == hipSuccess; ++i) e = hipEventCreate(&c->ev[i]);
-    if (e == hipSuccess) e = hipMalloc((void**)&c->counters, 4 * sizeof(unsigned long long));
+    if (e == hipSuccess) e = hipMalloc((void**)&c->counters, 8 * sizeof(unsigned long long));
     if (e != hipSuccess) {
         rt_ctx_destroy(c);
         return hip_fail(e, "rt_ctx_create");
@@ -459,6 +462,14 @@ int rt_ctx_upload_soa(rt_ctx* c, const rt_scene_soa* s)
     c->S.perlin_perm = (const int32_t*)(base + off[7]);
     c->S.image = (const uint8_t*)(base + off[8]);
     c->S.tlas_root = s->tlas_root;
+    // traversal stack: TLAS walk, then a nested BLAS walk (instances) above it
+    if (s->tlas_depth > 0 && s->tlas_depth <= 32 && s->blas_depth >= 0 && s->blas_depth <= 32) {
+        c->S.blas_base = s->tlas_depth;
+        c->S.stack_entries = std::max(1, s->tlas_depth + s->blas_depth);
+    } else {  // unknown depths (a foreign host's tables): the 64-entry scratch stack
+        c->S.blas_base = 32;
+        c->S.stack_entries = 64;
+    }
     c->has_scene = true;
     uint32_t feat = 0;
     for (int i = 0; i < s->n_prims; ++i) {
@@ -559,14 +570,14 @@ int rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, void* 
     rtk::LaunchOpts o;
     o.features = c->features;
     o.slab32 = c->opt_slab32 && c->pad_extent > 0.0 && cam_mag <= 2.0 * c->pad_extent;
-    o.loop = c->opt_loop;
+    o.lds_stack = c->opt_lds && c->S.stack_entries <= kMaxLdsStack;
     o.count = count;
-    if (count) HIP_TRY(hipMemsetAsync(c->counters, 0, 4 * sizeof(unsigned long long), stream));
+    if (count) HIP_TRY(hipMemsetAsync(c->counters, 0, 8 * sizeof(unsigned long long), stream));
     HIP_TRY(hipEventRecord(c->ev[0], stream));
     HIP_TRY(rtk::launch_trace(c->S, K, c->partial, c->counters, o, stream));
     c->stats.variant_features = (int32_t)rtk::variant_features(o.features);
     c->stats.slab32 = o.slab32;
-    c->stats.loop = o.loop;
+    c->stats.lds_stack = o.lds_stack;
     HIP_TRY(hipEventRecord(c->ev[1], stream));
     HIP_TRY(rtk::launch_reduce(c->partial, dev_out, p->out_format == RT_OUT_F64, n_px, n_chunks,
                                1.0 / (double)p->spp, stream));
@@ -603,13 +614,17 @@ int rt_last_stats(rt_ctx* c, rt_stats* out)
         c->stats.kernel_ms = a;
         c->stats.reduce_ms = b;
         if (c->pending_counts) {
-            unsigned long long h[4];
+            unsigned long long h[8];
             HIP_TRY(hipMemcpy(h, c->counters, sizeof h, hipMemcpyDeviceToHost));
             c->stats.casts = h[0];
             c->stats.node_visits = h[1];
             c->stats.prim_tests = h[2];
+            c->stats.cycles_camera = h[3];
+            c->stats.cycles_trace = h[4];
+            c->stats.cycles_shade = h[5];
         } else {
             c->stats.casts = c->stats.node_visits = c->stats.prim_tests = 0;
+            c->stats.cycles_camera = c->stats.cycles_trace = c->stats.cycles_shade = 0;
         }
         c->pending_stats = false;
     }
@@ -639,11 +654,11 @@ int rt_write_ppm(const float* mean, int width, int height, const char* path)
 }
 
 // ---- self test ----------------------------------------------------------------------------------
-int rt_ctx_set_variant(rt_ctx* c, int slab32, int loop)
+int rt_ctx_set_variant(rt_ctx* c, int slab32, int lds_stack)
 {
-    if (!c || slab32 < 0 || slab32 > 1 || loop < 0 || loop > 1) return fail(RT_ERR_INVALID, "bad variant");
+    if (!c || slab32 < 0 || slab32 > 1 || lds_stack < 0 || lds_stack > 1) return fail(RT_ERR_INVALID, "bad variant");
     c->opt_slab32 = slab32;
-    c->opt_loop = loop;
+    c->opt_lds = lds_stack;
     return RT_OK;
 }
 

@@ -156,6 +156,7 @@ struct Builder {
             const double saved = pad_abs;
             pad_abs = 0x1.0p-18 * (world_extent + off);
             in.child = build_bvh(items);
+            blas_depth = std::max(blas_depth, last_depth);
             pad_abs = saved;
         } else {
             err = "instance over an instance or a medium";
@@ -337,10 +338,21 @@ struct Builder {
         return node;
     }
 
+    int last_depth = 0;   // stack entries a walk of the last built BVH needs
+    int blas_depth = 0;   // max over instance BLASes
+
     int build_bvh(std::vector<Item>& items)
     {
-        if (items.empty()) return RT_LEAF_CODE((int)f.prim_refs.size(), 0);
-        return build_rec(items, 0, (int)items.size(), 0);
+        if (items.empty()) {
+            last_depth = 1;
+            return RT_LEAF_CODE((int)f.prim_refs.size(), 0);
+        }
+        const int saved = max_depth_seen;
+        max_depth_seen = 0;
+        const int root = build_rec(items, 0, (int)items.size(), 0);
+        last_depth = max_depth_seen + 1;
+        max_depth_seen = std::max(saved, max_depth_seen);
+        return root;
     }
 };
 
@@ -374,6 +386,7 @@ int flatten(World& w, int accel, std::string& err)
     }
     // instances build their BLAS while being lowered, so take M from the world's boxes first
     f.tlas_root = bld.build_bvh(top);
+    const int tlas_depth = bld.last_depth;
     f.media = w.n_media;
     // the kernel's traversal stack holds 64 entries shared by a TLAS walk and a nested BLAS walk
     if (2 * bld.max_depth_seen > 62) {
@@ -434,6 +447,8 @@ int flatten(World& w, int accel, std::string& err)
     s.accel = accel;
     s.image_bytes = (int64_t)f.image.size();
     s.pad_extent = bld.world_extent;
+    s.tlas_depth = tlas_depth;
+    s.blas_depth = bld.blas_depth;
     w.flat = std::move(f);
     FlatScene& g = w.flat;
     rt_scene_soa& t = g.soa;

@@ -66,15 +66,37 @@ struct Count {
 //   F      scene features the variant handles (trace_kernel.hpp FEAT_*); code for the
 //          others is not emitted, which keeps register pressure and code size down
 //   S32    conservative f32 slab tests (boxes padded on the host, see flatten.cpp)
-//   LOOP   0: one node-or-leaf step per iteration; 1: while-while (Aila & Laine 2009)
-//   COUNT  also count casts / node visits / primitive tests
-template <uint32_t F_, bool S32_, int LOOP_, bool COUNT_>
+//   LDS    traversal stack in LDS (interleaved per lane) instead of scratch
+//   COUNT  diagnostic: count casts / node visits / primitive tests and time the phases
+// Traversal is while-while (Aila & Laine 2009); the if-if form and a per-lane state
+// machine with ballot-gated shading both measured slower.
+template <uint32_t F_, bool S32_, bool LDS_, bool COUNT_>
 struct Cfg {
     static constexpr uint32_t F = F_;
     static constexpr bool S32 = S32_;
-    static constexpr int LOOP = LOOP_;
+    static constexpr bool LDS = LDS_;
     static constexpr bool COUNT = COUNT_;
+    static constexpr int LOOP = 1;
 };
+
+// Traversal stack. LDS: a lane-interleaved dynamic LDS array [entry][256 threads]
+// (consecutive lanes hit consecutive banks) sized per scene by the host (TLAS depth +
+// BLAS depth); scratch: a private array (deep scenes).
+template <bool LDS>
+struct Stack;
+template <>
+struct Stack<true> {
+    int* base;
+    __device__ __forceinline__ int& operator[](int i) const { return base[i * 256]; }
+};
+template <>
+struct Stack<false> {
+    int v[64];
+    __device__ __forceinline__ int& operator[](int i) { return v[i]; }
+};
+template <class C>
+using StackT = Stack<C::LDS>;
+extern __shared__ int rt_lds_stack[];
 
 __device__ __forceinline__ float f32_inv_dir(double d)
 {
@@ -343,7 +365,7 @@ constexpr int RT_DONE = (int)0x80000000;
 // tests one primitive; on a closer hit it fills best (t and sub ids) and returns true.
 template <class C, class LeafFn>
 __device__ __forceinline__ bool traverse(const SceneDev& S, int root, const Ray& r, double t_min, double t_max,
-                                         HitRef& best, int* stack, int sp0, Count& cnt, LeafFn&& leaf)
+                                         HitRef& best, StackT<C>& stack, int sp0, Count& cnt, LeafFn&& leaf)
 {
     bool any = false;
     int sp = sp0;
@@ -438,7 +460,7 @@ __device__ __forceinline__ void instance_ray(const rt_instance& in, Ray& r, doub
 // side = winning box side.
 template <class C>
 __device__ bool instance_t(const SceneDev& S, const rt_instance& in, const Ray& ray, double t_min, double t_max,
-                           HitRef& ref, int* stack, int sp0, Count& cnt)
+                           HitRef& ref, StackT<C>& stack, int sp0, Count& cnt)
 {
     Ray r = ray;
     instance_ray(in, r, nullptr, nullptr, nullptr);
@@ -492,7 +514,7 @@ __device__ void instance_finish(const SceneDev& S, const rt_instance& in, const 
 // t of a medium boundary (a simple prim or an instance).
 template <class C>
 __device__ __forceinline__ bool boundary_t(const SceneDev& S, int prim, const Ray& r, double t_min, double t_max,
-                                           double& t, int* stack, int sp0, Count& cnt)
+                                           double& t, StackT<C>& stack, int sp0, Count& cnt)
 {
     const rt_prim& p = S.prims[prim];
     if constexpr ((C::F & FEAT_INST) != 0) {
@@ -510,7 +532,7 @@ __device__ __forceinline__ bool boundary_t(const SceneDev& S, int prim, const Ra
 // ConstantMedium (hittable.rs:417-473), keyed draw instead of the in-hit thread_rng().
 template <class C>
 __device__ bool medium_t(const SceneDev& S, const rt_prim& m, const Ray& r, double t_min, double t_max, double& t,
-                         int* stack, int sp0, const Keyed& key, Count& cnt)
+                         StackT<C>& stack, int sp0, const Keyed& key, Count& cnt)
 {
     double t1, t2;
     if (!boundary_t<C>(S, m.a, r, -RT_INF, RT_INF, t1, stack, sp0, cnt)) return false;
@@ -545,7 +567,8 @@ __device__ __forceinline__ void medium_finish(const rt_prim& m, const Ray& r, do
 // hit_hittables(world, ray, 0.001, inf) (hittable.rs:43-55) over the TLAS, then the
 // HitRecord of the closest primitive.
 template <class C>
-__device__ bool trace_world(const SceneDev& S, const Ray& r, Hit& h, int* stack, const Keyed& key, Count& cnt)
+__device__ bool trace_world(const SceneDev& S, const Ray& r, Hit& h, StackT<C>& stack, const Keyed& key,
+                            Count& cnt)
 {
     const double t_min = 0.001;
     HitRef best;
@@ -556,9 +579,9 @@ __device__ bool trace_world(const SceneDev& S, const Ray& r, Hit& h, int* stack,
         const rt_prim& p = S.prims[prim];
         if constexpr ((C::F & FEAT_INST) != 0)
             if (p.kind == RT_PRIM_INSTANCE)
-                return instance_t<C>(S, S.instances[p.a], r, t_min, tmax, b, stack, 32, cnt);
+                return instance_t<C>(S, S.instances[p.a], r, t_min, tmax, b, stack, S.blas_base, cnt);
         if constexpr ((C::F & FEAT_MEDIUM) != 0)
-            if (p.kind == RT_PRIM_MEDIUM) return medium_t<C>(S, p, r, t_min, tmax, b.t, stack, 32, key, cnt);
+            if (p.kind == RT_PRIM_MEDIUM) return medium_t<C>(S, p, r, t_min, tmax, b.t, stack, S.blas_base, key, cnt);
         return simple_t<C>(p, r, t_min, tmax, b.t, b.side, cnt);
     });
     if (!hit) return false;
@@ -721,184 +744,217 @@ __device__ __forceinline__ void random_in_unit_sphere(rt_stream& st, double scal
 // ---------------------------------------------------------------------------
 // the integrator
 // ---------------------------------------------------------------------------
+
+// main.rs:517-520 + Camera::get_ray (camera.rs:58-66)
+__device__ __forceinline__ void camera_ray(const KParams& P, int x, int y, rt_stream& st, Ray& r)
+{
+    const double u = ((double)x + rnd01(st)) / ((double)P.width - 1.0);
+    const double v = ((double)y + rnd01(st)) / ((double)P.height - 1.0);
+    double dxl, dyl;
+    for (;;) {
+        dxl = rnd_m11(st, P.scale_m11);
+        dyl = rnd_m11(st, P.scale_m11);
+        if (dxl * dxl + dyl * dyl + 0.0 * 0.0 < 1.0) break;
+    }
+    const double rdx = dxl * P.cam.lens_radius, rdy = dyl * P.cam.lens_radius;
+    const double offx = P.cam.u[0] * rdx + P.cam.v[0] * rdy;
+    const double offy = P.cam.u[1] * rdx + P.cam.v[1] * rdy;
+    const double offz = P.cam.u[2] * rdx + P.cam.v[2] * rdy;
+    r.ox = P.cam.origin[0] + offx;
+    r.oy = P.cam.origin[1] + offy;
+    r.oz = P.cam.origin[2] + offz;
+    r.dx = P.cam.lower_left_corner[0] + P.cam.horizontal[0] * u + P.cam.vertical[0] * v - P.cam.origin[0] - offx;
+    r.dy = P.cam.lower_left_corner[1] + P.cam.horizontal[1] * u + P.cam.vertical[1] * v - P.cam.origin[1] - offy;
+    r.dz = P.cam.lower_left_corner[2] + P.cam.horizontal[2] * u + P.cam.vertical[2] * v - P.cam.origin[2] - offz;
+    r.time = rt_uniform_sample(rt_stream_next_u64(&st), P.cam.time0, P.scale_time);
+}
+
+// One hit of ray_color (main.rs:25-34): emitted + attenuation * (next), with the
+// recursion unrolled into the throughput T. A path carries at most one emission (a
+// DiffuseLight ends it), so adding T*e straight into the chunk sum gives the same bits
+// as the reference's per-sample sum. Returns true if the path continues with r.
+template <class C>
+__device__ __forceinline__ bool shade(const SceneDev& S, const KParams& P, const Hit& h, Ray& r, rt_stream& st,
+                                      double& Tr, double& Tg, double& Tb, double& sum_r, double& sum_g,
+                                      double& sum_b)
+{
+    const rt_material& m = S.materials[h.mat];
+    if (m.kind == RT_MAT_DIFFUSE_LIGHT) {  // material.rs:25-34 (emits on both faces, never scatters)
+        double er, eg, eb;
+        tex_value<C>(S, m.tex, h, er, eg, eb);
+        sum_r = sum_r + Tr * er;
+        sum_g = sum_g + Tg * eg;
+        sum_b = sum_b + Tb * eb;
+        return false;
+    }
+    double sdx, sdy, sdz, ar = 1.0, ag = 1.0, ab = 1.0;
+    bool scattered = true;
+    switch (m.kind) {
+    case RT_MAT_LAMBERTIAN: {  // material.rs:36-48
+        double qx, qy, qz, l2;
+        random_in_unit_sphere(st, P.scale_m11, qx, qy, qz, l2);
+        const double inv = 1.0 / __builtin_sqrt(l2);
+        sdx = h.nx + qx * inv;
+        sdy = h.ny + qy * inv;
+        sdz = h.nz + qz * inv;
+        if (__builtin_fabs(sdx) < 1e-8 && __builtin_fabs(sdy) < 1e-8 && __builtin_fabs(sdz) < 1e-8) {
+            sdx = h.nx; sdy = h.ny; sdz = h.nz;
+        }
+        tex_value<C>(S, m.tex, h, ar, ag, ab);
+        break;
+    }
+    case RT_MAT_METAL: {  // material.rs:50-60
+        const double inv = 1.0 / __builtin_sqrt(r.a);
+        const double ux = r.dx * inv, uy = r.dy * inv, uz = r.dz * inv;
+        const double k2 = 2.0 * (ux * h.nx + uy * h.ny + uz * h.nz);
+        double qx, qy, qz, l2;
+        random_in_unit_sphere(st, P.scale_m11, qx, qy, qz, l2);
+        sdx = (ux - h.nx * k2) + qx * m.fuzz;
+        sdy = (uy - h.ny * k2) + qy * m.fuzz;
+        sdz = (uz - h.nz * k2) + qz * m.fuzz;
+        scattered = sdx * h.nx + sdy * h.ny + sdz * h.nz > 0.0;
+        ar = m.albedo[0]; ag = m.albedo[1]; ab = m.albedo[2];
+        break;
+    }
+    case RT_MAT_DIELECTRIC: {  // material.rs:62-82, 89-94
+        const double ratio = h.front ? (1.0 / m.ir) : m.ir;
+        const double inv = 1.0 / __builtin_sqrt(r.a);
+        const double ux = r.dx * inv, uy = r.dy * inv, uz = r.dz * inv;
+        const double cos_theta = fmin((-ux) * h.nx + (-uy) * h.ny + (-uz) * h.nz, 1.0);
+        const double sin_theta = __builtin_sqrt(1.0 - cos_theta * cos_theta);
+        const bool cannot_refract = ratio * sin_theta > 1.0;
+        bool reflect = cannot_refract;
+        if (!reflect) {
+            double r0 = (1.0 - ratio) / (1.0 + ratio);
+            r0 = r0 * r0;
+            const double refl = r0 + (1.0 - r0) * rt_pow5(1.0 - cos_theta);
+            reflect = refl > rnd01(st);
+        }
+        if (reflect) {
+            const double k2 = 2.0 * (ux * h.nx + uy * h.ny + uz * h.nz);
+            sdx = ux - h.nx * k2;
+            sdy = uy - h.ny * k2;
+            sdz = uz - h.nz * k2;
+        } else {  // math.rs:110-117 (cos_theta recomputed there from the same inputs)
+            const double px = (ux + h.nx * cos_theta) * ratio;
+            const double py = (uy + h.ny * cos_theta) * ratio;
+            const double pz = (uz + h.nz * cos_theta) * ratio;
+            const double pl = px * px + py * py + pz * pz;
+            const double kk = -__builtin_sqrt(__builtin_fabs(1.0 - pl));
+            sdx = px + h.nx * kk;
+            sdy = py + h.ny * kk;
+            sdz = pz + h.nz * kk;
+        }
+        break;
+    }
+    default: {  // isotropic, material.rs:84-87
+        double l2;
+        random_in_unit_sphere(st, P.scale_m11, sdx, sdy, sdz, l2);
+        tex_value<C>(S, m.tex, h, ar, ag, ab);
+        break;
+    }
+    }
+    if (!scattered) return false;  // emitted (0) only
+    Tr = Tr * ar;
+    Tg = Tg * ag;
+    Tb = Tb * ab;
+    r.ox = h.px; r.oy = h.py; r.oz = h.pz;
+    r.dx = sdx; r.dy = sdy; r.dz = sdz;
+    finish_ray<C>(r);
+    return true;
+}
+
+// lane -> (chunk, pixel): a wave64 owns an 8x8 tile of one chunk
+struct LaneWork {
+    int x, y, k, chunk, s_begin, s_end;
+    uint32_t pixel;
+};
+__device__ __forceinline__ bool lane_work(const KParams& P, LaneWork& w)
+{
+    const int lane = threadIdx.x & 63;
+    const long long wave = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const long long n_tiles = (long long)P.tiles_x * P.tiles_y;
+    if (wave >= n_tiles * P.n_chunks) return false;
+    w.chunk = (int)(wave / n_tiles);
+    const int tile = (int)(wave % n_tiles);
+    w.x = (tile % P.tiles_x) * 8 + (lane & 7);
+    w.k = (tile / P.tiles_x) * 8 + (lane >> 3);
+    if (w.x >= P.width || w.k >= P.n_rows) return false;
+    w.y = P.row_begin + w.k * P.row_stride;
+    w.pixel = (uint32_t)w.y * (uint32_t)P.width + (uint32_t)w.x;
+    w.s_begin = w.chunk * P.spp_chunk;
+    w.s_end = min(P.spp, w.s_begin + P.spp_chunk);
+    return true;
+}
+
+// LOOP 0/1: every lane traces its cast to the end, then every lane shades.
 template <class C>
 __global__ void __launch_bounds__(256) trace_chunks(SceneDev S, KParams P, double* __restrict__ partial,
                                                     unsigned long long* __restrict__ counters)
 {
-    constexpr bool COUNT = C::COUNT;
-    const int lane = threadIdx.x & 63;
-    const long long wave = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    const long long n_tiles = (long long)P.tiles_x * P.tiles_y;
-    if (wave >= n_tiles * P.n_chunks) return;
-    const int chunk = (int)(wave / n_tiles);
-    const int tile = (int)(wave % n_tiles);
-    const int x = (tile % P.tiles_x) * 8 + (lane & 7);
-    const int k = (tile / P.tiles_x) * 8 + (lane >> 3);
-    if (x >= P.width || k >= P.n_rows) return;
-    const int y = P.row_begin + k * P.row_stride;
-    const uint32_t pixel = (uint32_t)y * (uint32_t)P.width + (uint32_t)x;
-    const int s_begin = chunk * P.spp_chunk;
-    const int s_end = min(P.spp, s_begin + P.spp_chunk);
-
-    int stack[64];
+    LaneWork w;
+    if (!lane_work(P, w)) return;
+    StackT<C> stack;
+    if constexpr (C::LDS) stack.base = rt_lds_stack + threadIdx.x;
     Count cnt{0, 0, 0};
+    uint64_t t_cam = 0, t_trace = 0, t_shade = 0, t_prev = 0;
+    if (C::COUNT) t_prev = __builtin_amdgcn_s_memtime();
     double sum_r = 0.0, sum_g = 0.0, sum_b = 0.0;
-    Keyed key{P.seed, pixel, 0, 0};
+    Keyed key{P.seed, w.pixel, 0, 0};
     rt_stream st;
     Ray r;
-    double Lr = 0, Lg = 0, Lb = 0, Tr = 1, Tg = 1, Tb = 1;
+    double Tr = 1, Tg = 1, Tb = 1;
     int depth = 0;
-    int s = s_begin;
+    int s = w.s_begin;
     bool new_sample = true;
-    while (s < s_end) {
-        if (new_sample) {  // main.rs:517-520 + camera.rs:58-66
+    while (s < w.s_end) {
+        if (new_sample) {
             new_sample = false;
-            rt_stream_init(&st, P.seed, pixel, (uint32_t)s, RT_STREAM_MAIN);
+            rt_stream_init(&st, P.seed, w.pixel, (uint32_t)s, RT_STREAM_MAIN);
             key.sample = (uint32_t)s;
-            const double u = ((double)x + rnd01(st)) / ((double)P.width - 1.0);
-            const double v = ((double)y + rnd01(st)) / ((double)P.height - 1.0);
-            double dxl, dyl;
-            for (;;) {
-                dxl = rnd_m11(st, P.scale_m11);
-                dyl = rnd_m11(st, P.scale_m11);
-                if (dxl * dxl + dyl * dyl + 0.0 * 0.0 < 1.0) break;
-            }
-            const double rdx = dxl * P.cam.lens_radius, rdy = dyl * P.cam.lens_radius;
-            const double offx = P.cam.u[0] * rdx + P.cam.v[0] * rdy;
-            const double offy = P.cam.u[1] * rdx + P.cam.v[1] * rdy;
-            const double offz = P.cam.u[2] * rdx + P.cam.v[2] * rdy;
-            r.ox = P.cam.origin[0] + offx;
-            r.oy = P.cam.origin[1] + offy;
-            r.oz = P.cam.origin[2] + offz;
-            r.dx = P.cam.lower_left_corner[0] + P.cam.horizontal[0] * u + P.cam.vertical[0] * v - P.cam.origin[0] - offx;
-            r.dy = P.cam.lower_left_corner[1] + P.cam.horizontal[1] * u + P.cam.vertical[1] * v - P.cam.origin[1] - offy;
-            r.dz = P.cam.lower_left_corner[2] + P.cam.horizontal[2] * u + P.cam.vertical[2] * v - P.cam.origin[2] - offz;
-            r.time = rt_uniform_sample(rt_stream_next_u64(&st), P.cam.time0, P.scale_time);
+            camera_ray(P, w.x, w.y, st, r);
             finish_ray<C>(r);
-            Lr = Lg = Lb = 0.0;
             Tr = Tg = Tb = 1.0;
             depth = P.max_depth;
         }
-        bool done = false;
-        if (depth <= 0) {  // main.rs:21-23
-            done = true;
-        } else {
+        if (C::COUNT) { const uint64_t t = __builtin_amdgcn_s_memtime(); t_cam += t - t_prev; t_prev = t; }
+        bool cont = false;
+        if (depth > 0) {  // main.rs:21-23: depth 0 is black
             key.bounce = (uint32_t)(P.max_depth - depth);
-            if (COUNT) cnt.casts++;
+            if (C::COUNT) cnt.casts++;
             Hit h;
-            if (!trace_world<C>(S, r, h, stack, key, cnt)) {  // main.rs:37
-                Lr = Lr + Tr * P.bg[0];
-                Lg = Lg + Tg * P.bg[1];
-                Lb = Lb + Tb * P.bg[2];
-                done = true;
+            const bool hit = trace_world<C>(S, r, h, stack, key, cnt);
+            if (C::COUNT) { const uint64_t t = __builtin_amdgcn_s_memtime(); t_trace += t - t_prev; t_prev = t; }
+            if (!hit) {  // main.rs:37: background
+                sum_r = sum_r + Tr * P.bg[0];
+                sum_g = sum_g + Tg * P.bg[1];
+                sum_b = sum_b + Tb * P.bg[2];
             } else {
-                const rt_material& m = S.materials[h.mat];
-                if (m.kind == RT_MAT_DIFFUSE_LIGHT) {  // material.rs:25-34
-                    double er, eg, eb;
-                    tex_value<C>(S, m.tex, h, er, eg, eb);
-                    Lr = Lr + Tr * er;
-                    Lg = Lg + Tg * eg;
-                    Lb = Lb + Tb * eb;
-                    done = true;  // DiffuseLight never scatters
-                } else {
-                    double sdx, sdy, sdz, ar = 1.0, ag = 1.0, ab = 1.0;
-                    bool scattered = true;
-                    switch (m.kind) {
-                    case RT_MAT_LAMBERTIAN: {  // material.rs:36-48
-                        double qx, qy, qz, l2;
-                        random_in_unit_sphere(st, P.scale_m11, qx, qy, qz, l2);
-                        const double inv = 1.0 / __builtin_sqrt(l2);
-                        sdx = h.nx + qx * inv;
-                        sdy = h.ny + qy * inv;
-                        sdz = h.nz + qz * inv;
-                        if (__builtin_fabs(sdx) < 1e-8 && __builtin_fabs(sdy) < 1e-8 && __builtin_fabs(sdz) < 1e-8) {
-                            sdx = h.nx; sdy = h.ny; sdz = h.nz;
-                        }
-                        tex_value<C>(S, m.tex, h, ar, ag, ab);
-                        break;
-                    }
-                    case RT_MAT_METAL: {  // material.rs:50-60
-                        const double inv = 1.0 / __builtin_sqrt(r.a);
-                        const double ux = r.dx * inv, uy = r.dy * inv, uz = r.dz * inv;
-                        const double k2 = 2.0 * (ux * h.nx + uy * h.ny + uz * h.nz);
-                        double qx, qy, qz, l2;
-                        random_in_unit_sphere(st, P.scale_m11, qx, qy, qz, l2);
-                        sdx = (ux - h.nx * k2) + qx * m.fuzz;
-                        sdy = (uy - h.ny * k2) + qy * m.fuzz;
-                        sdz = (uz - h.nz * k2) + qz * m.fuzz;
-                        scattered = sdx * h.nx + sdy * h.ny + sdz * h.nz > 0.0;
-                        ar = m.albedo[0]; ag = m.albedo[1]; ab = m.albedo[2];
-                        break;
-                    }
-                    case RT_MAT_DIELECTRIC: {  // material.rs:62-82, 89-94
-                        const double ratio = h.front ? (1.0 / m.ir) : m.ir;
-                        const double inv = 1.0 / __builtin_sqrt(r.a);
-                        const double ux = r.dx * inv, uy = r.dy * inv, uz = r.dz * inv;
-                        const double cos_theta = fmin((-ux) * h.nx + (-uy) * h.ny + (-uz) * h.nz, 1.0);
-                        const double sin_theta = __builtin_sqrt(1.0 - cos_theta * cos_theta);
-                        const bool cannot_refract = ratio * sin_theta > 1.0;
-                        bool reflect = cannot_refract;
-                        if (!reflect) {
-                            double r0 = (1.0 - ratio) / (1.0 + ratio);
-                            r0 = r0 * r0;
-                            const double refl = r0 + (1.0 - r0) * rt_pow5(1.0 - cos_theta);
-                            reflect = refl > rnd01(st);
-                        }
-                        if (reflect) {
-                            const double k2 = 2.0 * (ux * h.nx + uy * h.ny + uz * h.nz);
-                            sdx = ux - h.nx * k2;
-                            sdy = uy - h.ny * k2;
-                            sdz = uz - h.nz * k2;
-                        } else {  // math.rs:110-117
-                            const double ct = fmin((-ux) * h.nx + (-uy) * h.ny + (-uz) * h.nz, 1.0);
-                            const double px = (ux + h.nx * ct) * ratio;
-                            const double py = (uy + h.ny * ct) * ratio;
-                            const double pz = (uz + h.nz * ct) * ratio;
-                            const double pl = px * px + py * py + pz * pz;
-                            const double kk = -__builtin_sqrt(__builtin_fabs(1.0 - pl));
-                            sdx = px + h.nx * kk;
-                            sdy = py + h.ny * kk;
-                            sdz = pz + h.nz * kk;
-                        }
-                        break;
-                    }
-                    default: {  // isotropic, material.rs:84-87
-                        double l2;
-                        random_in_unit_sphere(st, P.scale_m11, sdx, sdy, sdz, l2);
-                        tex_value<C>(S, m.tex, h, ar, ag, ab);
-                        break;
-                    }
-                    }
-                    if (!scattered) {
-                        done = true;  // emitted (0) only
-                    } else {
-                        Tr = Tr * ar;
-                        Tg = Tg * ag;
-                        Tb = Tb * ab;
-                        r.ox = h.px; r.oy = h.py; r.oz = h.pz;
-                        r.dx = sdx; r.dy = sdy; r.dz = sdz;
-                        finish_ray<C>(r);
-                        depth -= 1;
-                    }
-                }
+                cont = shade<C>(S, P, h, r, st, Tr, Tg, Tb, sum_r, sum_g, sum_b);
             }
         }
-        if (done) {
-            sum_r = sum_r + Lr;
-            sum_g = sum_g + Lg;
-            sum_b = sum_b + Lb;
+        if (C::COUNT) { const uint64_t t = __builtin_amdgcn_s_memtime(); t_shade += t - t_prev; t_prev = t; }
+        if (cont) {
+            depth -= 1;
+        } else {
             s += 1;
             new_sample = true;
         }
     }
-    double* o = partial + (((size_t)chunk * P.n_rows + k) * P.width + x) * 3;
+    double* o = partial + (((size_t)w.chunk * P.n_rows + w.k) * P.width + w.x) * 3;
     o[0] = sum_r;
     o[1] = sum_g;
     o[2] = sum_b;
-    if (COUNT) {
+    if (C::COUNT) {
         atomicAdd(&counters[0], (unsigned long long)cnt.casts);
         atomicAdd(&counters[1], (unsigned long long)cnt.nodes);
         atomicAdd(&counters[2], (unsigned long long)cnt.prims);
+        // phase times are per wave (every active lane sees the same clock): one lane adds
+        if ((int)(threadIdx.x & 63) == __ffsll((long long)__ballot(1)) - 1) {
+            atomicAdd(&counters[3], (unsigned long long)t_cam);
+            atomicAdd(&counters[4], (unsigned long long)t_trace);
+            atomicAdd(&counters[5], (unsigned long long)t_shade);
+        }
     }
 }
 
@@ -954,26 +1010,27 @@ __global__ void eval_numerics(int fn, const double* x, const double* y, const do
 // ---------------------------------------------------------------------------
 // host-side launchers
 // ---------------------------------------------------------------------------
-template <uint32_t F, bool S32, int LOOP, bool COUNT>
+template <uint32_t F, bool S32, bool LDS, bool COUNT>
 static void launch_one(unsigned blocks, hipStream_t stream, const SceneDev& S, const KParams& P, double* partial,
                        unsigned long long* counters)
 {
-    hipLaunchKernelGGL((trace_chunks<Cfg<F, S32, LOOP, COUNT>>), dim3(blocks), dim3(256), 0, stream, S, P, partial,
-                       counters);
+    const size_t lds = LDS ? (size_t)S.stack_entries * 256 * sizeof(int) : 0;
+    hipLaunchKernelGGL((trace_chunks<Cfg<F, S32, LDS, COUNT>>), dim3(blocks), dim3(256), lds, stream, S, P,
+                       partial, counters);
 }
 
 // Variant table: feature set x slab precision x loop form. The launcher takes the
 // smallest feature set covering the scene.
 template <uint32_t F, bool COUNT>
-static void launch_f(int slab32, int loop, unsigned blocks, hipStream_t stream, const SceneDev& S, const KParams& P,
+static void launch_f(int slab32, int lds, unsigned blocks, hipStream_t stream, const SceneDev& S, const KParams& P,
                      double* partial, unsigned long long* counters)
 {
     if (slab32) {
-        if (loop) launch_one<F, true, 1, COUNT>(blocks, stream, S, P, partial, counters);
-        else launch_one<F, true, 0, COUNT>(blocks, stream, S, P, partial, counters);
+        if (lds) launch_one<F, true, true, COUNT>(blocks, stream, S, P, partial, counters);
+        else launch_one<F, true, false, COUNT>(blocks, stream, S, P, partial, counters);
     } else {
-        if (loop) launch_one<F, false, 1, COUNT>(blocks, stream, S, P, partial, counters);
-        else launch_one<F, false, 0, COUNT>(blocks, stream, S, P, partial, counters);
+        if (lds) launch_one<F, false, true, COUNT>(blocks, stream, S, P, partial, counters);
+        else launch_one<F, false, false, COUNT>(blocks, stream, S, P, partial, counters);
     }
 }
 
@@ -994,13 +1051,13 @@ hipError_t launch_trace(const SceneDev& S, const KParams& P, double* partial, un
     const unsigned nb = (unsigned)blocks;
     const uint32_t f = variant_features(o.features);
     if (o.count) {
-        if (f == FEAT_SET_SPHERES) launch_f<FEAT_SET_SPHERES, true>(o.slab32, o.loop, nb, stream, S, P, partial, counters);
-        else if (f == FEAT_SET_RECTINST) launch_f<FEAT_SET_RECTINST, true>(o.slab32, o.loop, nb, stream, S, P, partial, counters);
-        else launch_f<FEAT_ALL, true>(o.slab32, o.loop, nb, stream, S, P, partial, counters);
+        if (f == FEAT_SET_SPHERES) launch_f<FEAT_SET_SPHERES, true>(o.slab32, o.lds_stack, nb, stream, S, P, partial, counters);
+        else if (f == FEAT_SET_RECTINST) launch_f<FEAT_SET_RECTINST, true>(o.slab32, o.lds_stack, nb, stream, S, P, partial, counters);
+        else launch_f<FEAT_ALL, true>(o.slab32, o.lds_stack, nb, stream, S, P, partial, counters);
     } else {
-        if (f == FEAT_SET_SPHERES) launch_f<FEAT_SET_SPHERES, false>(o.slab32, o.loop, nb, stream, S, P, partial, counters);
-        else if (f == FEAT_SET_RECTINST) launch_f<FEAT_SET_RECTINST, false>(o.slab32, o.loop, nb, stream, S, P, partial, counters);
-        else launch_f<FEAT_ALL, false>(o.slab32, o.loop, nb, stream, S, P, partial, counters);
+        if (f == FEAT_SET_SPHERES) launch_f<FEAT_SET_SPHERES, false>(o.slab32, o.lds_stack, nb, stream, S, P, partial, counters);
+        else if (f == FEAT_SET_RECTINST) launch_f<FEAT_SET_RECTINST, false>(o.slab32, o.lds_stack, nb, stream, S, P, partial, counters);
+        else launch_f<FEAT_ALL, false>(o.slab32, o.lds_stack, nb, stream, S, P, partial, counters);
     }
     return hipGetLastError();
 }

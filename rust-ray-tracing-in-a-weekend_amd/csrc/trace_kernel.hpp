@@ -19,6 +19,8 @@ struct SceneDev {
     const int32_t* perlin_perm;
     const uint8_t* image;
     int32_t tlas_root;
+    int32_t blas_base;      // first stack entry of a nested (instance) BLAS walk
+    int32_t stack_entries;  // traversal stack entries per lane (TLAS + BLAS walk)
     int32_t pad;
 };
 
@@ -50,7 +52,7 @@ enum : uint32_t {
 struct LaunchOpts {
     uint32_t features;  // scene features (FEAT_*)
     int slab32;         // conservative f32 slab tests
-    int loop;           // 0 if-if, 1 while-while traversal
+    int lds_stack;      // traversal stack in LDS (1) or scratch (0)
     int count;          // count_work variant
 };
 

@@ -80,6 +80,7 @@ class SceneSoA(ctypes.Structure):
                 ("n_instances", ctypes.c_int32), ("n_materials", ctypes.c_int32), ("n_textures", ctypes.c_int32),
                 ("n_perlin", ctypes.c_int32), ("n_media", ctypes.c_int32), ("tlas_root", ctypes.c_int32),
                 ("accel", ctypes.c_int32), ("image_bytes", ctypes.c_int64), ("pad_extent", ctypes.c_double),
+                ("tlas_depth", ctypes.c_int32), ("blas_depth", ctypes.c_int32),
                 ("prims", ctypes.c_void_p), ("prim_refs", ctypes.c_void_p), ("nodes", ctypes.c_void_p),
                 ("instances", ctypes.c_void_p), ("materials", ctypes.c_void_p), ("textures", ctypes.c_void_p),
                 ("perlin_ranvec", ctypes.c_void_p), ("perlin_perm", ctypes.c_void_p),
@@ -101,7 +102,8 @@ class Stats(ctypes.Structure):
                 ("n_items", ctypes.c_uint64), ("n_chunks", ctypes.c_int32), ("spp_chunk", ctypes.c_int32),
                 ("scene_bytes", ctypes.c_int64), ("node_bytes", ctypes.c_int32), ("prim_bytes", ctypes.c_int32),
                 ("material_bytes", ctypes.c_int32), ("variant_features", ctypes.c_int32),
-                ("slab32", ctypes.c_int32), ("loop", ctypes.c_int32)]
+                ("slab32", ctypes.c_int32), ("lds_stack", ctypes.c_int32), ("cycles_camera", ctypes.c_uint64),
+                ("cycles_trace", ctypes.c_uint64), ("cycles_shade", ctypes.c_uint64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -351,8 +353,8 @@ class Renderer:
         _check(self.lib.rt_render(self.h, ctypes.byref(camera), ctypes.byref(params), ctypes.c_void_p(dev_ptr)),
                "rt_render")
 
-    def set_variant(self, slab32: int = 1, loop: int = 0):
-        _check(self.lib.rt_ctx_set_variant(self.h, slab32, loop), "rt_ctx_set_variant")
+    def set_variant(self, slab32: int = 1, lds_stack: int = 1):
+        _check(self.lib.rt_ctx_set_variant(self.h, slab32, lds_stack), "rt_ctx_set_variant")
 
     def stats(self) -> Stats:
         s = Stats()

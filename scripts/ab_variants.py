@@ -20,7 +20,7 @@ def main():
     ap.add_argument("--spp", type=int, default=500)
     ap.add_argument("--depth", type=int, default=50)
     ap.add_argument("--rounds", type=int, default=3)
-    ap.add_argument("--variants", default="0:0,1:0,0:1,1:1", help="slab32:loop pairs")
+    ap.add_argument("--variants", default="1:0,1:1,0:0,0:1", help="slab32:lds_stack pairs")
     args = ap.parse_args()
     import numpy as np
     import torch  # noqa: F401  (same HIP runtime as bench.py)
@@ -54,13 +54,22 @@ def main():
             st = r.stats()
             if rnd > 0:
                 times[v].append(st.kernel_ms)
-            used = (st.variant_features, st.slab32, st.loop)
+            used = (st.variant_features, st.slab32, st.lds_stack)
     for v in variants:
         t = times[v]
         ms = float(np.median(t))
-        print(f"slab32={v[0]} loop={v[1]}: median {ms:.2f} ms  min {min(t):.2f} ms  "
+        print(f"variant {v}: median {ms:.2f} ms  min {min(t):.2f} ms  "
               f"-> {W * H * args.spp / ms / 1e3:.1f} Msamples/s")
-    print("last variant features/slab32/loop:", used)
+    print("last variant features/slab32/lds_stack:", used)
+    # phase shares from the diagnostic count_work variant (first variant's knobs)
+    r.set_variant(*variants[0])
+    r.render(cam, rt.Renderer.params(W, H, min(args.spp, 16), args.depth, bg, 1, count_work=1))
+    st = r.stats()
+    tot = st.cycles_camera + st.cycles_trace + st.cycles_shade
+    if tot:
+        print(f"phase shares (wave-cycles): camera {st.cycles_camera / tot:.3f}  trace {st.cycles_trace / tot:.3f}  "
+              f"shade {st.cycles_shade / tot:.3f};  casts/sample {st.casts / st.samples:.3f}  "
+              f"nodes/cast {st.node_visits / max(st.casts, 1):.2f}  prims/cast {st.prim_tests / max(st.casts, 1):.2f}")
 
 
 if __name__ == "__main__":
