@@ -95,9 +95,7 @@ def main():
         if world > 1:
             dist.gather(slab, gathered if rank == 0 else None, dst=0)
             if rank == 0:
-                for r in range(world):   # rows y = r + k*world
-                    n = rt.rows_in_shard(H, r, world)
-                    frame[r::world] = gathered[r][:n]
+                rt.assemble_rows(gathered, H, world, out=frame)   # rows y = r + k*world
         else:
             frame[:] = slab[:H]
 

@@ -290,6 +290,23 @@ def rows_in_shard(height: int, row_begin: int, row_stride: int) -> int:
     return load_library().rt_rows_in_shard(height, row_begin, row_stride)
 
 
+def shard_rows(height: int, rank: int, world: int):
+    """Rows of rank `rank` in the interleaved N-way row partition (y = rank + k*world)."""
+    return list(range(rank, height, world))
+
+
+def assemble_rows(slabs, height: int, world: int, out=None):
+    """Inverse of the row partition: slabs[r] holds rank r's rows (padded to ceil(H/N)).
+    Works on numpy arrays and torch tensors alike."""
+    if out is None:
+        import numpy as _np
+        out = _np.empty((height,) + tuple(slabs[0].shape[1:]), dtype=slabs[0].dtype)
+    for r in range(world):
+        n = len(range(r, height, world))
+        out[r::world] = slabs[r][:n]
+    return out
+
+
 def write_ppm(mean_rgb: np.ndarray, path: str) -> None:
     """P3 writer with the reference's write_color semantics (math.rs:119-132)."""
     lib = load_library()

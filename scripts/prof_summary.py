@@ -19,14 +19,14 @@ import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PROF = os.path.join(REPO, "gpurun_out", "prof")
-KERNEL = "trace_chunks<false>"
+KERNEL = "trace_chunks"   # the timed variant (COUNT = false)
 
 
 def per_launch(path, kernel=KERNEL):
     vals = {}
     meta = {}
     for r in csv.DictReader(open(path)):
-        if kernel not in r["Kernel_Name"]:
+        if kernel not in r["Kernel_Name"] or "true> >" in r["Kernel_Name"]:
             continue
         vals.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
         meta = {k: r[k] for k in ("Grid_Size", "Workgroup_Size", "VGPR_Count", "SGPR_Count", "Scratch_Size",
@@ -44,7 +44,7 @@ def main():
     shutil.copy(stats, os.path.join(out, f"{tag}_kernel_stats.csv"))
     avg_ns = None
     for r in csv.DictReader(open(stats)):
-        if KERNEL in r["Name"]:
+        if KERNEL in r["Name"] and "true> >" not in r["Name"]:
             avg_ns = float(r["AverageNs"])
     counters, meta = {}, {}
     for sub in ("fetch", "write", "sq"):

@@ -173,3 +173,34 @@ def test_kernel_variants_identical(rt, renderer, scene_id, W, H):
     for im in imgs[1:]:
         assert np.array_equal(im, imgs[0])
     assert_parity(imgs[0], ob.render(scene_id, W, H, 4), f"variants scene {scene_id}")
+
+
+def _golden_cases():
+    from tests.golden import make_golden as mg
+    return mg.CASES, mg.key
+
+
+@pytest.mark.parametrize("case", _golden_cases()[0], ids=[_golden_cases()[1](c) for c in _golden_cases()[0]])
+def test_kernel_matches_committed_golden(rt, renderer, case):
+    """The committed oracle renders (tests/golden/oracle_renders.npz, make_golden.py)."""
+    import os
+    _, key = _golden_cases()
+    gold = np.load(os.path.join(os.path.dirname(__file__), "golden", "oracle_renders.npz"))[key(case)]
+    s, w, h, spp, d, ss, rs = case
+    got = gpu_render(rt, renderer, s, w, h, spp, d, ss, rs)
+    assert_parity(got, gold, key(case))
+
+
+def test_earth_matches_reference_output_on_gpu(rt, renderer):
+    """The megakernel's earth render against the reference's own earth.ppm (see test_oracle)."""
+    import os
+    from PIL import Image
+    ref = np.asarray(Image.open(os.path.join(os.path.dirname(__file__), "golden", "ref_earth_400x225.png")),
+                     dtype=np.int32)
+    img = gpu_render(rt, renderer, 3, 400, 225, 100)
+    mine = (256.0 * np.clip(np.sqrt(img[::-1]), 0.0, 0.999)).astype(np.int32)
+    bg = (256.0 * np.clip(np.sqrt(np.array([0.7, 0.8, 1.0])), 0, 0.999)).astype(np.int32)
+    sphere = np.any(mine != bg, axis=2)
+    a, b = ref[sphere].astype(float), mine[sphere].astype(float)
+    for c in range(3):
+        assert np.corrcoef(a[:, c], b[:, c])[0, 1] > 0.99

@@ -1,0 +1,68 @@
+"""The N > 1 path on CPU: world_size-2 (and 3) gloo process groups, each rank renders its
+interleaved row shard (with the CPU oracle, no GPU here), rank 0 gathers the padded slabs
+the way bench.py does over RCCL and re-interleaves them; the frame must equal the
+single-process render bit-for-bit (every draw is keyed by pixel and sample)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from tests import oracle_binding as ob
+
+W, H, SPP, SCENE = 24, 19, 3, 7
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _rank_main(rank, world, port, out_path):
+    import __graft_entry__ as ge
+    rt = ge.import_binding()
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    rows_max = (H + world - 1) // world
+    mine = ob.render(SCENE, W, H, SPP, row_begin=rank, row_stride=world, threads=1)
+    assert mine.shape[0] == rt.rows_in_shard(H, rank, world) == len(rt.shard_rows(H, rank, world))
+    slab = torch.zeros((rows_max, W, 3), dtype=torch.float64)
+    slab[: mine.shape[0]] = torch.from_numpy(mine)
+    gathered = [torch.empty_like(slab) for _ in range(world)] if rank == 0 else None
+    dist.gather(slab, gathered, dst=0)
+    if rank == 0:
+        frame = rt.assemble_rows([g.numpy() for g in gathered], H, world)
+        np.save(out_path, frame)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_row_sharded_gather_equals_single_render(tmp_path, world):
+    out = str(tmp_path / "frame.npy")
+    mp.start_processes(_rank_main, args=(world, _free_port(), out), nprocs=world, join=True, start_method="spawn")
+    frame = np.load(out)
+    full = ob.render(SCENE, W, H, SPP, threads=2)
+    assert np.array_equal(frame, full)
+
+
+def test_assemble_rows_inverse():
+    import __graft_entry__ as ge
+    rt = ge.import_binding()
+    img = np.arange(7 * 2 * 3).reshape(7, 2, 3)
+    for world in (1, 2, 3, 8):
+        rows_max = (7 + world - 1) // world
+        slabs = []
+        for r in range(world):
+            s = np.zeros((rows_max, 2, 3), img.dtype)
+            part = img[r::world]
+            s[: len(part)] = part
+            slabs.append(s)
+        assert np.array_equal(rt.assemble_rows(slabs, 7, world), img)
