@@ -172,6 +172,7 @@ typedef struct rt_stats {
     int32_t variant_features;    /* feature set of the kernel variant launched */
     int32_t slab32;              /* 1 if the conservative f32 slab test was used */
     int32_t lds_stack;           /* 1 if the traversal stack lived in LDS */
+    int32_t lds_nodes;           /* TLAS nodes kept in LDS (0: read from L1/L2) */
     uint64_t cycles_camera;      /* count_work only: wave-cycles in camera-ray generation */
     uint64_t cycles_trace;       /* count_work only: wave-cycles in traversal + hit records */
     uint64_t cycles_shade;       /* count_work only: wave-cycles in materials / textures */
@@ -184,10 +185,11 @@ int rt_last_stats(rt_ctx* ctx, rt_stats* out);
  * mean_rgb is height x width x 3 f32 with row 0 = bottom (y = 0). */
 int rt_write_ppm(const float* mean_rgb, int width, int height, const char* path);
 
-/* Kernel variant knobs of a context: slab32 (conservative f32 BVH slab tests) and
- * lds_stack (traversal stack in LDS instead of scratch). Defaults, or the RT_SLAB32 /
- * RT_LDS_STACK environment variables. Results do not depend on them (tests check this). */
-int rt_ctx_set_variant(rt_ctx* ctx, int slab32, int lds_stack);
+/* Kernel variant knobs of a context: slab32 (conservative f32 BVH slab tests),
+ * lds_stack (traversal stack in LDS instead of scratch), lds_nodes (keep the TLAS in LDS
+ * when it fits). Defaults 1/1/1, or the RT_SLAB32 / RT_LDS_STACK / RT_LDS_NODES
+ * environment variables. Results do not depend on them (tests check this). */
+int rt_ctx_set_variant(rt_ctx* ctx, int slab32, int lds_stack, int lds_nodes);
 
 /* ---- self test ------------------------------------------------------------------------------ */
 /* Evaluates rt_numerics.h functions on the device (same fn ids as the oracle's

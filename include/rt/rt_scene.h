@@ -109,6 +109,9 @@ typedef struct rt_scene_soa {
     /* stack entries a walk of the TLAS / of the deepest instance BLAS needs (<= 32 each);
      * 0: unknown (the kernel then uses a 64-entry scratch stack) */
     int32_t tlas_depth, blas_depth;
+    /* the TLAS occupies nodes[0, n_tlas_nodes) in BFS order (root = 0), so the kernel can
+     * keep it in LDS; 0: not arranged that way */
+    int32_t n_tlas_nodes, pad0;
     const rt_prim* prims;
     const int32_t* prim_refs;
     const rt_bvh_node* nodes;

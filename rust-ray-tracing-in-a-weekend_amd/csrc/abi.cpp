@@ -40,6 +40,9 @@ size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
 // LDS stack entries per lane above which the scratch stack is used (48 KB per block)
 constexpr int kMaxLdsStack = 48;
+// TLAS nodes kept in LDS (32 KB per block): the first kMaxLdsNodes in BFS order, i.e.
+// the top levels; deeper ones are read from L1/L2
+constexpr int kMaxLdsNodes = 512;
 
 }  // namespace
 
@@ -68,6 +71,8 @@ struct rt_ctx {
     double pad_extent = 0.0;
     int opt_slab32 = 1;                 // rt_ctx_set_variant / RT_SLAB32
     int opt_lds = 1;                    // rt_ctx_set_variant / RT_LDS_STACK
+    int opt_lds_nodes = 1;              // RT_LDS_NODES: keep the TLAS in LDS when it fits
+    int n_tlas_nodes = 0;
 };
 
 extern "C" {
@@ -101,6 +106,7 @@ int rt_ctx_create(int device, rt_ctx** out)
     c->device = device;
     if (const char* e = std::getenv("RT_SLAB32")) c->opt_slab32 = std::atoi(e) != 0;
     if (const char* e = std::getenv("RT_LDS_STACK")) c->opt_lds = std::atoi(e) != 0;
+    if (const char* e = std::getenv("RT_LDS_NODES")) c->opt_lds_nodes = std::atoi(e) != 0;
     hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     for (int i = 0; i < 3 && e == hipSuccess; ++i) e = hipEventCreate(&c->ev[i]);
     if (e == hipSuccess) e = hipMalloc((void**)&c->counters, 8 * sizeof(unsigned long long));
@@ -462,6 +468,7 @@ int rt_ctx_upload_soa(rt_ctx* c, const rt_scene_soa* s)
     c->S.perlin_perm = (const int32_t*)(base + off[7]);
     c->S.image = (const uint8_t*)(base + off[8]);
     c->S.tlas_root = s->tlas_root;
+    c->S.n_lds_nodes = 0;
     // traversal stack: TLAS walk, then a nested BLAS walk (instances) above it
     if (s->tlas_depth > 0 && s->tlas_depth <= 32 && s->blas_depth >= 0 && s->blas_depth <= 32) {
         c->S.blas_base = s->tlas_depth;
@@ -470,6 +477,8 @@ int rt_ctx_upload_soa(rt_ctx* c, const rt_scene_soa* s)
         c->S.blas_base = 32;
         c->S.stack_entries = 64;
     }
+    c->n_tlas_nodes = (s->n_tlas_nodes > 0 && s->n_tlas_nodes <= s->n_nodes && s->tlas_root == 0) ? s->n_tlas_nodes : 0;
+    c->S.n_tlas_nodes = c->n_tlas_nodes;
     c->has_scene = true;
     uint32_t feat = 0;
     for (int i = 0; i < s->n_prims; ++i) {
@@ -571,10 +580,14 @@ int rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, void* 
     o.features = c->features;
     o.slab32 = c->opt_slab32 && c->pad_extent > 0.0 && cam_mag <= 2.0 * c->pad_extent;
     o.lds_stack = c->opt_lds && c->S.stack_entries <= kMaxLdsStack;
+    // the TLAS in LDS (read-only, shared by the block) when it fits the per-block budget
+    rtk::SceneDev S = c->S;
+    S.n_lds_nodes = c->opt_lds_nodes ? std::min(c->n_tlas_nodes, kMaxLdsNodes) : 0;
     o.count = count;
     if (count) HIP_TRY(hipMemsetAsync(c->counters, 0, 8 * sizeof(unsigned long long), stream));
     HIP_TRY(hipEventRecord(c->ev[0], stream));
-    HIP_TRY(rtk::launch_trace(c->S, K, c->partial, c->counters, o, stream));
+    HIP_TRY(rtk::launch_trace(S, K, c->partial, c->counters, o, stream));
+    c->stats.lds_nodes = S.n_lds_nodes;
     c->stats.variant_features = (int32_t)rtk::variant_features(o.features);
     c->stats.slab32 = o.slab32;
     c->stats.lds_stack = o.lds_stack;
@@ -654,11 +667,13 @@ int rt_write_ppm(const float* mean, int width, int height, const char* path)
 }
 
 // ---- self test ----------------------------------------------------------------------------------
-int rt_ctx_set_variant(rt_ctx* c, int slab32, int lds_stack)
+int rt_ctx_set_variant(rt_ctx* c, int slab32, int lds_stack, int lds_nodes)
 {
-    if (!c || slab32 < 0 || slab32 > 1 || lds_stack < 0 || lds_stack > 1) return fail(RT_ERR_INVALID, "bad variant");
+    if (!c || slab32 < 0 || slab32 > 1 || lds_stack < 0 || lds_stack > 1 || lds_nodes < 0 || lds_nodes > 1)
+        return fail(RT_ERR_INVALID, "bad variant");
     c->opt_slab32 = slab32;
     c->opt_lds = lds_stack;
+    c->opt_lds_nodes = lds_nodes;
     return RT_OK;
 }
 

@@ -14,6 +14,7 @@
 // not lowered (RT_ERR_UNSUPPORTED); none of the reference scenes builds one.
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <numeric>
 
@@ -263,11 +264,16 @@ struct Builder {
     int max_depth_seen = 0;
     double world_extent = 0.0;  // M: max |coordinate| over the top-level items' boxes
 
+    // SAH costs (traversal step vs primitive test) and the largest leaf; RT_BVH_CI /
+    // RT_BVH_MAXLEAF override them for tuning experiments (the image does not change).
+    double c_isect = 1.5;
+    int max_leaf = 4;
+
     int build_rec(std::vector<Item>& items, int b, int e, int depth)
     {
         max_depth_seen = std::max(max_depth_seen, depth);
         const int n = e - b;
-        const double c_trav = 1.0, c_isect = 1.5;
+        const double c_trav = 1.0;
         double plo[3], phi[3];
         bounds(items, b, e, plo, phi);
         double parea = area(plo, phi);
@@ -311,7 +317,7 @@ struct Builder {
             }
         }
         double leaf_cost = c_isect * n;
-        if (n <= 4 && leaf_cost <= best_cost) return make_leaf(items, b, e);
+        if (n <= max_leaf && leaf_cost <= best_cost) return make_leaf(items, b, e);
         if (best_axis < 0) best_axis = 0, best_split = n / 2;
         return split_at(items, b, e, best_axis, best_split, depth);
     }
@@ -366,6 +372,8 @@ int flatten(World& w, int accel, std::string& err)
     }
     FlatScene f;
     Builder bld{w, f, err};
+    if (const char* e = std::getenv("RT_BVH_CI")) bld.c_isect = std::max(0.01, std::atof(e));
+    if (const char* e = std::getenv("RT_BVH_MAXLEAF")) bld.max_leaf = std::min(31, std::max(2, std::atoi(e)));
     std::vector<Item> top;
     for (int id : w.hittables) {  // M for the f32-slab padding (see to_f32_box)
         AABB b;
@@ -387,6 +395,32 @@ int flatten(World& w, int accel, std::string& err)
     // instances build their BLAS while being lowered, so take M from the world's boxes first
     f.tlas_root = bld.build_bvh(top);
     const int tlas_depth = bld.last_depth;
+    // Renumber: the TLAS's nodes first, in BFS order (the kernel copies that prefix into
+    // LDS), then every BLAS node in build order.
+    int n_tlas_nodes = 0;
+    if (f.tlas_root >= 0) {
+        std::vector<int> order, remap(f.nodes.size(), -1);
+        order.push_back(f.tlas_root);
+        for (size_t i = 0; i < order.size(); ++i)
+            for (int c : f.nodes[order[i]].child)
+                if (c >= 0) order.push_back(c);
+        n_tlas_nodes = (int)order.size();
+        for (int i = 0; i < (int)order.size(); ++i) remap[order[i]] = i;
+        int next = n_tlas_nodes;
+        for (size_t i = 0; i < f.nodes.size(); ++i)
+            if (remap[i] < 0) remap[i] = next++;
+        std::vector<rt_bvh_node> nodes(f.nodes.size());
+        for (size_t i = 0; i < f.nodes.size(); ++i) {
+            rt_bvh_node nd = f.nodes[i];
+            for (int& c : nd.child)
+                if (c >= 0) c = remap[c];
+            nodes[remap[i]] = nd;
+        }
+        f.nodes.swap(nodes);
+        f.tlas_root = remap[f.tlas_root];
+        for (rt_instance& in : f.instances)
+            if (in.child_kind == RT_CHILD_BVH && in.child >= 0) in.child = remap[in.child];
+    }
     f.media = w.n_media;
     // the kernel's traversal stack holds 64 entries shared by a TLAS walk and a nested BLAS walk
     if (2 * bld.max_depth_seen > 62) {
@@ -448,6 +482,7 @@ int flatten(World& w, int accel, std::string& err)
     s.image_bytes = (int64_t)f.image.size();
     s.pad_extent = bld.world_extent;
     s.tlas_depth = tlas_depth;
+    s.n_tlas_nodes = n_tlas_nodes;
     s.blas_depth = bld.blas_depth;
     w.flat = std::move(f);
     FlatScene& g = w.flat;

@@ -70,11 +70,13 @@ struct Count {
 //   COUNT  diagnostic: count casts / node visits / primitive tests and time the phases
 // Traversal is while-while (Aila & Laine 2009); the if-if form and a per-lane state
 // machine with ballot-gated shading both measured slower.
-template <uint32_t F_, bool S32_, bool LDS_, bool COUNT_>
+//   NALL   every TLAS node is in LDS (no per-node LDS/global choice)
+template <uint32_t F_, bool S32_, bool LDS_, bool NALL_, bool COUNT_>
 struct Cfg {
     static constexpr uint32_t F = F_;
     static constexpr bool S32 = S32_;
     static constexpr bool LDS = LDS_;
+    static constexpr bool NALL = NALL_;
     static constexpr bool COUNT = COUNT_;
     static constexpr int LOOP = 1;
 };
@@ -96,7 +98,7 @@ struct Stack<false> {
 };
 template <class C>
 using StackT = Stack<C::LDS>;
-extern __shared__ int rt_lds_stack[];
+extern __shared__ int rt_lds[];  // [stack entries x 256 lanes] [cached TLAS nodes]
 
 __device__ __forceinline__ float f32_inv_dir(double d)
 {
@@ -361,12 +363,35 @@ __device__ __forceinline__ bool slab(const float* lo, const float* hi, const Ray
 
 constexpr int RT_DONE = (int)0x80000000;
 
+// A node as four 16-B loads (ds_read_b128 from LDS, global_load_dwordx4 from L1/L2).
+struct Node {
+    float lo0[3], hi0[3], lo1[3], hi1[3];
+    int child[2];
+};
+__device__ __forceinline__ Node load_node(const rt_bvh_node* base, int i)
+{
+    const uint4* q = reinterpret_cast<const uint4*>(base + i);
+    const uint4 a = q[0], b = q[1], c = q[2], d = q[3];
+    Node n;
+    n.lo0[0] = __uint_as_float(a.x); n.lo0[1] = __uint_as_float(a.y); n.lo0[2] = __uint_as_float(a.z);
+    n.hi0[0] = __uint_as_float(a.w); n.hi0[1] = __uint_as_float(b.x); n.hi0[2] = __uint_as_float(b.y);
+    n.lo1[0] = __uint_as_float(b.z); n.lo1[1] = __uint_as_float(b.w); n.lo1[2] = __uint_as_float(c.x);
+    n.hi1[0] = __uint_as_float(c.y); n.hi1[1] = __uint_as_float(c.z); n.hi1[2] = __uint_as_float(c.w);
+    n.child[0] = (int)d.x;
+    n.child[1] = (int)d.y;
+    return n;
+}
+
 // Closest hit in a BVH (nodes + leaf ranges of prim_refs). `leaf(prim, t_max, best)`
 // tests one primitive; on a closer hit it fills best (t and sub ids) and returns true.
-template <class C, class LeafFn>
+template <class C, bool NL = false, class LeafFn>
 __device__ __forceinline__ bool traverse(const SceneDev& S, int root, const Ray& r, double t_min, double t_max,
                                          HitRef& best, StackT<C>& stack, int sp0, Count& cnt, LeafFn&& leaf)
 {
+    // NL: this is the TLAS, whose first S.n_lds_nodes nodes (BFS order) were copied into
+    // LDS at block start; deeper nodes are read from L1/L2
+    const rt_bvh_node* lds_nodes =
+        reinterpret_cast<const rt_bvh_node*>(rt_lds + (C::LDS ? S.stack_entries * 256 : 0));
     bool any = false;
     int sp = sp0;
     int cur = root;
@@ -378,7 +403,8 @@ __device__ __forceinline__ bool traverse(const SceneDev& S, int root, const Ray&
     // one node visit: test both children, continue with the nearer, push the farther
     auto visit = [&](int node) -> int {
         if (C::COUNT) cnt.nodes++;
-        const rt_bvh_node& nd = S.nodes[node];
+        const Node nd = (NL && (C::NALL || node < S.n_lds_nodes)) ? load_node(lds_nodes, node)
+                                                                  : load_node(S.nodes, node);
         bool h0, h1, near0;
         if constexpr (C::S32) {
             float tn0, tn1;
@@ -574,8 +600,7 @@ __device__ bool trace_world(const SceneDev& S, const Ray& r, Hit& h, StackT<C>& 
     HitRef best;
     best.sub = 0;
     best.side = 0;
-    const bool hit = traverse<C>(S, S.tlas_root, r, t_min, RT_INF, best, stack, 0, cnt,
-                                 [&](int prim, double tmax, HitRef& b) {
+    auto leaf = [&](int prim, double tmax, HitRef& b) {
         const rt_prim& p = S.prims[prim];
         if constexpr ((C::F & FEAT_INST) != 0)
             if (p.kind == RT_PRIM_INSTANCE)
@@ -583,7 +608,8 @@ __device__ bool trace_world(const SceneDev& S, const Ray& r, Hit& h, StackT<C>& 
         if constexpr ((C::F & FEAT_MEDIUM) != 0)
             if (p.kind == RT_PRIM_MEDIUM) return medium_t<C>(S, p, r, t_min, tmax, b.t, stack, S.blas_base, key, cnt);
         return simple_t<C>(p, r, t_min, tmax, b.t, b.side, cnt);
-    });
+    };
+    const bool hit = traverse<C, true>(S, S.tlas_root, r, t_min, RT_INF, best, stack, 0, cnt, leaf);
     if (!hit) return false;
     const rt_prim& p = S.prims[best.prim];
     if constexpr ((C::F & FEAT_INST) != 0) {
@@ -888,14 +914,38 @@ __device__ __forceinline__ bool lane_work(const KParams& P, LaneWork& w)
 }
 
 // LOOP 0/1: every lane traces its cast to the end, then every lane shades.
+#ifndef RT_MIN_WAVES_SPHERES
+#define RT_MIN_WAVES_SPHERES 1
+#endif
+#ifndef RT_MIN_WAVES_RECTINST
+#define RT_MIN_WAVES_RECTINST 4   // measured: Cornell 202 -> 190 ms (800x800x200)
+#endif
+#ifndef RT_MIN_WAVES_ALL
+#define RT_MIN_WAVES_ALL 4        // measured: final scene 255 -> 169 ms (960x540x200); 2: 239, 3: 176
+#endif
+// minimum waves per SIMD requested from the register allocator, per feature set
 template <class C>
-__global__ void __launch_bounds__(256) trace_chunks(SceneDev S, KParams P, double* __restrict__ partial,
-                                                    unsigned long long* __restrict__ counters)
+constexpr int min_waves()
 {
+    return C::F == FEAT_SET_SPHERES ? RT_MIN_WAVES_SPHERES
+           : C::F == FEAT_SET_RECTINST ? RT_MIN_WAVES_RECTINST : RT_MIN_WAVES_ALL;
+}
+
+template <class C>
+__global__ void __launch_bounds__(256, min_waves<C>()) trace_chunks(SceneDev S, KParams P, double* __restrict__ partial,
+                                                                    unsigned long long* __restrict__ counters)
+{
+    if (S.n_lds_nodes > 0) {  // every thread of the block takes part, before any early return
+        const int off = C::LDS ? S.stack_entries * 256 : 0;
+        uint4* dst = reinterpret_cast<uint4*>(rt_lds + off);
+        const uint4* src = reinterpret_cast<const uint4*>(S.nodes);
+        for (int i = threadIdx.x; i < S.n_lds_nodes * 4; i += 256) dst[i] = src[i];
+        __syncthreads();
+    }
     LaneWork w;
     if (!lane_work(P, w)) return;
     StackT<C> stack;
-    if constexpr (C::LDS) stack.base = rt_lds_stack + threadIdx.x;
+    if constexpr (C::LDS) stack.base = rt_lds + threadIdx.x;
     Count cnt{0, 0, 0};
     uint64_t t_cam = 0, t_trace = 0, t_shade = 0, t_prev = 0;
     if (C::COUNT) t_prev = __builtin_amdgcn_s_memtime();
@@ -1012,11 +1062,15 @@ __global__ void eval_numerics(int fn, const double* x, const double* y, const do
 // ---------------------------------------------------------------------------
 template <uint32_t F, bool S32, bool LDS, bool COUNT>
 static void launch_one(unsigned blocks, hipStream_t stream, const SceneDev& S, const KParams& P, double* partial,
-                       unsigned long long* counters)
+                       unsigned long long* counters, bool nall)
 {
-    const size_t lds = LDS ? (size_t)S.stack_entries * 256 * sizeof(int) : 0;
-    hipLaunchKernelGGL((trace_chunks<Cfg<F, S32, LDS, COUNT>>), dim3(blocks), dim3(256), lds, stream, S, P,
-                       partial, counters);
+    const size_t lds = (LDS ? (size_t)S.stack_entries * 256 * sizeof(int) : 0) + (size_t)S.n_lds_nodes * 64;
+    if (nall)
+        hipLaunchKernelGGL((trace_chunks<Cfg<F, S32, LDS, true, COUNT>>), dim3(blocks), dim3(256), lds, stream, S,
+                           P, partial, counters);
+    else
+        hipLaunchKernelGGL((trace_chunks<Cfg<F, S32, LDS, false, COUNT>>), dim3(blocks), dim3(256), lds, stream, S,
+                           P, partial, counters);
 }
 
 // Variant table: feature set x slab precision x loop form. The launcher takes the
@@ -1025,12 +1079,13 @@ template <uint32_t F, bool COUNT>
 static void launch_f(int slab32, int lds, unsigned blocks, hipStream_t stream, const SceneDev& S, const KParams& P,
                      double* partial, unsigned long long* counters)
 {
+    const bool nall = S.n_lds_nodes > 0 && S.n_lds_nodes == S.n_tlas_nodes;
     if (slab32) {
-        if (lds) launch_one<F, true, true, COUNT>(blocks, stream, S, P, partial, counters);
-        else launch_one<F, true, false, COUNT>(blocks, stream, S, P, partial, counters);
+        if (lds) launch_one<F, true, true, COUNT>(blocks, stream, S, P, partial, counters, nall);
+        else launch_one<F, true, false, COUNT>(blocks, stream, S, P, partial, counters, nall);
     } else {
-        if (lds) launch_one<F, false, true, COUNT>(blocks, stream, S, P, partial, counters);
-        else launch_one<F, false, false, COUNT>(blocks, stream, S, P, partial, counters);
+        if (lds) launch_one<F, false, true, COUNT>(blocks, stream, S, P, partial, counters, nall);
+        else launch_one<F, false, false, COUNT>(blocks, stream, S, P, partial, counters, nall);
     }
 }
 

@@ -21,7 +21,9 @@ struct SceneDev {
     int32_t tlas_root;
     int32_t blas_base;      // first stack entry of a nested (instance) BLAS walk
     int32_t stack_entries;  // traversal stack entries per lane (TLAS + BLAS walk)
-    int32_t pad;
+    int32_t n_lds_nodes;    // the first n TLAS nodes (BFS order, nodes[0, n)) are copied into LDS
+    int32_t n_tlas_nodes;   // TLAS size (its nodes are nodes[0, n_tlas_nodes))
+    int32_t pad2;
 };
 
 struct KParams {

@@ -19,7 +19,7 @@ from typing import Optional, Sequence
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "librtiow_amd.so")
+LIB_PATH = os.environ.get("RT_LIB_PATH", os.path.join(HERE, "lib", "librtiow_amd.so"))
 REPO = os.path.dirname(HERE)
 EARTH_JPG = os.path.join(REPO, "assets", "earthmap.jpg")
 
@@ -81,6 +81,7 @@ class SceneSoA(ctypes.Structure):
                 ("n_perlin", ctypes.c_int32), ("n_media", ctypes.c_int32), ("tlas_root", ctypes.c_int32),
                 ("accel", ctypes.c_int32), ("image_bytes", ctypes.c_int64), ("pad_extent", ctypes.c_double),
                 ("tlas_depth", ctypes.c_int32), ("blas_depth", ctypes.c_int32),
+                ("n_tlas_nodes", ctypes.c_int32), ("pad0", ctypes.c_int32),
                 ("prims", ctypes.c_void_p), ("prim_refs", ctypes.c_void_p), ("nodes", ctypes.c_void_p),
                 ("instances", ctypes.c_void_p), ("materials", ctypes.c_void_p), ("textures", ctypes.c_void_p),
                 ("perlin_ranvec", ctypes.c_void_p), ("perlin_perm", ctypes.c_void_p),
@@ -102,7 +103,8 @@ class Stats(ctypes.Structure):
                 ("n_items", ctypes.c_uint64), ("n_chunks", ctypes.c_int32), ("spp_chunk", ctypes.c_int32),
                 ("scene_bytes", ctypes.c_int64), ("node_bytes", ctypes.c_int32), ("prim_bytes", ctypes.c_int32),
                 ("material_bytes", ctypes.c_int32), ("variant_features", ctypes.c_int32),
-                ("slab32", ctypes.c_int32), ("lds_stack", ctypes.c_int32), ("cycles_camera", ctypes.c_uint64),
+                ("slab32", ctypes.c_int32), ("lds_stack", ctypes.c_int32), ("lds_nodes", ctypes.c_int32),
+                ("cycles_camera", ctypes.c_uint64),
                 ("cycles_trace", ctypes.c_uint64), ("cycles_shade", ctypes.c_uint64)]
 
     def as_dict(self):
@@ -147,7 +149,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "rt_render": ([P, ctypes.POINTER(Camera), ctypes.POINTER(RenderParams), P], I),
         "rt_rows_in_shard": ([I, I, I], I), "rt_last_stats": ([P, ctypes.POINTER(Stats)], I),
         "rt_write_ppm": ([P, I, I, ctypes.c_char_p], I),
-        "rt_device_eval": ([P, I, P, P, P, P, I], I), "rt_ctx_set_variant": ([P, I, I], I),
+        "rt_device_eval": ([P, I, P, P, P, P, I], I), "rt_ctx_set_variant": ([P, I, I, I], I),
     }
     for name, (args, res) in sigs.items():
         fn = getattr(lib, name)
@@ -370,8 +372,8 @@ class Renderer:
         _check(self.lib.rt_render(self.h, ctypes.byref(camera), ctypes.byref(params), ctypes.c_void_p(dev_ptr)),
                "rt_render")
 
-    def set_variant(self, slab32: int = 1, lds_stack: int = 1):
-        _check(self.lib.rt_ctx_set_variant(self.h, slab32, lds_stack), "rt_ctx_set_variant")
+    def set_variant(self, slab32: int = 1, lds_stack: int = 1, lds_nodes: int = 1):
+        _check(self.lib.rt_ctx_set_variant(self.h, slab32, lds_stack, lds_nodes), "rt_ctx_set_variant")
 
     def stats(self) -> Stats:
         s = Stats()

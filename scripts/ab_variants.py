@@ -20,7 +20,8 @@ def main():
     ap.add_argument("--spp", type=int, default=500)
     ap.add_argument("--depth", type=int, default=50)
     ap.add_argument("--rounds", type=int, default=3)
-    ap.add_argument("--variants", default="1:0,1:1,0:0,0:1", help="slab32:lds_stack pairs")
+    ap.add_argument("--variants", default="1:1:1,1:1:0", help="slab32:lds_stack:lds_nodes tuples")
+    ap.add_argument("--bvh", default="", help="comma list of CI:MAXLEAF BVH builds to A/B (default variant)")
     args = ap.parse_args()
     import numpy as np
     import torch  # noqa: F401  (same HIP runtime as bench.py)
@@ -54,13 +55,31 @@ def main():
             st = r.stats()
             if rnd > 0:
                 times[v].append(st.kernel_ms)
-            used = (st.variant_features, st.slab32, st.lds_stack)
+            used = (st.variant_features, st.slab32, st.lds_stack, st.lds_nodes)
     for v in variants:
         t = times[v]
         ms = float(np.median(t))
         print(f"variant {v}: median {ms:.2f} ms  min {min(t):.2f} ms  "
               f"-> {W * H * args.spp / ms / 1e3:.1f} Msamples/s")
     print("last variant features/slab32/lds_stack:", used)
+    if args.bvh:
+        builds = [tuple(x.split(":")) for x in args.bvh.split(",")]
+        bt = {b: [] for b in builds}
+        r.set_variant(*variants[0])
+        for rnd in range(args.rounds + 1):
+            for b in builds:
+                os.environ["RT_BVH_CI"], os.environ["RT_BVH_MAXLEAF"] = b
+                r.upload(world)
+                r.render(cam, p, out)
+                if rnd > 0:
+                    bt[b].append(r.stats().kernel_ms)
+        for b in builds:
+            os.environ["RT_BVH_CI"], os.environ["RT_BVH_MAXLEAF"] = b
+            soa = world.flatten()
+            print(f"bvh ci={b[0]} maxleaf={b[1]} nodes={soa.n_nodes} depth={soa.tlas_depth}/{soa.blas_depth}: "
+                  f"median {float(np.median(bt[b])):.2f} ms")
+        os.environ.pop("RT_BVH_CI"); os.environ.pop("RT_BVH_MAXLEAF")
+        r.upload(world)
     # phase shares from the diagnostic count_work variant (first variant's knobs)
     r.set_variant(*variants[0])
     r.render(cam, rt.Renderer.params(W, H, min(args.spp, 16), args.depth, bg, 1, count_work=1))

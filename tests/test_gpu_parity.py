@@ -159,17 +159,17 @@ def test_custom_world_parity_against_preset(rt, renderer):
 
 @pytest.mark.parametrize("scene_id,W,H", [(0, 48, 32), (5, 32, 32), (6, 32, 32), (7, 48, 27)])
 def test_kernel_variants_identical(rt, renderer, scene_id, W, H):
-    """The variant knobs (f32/f64 slab tests, LDS/scratch traversal stack) only change
-    speed: the image is bit-identical, and equal to the oracle's."""
+    """The variant knobs (f32/f64 slab tests, LDS/scratch traversal stack, TLAS in LDS)
+    only change speed: the image is bit-identical, and equal to the oracle's."""
     world = rt.World(1).build_scene(scene_id)
     cam, bg = rt.scene_camera(scene_id, W, H)
     renderer.upload(world)
     p = rt.Renderer.params(W, H, 4, 50, bg, 1, out_format=rt.RT_OUT_F64)
     imgs = []
-    for v in [(1, 0), (0, 0), (1, 1), (0, 1)]:
+    for v in [(1, 1, 1), (0, 0, 0), (1, 1, 0), (0, 1, 1), (1, 0, 1)]:
         renderer.set_variant(*v)
         imgs.append(renderer.render(cam, p))
-    renderer.set_variant(1, 0)
+    renderer.set_variant(1, 1, 1)
     for im in imgs[1:]:
         assert np.array_equal(im, imgs[0])
     assert_parity(imgs[0], ob.render(scene_id, W, H, 4), f"variants scene {scene_id}")
