@@ -38,6 +38,10 @@ int hip_fail(hipError_t e, const char* what)
 
 size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
+// device slots for launch params: renders queued on different streams of one context
+// may overlap up to this many in flight
+constexpr int kParamSlots = 16;
+
 // LDS stack entries per lane above which the scratch stack is used (48 KB per block)
 constexpr int kMaxLdsStack = 48;
 // TLAS nodes kept in LDS (32 KB per block): the first kMaxLdsNodes in BFS order, i.e.
@@ -63,6 +67,8 @@ struct rt_ctx {
     void* out_buf = nullptr;
     size_t out_cap = 0;
     unsigned long long* counters = nullptr;
+    rtk::KParams* params = nullptr;     // ring of kParamSlots device copies of the launch params
+    int param_slot = 0;
     hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
     bool pending_stats = false;
     bool pending_counts = false;
@@ -110,6 +116,7 @@ int rt_ctx_create(int device, rt_ctx** out)
     hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     for (int i = 0; i < 3 && e == hipSuccess; ++i) e = hipEventCreate(&c->ev[i]);
     if (e == hipSuccess) e = hipMalloc((void**)&c->counters, 8 * sizeof(unsigned long long));
+    if (e == hipSuccess) e = hipMalloc((void**)&c->params, kParamSlots * sizeof(rtk::KParams));
     if (e != hipSuccess) {
         rt_ctx_destroy(c);
         return hip_fail(e, "rt_ctx_create");
@@ -127,6 +134,7 @@ void rt_ctx_destroy(rt_ctx* c)
     (void)hipFree(c->partial);
     (void)hipFree(c->out_buf);
     (void)hipFree(c->counters);
+    (void)hipFree(c->params);
     for (auto& e : c->ev)
         if (e) (void)hipEventDestroy(e);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -585,8 +593,11 @@ int rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, void* 
     S.n_lds_nodes = c->opt_lds_nodes ? std::min(c->n_tlas_nodes, kMaxLdsNodes) : 0;
     o.count = count;
     if (count) HIP_TRY(hipMemsetAsync(c->counters, 0, 8 * sizeof(unsigned long long), stream));
+    rtk::KParams* dK = c->params + c->param_slot;
+    c->param_slot = (c->param_slot + 1) % kParamSlots;
+    HIP_TRY(hipMemcpyAsync(dK, &K, sizeof K, hipMemcpyHostToDevice, stream));
     HIP_TRY(hipEventRecord(c->ev[0], stream));
-    HIP_TRY(rtk::launch_trace(S, K, c->partial, c->counters, o, stream));
+    HIP_TRY(rtk::launch_trace(S, K, dK, c->partial, c->counters, o, stream));
     c->stats.lds_nodes = S.n_lds_nodes;
     c->stats.variant_features = (int32_t)rtk::variant_features(o.features);
     c->stats.slab32 = o.slab32;

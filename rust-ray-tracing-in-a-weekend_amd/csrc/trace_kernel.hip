@@ -931,10 +931,14 @@ constexpr int min_waves()
            : C::F == FEAT_SET_RECTINST ? RT_MIN_WAVES_RECTINST : RT_MIN_WAVES_ALL;
 }
 
+// KParams comes by pointer: read where used (scalar loads) instead of pinning ~70 SGPRs
+// for the whole kernel (by value it spilled SGPRs into VGPR lanes).
 template <class C>
-__global__ void __launch_bounds__(256, min_waves<C>()) trace_chunks(SceneDev S, KParams P, double* __restrict__ partial,
+__global__ void __launch_bounds__(256, min_waves<C>()) trace_chunks(SceneDev S, const KParams* __restrict__ Pp,
+                                                                    double* __restrict__ partial,
                                                                     unsigned long long* __restrict__ counters)
 {
+    const KParams& P = *Pp;
     if (S.n_lds_nodes > 0) {  // every thread of the block takes part, before any early return
         const int off = C::LDS ? S.stack_entries * 256 : 0;
         uint4* dst = reinterpret_cast<uint4*>(rt_lds + off);
@@ -1061,7 +1065,7 @@ __global__ void eval_numerics(int fn, const double* x, const double* y, const do
 // host-side launchers
 // ---------------------------------------------------------------------------
 template <uint32_t F, bool S32, bool LDS, bool COUNT>
-static void launch_one(unsigned blocks, hipStream_t stream, const SceneDev& S, const KParams& P, double* partial,
+static void launch_one(unsigned blocks, hipStream_t stream, const SceneDev& S, const KParams* P, double* partial,
                        unsigned long long* counters, bool nall)
 {
     const size_t lds = (LDS ? (size_t)S.stack_entries * 256 * sizeof(int) : 0) + (size_t)S.n_lds_nodes * 64;
@@ -1076,7 +1080,7 @@ static void launch_one(unsigned blocks, hipStream_t stream, const SceneDev& S, c
 // Variant table: feature set x slab precision x loop form. The launcher takes the
 // smallest feature set covering the scene.
 template <uint32_t F, bool COUNT>
-static void launch_f(int slab32, int lds, unsigned blocks, hipStream_t stream, const SceneDev& S, const KParams& P,
+static void launch_f(int slab32, int lds, unsigned blocks, hipStream_t stream, const SceneDev& S, const KParams* P,
                      double* partial, unsigned long long* counters)
 {
     const bool nall = S.n_lds_nodes > 0 && S.n_lds_nodes == S.n_tlas_nodes;
@@ -1096,10 +1100,10 @@ uint32_t variant_features(uint32_t scene_features)
     return FEAT_ALL;
 }
 
-hipError_t launch_trace(const SceneDev& S, const KParams& P, double* partial, unsigned long long* counters,
-                        const LaunchOpts& o, hipStream_t stream)
+hipError_t launch_trace(const SceneDev& S, const KParams& Ph, const KParams* P, double* partial,
+                        unsigned long long* counters, const LaunchOpts& o, hipStream_t stream)
 {
-    const long long waves = (long long)P.tiles_x * P.tiles_y * P.n_chunks;
+    const long long waves = (long long)Ph.tiles_x * Ph.tiles_y * Ph.n_chunks;
     const long long blocks = (waves + 3) / 4;
     if (blocks <= 0) return hipSuccess;
     if (blocks > 0x7fffffffLL) return hipErrorInvalidValue;

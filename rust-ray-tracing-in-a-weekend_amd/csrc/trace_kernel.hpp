@@ -59,8 +59,9 @@ struct LaunchOpts {
 };
 
 uint32_t variant_features(uint32_t scene_features);
-hipError_t launch_trace(const SceneDev& S, const KParams& P, double* partial, unsigned long long* counters,
-                        const LaunchOpts& o, hipStream_t stream);
+// Ph: host copy of the params (grid size); P: the same params in device memory
+hipError_t launch_trace(const SceneDev& S, const KParams& Ph, const KParams* P, double* partial,
+                        unsigned long long* counters, const LaunchOpts& o, hipStream_t stream);
 hipError_t launch_reduce(const double* partial, void* out, bool f64, long long n_px, int n_chunks, double scale,
                          hipStream_t stream);
 hipError_t launch_eval(int fn, const double* x, const double* y, const double* z, double* out, int n,
