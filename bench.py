@@ -31,23 +31,41 @@ HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 CPU_BASELINE_CORES = 16        # the GPU box's CPU share per GPU
 
 
+# BASELINE.json configs (SURVEY §8 shorthand). The headline metric is C2; the others are
+# reachable for measurement with --config (C4/C5 are quoted on 8 GPUs).
+CONFIGS = {
+    "C1": dict(scene=0, width=1200, height=800, spp=10, depth=8),
+    "C2": dict(scene=0, width=1200, height=800, spp=500, depth=50),
+    "C3": dict(scene=5, width=800, height=800, spp=1000, depth=50),
+    "C4": dict(scene=7, width=1920, height=1080, spp=1000, depth=50),
+    "C5": dict(scene=0, width=4096, height=4096, spp=4096, depth=50),
+}
+SCENE_NAMES = {0: "random_scene (main.rs:245-289)", 5: "cornell_box_scene (main.rs:107-136)",
+               7: "final_scene (main.rs:173-243)"}
+
+
 def parse():
     ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="C2", choices=sorted(CONFIGS), help="BASELINE.json config preset")
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--scene", type=int, default=0)
-    ap.add_argument("--width", type=int, default=1200)
-    ap.add_argument("--height", type=int, default=800)
-    ap.add_argument("--spp", type=int, default=500)
-    ap.add_argument("--depth", type=int, default=50)
+    ap.add_argument("--scene", type=int, default=None)
+    ap.add_argument("--width", type=int, default=None)
+    ap.add_argument("--height", type=int, default=None)
+    ap.add_argument("--spp", type=int, default=None)
+    ap.add_argument("--depth", type=int, default=None)
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--count-spp", type=int, default=16, help="spp of the untimed count_work pass")
     ap.add_argument("--no-count", action="store_true", help="skip the count_work pass (profiling runs)")
     ap.add_argument("--ppm", default="", help="write the rendered frame (rank 0) as a P3 PPM")
-    return ap.parse_args()
+    args = ap.parse_args()
+    for k, v in CONFIGS[args.config].items():
+        if getattr(args, k) is None:
+            setattr(args, k, v)
+    return args
 
 
 def main():
@@ -173,7 +191,8 @@ def main():
 
     if rank == 0:
         out = {
-            "metric": "Msamples/s (pixels x spp) for 1200x800 random-spheres scene",
+            "metric": ("Msamples/s (pixels x spp) for 1200x800 random-spheres scene" if args.config == "C2"
+                       else "Msamples/s (pixels x spp), %s" % args.config),
             "value": round(value, 3),
             "unit": "Msamples/s",
             "n_gpus": world,
@@ -185,8 +204,9 @@ def main():
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (seeded scene builders, scene_seed=render_seed=%d)" % args.seed,
-            "config": {"workload": "random_scene (main.rs:245-289) %dx%d, %d spp, max depth %d, row-sharded over %d GPU"
-                                   % (W, H, spp, depth, world),
+            "config": {"workload": "%s %s %dx%d, %d spp, max depth %d, row-sharded over %d GPU"
+                                   % (args.config, SCENE_NAMES.get(args.scene, "scene %d" % args.scene), W, H, spp,
+                                      depth, world),
                        "scene": args.scene, "width": W, "height": H, "spp": spp, "max_depth": depth,
                        "parallelism": "rows interleaved over %d rank(s), RCCL gather" % world},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
