@@ -129,7 +129,7 @@ int rt_scene_camera(int scene_id, int width, int height, rt_camera* cam_out, dou
 
 /* ---- lowering + upload ---------------------------------------------------------------- */
 /* Flattens the world into SoA tables owned by the world (valid until the next
- * flatten or rt_world_destroy). accel: RT_ACCEL_SAH. */
+ * flatten or rt_world_destroy). accel: RT_ACCEL_SAH / _LINEAR / _MEDIAN (rt_scene.h). */
 int rt_world_flatten(rt_world* w, int accel, const rt_scene_soa** soa_out);
 int rt_ctx_upload_soa(rt_ctx* ctx, const rt_scene_soa* soa);
 int rt_ctx_upload_world(rt_ctx* ctx, rt_world* w, int accel);

@@ -123,7 +123,15 @@ typedef struct rt_scene_soa {
     const uint8_t* image_data;
 } rt_scene_soa;
 
-enum { RT_ACCEL_SAH = 0 };
+/* Acceleration structure the flattener builds. The image does not depend
+ * on it (closest hit is independent of the hierarchy); only the traversal cost does.
+ *   SAH    : full-sweep SAH BVHs over the dissolved reference BvhNodes (default, fastest)
+ *   LINEAR : every list scanned in order, as hit_hittables (hittable.rs:31-41) does:
+ *            a chain of unbounded nodes over <=31-primitive leaves
+ *   MEDIAN : the reference's own hierarchy: each BvhNode (hittable.rs:77-130, random
+ *            axis + median split as drawn by the scene builder) kept as a node, the
+ *            top-level list scanned in order */
+enum { RT_ACCEL_SAH = 0, RT_ACCEL_LINEAR = 1, RT_ACCEL_MEDIAN = 2 };
 
 /* Camera::new output (camera.rs:4-15). */
 typedef struct rt_camera {

@@ -12,6 +12,10 @@
 //                                                     hidden prim (sphere / box / instance)
 // The top-level list becomes the TLAS. A medium or an instance below an instance is
 // not lowered (RT_ERR_UNSUPPORTED); none of the reference scenes builds one.
+//
+// accel (rt_scene.h) picks the hierarchy: SAH (above), LINEAR (every list a chain of
+// unbounded nodes over <=31-prim leaves, in list order: hit_hittables' linear scan), or
+// MEDIAN (the reference's BvhNodes kept node for node, the top-level list a chain).
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
@@ -26,7 +30,8 @@ namespace rtw {
 namespace {
 
 struct Item {
-    int prim;
+    int prim;   // >= 0: a primitive; -1: a prebuilt subtree (MEDIAN mode), see ref
+    int ref;
     double lo[3], hi[3];
     double c[3];
 };
@@ -35,6 +40,7 @@ struct Builder {
     World& w;
     FlatScene& f;
     std::string& err;
+    int accel = RT_ACCEL_SAH;
 
     int add_prim(const rt_prim& p)
     {
@@ -111,6 +117,7 @@ struct Builder {
     {
         Item it;
         it.prim = prim;
+        it.ref = 0;
         AABB b;
         w.bounding_box(hid, 0.0, 1.0, b);
         it.lo[0] = b.minimum.x; it.lo[1] = b.minimum.y; it.lo[2] = b.minimum.z;
@@ -142,13 +149,6 @@ struct Builder {
             in.child_kind = RT_CHILD_PRIM;
             in.child = lower_simple(cur);
         } else if (child.kind == HKind::BvhNode) {
-            std::vector<int> leaves;
-            if (!collect_simple(cur, leaves)) {
-                err = "instance over a BVH that contains an instance or a medium";
-                return RT_ERR_UNSUPPORTED;
-            }
-            std::vector<Item> items;
-            for (int hid : leaves) items.push_back(item_of(lower_simple(hid), hid));
             in.child_kind = RT_CHILD_BVH;
             double off = 0.0;  // object-space origins: |o_obj| <= |o_world| + sum |offsets|
             for (int i = 0; i < in.n_ops; ++i)
@@ -156,9 +156,22 @@ struct Builder {
                     off += std::sqrt(in.op[i][0] * in.op[i][0] + in.op[i][1] * in.op[i][1] + in.op[i][2] * in.op[i][2]);
             const double saved = pad_abs;
             pad_abs = 0x1.0p-18 * (world_extent + off);
-            in.child = build_bvh(items);
-            blas_depth = std::max(blas_depth, last_depth);
+            if (accel == RT_ACCEL_MEDIAN) {
+                int rc = RT_OK;
+                in.child = lower_ref_bvh(cur, /*in_instance=*/true, rc);
+                if (rc) return rc;
+            } else {
+                std::vector<int> leaves;
+                if (!collect_simple(cur, leaves)) {
+                    err = "instance over a BVH that contains an instance or a medium";
+                    return RT_ERR_UNSUPPORTED;
+                }
+                std::vector<Item> items;
+                for (int hid : leaves) items.push_back(item_of(lower_simple(hid), hid));
+                in.child = build_bvh(items);
+            }
             pad_abs = saved;
+            blas_depth = std::max(blas_depth, stack_need(in.child) + 1);
         } else {
             err = "instance over an instance or a medium";
             return RT_ERR_UNSUPPORTED;
@@ -183,11 +196,59 @@ struct Builder {
         return RT_ERR_UNSUPPORTED;
     }
 
+    // MEDIAN mode: a reference BvhNode subtree lowered node for node (both child boxes from
+    // bounding_box, hittable.rs:118-130); a non-BVH child becomes a one-primitive leaf.
+    // A span-1 node (left == right, :100-102) tests the same leaf twice, as the reference does.
+    int lower_ref_bvh(int id, bool in_instance, int& rc)
+    {
+        const HNode& h = w.nodes[id];
+        if (h.kind != HKind::BvhNode) {
+            int prim = -1;
+            if (is_simple(h.kind)) {
+                prim = lower_simple(id);
+            } else if (in_instance) {
+                err = "instance over a BVH that contains an instance or a medium";
+                rc = RT_ERR_UNSUPPORTED;
+                return 0;
+            } else {
+                std::vector<Item> one;
+                rc = lower_top(id, one);
+                if (rc) return 0;
+                prim = one[0].prim;
+            }
+            const int first = (int)f.prim_refs.size();
+            f.prim_refs.push_back(prim);
+            return RT_LEAF_CODE(first, 1);
+        }
+        const int node = (int)f.nodes.size();
+        f.nodes.emplace_back();
+        const int lc = lower_ref_bvh(h.left, in_instance, rc);
+        if (rc) return 0;
+        const int rc_ref = h.right == h.left ? lc : lower_ref_bvh(h.right, in_instance, rc);
+        if (rc) return 0;
+        const Item li = item_of(-1, h.left), ri = item_of(-1, h.right);
+        rt_bvh_node& nd = f.nodes[node];
+        std::memset(&nd, 0, sizeof nd);
+        to_f32_box(li.lo, li.hi, nd.lo0, nd.hi0);
+        to_f32_box(ri.lo, ri.hi, nd.lo1, nd.hi1);
+        nd.child[0] = lc;
+        nd.child[1] = rc_ref;
+        return node;
+    }
+
     int lower_top(int id, std::vector<Item>& items)
     {
         const HNode& h = w.nodes[id];
         switch (h.kind) {
         case HKind::BvhNode: {
+            if (accel == RT_ACCEL_MEDIAN) {
+                int rc = RT_OK;
+                Item it = item_of(-1, id);
+                it.ref = lower_ref_bvh(id, false, rc);
+                if (rc) return rc;
+                items.push_back(it);
+                return RT_OK;
+            }
             int rc = lower_top(h.left, items);
             if (rc) return rc;
             if (h.right != h.left) return lower_top(h.right, items);
@@ -261,7 +322,6 @@ struct Builder {
         return RT_LEAF_CODE(first, e - b);
     }
 
-    int max_depth_seen = 0;
     double world_extent = 0.0;  // M: max |coordinate| over the top-level items' boxes
 
     // SAH costs (traversal step vs primitive test) and the largest leaf; RT_BVH_CI /
@@ -271,7 +331,6 @@ struct Builder {
 
     int build_rec(std::vector<Item>& items, int b, int e, int depth)
     {
-        max_depth_seen = std::max(max_depth_seen, depth);
         const int n = e - b;
         const double c_trav = 1.0;
         double plo[3], phi[3];
@@ -344,21 +403,75 @@ struct Builder {
         return node;
     }
 
-    int last_depth = 0;   // stack entries a walk of the last built BVH needs
     int blas_depth = 0;   // max over instance BLASes
+
+    // LINEAR / MEDIAN: the list in order. Runs of primitives become <=31-prim leaves, a
+    // subtree stays a child; node k = (segment k, node k+1), both boxes unbounded, so the
+    // slab tests return t_near = t_min for both and the walk always takes segment k first
+    // (list order) with the rest of the chain as its one stack entry.
+    int build_chain(std::vector<Item>& items)
+    {
+        std::vector<int> segs;
+        for (size_t i = 0; i < items.size();) {
+            if (items[i].prim < 0) {
+                segs.push_back(items[i].ref);
+                ++i;
+                continue;
+            }
+            size_t j = i;
+            while (j < items.size() && items[j].prim >= 0 && j - i < 31) ++j;
+            segs.push_back(make_leaf(items, (int)i, (int)j));
+            i = j;
+        }
+        if (segs.empty()) return RT_LEAF_CODE((int)f.prim_refs.size(), 0);
+        if (segs.size() == 1) return segs[0];
+        const int base = (int)f.nodes.size(), n = (int)segs.size() - 1;
+        f.nodes.resize(base + n);
+        for (int k = 0; k < n; ++k) {
+            rt_bvh_node& nd = f.nodes[base + k];
+            std::memset(&nd, 0, sizeof nd);
+            for (int a = 0; a < 3; ++a) {
+                nd.lo0[a] = nd.lo1[a] = -INFINITY;
+                nd.hi0[a] = nd.hi1[a] = INFINITY;
+            }
+            nd.child[0] = segs[k];
+            nd.child[1] = k + 1 < n ? base + k + 1 : segs[n];
+        }
+        return base;
+    }
+
+    // Stack entries a walk from ref can need (the kernel's visit pushes the farther child
+    // when both are hit). With two identical child boxes both t_near are equal and child 0
+    // is always taken first, so only it stacks on top of the pushed child 1.
+    int stack_need(int ref) const
+    {
+        if (ref < 0) return 0;
+        std::vector<int> need(f.nodes.size(), -1);
+        std::vector<int> todo{ref};  // iterative post-order (a LINEAR chain can be long)
+        while (!todo.empty()) {
+            const int i = todo.back();
+            const rt_bvh_node& nd = f.nodes[i];
+            bool ready = true;
+            for (int c : nd.child)
+                if (c >= 0 && need[c] < 0) {
+                    todo.push_back(c);
+                    ready = false;
+                }
+            if (!ready) continue;
+            todo.pop_back();
+            auto nc = [&](int c) { return c < 0 ? 0 : need[c]; };
+            const bool same = std::memcmp(nd.lo0, nd.lo1, 12) == 0 && std::memcmp(nd.hi0, nd.hi1, 12) == 0;
+            need[i] = same ? std::max(1 + nc(nd.child[0]), nc(nd.child[1]))
+                           : 1 + std::max(nc(nd.child[0]), nc(nd.child[1]));
+        }
+        return need[ref];
+    }
 
     int build_bvh(std::vector<Item>& items)
     {
-        if (items.empty()) {
-            last_depth = 1;
-            return RT_LEAF_CODE((int)f.prim_refs.size(), 0);
-        }
-        const int saved = max_depth_seen;
-        max_depth_seen = 0;
-        const int root = build_rec(items, 0, (int)items.size(), 0);
-        last_depth = max_depth_seen + 1;
-        max_depth_seen = std::max(saved, max_depth_seen);
-        return root;
+        if (accel != RT_ACCEL_SAH) return build_chain(items);
+        if (items.empty()) return RT_LEAF_CODE((int)f.prim_refs.size(), 0);
+        return build_rec(items, 0, (int)items.size(), 0);
     }
 };
 
@@ -366,12 +479,13 @@ struct Builder {
 
 int flatten(World& w, int accel, std::string& err)
 {
-    if (accel != RT_ACCEL_SAH) {
+    if (accel != RT_ACCEL_SAH && accel != RT_ACCEL_LINEAR && accel != RT_ACCEL_MEDIAN) {
         err = "unknown accel mode";
         return RT_ERR_INVALID;
     }
     FlatScene f;
     Builder bld{w, f, err};
+    bld.accel = accel;
     if (const char* e = std::getenv("RT_BVH_CI")) bld.c_isect = std::max(0.01, std::atof(e));
     if (const char* e = std::getenv("RT_BVH_MAXLEAF")) bld.max_leaf = std::min(31, std::max(2, std::atoi(e)));
     std::vector<Item> top;
@@ -394,7 +508,12 @@ int flatten(World& w, int accel, std::string& err)
     }
     // instances build their BLAS while being lowered, so take M from the world's boxes first
     f.tlas_root = bld.build_bvh(top);
-    const int tlas_depth = bld.last_depth;
+    const int tlas_depth = bld.stack_need(f.tlas_root) + 1;
+    // the kernel's traversal stack: a TLAS walk, and a nested BLAS walk above it (<= 32 each)
+    if (tlas_depth > 32 || bld.blas_depth > 32) {
+        err = "BVH too deep for the kernel's traversal stack";
+        return RT_ERR_UNSUPPORTED;
+    }
     // Renumber: the TLAS's nodes first, in BFS order (the kernel copies that prefix into
     // LDS), then every BLAS node in build order.
     int n_tlas_nodes = 0;
@@ -422,11 +541,6 @@ int flatten(World& w, int accel, std::string& err)
             if (in.child_kind == RT_CHILD_BVH && in.child >= 0) in.child = remap[in.child];
     }
     f.media = w.n_media;
-    // the kernel's traversal stack holds 64 entries shared by a TLAS walk and a nested BLAS walk
-    if (2 * bld.max_depth_seen > 62) {
-        err = "BVH too deep for the kernel's 64-entry traversal stack";
-        return RT_ERR_UNSUPPORTED;
-    }
 
     for (const Material& m : w.materials) {
         rt_material rm;

@@ -33,6 +33,8 @@ SCENES_NEEDING_IMAGE = (3, 7)
 
 RT_OUT_F32, RT_OUT_F64 = 0, 1
 RT_ACCEL_SAH = 0
+RT_ACCEL_LINEAR = 1     # hit_hittables linear scan (hittable.rs:31-41)
+RT_ACCEL_MEDIAN = 2     # the reference BvhNode hierarchy (hittable.rs:77-130)
 
 # every symbol include/rt/rt_abi.h declares
 EXPORTED = [
@@ -393,12 +395,12 @@ class Renderer:
 def render_scene(scene_id: int, width: int, height: int, spp: int, max_depth: int = 50, scene_seed: int = 1,
                  render_seed: int = 1, row_begin: int = 0, row_stride: int = 1, out_format: int = RT_OUT_F32,
                  spp_chunk: int = 0, device: int = 0, renderer: Optional[Renderer] = None,
-                 image: Optional[np.ndarray] = None):
+                 image: Optional[np.ndarray] = None, accel: int = RT_ACCEL_SAH):
     """One-call path: build the preset scene, upload, render the row shard. Returns (image, stats)."""
     world = World(scene_seed).build_scene(scene_id, image)
     cam, bg = scene_camera(scene_id, width, height)
     r = renderer or Renderer(device)
-    r.upload(world)
+    r.upload(world, accel)
     p = Renderer.params(width, height, spp, max_depth, bg, render_seed, row_begin, row_stride, spp_chunk,
                         out_format)
     img = r.render(cam, p)

@@ -60,6 +60,76 @@ def test_flatten_all_scenes(rt, scene_id):
         assert soa.n_media == 2 and soa.n_instances == 2
 
 
+NODE_DT = np.dtype([("lo0", "<f4", 3), ("hi0", "<f4", 3), ("lo1", "<f4", 3), ("hi1", "<f4", 3),
+                    ("child", "<i4", 2), ("pad", "<i4", 2)])
+
+
+def soa_tables(soa):
+    def arr(ptr, dtype, n):
+        if n == 0:
+            return np.zeros(0, dtype)
+        buf = (ctypes.c_char * (n * np.dtype(dtype).itemsize)).from_address(ptr)
+        return np.frombuffer(bytes(buf), dtype=dtype)
+    prims = arr(soa.prims, np.dtype((np.void, 96)), soa.n_prims)
+    refs = arr(soa.prim_refs, "<i4", soa.n_prim_refs)
+    nodes = arr(soa.nodes, NODE_DT, soa.n_nodes)
+    inst = arr(soa.instances, np.dtype([("n_ops", "<i4"), ("kind", "<i4"), ("child", "<i4"), ("rest", "V116")]),
+               soa.n_instances)
+    return prims, refs, nodes, inst
+
+
+def leaf_prims(code, refs):
+    code = ~code
+    return refs[(code >> 5):(code >> 5) + (code & 31)].tolist()
+
+
+def reachable(root, refs, nodes):
+    """Multiset of the primitives a full walk from a root reference tests."""
+    out, todo = [], [root]
+    while todo:
+        r = todo.pop()
+        if r < 0:
+            out.extend(leaf_prims(r, refs))
+        else:
+            todo.extend(nodes[r]["child"].tolist())
+    return out
+
+
+@pytest.mark.parametrize("scene_id", range(8))
+def test_accel_modes_cover_the_same_primitives(rt, scene_id):
+    """LINEAR (hit_hittables' scan) and MEDIAN (the reference BvhNodes) lower the
+    same primitive table as SAH; every primitive is reachable in every mode; LINEAR is a chain
+    of unbounded nodes whose leaves come in list order; the recorded stack needs fit."""
+    tabs, walks = {}, {}
+    world = rt.World(1).build_scene(scene_id)      # owns the tables until the next flatten
+    for accel in (rt.RT_ACCEL_SAH, rt.RT_ACCEL_LINEAR, rt.RT_ACCEL_MEDIAN):
+        soa = rt.SceneSoA.from_buffer_copy(world.flatten(accel))   # the view is reused by the next flatten
+        assert soa.accel == accel
+        prims, refs, nodes, inst = soa_tables(soa)
+        tabs[accel] = (prims, refs, nodes, soa)
+        walk = reachable(soa.tlas_root, refs, nodes)
+        for i in inst:
+            if i["kind"] == 1:
+                walk += reachable(int(i["child"]), refs, nodes)
+        walks[accel] = walk
+        assert 1 <= soa.tlas_depth <= 32 and 0 <= soa.blas_depth <= 32
+    p0 = tabs[rt.RT_ACCEL_SAH][0]
+    for accel in (rt.RT_ACCEL_LINEAR, rt.RT_ACCEL_MEDIAN):
+        assert np.array_equal(tabs[accel][0], p0)            # identical primitive table
+        assert set(walks[accel]) == set(walks[rt.RT_ACCEL_SAH])
+    assert sorted(walks[rt.RT_ACCEL_LINEAR]) == sorted(walks[rt.RT_ACCEL_SAH])   # each exactly once
+    _, refs, nodes, soa = tabs[rt.RT_ACCEL_LINEAR]
+    if soa.n_nodes:
+        assert np.all(np.isinf(nodes["lo0"])) and np.all(np.isinf(nodes["hi1"]))
+        assert soa.tlas_depth == 2                           # a chain needs one stack entry
+    order, r = [], soa.tlas_root                             # child 0 first = list order
+    while r >= 0:
+        c0, r = nodes[r]["child"].tolist()
+        order += leaf_prims(c0, refs)
+    order += leaf_prims(r, refs)
+    assert order == sorted(order)
+
+
 @pytest.mark.parametrize("scene_id,w,h", [(0, 1200, 800), (5, 800, 800), (7, 1920, 1080), (4, 64, 36)])
 def test_camera_matches_oracle_bitwise(rt, scene_id, w, h):
     cam, _ = rt.scene_camera(scene_id, w, h)

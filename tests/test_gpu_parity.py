@@ -204,3 +204,30 @@ def test_earth_matches_reference_output_on_gpu(rt, renderer):
     a, b = ref[sphere].astype(float), mine[sphere].astype(float)
     for c in range(3):
         assert np.corrcoef(a[:, c], b[:, c])[0, 1] > 0.99
+
+
+@pytest.mark.parametrize("scene_id,W,H", [(0, 40, 24), (5, 24, 24), (6, 24, 24), (7, 32, 18)])
+def test_accel_modes_render_identically(rt, renderer, scene_id, W, H):
+    """the LINEAR (hit_hittables scan) and MEDIAN (reference BvhNode) hierarchies
+    give the SAH image bit for bit (closest hit does not depend on the hierarchy), and all
+    three match the oracle, which walks the reference's own median BVH."""
+    imgs = {}
+    for accel in (rt.RT_ACCEL_SAH, rt.RT_ACCEL_LINEAR, rt.RT_ACCEL_MEDIAN):
+        imgs[accel], _ = rt.render_scene(scene_id, W, H, 4, out_format=rt.RT_OUT_F64, renderer=renderer, accel=accel)
+    assert np.array_equal(imgs[rt.RT_ACCEL_LINEAR], imgs[rt.RT_ACCEL_SAH])
+    assert np.array_equal(imgs[rt.RT_ACCEL_MEDIAN], imgs[rt.RT_ACCEL_SAH])
+    assert_parity(imgs[rt.RT_ACCEL_MEDIAN], ob.render(scene_id, W, H, 4), f"median scene {scene_id}")
+
+
+def test_linear_mode_tests_every_primitive_per_cast(rt, renderer):
+    """A LINEAR walk is the reference's list scan: every cast visits every chain node and
+    tests every top-level primitive (random scene: no instances or media)."""
+    world = rt.World(1).build_scene(0)
+    soa = rt.SceneSoA.from_buffer_copy(world.flatten(rt.RT_ACCEL_LINEAR))
+    cam, bg = rt.scene_camera(0, 48, 32)
+    renderer.upload(world, rt.RT_ACCEL_LINEAR)
+    renderer.render(cam, rt.Renderer.params(48, 32, 4, 50, bg, 1, count_work=1, out_format=rt.RT_OUT_F64))
+    st = renderer.stats()
+    assert st.prim_tests == st.casts * soa.n_prims
+    assert st.node_visits == st.casts * soa.n_nodes
+    renderer.upload(world)
