@@ -20,6 +20,9 @@
  *   rt_ctx_upload_*           (new) copies the SoA tables into HBM
  *   rt_write_ppm              write_color + the P3 writer (math.rs:119-132,
  *                             main.rs:472, 591-596)
+ *   rt_accum_* /              the per-thread partial sums, their merge into the shared
+ *   rt_render_progressive     buffer and the progress channel (main.rs:504-582), as
+ *                             resumable sample batches with a progress callback
  *
  * Threading: a context is bound to one device and is used by one host thread at
  * a time. Worlds are plain host objects.
@@ -178,6 +181,39 @@ typedef struct rt_stats {
     uint64_t cycles_shade;       /* count_work only: wave-cycles in materials / textures */
 } rt_stats;
 int rt_last_stats(rt_ctx* ctx, rt_stats* out);
+
+/* ---- progressive / resumable accumulation ------------------------------------ */
+/* A device f64 running sum per pixel of one row shard. Batches render consecutive sample
+ * ranges [done, done + n) and add their per-pixel sums; rt_accum_resolve divides. When
+ * every batch boundary is a multiple of the chunk size (rt_render_params.spp_chunk at
+ * create time; 0 = rt_render's auto choice for p->spp), the result is bit-identical to
+ * one rt_render of the same total spp: the sums are added in the same order.
+ * The reference's version of this is each thread's local_pixel_colors merged into the
+ * mutex-guarded buffer (main.rs:508-547) plus the progress channel (main.rs:504-582). */
+typedef struct rt_accum rt_accum;
+/* p: width, height, row_begin, row_stride, spp (for the auto chunk) and spp_chunk. */
+int rt_accum_create(rt_ctx* ctx, const rt_render_params* p, rt_accum** out);
+void rt_accum_destroy(rt_accum* acc);
+/* Renders samples [done, done + sample_count) of the shard with p's camera-independent
+ * settings (max_depth, background, render_seed, count_work, stream; its geometry fields
+ * must match the accumulator's) and adds them. Enqueued on the stream; rt_last_stats
+ * describes the batch. */
+int rt_accum_add(rt_ctx* ctx, rt_accum* acc, const rt_camera* cam, const rt_render_params* p, int sample_count);
+/* Checkpoint: samples done, and (if sums is not NULL) the rows_local x width x 3 f64 sums. */
+int rt_accum_get(rt_accum* acc, double* sums, int64_t* samples_done);
+/* Restore a checkpoint taken with rt_accum_get (same geometry and chunk size). */
+int rt_accum_set(rt_accum* acc, const double* sums, int64_t samples_done);
+/* out = sums * (1/divisor) (divisor 0: the samples done), as rt_render writes it. The
+ * reference divides by its nominal spp even when spp/thread_count truncated the samples
+ * actually taken (main.rs:516, 596): pass that spp as divisor to reproduce it. */
+int rt_accum_resolve(rt_ctx* ctx, rt_accum* acc, double divisor, int out_format, int out_on_device, void* out);
+
+/* Progress callback: return 0 to continue, nonzero to stop after this batch. */
+typedef int (*rt_progress_fn)(void* user, int64_t samples_done, int64_t samples_total);
+/* rt_render in batches of batch_spp samples (rounded up to the chunk size), calling
+ * progress after each batch; out as rt_render (sums / samples done if stopped early). */
+int rt_render_progressive(rt_ctx* ctx, const rt_camera* cam, const rt_render_params* p, int batch_spp,
+                          rt_progress_fn progress, void* user, void* out);
 
 /* ---- output ------------------------------------------------------------------------------ */
 /* P3 PPM exactly as the reference writes it: header "P3\nW H\n255\n\n", rows top to

@@ -522,17 +522,20 @@ int rt_rows_in_shard(int height, int row_begin, int row_stride)
 
 static int auto_chunk(int spp) { return std::max(1, (spp + 15) / 16); }
 
-int rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, void* out)
+static bool bad_geometry(const rt_render_params* p)
 {
-    if (!c || !cam || !p || !out) return fail(RT_ERR_INVALID, "null argument");
-    if (!c->has_scene) return fail(RT_ERR_NO_SCENE, "no scene uploaded");
-    if (p->width < 2 || p->height < 2 || p->spp < 1 || p->max_depth < 0 || p->row_stride < 1 || p->row_begin < 0 ||
-        p->spp_chunk < 0 || (p->out_format != RT_OUT_F32 && p->out_format != RT_OUT_F64))
-        return fail(RT_ERR_INVALID, "bad render params");
-    if ((long long)p->width * p->height > 0xffffffffLL) return fail(RT_ERR_INVALID, "image too large for 32-bit pixel keys");
+    return p->width < 2 || p->height < 2 || p->row_stride < 1 || p->row_begin < 0 || p->spp_chunk < 0 ||
+           (long long)p->width * p->height > 0xffffffffLL;
+}
+
+// Launches the trace kernel for samples [s_begin, s_end) of the shard in chunks of `chunk`
+// into c->partial (n_chunks x n_px x 3), between events ev[0] and ev[1]. Fills the launch
+// part of c->stats; the caller enqueues the reduction and records ev[2].
+static int launch_samples(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, int s_begin, int s_end,
+                          int chunk, hipStream_t stream, int& n_chunks_out)
+{
     const int n_rows = rt_rows_in_shard(p->height, p->row_begin, p->row_stride);
-    const int chunk = p->spp_chunk > 0 ? std::min(p->spp_chunk, p->spp) : auto_chunk(p->spp);
-    const int n_chunks = (p->spp + chunk - 1) / chunk;
+    const int n_chunks = (s_end - s_begin + chunk - 1) / chunk;
     const long long n_px = (long long)n_rows * p->width;
 
     rtk::KParams K;
@@ -544,7 +547,8 @@ int rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, void* 
     K.seed = p->render_seed;
     K.width = p->width;
     K.height = p->height;
-    K.spp = p->spp;
+    K.spp = s_end;
+    K.sample_begin = s_begin;
     K.max_depth = p->max_depth;
     K.spp_chunk = chunk;
     K.n_chunks = n_chunks;
@@ -554,8 +558,6 @@ int rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, void* 
     K.tiles_x = (p->width + 7) / 8;
     K.tiles_y = (n_rows + 7) / 8;
 
-    HIP_TRY(hipSetDevice(c->device));
-    hipStream_t stream = p->stream ? (hipStream_t)p->stream : c->stream;
     const size_t need = (size_t)n_chunks * (size_t)std::max<long long>(n_px, 1) * 3 * sizeof(double);
     if (need > c->partial_cap) {
         HIP_TRY(hipStreamSynchronize(stream));
@@ -564,18 +566,6 @@ int rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, void* 
         c->partial_cap = 0;
         HIP_TRY(hipMalloc((void**)&c->partial, need));
         c->partial_cap = need;
-    }
-    const size_t out_bytes = (size_t)n_px * 3 * (p->out_format == RT_OUT_F64 ? 8 : 4);
-    void* dev_out = out;
-    if (!p->out_on_device) {
-        if (out_bytes > c->out_cap) {
-            (void)hipFree(c->out_buf);
-            c->out_buf = nullptr;
-            c->out_cap = 0;
-            HIP_TRY(hipMalloc(&c->out_buf, std::max<size_t>(out_bytes, 16)));
-            c->out_cap = std::max<size_t>(out_bytes, 16);
-        }
-        dev_out = c->out_buf;
     }
     const bool count = p->count_work != 0;
     // conservative f32 slab tests need every ray origin within 2M of the origin (flatten.cpp):
@@ -598,16 +588,12 @@ int rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, void* 
     HIP_TRY(hipMemcpyAsync(dK, &K, sizeof K, hipMemcpyHostToDevice, stream));
     HIP_TRY(hipEventRecord(c->ev[0], stream));
     HIP_TRY(rtk::launch_trace(S, K, dK, c->partial, c->counters, o, stream));
+    HIP_TRY(hipEventRecord(c->ev[1], stream));
     c->stats.lds_nodes = S.n_lds_nodes;
     c->stats.variant_features = (int32_t)rtk::variant_features(o.features);
     c->stats.slab32 = o.slab32;
     c->stats.lds_stack = o.lds_stack;
-    HIP_TRY(hipEventRecord(c->ev[1], stream));
-    HIP_TRY(rtk::launch_reduce(c->partial, dev_out, p->out_format == RT_OUT_F64, n_px, n_chunks,
-                               1.0 / (double)p->spp, stream));
-    HIP_TRY(hipEventRecord(c->ev[2], stream));
-
-    c->stats.samples = (uint64_t)n_px * (uint64_t)p->spp;
+    c->stats.samples = (uint64_t)n_px * (uint64_t)(s_end - s_begin);
     c->stats.n_items = (uint64_t)n_px * (uint64_t)n_chunks;
     c->stats.n_chunks = n_chunks;
     c->stats.spp_chunk = chunk;
@@ -616,14 +602,205 @@ int rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, void* 
     c->stats.material_bytes = (int32_t)sizeof(rt_material);
     c->pending_stats = true;
     c->pending_counts = count;
-    if (!c->stats.samples) {
-        c->stats.casts = c->stats.node_visits = c->stats.prim_tests = 0;
+    if (!c->stats.samples) c->stats.casts = c->stats.node_visits = c->stats.prim_tests = 0;
+    n_chunks_out = n_chunks;
+    return RT_OK;
+}
+
+// Device buffer for a host-bound result (grown on demand).
+static int out_staging(rt_ctx* c, size_t out_bytes, void*& dev_out)
+{
+    if (out_bytes > c->out_cap) {
+        (void)hipFree(c->out_buf);
+        c->out_buf = nullptr;
+        c->out_cap = 0;
+        HIP_TRY(hipMalloc(&c->out_buf, std::max<size_t>(out_bytes, 16)));
+        c->out_cap = std::max<size_t>(out_bytes, 16);
     }
+    dev_out = c->out_buf;
+    return RT_OK;
+}
+
+int rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, void* out)
+{
+    if (!c || !cam || !p || !out) return fail(RT_ERR_INVALID, "null argument");
+    if (!c->has_scene) return fail(RT_ERR_NO_SCENE, "no scene uploaded");
+    if (bad_geometry(p) || p->spp < 1 || p->max_depth < 0 || (p->out_format != RT_OUT_F32 && p->out_format != RT_OUT_F64))
+        return fail(RT_ERR_INVALID, "bad render params");
+    const int n_rows = rt_rows_in_shard(p->height, p->row_begin, p->row_stride);
+    const int chunk = p->spp_chunk > 0 ? std::min(p->spp_chunk, p->spp) : auto_chunk(p->spp);
+    const long long n_px = (long long)n_rows * p->width;
+
+    HIP_TRY(hipSetDevice(c->device));
+    hipStream_t stream = p->stream ? (hipStream_t)p->stream : c->stream;
+    const size_t out_bytes = (size_t)n_px * 3 * (p->out_format == RT_OUT_F64 ? 8 : 4);
+    void* dev_out = out;
+    if (!p->out_on_device) {
+        int rc = out_staging(c, out_bytes, dev_out);
+        if (rc) return rc;
+    }
+    int n_chunks = 0;
+    int rc = launch_samples(c, cam, p, 0, p->spp, chunk, stream, n_chunks);
+    if (rc) return rc;
+    HIP_TRY(rtk::launch_reduce(c->partial, dev_out, p->out_format == RT_OUT_F64, n_px, n_chunks,
+                               1.0 / (double)p->spp, stream));
+    HIP_TRY(hipEventRecord(c->ev[2], stream));
     if (!p->out_on_device) {
         HIP_TRY(hipMemcpyAsync(out, dev_out, out_bytes, hipMemcpyDeviceToHost, stream));
         HIP_TRY(hipStreamSynchronize(stream));
     }
     return RT_OK;
+}
+
+// ---- progressive accumulation -----------------------------------------------------------------
+struct rt_accum {
+    rt_ctx* ctx = nullptr;
+    int width = 0, height = 0, row_begin = 0, row_stride = 1, n_rows = 0, chunk = 1;
+    long long n_px = 0;
+    int64_t done = 0;
+    double* sums = nullptr;             // device, n_px x 3
+    hipStream_t last_stream = nullptr;  // the stream the last batch was enqueued on
+};
+
+int rt_accum_create(rt_ctx* c, const rt_render_params* p, rt_accum** out)
+{
+    if (!c || !p || !out) return fail(RT_ERR_INVALID, "null argument");
+    *out = nullptr;
+    if (bad_geometry(p) || p->spp < 0 || (p->spp_chunk == 0 && p->spp < 1))
+        return fail(RT_ERR_INVALID, "bad accumulator geometry");
+    auto* a = new (std::nothrow) rt_accum;
+    if (!a) return fail(RT_ERR_OOM, "out of host memory");
+    a->ctx = c;
+    a->width = p->width;
+    a->height = p->height;
+    a->row_begin = p->row_begin;
+    a->row_stride = p->row_stride;
+    a->n_rows = rt_rows_in_shard(p->height, p->row_begin, p->row_stride);
+    a->chunk = p->spp_chunk > 0 ? p->spp_chunk : auto_chunk(p->spp);
+    a->n_px = (long long)a->n_rows * p->width;
+    a->last_stream = c->stream;
+    const size_t bytes = (size_t)std::max<long long>(a->n_px, 1) * 3 * sizeof(double);
+    hipError_t e = hipSetDevice(c->device);
+    if (e == hipSuccess) e = hipMalloc((void**)&a->sums, bytes);
+    if (e == hipSuccess) e = hipMemset(a->sums, 0, bytes);
+    if (e != hipSuccess) {
+        (void)hipFree(a->sums);
+        delete a;
+        return hip_fail(e, "rt_accum_create");
+    }
+    *out = a;
+    return RT_OK;
+}
+
+void rt_accum_destroy(rt_accum* a)
+{
+    if (!a) return;
+    (void)hipSetDevice(a->ctx->device);
+    (void)hipStreamSynchronize(a->last_stream);
+    (void)hipFree(a->sums);
+    delete a;
+}
+
+int rt_accum_add(rt_ctx* c, rt_accum* a, const rt_camera* cam, const rt_render_params* p, int sample_count)
+{
+    if (!c || !a || !cam || !p) return fail(RT_ERR_INVALID, "null argument");
+    if (a->ctx != c) return fail(RT_ERR_INVALID, "accumulator belongs to another context");
+    if (!c->has_scene) return fail(RT_ERR_NO_SCENE, "no scene uploaded");
+    if (p->width != a->width || p->height != a->height || p->row_begin != a->row_begin ||
+        p->row_stride != a->row_stride)
+        return fail(RT_ERR_INVALID, "render params do not match the accumulator's shard");
+    if (sample_count < 0 || p->max_depth < 0 || a->done + sample_count > 0x7fffffffLL)
+        return fail(RT_ERR_INVALID, "bad sample range");
+    if (sample_count == 0) return RT_OK;
+    HIP_TRY(hipSetDevice(c->device));
+    hipStream_t stream = p->stream ? (hipStream_t)p->stream : c->stream;
+    if (stream != a->last_stream) HIP_TRY(hipStreamSynchronize(a->last_stream));
+    int n_chunks = 0;
+    int rc = launch_samples(c, cam, p, (int)a->done, (int)(a->done + sample_count), a->chunk, stream, n_chunks);
+    if (rc) return rc;
+    HIP_TRY(rtk::launch_accumulate(c->partial, a->sums, a->n_px, n_chunks, stream));
+    HIP_TRY(hipEventRecord(c->ev[2], stream));
+    a->done += sample_count;
+    a->last_stream = stream;
+    return RT_OK;
+}
+
+int rt_accum_get(rt_accum* a, double* sums, int64_t* samples_done)
+{
+    if (!a) return fail(RT_ERR_INVALID, "null argument");
+    if (samples_done) *samples_done = a->done;
+    if (!sums) return RT_OK;
+    HIP_TRY(hipSetDevice(a->ctx->device));
+    HIP_TRY(hipStreamSynchronize(a->last_stream));
+    HIP_TRY(hipMemcpy(sums, a->sums, (size_t)a->n_px * 3 * sizeof(double), hipMemcpyDeviceToHost));
+    return RT_OK;
+}
+
+int rt_accum_set(rt_accum* a, const double* sums, int64_t samples_done)
+{
+    if (!a || !sums) return fail(RT_ERR_INVALID, "null argument");
+    if (samples_done < 0 || samples_done > 0x7fffffffLL) return fail(RT_ERR_INVALID, "bad sample count");
+    HIP_TRY(hipSetDevice(a->ctx->device));
+    HIP_TRY(hipStreamSynchronize(a->last_stream));
+    HIP_TRY(hipMemcpy(a->sums, sums, (size_t)a->n_px * 3 * sizeof(double), hipMemcpyHostToDevice));
+    a->done = samples_done;
+    return RT_OK;
+}
+
+int rt_accum_resolve(rt_ctx* c, rt_accum* a, double divisor, int out_format, int out_on_device, void* out)
+{
+    if (!c || !a || !out) return fail(RT_ERR_INVALID, "null argument");
+    if (a->ctx != c) return fail(RT_ERR_INVALID, "accumulator belongs to another context");
+    if (out_format != RT_OUT_F32 && out_format != RT_OUT_F64) return fail(RT_ERR_INVALID, "bad output format");
+    if (divisor == 0.0) divisor = (double)a->done;
+    if (!(divisor > 0.0) || !std::isfinite(divisor)) return fail(RT_ERR_INVALID, "nothing accumulated / bad divisor");
+    HIP_TRY(hipSetDevice(c->device));
+    hipStream_t stream = a->last_stream;
+    const size_t out_bytes = (size_t)a->n_px * 3 * (out_format == RT_OUT_F64 ? 8 : 4);
+    void* dev_out = out;
+    if (!out_on_device) {
+        int rc = out_staging(c, out_bytes, dev_out);
+        if (rc) return rc;
+    }
+    // one "chunk" holding the running sums: 0.0 + sum = sum, then * (1/divisor) as rt_render
+    HIP_TRY(rtk::launch_reduce(a->sums, dev_out, out_format == RT_OUT_F64, a->n_px, 1, 1.0 / divisor, stream));
+    if (!out_on_device) {
+        HIP_TRY(hipMemcpyAsync(out, dev_out, out_bytes, hipMemcpyDeviceToHost, stream));
+        HIP_TRY(hipStreamSynchronize(stream));
+    }
+    return RT_OK;
+}
+
+int rt_render_progressive(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, int batch_spp,
+                          rt_progress_fn progress, void* user, void* out)
+{
+    if (!c || !cam || !p || !out) return fail(RT_ERR_INVALID, "null argument");
+    if (p->spp < 1 || batch_spp < 1) return fail(RT_ERR_INVALID, "bad spp / batch");
+    rt_accum* a = nullptr;
+    int rc = rt_accum_create(c, p, &a);
+    if (rc) return rc;
+    const int batch = (batch_spp + a->chunk - 1) / a->chunk * a->chunk;  // keep chunk boundaries
+    while (rc == RT_OK && a->done < p->spp) {
+        const int n = (int)std::min<int64_t>(batch, p->spp - a->done);
+        rc = rt_accum_add(c, a, cam, p, n);
+        if (rc) break;
+        if (progress) {
+            hipError_t e = hipStreamSynchronize(a->last_stream);
+            if (e != hipSuccess) {
+                rc = hip_fail(e, "rt_render_progressive");
+                break;
+            }
+            if (progress(user, a->done, p->spp)) break;
+        }
+    }
+    if (rc == RT_OK)
+        rc = rt_accum_resolve(c, a, a->done == p->spp ? (double)p->spp : 0.0, p->out_format, p->out_on_device, out);
+    if (rc == RT_OK && p->out_on_device) {
+        hipError_t e = hipStreamSynchronize(a->last_stream);  // the accumulator is freed below
+        if (e != hipSuccess) rc = hip_fail(e, "rt_render_progressive");
+    }
+    rt_accum_destroy(a);
+    return rc;
 }
 
 int rt_last_stats(rt_ctx* c, rt_stats* out)

@@ -908,7 +908,7 @@ __device__ __forceinline__ bool lane_work(const KParams& P, LaneWork& w)
     if (w.x >= P.width || w.k >= P.n_rows) return false;
     w.y = P.row_begin + w.k * P.row_stride;
     w.pixel = (uint32_t)w.y * (uint32_t)P.width + (uint32_t)w.x;
-    w.s_begin = w.chunk * P.spp_chunk;
+    w.s_begin = P.sample_begin + w.chunk * P.spp_chunk;
     w.s_end = min(P.spp, w.s_begin + P.spp_chunk);
     return true;
 }
@@ -1031,6 +1031,25 @@ __global__ void __launch_bounds__(256) reduce_chunks(const double* __restrict__ 
     out[3 * i + 2] = (T)(b * scale);
 }
 
+// Progressive accumulation: continues reduce_chunks' running sum across batches, so a
+// render split at chunk boundaries sums in the same order as one launch.
+__global__ void __launch_bounds__(256) accumulate_chunks(const double* __restrict__ partial,
+                                                         double* __restrict__ acc, long long n_px, int n_chunks)
+{
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n_px) return;
+    double r = acc[3 * i + 0], g = acc[3 * i + 1], b = acc[3 * i + 2];
+    for (int c = 0; c < n_chunks; ++c) {
+        const double* p = partial + ((size_t)c * n_px + i) * 3;
+        r = r + p[0];
+        g = g + p[1];
+        b = b + p[2];
+    }
+    acc[3 * i + 0] = r;
+    acc[3 * i + 1] = g;
+    acc[3 * i + 2] = b;
+}
+
 __global__ void eval_numerics(int fn, const double* x, const double* y, const double* z, double* out, int n)
 {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1132,6 +1151,14 @@ hipError_t launch_reduce(const double* partial, void* out, bool f64, long long n
     else
         hipLaunchKernelGGL(reduce_chunks<float>, dim3((unsigned)blocks), dim3(256), 0, stream, partial, (float*)out,
                            n_px, n_chunks, scale);
+    return hipGetLastError();
+}
+
+hipError_t launch_accumulate(const double* partial, double* acc, long long n_px, int n_chunks, hipStream_t stream)
+{
+    const long long blocks = (n_px + 255) / 256;
+    if (blocks <= 0) return hipSuccess;
+    hipLaunchKernelGGL(accumulate_chunks, dim3((unsigned)blocks), dim3(256), 0, stream, partial, acc, n_px, n_chunks);
     return hipGetLastError();
 }
 

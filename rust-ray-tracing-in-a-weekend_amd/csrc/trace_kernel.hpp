@@ -36,7 +36,7 @@ struct KParams {
     int32_t spp_chunk, n_chunks;
     int32_t row_begin, row_stride, n_rows;
     int32_t tiles_x, tiles_y;   // 8x8 pixel tiles over (width, n_rows)
-    int32_t pad;
+    int32_t sample_begin;       // chunk c covers samples [sample_begin + c*spp_chunk, ..) up to spp
 };
 
 // Scene features (which code a kernel variant must contain).
@@ -64,6 +64,8 @@ hipError_t launch_trace(const SceneDev& S, const KParams& Ph, const KParams* P, 
                         unsigned long long* counters, const LaunchOpts& o, hipStream_t stream);
 hipError_t launch_reduce(const double* partial, void* out, bool f64, long long n_px, int n_chunks, double scale,
                          hipStream_t stream);
+// acc[i] += chunk partials in chunk order (progressive accumulation, rt_accum_add)
+hipError_t launch_accumulate(const double* partial, double* acc, long long n_px, int n_chunks, hipStream_t stream);
 hipError_t launch_eval(int fn, const double* x, const double* y, const double* z, double* out, int n,
                        hipStream_t stream);
 

@@ -47,8 +47,12 @@ EXPORTED = [
     "rt_world_bvh", "rt_world_push", "rt_world_build_scene", "rt_world_info_get", "rt_camera_new",
     "rt_scene_preset_get", "rt_scene_camera", "rt_world_flatten", "rt_ctx_upload_soa",
     "rt_ctx_upload_world", "rt_render", "rt_rows_in_shard", "rt_last_stats", "rt_write_ppm",
-    "rt_ctx_set_variant", "rt_device_eval",
+    "rt_ctx_set_variant", "rt_device_eval", "rt_accum_create", "rt_accum_destroy", "rt_accum_add",
+    "rt_accum_get", "rt_accum_set", "rt_accum_resolve", "rt_render_progressive",
 ]
+
+# int (*rt_progress_fn)(void* user, int64_t samples_done, int64_t samples_total)
+PROGRESS_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64)
 
 
 class RTError(RuntimeError):
@@ -152,6 +156,14 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "rt_rows_in_shard": ([I, I, I], I), "rt_last_stats": ([P, ctypes.POINTER(Stats)], I),
         "rt_write_ppm": ([P, I, I, ctypes.c_char_p], I),
         "rt_device_eval": ([P, I, P, P, P, P, I], I), "rt_ctx_set_variant": ([P, I, I, I], I),
+        "rt_accum_create": ([P, ctypes.POINTER(RenderParams), ctypes.POINTER(P)], I),
+        "rt_accum_destroy": ([P], None),
+        "rt_accum_add": ([P, P, ctypes.POINTER(Camera), ctypes.POINTER(RenderParams), I], I),
+        "rt_accum_get": ([P, P, ctypes.POINTER(ctypes.c_int64)], I),
+        "rt_accum_set": ([P, P, ctypes.c_int64], I),
+        "rt_accum_resolve": ([P, P, D, I, I, P], I),
+        "rt_render_progressive": ([P, ctypes.POINTER(Camera), ctypes.POINTER(RenderParams), I, PROGRESS_FN, P,
+                                   P], I),
     }
     for name, (args, res) in sigs.items():
         fn = getattr(lib, name)
@@ -374,6 +386,20 @@ class Renderer:
         _check(self.lib.rt_render(self.h, ctypes.byref(camera), ctypes.byref(params), ctypes.c_void_p(dev_ptr)),
                "rt_render")
 
+    def render_progressive(self, camera: Camera, params: RenderParams, batch_spp: int, progress=None) -> np.ndarray:
+        """rt_render in sample batches; progress(samples_done, samples_total) -> truthy stops early."""
+        n_rows = rows_in_shard(params.height, params.row_begin, params.row_stride)
+        dt = np.float64 if params.out_format == RT_OUT_F64 else np.float32
+        out = np.empty((n_rows, params.width, 3), dtype=dt)
+        params.out_on_device = 0
+        cb = PROGRESS_FN(lambda _u, done, total: int(bool(progress(done, total)))) if progress else PROGRESS_FN()
+        _check(self.lib.rt_render_progressive(self.h, ctypes.byref(camera), ctypes.byref(params), batch_spp, cb,
+                                              None, out.ctypes.data), "rt_render_progressive")
+        return out
+
+    def accumulator(self, params: RenderParams) -> "Accumulator":
+        return Accumulator(self, params)
+
     def set_variant(self, slab32: int = 1, lds_stack: int = 1, lds_nodes: int = 1):
         _check(self.lib.rt_ctx_set_variant(self.h, slab32, lds_stack, lds_nodes), "rt_ctx_set_variant")
 
@@ -389,6 +415,58 @@ class Renderer:
         out = np.empty_like(x)
         _check(self.lib.rt_device_eval(self.h, fn, x.ctypes.data, y.ctypes.data, z.ctypes.data, out.ctypes.data,
                                        x.size), "rt_device_eval")
+        return out
+
+
+class Accumulator:
+    """Progressive / resumable accumulation over one row shard (rt_accum_*)."""
+
+    def __init__(self, renderer: Renderer, params: RenderParams):
+        self.r, self.lib = renderer, renderer.lib
+        self.rows = rows_in_shard(params.height, params.row_begin, params.row_stride)
+        self.width = params.width
+        h = ctypes.c_void_p()
+        _check(self.lib.rt_accum_create(renderer.h, ctypes.byref(params), ctypes.byref(h)), "rt_accum_create")
+        self.h = h
+
+    def close(self):
+        if self.h:
+            self.lib.rt_accum_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def add(self, camera: Camera, params: RenderParams, sample_count: int):
+        _check(self.lib.rt_accum_add(self.r.h, self.h, ctypes.byref(camera), ctypes.byref(params), sample_count),
+               "rt_accum_add")
+
+    @property
+    def samples_done(self) -> int:
+        n = ctypes.c_int64()
+        _check(self.lib.rt_accum_get(self.h, None, ctypes.byref(n)), "rt_accum_get")
+        return n.value
+
+    def checkpoint(self):
+        """(sums rows x width x 3 f64, samples done) — what rt_accum_set restores."""
+        sums = np.empty((self.rows, self.width, 3), dtype=np.float64)
+        n = ctypes.c_int64()
+        _check(self.lib.rt_accum_get(self.h, sums.ctypes.data, ctypes.byref(n)), "rt_accum_get")
+        return sums, n.value
+
+    def restore(self, sums: np.ndarray, samples_done: int):
+        sums = np.ascontiguousarray(sums, dtype=np.float64)
+        assert sums.shape == (self.rows, self.width, 3)
+        _check(self.lib.rt_accum_set(self.h, sums.ctypes.data, samples_done), "rt_accum_set")
+
+    def resolve(self, divisor: float = 0.0, out_format: int = RT_OUT_F32) -> np.ndarray:
+        dt = np.float64 if out_format == RT_OUT_F64 else np.float32
+        out = np.empty((self.rows, self.width, 3), dtype=dt)
+        _check(self.lib.rt_accum_resolve(self.r.h, self.h, divisor, out_format, 0, out.ctypes.data),
+               "rt_accum_resolve")
         return out
 
 

@@ -174,6 +174,16 @@ def test_errors_do_not_abort(rt):
     assert lib.rt_rows_in_shard(800, 3, 8) == 100
     assert lib.rt_rows_in_shard(7, 3, 8) == 1
     assert lib.rt_rows_in_shard(7, 7, 8) == 0
+    # progressive accumulation entry points reject null handles before touching a device
+    assert lib.rt_accum_create(None, None, None) == -1
+    assert lib.rt_accum_add(None, None, None, None, 4) == -1
+    assert lib.rt_accum_get(None, None, None) == -1
+    assert lib.rt_accum_set(None, None, 0) == -1
+    assert lib.rt_accum_resolve(None, None, 0.0, 0, 0, None) == -1
+    assert lib.rt_render_progressive(None, None, None, 1, rt.PROGRESS_FN(), None, None) == -1
+    lib.rt_accum_destroy(None)
+    with pytest.raises(rt.RTError):
+        w.flatten(7)                         # unknown accel mode
 
 
 def test_unsupported_nesting_reported(rt):

@@ -231,3 +231,65 @@ def test_linear_mode_tests_every_primitive_per_cast(rt, renderer):
     assert st.prim_tests == st.casts * soa.n_prims
     assert st.node_visits == st.casts * soa.n_nodes
     renderer.upload(world)
+
+
+def _final_setup(rt, renderer, W=32, H=18):
+    world = rt.World(1).build_scene(7)       # every feature, incl. media (keyed in-hit draws)
+    cam, bg = rt.scene_camera(7, W, H)
+    renderer.upload(world)
+    return cam, bg
+
+
+def test_progressive_batches_equal_one_render(rt, renderer):
+    """SURVEY §8 f4: batches split at chunk boundaries sum in rt_render's order (bit-identical);
+    the progress callback sees every batch; the accumulator composes per row shard."""
+    W, H, spp = 32, 18, 40                   # auto chunk = ceil(40/16) = 3
+    cam, bg = _final_setup(rt, renderer, W, H)
+    p = rt.Renderer.params(W, H, spp, 50, bg, 1, out_format=rt.RT_OUT_F64)
+    one = renderer.render(cam, p)
+    seen = []
+    prog = renderer.render_progressive(cam, p, 5, lambda done, total: seen.append((done, total)))  # 5 -> 6
+    assert np.array_equal(prog, one)
+    assert seen == [(d, spp) for d in (6, 12, 18, 24, 30, 36, 40)]
+    acc = renderer.accumulator(p)
+    for n in (3, 9, 6, 22):
+        acc.add(cam, p, n)
+    assert acc.samples_done == 40
+    assert np.array_equal(acc.resolve(out_format=rt.RT_OUT_F64), one)
+    assert np.array_equal(acc.resolve(), one.astype(np.float32))
+    assert_parity(one, ob.render(7, W, H, spp), "final 40 spp")
+
+
+def test_accumulator_checkpoint_resume(rt, renderer):
+    """Checkpoint after 12 samples, restore into a fresh accumulator (the resumable C5 run),
+    finish: identical to the uninterrupted render."""
+    W, H, spp = 32, 18, 24
+    cam, bg = _final_setup(rt, renderer, W, H)
+    p = rt.Renderer.params(W, H, spp, 50, bg, 7, row_begin=1, row_stride=2, out_format=rt.RT_OUT_F64)
+    one = renderer.render(cam, p)
+    a = renderer.accumulator(p)
+    a.add(cam, p, 12)
+    sums, done = a.checkpoint()
+    a.close()
+    b = renderer.accumulator(p)
+    b.restore(sums, done)
+    b.add(cam, p, spp - done)
+    assert np.array_equal(b.resolve(out_format=rt.RT_OUT_F64), one)
+
+
+def test_progressive_early_stop_and_divisor(rt, renderer):
+    W, H = 24, 16
+    cam, bg = _final_setup(rt, renderer, W, H)
+    p = rt.Renderer.params(W, H, 32, 50, bg, 1, spp_chunk=4, out_format=rt.RT_OUT_F64)
+    stop = renderer.render_progressive(cam, p, 8, lambda done, total: done >= 8)
+    ref8 = ob.render(7, W, H, 8, spp_chunk=4)       # the first 8 samples of every pixel
+    assert_parity(stop, ref8, "stopped after 8")
+    # the reference's truncation (spp / thread_count samples per thread, divided by spp):
+    acc = renderer.accumulator(p)
+    acc.add(cam, p, 30)
+    a = acc.resolve(out_format=rt.RT_OUT_F64)
+    b = acc.resolve(32.0, out_format=rt.RT_OUT_F64)
+    assert np.allclose(b, a * (30.0 / 32.0), rtol=1e-14, atol=0)
+    q = rt.Renderer.params(W, H, 32, 50, bg, 1, row_begin=1, out_format=rt.RT_OUT_F64)
+    with pytest.raises(rt.RTError):
+        acc.add(cam, q, 2)                          # another shard
