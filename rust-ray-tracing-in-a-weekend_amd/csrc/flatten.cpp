@@ -326,8 +326,13 @@ struct Builder {
 
     // SAH costs (traversal step vs primitive test) and the largest leaf; RT_BVH_CI /
     // RT_BVH_MAXLEAF override them for tuning experiments (the image does not change).
-    double c_isect = 1.5;
-    int max_leaf = 4;
+    // Measured on MI355X (DESIGN.md §BVH build): c_isect 1.0 / max_leaf 8 keeps the sphere
+    // scenes' trees and lets a Cornell box's top level (8 wall / box items that every bounce
+    // from inside hits anyway) collapse: 177 -> 118 ms on C3's geometry.
+    double c_isect = 1.0;
+    int max_leaf = 8;
+    int force_leaf = 2;   // RT_BVH_LEAFN: a set this small is always one leaf
+    int root_leaf = 8;    // a whole BVH of at most this many items is one leaf
 
     int build_rec(std::vector<Item>& items, int b, int e, int depth)
     {
@@ -336,7 +341,7 @@ struct Builder {
         double plo[3], phi[3];
         bounds(items, b, e, plo, phi);
         double parea = area(plo, phi);
-        if (n <= 2) return make_leaf(items, b, e);
+        if (n <= std::max(1, force_leaf) || (depth == 0 && n <= root_leaf)) return make_leaf(items, b, e);
         if (depth >= 20) {  // bound the traversal stack: median split on the widest centroid axis
             double clo[3] = {INFINITY, INFINITY, INFINITY}, chi[3] = {-INFINITY, -INFINITY, -INFINITY};
             for (int i = b; i < e; ++i)
@@ -488,6 +493,8 @@ int flatten(World& w, int accel, std::string& err)
     bld.accel = accel;
     if (const char* e = std::getenv("RT_BVH_CI")) bld.c_isect = std::max(0.01, std::atof(e));
     if (const char* e = std::getenv("RT_BVH_MAXLEAF")) bld.max_leaf = std::min(31, std::max(2, std::atoi(e)));
+    if (const char* e = std::getenv("RT_BVH_LEAFN")) bld.force_leaf = std::min(31, std::max(1, std::atoi(e)));
+    if (const char* e = std::getenv("RT_BVH_ROOTLEAF")) bld.root_leaf = std::min(31, std::max(0, std::atoi(e)));
     std::vector<Item> top;
     for (int id : w.hittables) {  // M for the f32-slab padding (see to_f32_box)
         AABB b;

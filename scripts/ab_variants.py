@@ -21,7 +21,8 @@ def main():
     ap.add_argument("--depth", type=int, default=50)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--variants", default="1:1:1,1:1:0", help="slab32:lds_stack:lds_nodes tuples")
-    ap.add_argument("--bvh", default="", help="comma list of CI:MAXLEAF BVH builds to A/B (default variant)")
+    ap.add_argument("--accel", default="", help="comma list of accel modes to A/B: 0 SAH, 1 LINEAR, 2 MEDIAN")
+    ap.add_argument("--bvh", default="", help="comma list of CI:MAXLEAF[:LEAFN] BVH builds to A/B (default variant)")
     args = ap.parse_args()
     import numpy as np
     import torch  # noqa: F401  (same HIP runtime as bench.py)
@@ -62,21 +63,48 @@ def main():
         print(f"variant {v}: median {ms:.2f} ms  min {min(t):.2f} ms  "
               f"-> {W * H * args.spp / ms / 1e3:.1f} Msamples/s")
     print("last variant features/slab32/lds_stack:", used)
+    if args.accel:
+        modes = [int(x) for x in args.accel.split(",")]
+        names = {0: "SAH", 1: "LINEAR", 2: "MEDIAN"}
+        r.set_variant(*variants[0])
+        at, work, ims = {m: [] for m in modes}, {}, {}
+        for m in modes:
+            r.upload(world, m)
+            ims[m] = r.render(cam, rt.Renderer.params(W, H, 2, args.depth, bg, 1, row_stride=8,
+                                                      out_format=rt.RT_OUT_F64))
+            r.render(cam, rt.Renderer.params(W, H, 4, args.depth, bg, 1, row_stride=4, count_work=1))
+            st = r.stats()
+            work[m] = (st.node_visits / st.casts, st.prim_tests / st.casts)
+        for rnd in range(args.rounds + 1):
+            for m in modes:
+                r.upload(world, m)
+                r.render(cam, p, out)
+                if rnd > 0:
+                    at[m].append(r.stats().kernel_ms)
+        for m in modes:
+            soa = world.flatten(m)
+            ms = float(np.median(at[m]))
+            print(f"accel {names[m]}: nodes={soa.n_nodes} stack={soa.tlas_depth}/{soa.blas_depth} "
+                  f"node visits/cast {work[m][0]:.2f} prim tests/cast {work[m][1]:.2f}  "
+                  f"median {ms:.2f} ms -> {W * H * args.spp / ms / 1e3:.1f} Msamples/s  "
+                  f"image == SAH: {np.array_equal(ims[m], ims[modes[0]])}")
+        r.upload(world)
     if args.bvh:
-        builds = [tuple(x.split(":")) for x in args.bvh.split(",")]
+        builds = [tuple((x + ":2").split(":")[:3]) if x.count(":") == 1 else tuple(x.split(":"))
+                  for x in args.bvh.split(",")]
         bt = {b: [] for b in builds}
         r.set_variant(*variants[0])
         for rnd in range(args.rounds + 1):
             for b in builds:
-                os.environ["RT_BVH_CI"], os.environ["RT_BVH_MAXLEAF"] = b
+                os.environ["RT_BVH_CI"], os.environ["RT_BVH_MAXLEAF"], os.environ["RT_BVH_LEAFN"] = b
                 r.upload(world)
                 r.render(cam, p, out)
                 if rnd > 0:
                     bt[b].append(r.stats().kernel_ms)
         for b in builds:
-            os.environ["RT_BVH_CI"], os.environ["RT_BVH_MAXLEAF"] = b
+            os.environ["RT_BVH_CI"], os.environ["RT_BVH_MAXLEAF"], os.environ["RT_BVH_LEAFN"] = b
             soa = world.flatten()
-            print(f"bvh ci={b[0]} maxleaf={b[1]} nodes={soa.n_nodes} depth={soa.tlas_depth}/{soa.blas_depth}: "
+            print(f"bvh ci={b[0]} maxleaf={b[1]} leafn={b[2]} nodes={soa.n_nodes} depth={soa.tlas_depth}/{soa.blas_depth}: "
                   f"median {float(np.median(bt[b])):.2f} ms")
         os.environ.pop("RT_BVH_CI"); os.environ.pop("RT_BVH_MAXLEAF")
         r.upload(world)
