@@ -179,6 +179,10 @@ typedef struct rt_stats {
     uint64_t cycles_camera;      /* count_work only: wave-cycles in camera-ray generation */
     uint64_t cycles_trace;       /* count_work only: wave-cycles in traversal + hit records */
     uint64_t cycles_shade;       /* count_work only: wave-cycles in materials / textures */
+    uint64_t wave_steps;         /* count_work only: bounce-loop iterations executed per wave, summed;
+                                    casts / (64 * wave_steps) = lane occupancy of the bounce loop */
+    uint64_t wave_node_steps;    /* count_work only: node-visit iterations per wave, summed;
+                                    node_visits / (64 * wave_node_steps) = its lane occupancy */
 } rt_stats;
 int rt_last_stats(rt_ctx* ctx, rt_stats* out);
 

@@ -823,9 +823,12 @@ int rt_last_stats(rt_ctx* c, rt_stats* out)
             c->stats.cycles_camera = h[3];
             c->stats.cycles_trace = h[4];
             c->stats.cycles_shade = h[5];
+            c->stats.wave_steps = h[6];
+            c->stats.wave_node_steps = h[7];
         } else {
             c->stats.casts = c->stats.node_visits = c->stats.prim_tests = 0;
             c->stats.cycles_camera = c->stats.cycles_trace = c->stats.cycles_shade = 0;
+            c->stats.wave_steps = c->stats.wave_node_steps = 0;
         }
         c->pending_stats = false;
     }

@@ -60,7 +60,13 @@ struct Keyed {                 // coordinates of the medium's keyed draw
 
 struct Count {
     uint32_t casts, nodes, prims;
+    uint32_t wave_steps, wave_nodes;  // loop iterations the wave executed (counted by its first active lane)
 };
+// COUNT only: true in exactly one active lane of the wave
+__device__ __forceinline__ bool first_active_lane()
+{
+    return (int)(threadIdx.x & 63) == __ffsll((long long)__ballot(1)) - 1;
+}
 
 // Compile-time kernel configuration (one instantiation per variant):
 //   F      scene features the variant handles (trace_kernel.hpp FEAT_*); code for the
@@ -71,6 +77,9 @@ struct Count {
 // Traversal is while-while (Aila & Laine 2009); the if-if form and a per-lane state
 // machine with ballot-gated shading both measured slower.
 //   NALL   every TLAS node is in LDS (no per-node LDS/global choice)
+#ifndef RT_TRACE_LOOP
+#define RT_TRACE_LOOP 1   // 0 if-if, 1 while-while, 2 while-while with speculative node visits
+#endif
 template <uint32_t F_, bool S32_, bool LDS_, bool NALL_, bool COUNT_>
 struct Cfg {
     static constexpr uint32_t F = F_;
@@ -78,7 +87,7 @@ struct Cfg {
     static constexpr bool LDS = LDS_;
     static constexpr bool NALL = NALL_;
     static constexpr bool COUNT = COUNT_;
-    static constexpr int LOOP = 1;
+    static constexpr int LOOP = RT_TRACE_LOOP;
 };
 
 // Traversal stack. LDS: a lane-interleaved dynamic LDS array [entry][256 threads]
@@ -447,12 +456,44 @@ __device__ __forceinline__ bool traverse(const SceneDev& S, int root, const Ray&
                 cur = visit(cur);
             }
         }
-    } else {
+    } else if constexpr (C::LOOP == 1) {
         while (cur != RT_DONE) {
-            while (cur >= 0) cur = visit(cur);
+            while (cur >= 0) {
+                if (C::COUNT && first_active_lane()) cnt.wave_nodes++;
+                cur = visit(cur);
+            }
             if (cur == RT_DONE) break;
             do_leaf(cur);
             cur = sp == sp0 ? RT_DONE : stack[--sp];
+        }
+    } else {
+        // Speculative while-while (Aila & Laine 2009, §4): a lane that reaches a leaf parks
+        // it and keeps visiting nodes until every lane still in the node loop holds one,
+        // so the node loop runs with more lanes busy; then each lane tests one leaf.
+        int parked = 0;  // 0: none; else a leaf code (< 0, never RT_DONE)
+        for (;;) {
+            while (cur >= 0) {
+                if (C::COUNT && first_active_lane()) cnt.wave_nodes++;
+                cur = visit(cur);
+                if (cur < 0 && cur != RT_DONE && parked == 0) {
+                    parked = cur;
+                    cur = sp == sp0 ? RT_DONE : stack[--sp];
+                }
+                if (__all(parked != 0)) break;
+            }
+            int lf;
+            if (parked != 0) {
+                lf = parked;
+                parked = 0;
+            } else if (cur != RT_DONE && cur < 0) {
+                lf = cur;
+                cur = sp == sp0 ? RT_DONE : stack[--sp];
+            } else if (cur == RT_DONE) {
+                break;
+            } else {
+                continue;
+            }
+            do_leaf(lf);
         }
     }
     return any;
@@ -950,7 +991,7 @@ __global__ void __launch_bounds__(256, min_waves<C>()) trace_chunks(SceneDev S, 
     if (!lane_work(P, w)) return;
     StackT<C> stack;
     if constexpr (C::LDS) stack.base = rt_lds + threadIdx.x;
-    Count cnt{0, 0, 0};
+    Count cnt{0, 0, 0, 0, 0};
     uint64_t t_cam = 0, t_trace = 0, t_shade = 0, t_prev = 0;
     if (C::COUNT) t_prev = __builtin_amdgcn_s_memtime();
     double sum_r = 0.0, sum_g = 0.0, sum_b = 0.0;
@@ -962,6 +1003,7 @@ __global__ void __launch_bounds__(256, min_waves<C>()) trace_chunks(SceneDev S, 
     int s = w.s_begin;
     bool new_sample = true;
     while (s < w.s_end) {
+        if (C::COUNT && first_active_lane()) cnt.wave_steps++;
         if (new_sample) {
             new_sample = false;
             rt_stream_init(&st, P.seed, w.pixel, (uint32_t)s, RT_STREAM_MAIN);
@@ -1003,6 +1045,8 @@ __global__ void __launch_bounds__(256, min_waves<C>()) trace_chunks(SceneDev S, 
         atomicAdd(&counters[0], (unsigned long long)cnt.casts);
         atomicAdd(&counters[1], (unsigned long long)cnt.nodes);
         atomicAdd(&counters[2], (unsigned long long)cnt.prims);
+        atomicAdd(&counters[6], (unsigned long long)cnt.wave_steps);
+        atomicAdd(&counters[7], (unsigned long long)cnt.wave_nodes);
         // phase times are per wave (every active lane sees the same clock): one lane adds
         if ((int)(threadIdx.x & 63) == __ffsll((long long)__ballot(1)) - 1) {
             atomicAdd(&counters[3], (unsigned long long)t_cam);

@@ -111,7 +111,8 @@ class Stats(ctypes.Structure):
                 ("material_bytes", ctypes.c_int32), ("variant_features", ctypes.c_int32),
                 ("slab32", ctypes.c_int32), ("lds_stack", ctypes.c_int32), ("lds_nodes", ctypes.c_int32),
                 ("cycles_camera", ctypes.c_uint64),
-                ("cycles_trace", ctypes.c_uint64), ("cycles_shade", ctypes.c_uint64)]
+                ("cycles_trace", ctypes.c_uint64), ("cycles_shade", ctypes.c_uint64),
+                ("wave_steps", ctypes.c_uint64), ("wave_node_steps", ctypes.c_uint64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

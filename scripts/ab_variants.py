@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--depth", type=int, default=50)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--variants", default="1:1:1,1:1:0", help="slab32:lds_stack:lds_nodes tuples")
+    ap.add_argument("--chunks", default="", help="comma list of spp_chunk values to A/B")
     ap.add_argument("--accel", default="", help="comma list of accel modes to A/B: 0 SAH, 1 LINEAR, 2 MEDIAN")
     ap.add_argument("--bvh", default="", help="comma list of CI:MAXLEAF[:LEAFN] BVH builds to A/B (default variant)")
     args = ap.parse_args()
@@ -117,6 +118,23 @@ def main():
         print(f"phase shares (wave-cycles): camera {st.cycles_camera / tot:.3f}  trace {st.cycles_trace / tot:.3f}  "
               f"shade {st.cycles_shade / tot:.3f};  casts/sample {st.casts / st.samples:.3f}  "
               f"nodes/cast {st.node_visits / max(st.casts, 1):.2f}  prims/cast {st.prim_tests / max(st.casts, 1):.2f}")
+        print(f"lane occupancy: bounce loop {st.casts / max(64 * st.wave_steps, 1):.3f}  "
+              f"node-visit loop {st.node_visits / max(64 * st.wave_node_steps, 1):.3f}")
+    if args.chunks:
+        cks = [int(x) for x in args.chunks.split(",")]
+        ct = {k: [] for k in cks}
+        for rnd in range(args.rounds + 1):
+            for k in cks:
+                q = rt.Renderer.params(W, H, args.spp, args.depth, bg, 1, spp_chunk=k, out_format=rt.RT_OUT_F32)
+                r.render(cam, q, out)
+                if rnd > 0:
+                    ct[k].append(r.stats().kernel_ms)
+        for k in cks:
+            q = rt.Renderer.params(W, H, min(args.spp, 4 * k), args.depth, bg, 1, spp_chunk=k, count_work=1)
+            r.render(cam, q)
+            st = r.stats()
+            print(f"spp_chunk {k}: median {float(np.median(ct[k])):.2f} ms  bounce-loop occupancy "
+                  f"{st.casts / max(64 * st.wave_steps, 1):.3f}")
 
 
 if __name__ == "__main__":

@@ -1,0 +1,37 @@
+#!/usr/bin/env python3
+"""Per-kernel register / scratch / occupancy of trace_kernel.hip (compiler remarks), compact.
+
+usage: python scripts/res_usage.py [-DRT_TRACE_LOOP=2 ...]   (extra hipcc flags)
+"""
+import os
+import re
+import subprocess
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+src = os.path.join(REPO, "rust-ray-tracing-in-a-weekend_amd", "csrc", "trace_kernel.hip")
+cmd = ["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math",
+       "--offload-arch=gfx950", "-I" + os.path.join(REPO, "include"), "--cuda-device-only", "-c", src,
+       "-o", "/tmp/res_usage.o", "-Rpass-analysis=kernel-resource-usage", *sys.argv[1:]]
+out = subprocess.run(cmd, capture_output=True, text=True).stderr
+cur, rows = None, []
+for line in out.splitlines():
+    m = re.search(r"Function Name: (\S+)", line)
+    if m:
+        cur = {"name": m.group(1)}
+        rows.append(cur)
+        continue
+    m = re.search(r"remark:\s+(.+?): (\d+) \[", line)
+    if m and cur is not None:
+        cur[m.group(1).strip()] = int(m.group(2))
+for r in rows:
+    n = r["name"]
+    m = re.search(r"trace_chunksINS_3CfgILj(\d+)ELb(\d)ELb(\d)ELb(\d)ELb(\d)E", n)
+    if not m:
+        continue
+    f, s32, lds, nall, count = m.groups()
+    if count == "1":
+        continue
+    print(f"F={f:>2} s32={s32} lds={lds} nall={nall}: VGPRs {r.get('VGPRs')} AGPRs {r.get('AGPRs')} "
+          f"SGPRs {r.get('TotalSGPRs')} spills {r.get('VGPRs Spill')}/{r.get('SGPRs Spill')} scratch {r.get('ScratchSize [bytes/lane]', r.get('ScratchSize'))} "
+          f"occupancy {r.get('Occupancy [waves/SIMD]', r.get('Occupancy'))} LDS {r.get('LDS Size [bytes/block]')}")
