@@ -183,6 +183,10 @@ typedef struct rt_stats {
                                     casts / (64 * wave_steps) = lane occupancy of the bounce loop */
     uint64_t wave_node_steps;    /* count_work only: node-visit iterations per wave, summed;
                                     node_visits / (64 * wave_node_steps) = its lane occupancy */
+    uint64_t cycles_nodes;       /* count_work only: wave-cycles in BVH node-visit loops (part of trace) */
+    uint64_t cycles_leaves;      /* count_work only: wave-cycles in leaf primitive tests (part of trace) */
+    int32_t schedule;            /* RT_SCHED_* the last render ran with */
+    int32_t n_batches;           /* trace launches it took (pool: per-sample buffer batches) */
 } rt_stats;
 int rt_last_stats(rt_ctx* ctx, rt_stats* out);
 
@@ -230,6 +234,15 @@ int rt_write_ppm(const float* mean_rgb, int width, int height, const char* path)
  * when it fits). Defaults 1/1/1, or the RT_SLAB32 / RT_LDS_STACK / RT_LDS_NODES
  * environment variables. Results do not depend on them (tests check this). */
 int rt_ctx_set_variant(rt_ctx* ctx, int slab32, int lds_stack, int lds_nodes);
+
+/* Work schedule of a context (default RT_SCHED_POOL, or the RT_SCHEDULE environment
+ * variable). CHUNKS: a wave owns an 8x8 tile x one chunk of samples, each lane one pixel's
+ * chunk. POOL: persistent waves take (tile, chunk) blocks from a device counter and a lane
+ * whose path ended takes the block's next (pixel, sample) at once; every sample's radiance
+ * goes to a [sample][pixel] buffer (batched to RT_SAMPLE_BUF_MB, default 32 GiB) that is
+ * summed per pixel in sample order. Images are bit-identical either way. */
+enum { RT_SCHED_CHUNKS = 0, RT_SCHED_POOL = 1 };
+int rt_ctx_set_schedule(rt_ctx* ctx, int schedule);
 
 /* ---- self test ------------------------------------------------------------------------------ */
 /* Evaluates rt_numerics.h functions on the device (same fn ids as the oracle's

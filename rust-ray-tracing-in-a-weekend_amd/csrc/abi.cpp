@@ -55,6 +55,8 @@ struct rt_world {
     rtw::World w;
 };
 
+constexpr int kCounters = 16;  // count_work counters (trace_kernel.hip: trace_chunks epilogue)
+
 struct rt_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -78,6 +80,11 @@ struct rt_ctx {
     int opt_slab32 = 1;                 // rt_ctx_set_variant / RT_SLAB32
     int opt_lds = 1;                    // rt_ctx_set_variant / RT_LDS_STACK
     int opt_lds_nodes = 1;              // RT_LDS_NODES: keep the TLAS in LDS when it fits
+    int opt_pool = 1;                   // rt_ctx_set_schedule / RT_SCHEDULE: sample-pool (1) or chunk (0)
+    size_t sample_buf_cap = (size_t)32 << 30;  // RT_SAMPLE_BUF_MB: per-sample buffer bound (pool)
+    unsigned* work = nullptr;           // pool schedule: work-block counter
+    double* acc_tmp = nullptr;          // pool schedule: running sums when a render takes several batches
+    size_t acc_tmp_cap = 0;
     int n_tlas_nodes = 0;
 };
 
@@ -113,10 +120,13 @@ int rt_ctx_create(int device, rt_ctx** out)
     if (const char* e = std::getenv("RT_SLAB32")) c->opt_slab32 = std::atoi(e) != 0;
     if (const char* e = std::getenv("RT_LDS_STACK")) c->opt_lds = std::atoi(e) != 0;
     if (const char* e = std::getenv("RT_LDS_NODES")) c->opt_lds_nodes = std::atoi(e) != 0;
+    if (const char* e = std::getenv("RT_SCHEDULE")) c->opt_pool = std::atoi(e) != 0;
+    if (const char* e = std::getenv("RT_SAMPLE_BUF_MB")) c->sample_buf_cap = (size_t)std::max(1L, std::atol(e)) << 20;
     hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     for (int i = 0; i < 3 && e == hipSuccess; ++i) e = hipEventCreate(&c->ev[i]);
-    if (e == hipSuccess) e = hipMalloc((void**)&c->counters, 8 * sizeof(unsigned long long));
+    if (e == hipSuccess) e = hipMalloc((void**)&c->counters, kCounters * sizeof(unsigned long long));
     if (e == hipSuccess) e = hipMalloc((void**)&c->params, kParamSlots * sizeof(rtk::KParams));
+    if (e == hipSuccess) e = hipMalloc((void**)&c->work, sizeof(unsigned));
     if (e != hipSuccess) {
         rt_ctx_destroy(c);
         return hip_fail(e, "rt_ctx_create");
@@ -135,6 +145,8 @@ void rt_ctx_destroy(rt_ctx* c)
     (void)hipFree(c->out_buf);
     (void)hipFree(c->counters);
     (void)hipFree(c->params);
+    (void)hipFree(c->work);
+    (void)hipFree(c->acc_tmp);
     for (auto& e : c->ev)
         if (e) (void)hipEventDestroy(e);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -528,15 +540,39 @@ static bool bad_geometry(const rt_render_params* p)
            (long long)p->width * p->height > 0xffffffffLL;
 }
 
-// Launches the trace kernel for samples [s_begin, s_end) of the shard in chunks of `chunk`
-// into c->partial (n_chunks x n_px x 3), between events ev[0] and ev[1]. Fills the launch
-// part of c->stats; the caller enqueues the reduction and records ev[2].
-static int launch_samples(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, int s_begin, int s_end,
-                          int chunk, hipStream_t stream, int& n_chunks_out)
+static int grow(rt_ctx* c, hipStream_t stream, double*& buf, size_t& cap, size_t need)
+{
+    if (need <= cap) return RT_OK;
+    HIP_TRY(hipStreamSynchronize(stream));
+    (void)hipFree(buf);
+    buf = nullptr;
+    cap = 0;
+    HIP_TRY(hipMalloc((void**)&buf, need));
+    cap = need;
+    return RT_OK;
+}
+
+// Where a sample range's per-pixel sums go: added to acc (n_px x 3 f64), or (acc null)
+// written as sum * scale to out (f32 / f64).
+struct Sink {
+    double* acc = nullptr;
+    void* out = nullptr;
+    bool f64 = true;
+    double scale = 1.0;
+};
+
+// Traces samples [s_begin, s_end) of the shard in chunks of `chunk` and reduces them into
+// the sink. Events: ev[0] before the first trace launch, ev[1] after the last one, ev[2]
+// after the last reduction. Chunk schedule: one launch into chunk partials. Pool schedule:
+// per-sample radiance in batches of whole chunks that fit sample_buf_cap; with more than
+// one batch the sums run through acc (the sink's, or acc_tmp), which keeps the additions
+// in the one-batch order.
+static int run_range(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, int s_begin, int s_end, int chunk,
+                     hipStream_t stream, const Sink& sink)
 {
     const int n_rows = rt_rows_in_shard(p->height, p->row_begin, p->row_stride);
-    const int n_chunks = (s_end - s_begin + chunk - 1) / chunk;
     const long long n_px = (long long)n_rows * p->width;
+    const size_t px = (size_t)std::max<long long>(n_px, 1);
 
     rtk::KParams K;
     std::memset(&K, 0, sizeof K);
@@ -547,26 +583,14 @@ static int launch_samples(rt_ctx* c, const rt_camera* cam, const rt_render_param
     K.seed = p->render_seed;
     K.width = p->width;
     K.height = p->height;
-    K.spp = s_end;
-    K.sample_begin = s_begin;
     K.max_depth = p->max_depth;
     K.spp_chunk = chunk;
-    K.n_chunks = n_chunks;
     K.row_begin = p->row_begin;
     K.row_stride = p->row_stride;
     K.n_rows = n_rows;
     K.tiles_x = (p->width + 7) / 8;
     K.tiles_y = (n_rows + 7) / 8;
 
-    const size_t need = (size_t)n_chunks * (size_t)std::max<long long>(n_px, 1) * 3 * sizeof(double);
-    if (need > c->partial_cap) {
-        HIP_TRY(hipStreamSynchronize(stream));
-        (void)hipFree(c->partial);
-        c->partial = nullptr;
-        c->partial_cap = 0;
-        HIP_TRY(hipMalloc((void**)&c->partial, need));
-        c->partial_cap = need;
-    }
     const bool count = p->count_work != 0;
     // conservative f32 slab tests need every ray origin within 2M of the origin (flatten.cpp):
     // hit points are inside the scene bounds; check the camera (+ lens) here
@@ -578,24 +602,66 @@ static int launch_samples(rt_ctx* c, const rt_camera* cam, const rt_render_param
     o.features = c->features;
     o.slab32 = c->opt_slab32 && c->pad_extent > 0.0 && cam_mag <= 2.0 * c->pad_extent;
     o.lds_stack = c->opt_lds && c->S.stack_entries <= kMaxLdsStack;
+    o.count = count;
+    o.pool = c->opt_pool;
     // the TLAS in LDS (read-only, shared by the block) when it fits the per-block budget
     rtk::SceneDev S = c->S;
     S.n_lds_nodes = c->opt_lds_nodes ? std::min(c->n_tlas_nodes, kMaxLdsNodes) : 0;
-    o.count = count;
-    if (count) HIP_TRY(hipMemsetAsync(c->counters, 0, 8 * sizeof(unsigned long long), stream));
-    rtk::KParams* dK = c->params + c->param_slot;
-    c->param_slot = (c->param_slot + 1) % kParamSlots;
-    HIP_TRY(hipMemcpyAsync(dK, &K, sizeof K, hipMemcpyHostToDevice, stream));
+
+    // batches of whole chunks
+    const long long total = s_end - s_begin;
+    long long batch = total;
+    if (o.pool) {
+        const long long fit = (long long)(c->sample_buf_cap / (px * 3 * sizeof(double)));
+        batch = std::max<long long>(chunk, fit / chunk * chunk);
+        batch = std::min(batch, total);
+    }
+    const int n_batches = (int)((total + batch - 1) / batch);
+    double* acc = sink.acc;
+    if (o.pool && n_batches > 1 && !acc) {
+        int rc = grow(c, stream, c->acc_tmp, c->acc_tmp_cap, px * 3 * sizeof(double));
+        if (rc) return rc;
+        HIP_TRY(hipMemsetAsync(c->acc_tmp, 0, px * 3 * sizeof(double), stream));
+        acc = c->acc_tmp;
+    }
+    const int max_chunks = (int)((batch + chunk - 1) / chunk);
+    const size_t need = o.pool ? (size_t)batch * px * 3 * sizeof(double) : (size_t)max_chunks * px * 3 * sizeof(double);
+    int rc = grow(c, stream, c->partial, c->partial_cap, need);
+    if (rc) return rc;
+    if (count) HIP_TRY(hipMemsetAsync(c->counters, 0, kCounters * sizeof(unsigned long long), stream));
     HIP_TRY(hipEventRecord(c->ev[0], stream));
-    HIP_TRY(rtk::launch_trace(S, K, dK, c->partial, c->counters, o, stream));
-    HIP_TRY(hipEventRecord(c->ev[1], stream));
+    for (int bi = 0; bi < n_batches; ++bi) {
+        const int b0 = s_begin + (int)(bi * batch);
+        const int b1 = (int)std::min<long long>(s_end, b0 + batch);
+        K.sample_begin = b0;
+        K.spp = b1;
+        K.n_chunks = (b1 - b0 + chunk - 1) / chunk;
+        rtk::KParams* dK = c->params + c->param_slot;
+        c->param_slot = (c->param_slot + 1) % kParamSlots;
+        HIP_TRY(hipMemcpyAsync(dK, &K, sizeof K, hipMemcpyHostToDevice, stream));
+        HIP_TRY(rtk::launch_trace(S, K, dK, c->partial, c->counters, c->work, o, stream));
+        if (bi == n_batches - 1) HIP_TRY(hipEventRecord(c->ev[1], stream));
+        if (!o.pool) {
+            if (sink.acc) HIP_TRY(rtk::launch_accumulate(c->partial, sink.acc, n_px, K.n_chunks, stream));
+            else HIP_TRY(rtk::launch_reduce(c->partial, sink.out, sink.f64, n_px, K.n_chunks, sink.scale, stream));
+        } else {
+            HIP_TRY(rtk::launch_reduce_samples(c->partial, acc, sink.out, sink.f64, n_px, b1 - b0, chunk, sink.scale,
+                                               stream));
+        }
+    }
+    if (o.pool && acc && !sink.acc)  // resolve the running sums: 0.0 + sum, times scale, as one batch does
+        HIP_TRY(rtk::launch_reduce(acc, sink.out, sink.f64, n_px, 1, sink.scale, stream));
+    HIP_TRY(hipEventRecord(c->ev[2], stream));
+
     c->stats.lds_nodes = S.n_lds_nodes;
     c->stats.variant_features = (int32_t)rtk::variant_features(o.features);
     c->stats.slab32 = o.slab32;
     c->stats.lds_stack = o.lds_stack;
-    c->stats.samples = (uint64_t)n_px * (uint64_t)(s_end - s_begin);
-    c->stats.n_items = (uint64_t)n_px * (uint64_t)n_chunks;
-    c->stats.n_chunks = n_chunks;
+    c->stats.schedule = o.pool;
+    c->stats.n_batches = n_batches;
+    c->stats.samples = (uint64_t)n_px * (uint64_t)total;
+    c->stats.n_chunks = (int32_t)((total + chunk - 1) / chunk);
+    c->stats.n_items = (uint64_t)n_px * (uint64_t)c->stats.n_chunks;
     c->stats.spp_chunk = chunk;
     c->stats.node_bytes = (int32_t)sizeof(rt_bvh_node);
     c->stats.prim_bytes = (int32_t)sizeof(rt_prim);
@@ -603,7 +669,6 @@ static int launch_samples(rt_ctx* c, const rt_camera* cam, const rt_render_param
     c->pending_stats = true;
     c->pending_counts = count;
     if (!c->stats.samples) c->stats.casts = c->stats.node_visits = c->stats.prim_tests = 0;
-    n_chunks_out = n_chunks;
     return RT_OK;
 }
 
@@ -639,12 +704,12 @@ int rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, void* 
         int rc = out_staging(c, out_bytes, dev_out);
         if (rc) return rc;
     }
-    int n_chunks = 0;
-    int rc = launch_samples(c, cam, p, 0, p->spp, chunk, stream, n_chunks);
+    Sink sink;
+    sink.out = dev_out;
+    sink.f64 = p->out_format == RT_OUT_F64;
+    sink.scale = 1.0 / (double)p->spp;
+    int rc = run_range(c, cam, p, 0, p->spp, chunk, stream, sink);
     if (rc) return rc;
-    HIP_TRY(rtk::launch_reduce(c->partial, dev_out, p->out_format == RT_OUT_F64, n_px, n_chunks,
-                               1.0 / (double)p->spp, stream));
-    HIP_TRY(hipEventRecord(c->ev[2], stream));
     if (!p->out_on_device) {
         HIP_TRY(hipMemcpyAsync(out, dev_out, out_bytes, hipMemcpyDeviceToHost, stream));
         HIP_TRY(hipStreamSynchronize(stream));
@@ -715,11 +780,10 @@ int rt_accum_add(rt_ctx* c, rt_accum* a, const rt_camera* cam, const rt_render_p
     HIP_TRY(hipSetDevice(c->device));
     hipStream_t stream = p->stream ? (hipStream_t)p->stream : c->stream;
     if (stream != a->last_stream) HIP_TRY(hipStreamSynchronize(a->last_stream));
-    int n_chunks = 0;
-    int rc = launch_samples(c, cam, p, (int)a->done, (int)(a->done + sample_count), a->chunk, stream, n_chunks);
+    Sink sink;
+    sink.acc = a->sums;
+    int rc = run_range(c, cam, p, (int)a->done, (int)(a->done + sample_count), a->chunk, stream, sink);
     if (rc) return rc;
-    HIP_TRY(rtk::launch_accumulate(c->partial, a->sums, a->n_px, n_chunks, stream));
-    HIP_TRY(hipEventRecord(c->ev[2], stream));
     a->done += sample_count;
     a->last_stream = stream;
     return RT_OK;
@@ -815,7 +879,7 @@ int rt_last_stats(rt_ctx* c, rt_stats* out)
         c->stats.kernel_ms = a;
         c->stats.reduce_ms = b;
         if (c->pending_counts) {
-            unsigned long long h[8];
+            unsigned long long h[kCounters];
             HIP_TRY(hipMemcpy(h, c->counters, sizeof h, hipMemcpyDeviceToHost));
             c->stats.casts = h[0];
             c->stats.node_visits = h[1];
@@ -825,10 +889,13 @@ int rt_last_stats(rt_ctx* c, rt_stats* out)
             c->stats.cycles_shade = h[5];
             c->stats.wave_steps = h[6];
             c->stats.wave_node_steps = h[7];
+            c->stats.cycles_nodes = h[8];
+            c->stats.cycles_leaves = h[9];
         } else {
             c->stats.casts = c->stats.node_visits = c->stats.prim_tests = 0;
             c->stats.cycles_camera = c->stats.cycles_trace = c->stats.cycles_shade = 0;
             c->stats.wave_steps = c->stats.wave_node_steps = 0;
+            c->stats.cycles_nodes = c->stats.cycles_leaves = 0;
         }
         c->pending_stats = false;
     }
@@ -865,6 +932,13 @@ int rt_ctx_set_variant(rt_ctx* c, int slab32, int lds_stack, int lds_nodes)
     c->opt_slab32 = slab32;
     c->opt_lds = lds_stack;
     c->opt_lds_nodes = lds_nodes;
+    return RT_OK;
+}
+
+int rt_ctx_set_schedule(rt_ctx* c, int schedule)
+{
+    if (!c || (schedule != RT_SCHED_CHUNKS && schedule != RT_SCHED_POOL)) return fail(RT_ERR_INVALID, "bad schedule");
+    c->opt_pool = schedule == RT_SCHED_POOL;
     return RT_OK;
 }
 

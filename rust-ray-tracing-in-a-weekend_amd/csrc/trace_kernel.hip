@@ -21,6 +21,8 @@
 // Built with -ffp-contract=off: bit-for-bit the operation order of the reference.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "rt/rt_numerics.h"
 #include "rt/rt_scene.h"
 #include "trace_kernel.hpp"
@@ -61,6 +63,7 @@ struct Keyed {                 // coordinates of the medium's keyed draw
 struct Count {
     uint32_t casts, nodes, prims;
     uint32_t wave_steps, wave_nodes;  // loop iterations the wave executed (counted by its first active lane)
+    uint64_t t_nodes, t_leaves;       // wave-cycles in node-visit loops / leaf tests (same in every lane)
 };
 // COUNT only: true in exactly one active lane of the wave
 __device__ __forceinline__ bool first_active_lane()
@@ -457,13 +460,17 @@ __device__ __forceinline__ bool traverse(const SceneDev& S, int root, const Ray&
             }
         }
     } else if constexpr (C::LOOP == 1) {
+        uint64_t t0 = 0;
         while (cur != RT_DONE) {
+            if (C::COUNT) t0 = __builtin_amdgcn_s_memtime();
             while (cur >= 0) {
                 if (C::COUNT && first_active_lane()) cnt.wave_nodes++;
                 cur = visit(cur);
             }
+            if (C::COUNT) { const uint64_t t = __builtin_amdgcn_s_memtime(); cnt.t_nodes += t - t0; t0 = t; }
             if (cur == RT_DONE) break;
             do_leaf(cur);
+            if (C::COUNT) cnt.t_leaves += __builtin_amdgcn_s_memtime() - t0;
             cur = sp == sp0 ? RT_DONE : stack[--sp];
         }
     } else {
@@ -991,7 +998,7 @@ __global__ void __launch_bounds__(256, min_waves<C>()) trace_chunks(SceneDev S, 
     if (!lane_work(P, w)) return;
     StackT<C> stack;
     if constexpr (C::LDS) stack.base = rt_lds + threadIdx.x;
-    Count cnt{0, 0, 0, 0, 0};
+    Count cnt{0, 0, 0, 0, 0, 0, 0};
     uint64_t t_cam = 0, t_trace = 0, t_shade = 0, t_prev = 0;
     if (C::COUNT) t_prev = __builtin_amdgcn_s_memtime();
     double sum_r = 0.0, sum_g = 0.0, sum_b = 0.0;
@@ -1052,7 +1059,188 @@ __global__ void __launch_bounds__(256, min_waves<C>()) trace_chunks(SceneDev S, 
             atomicAdd(&counters[3], (unsigned long long)t_cam);
             atomicAdd(&counters[4], (unsigned long long)t_trace);
             atomicAdd(&counters[5], (unsigned long long)t_shade);
+            atomicAdd(&counters[8], (unsigned long long)cnt.t_nodes);
+            atomicAdd(&counters[9], (unsigned long long)cnt.t_leaves);
         }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Sample-pool schedule. Persistent waves take work blocks (one 8x8 tile x one chunk of
+// samples) from a global counter; inside the wave, a lane whose path ended takes the
+// block's next (pixel, sample) unit at once (ballot + mbcnt), so lanes do not idle until
+// the last blocks run out. Each sample's radiance goes to its own slot of a
+// [sample][pixel] buffer; reduce_samples then sums every pixel's samples in sample order,
+// so the image does not depend on which lane or wave computed a sample.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ unsigned lanes_below(uint64_t mask)
+{
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+}
+
+template <class C>
+__global__ void __launch_bounds__(256, min_waves<C>()) trace_pool(SceneDev S, const KParams* __restrict__ Pp,
+                                                                  double* __restrict__ samples,
+                                                                  unsigned long long* __restrict__ counters,
+                                                                  unsigned* __restrict__ work)
+{
+    const KParams& P = *Pp;
+    if (S.n_lds_nodes > 0) {
+        const int off = C::LDS ? S.stack_entries * 256 : 0;
+        uint4* dst = reinterpret_cast<uint4*>(rt_lds + off);
+        const uint4* src = reinterpret_cast<const uint4*>(S.nodes);
+        for (int i = threadIdx.x; i < S.n_lds_nodes * 4; i += 256) dst[i] = src[i];
+        __syncthreads();
+    }
+    StackT<C> stack;
+    if constexpr (C::LDS) stack.base = rt_lds + threadIdx.x;
+    Count cnt{0, 0, 0, 0, 0, 0, 0};
+    uint64_t t_cam = 0, t_trace = 0, t_shade = 0, t_prev = 0;
+    if (C::COUNT) t_prev = __builtin_amdgcn_s_memtime();
+    const int lane = threadIdx.x & 63;
+    const unsigned n_tiles = (unsigned)P.tiles_x * (unsigned)P.tiles_y;
+    const unsigned n_blocks = n_tiles * (unsigned)P.n_chunks;
+    const size_t n_px = (size_t)P.n_rows * (size_t)P.width;
+    // current work block (wave-uniform)
+    unsigned blk_units = 0, blk_next = 0, nvalid = 1;
+    int tx0 = 0, tk0 = 0, vw = 1, s0 = 0;
+    bool exhausted = false;
+    // lane state
+    bool active = false, new_sample = false;
+    int x = 0, k = 0, s = 0, depth = 0;
+    double cr = 0, cg = 0, cb = 0, Tr = 1, Tg = 1, Tb = 1;
+    Keyed key{P.seed, 0, 0, 0};
+    rt_stream st;
+    Ray r;
+    for (;;) {
+        uint64_t need = __ballot(!active);
+        while (need != 0 && !exhausted) {
+            if (blk_next == blk_units) {
+                unsigned b = 0;
+                if (lane == 0) b = atomicAdd(work, 1u);
+                b = __builtin_amdgcn_readfirstlane(b);
+                if (b >= n_blocks) {
+                    exhausted = true;
+                    break;
+                }
+                const unsigned chunk = b / n_tiles, tile = b - chunk * n_tiles;
+                tx0 = (int)(tile % (unsigned)P.tiles_x) * 8;
+                tk0 = (int)(tile / (unsigned)P.tiles_x) * 8;
+                vw = min(8, P.width - tx0);
+                nvalid = (unsigned)(vw * min(8, P.n_rows - tk0));
+                s0 = P.sample_begin + (int)chunk * P.spp_chunk;
+                blk_units = nvalid * (unsigned)(min(P.spp, s0 + P.spp_chunk) - s0);
+                blk_next = 0;
+            }
+            const unsigned rank = lanes_below(need);
+            const unsigned take = min((unsigned)__popcll(need), blk_units - blk_next);
+            if (!active && rank < take) {
+                const unsigned u = blk_next + rank;
+                const unsigned si = u / nvalid, p = u - si * nvalid;
+                x = tx0 + (int)(p % (unsigned)vw);
+                k = tk0 + (int)(p / (unsigned)vw);
+                s = s0 + (int)si;
+                active = true;
+                new_sample = true;
+            }
+            blk_next += take;
+            need = __ballot(!active);
+        }
+        if (!__any(active)) break;
+        if (C::COUNT && first_active_lane()) cnt.wave_steps++;
+        if (!active) continue;
+        if (new_sample) {
+            new_sample = false;
+            const int y = P.row_begin + k * P.row_stride;
+            key.pixel = (uint32_t)y * (uint32_t)P.width + (uint32_t)x;
+            key.sample = (uint32_t)s;
+            rt_stream_init(&st, P.seed, key.pixel, (uint32_t)s, RT_STREAM_MAIN);
+            camera_ray(P, x, y, st, r);
+            finish_ray<C>(r);
+            Tr = Tg = Tb = 1.0;
+            cr = cg = cb = 0.0;
+            depth = P.max_depth;
+        }
+        if (C::COUNT) { const uint64_t t = __builtin_amdgcn_s_memtime(); t_cam += t - t_prev; t_prev = t; }
+        bool cont = false;
+        if (depth > 0) {  // main.rs:21-23: depth 0 is black
+            key.bounce = (uint32_t)(P.max_depth - depth);
+            if (C::COUNT) cnt.casts++;
+            Hit h;
+            const bool hit = trace_world<C>(S, r, h, stack, key, cnt);
+            if (C::COUNT) { const uint64_t t = __builtin_amdgcn_s_memtime(); t_trace += t - t_prev; t_prev = t; }
+            if (!hit) {  // main.rs:37: background
+                cr = cr + Tr * P.bg[0];
+                cg = cg + Tg * P.bg[1];
+                cb = cb + Tb * P.bg[2];
+            } else {
+                cont = shade<C>(S, P, h, r, st, Tr, Tg, Tb, cr, cg, cb);
+            }
+        }
+        if (C::COUNT) { const uint64_t t = __builtin_amdgcn_s_memtime(); t_shade += t - t_prev; t_prev = t; }
+        if (cont) {
+            depth -= 1;
+        } else {
+            double* o = samples + ((size_t)(s - P.sample_begin) * n_px + (size_t)k * P.width + x) * 3;
+            o[0] = cr;
+            o[1] = cg;
+            o[2] = cb;
+            active = false;
+        }
+    }
+    if (C::COUNT) {
+        atomicAdd(&counters[0], (unsigned long long)cnt.casts);
+        atomicAdd(&counters[1], (unsigned long long)cnt.nodes);
+        atomicAdd(&counters[2], (unsigned long long)cnt.prims);
+        atomicAdd(&counters[6], (unsigned long long)cnt.wave_steps);
+        atomicAdd(&counters[7], (unsigned long long)cnt.wave_nodes);
+        if (lane == 0) {  // every lane stays in the loop to the end: lane 0 saw the wave's whole time
+            atomicAdd(&counters[3], (unsigned long long)t_cam);
+            atomicAdd(&counters[4], (unsigned long long)t_trace);
+            atomicAdd(&counters[5], (unsigned long long)t_shade);
+            atomicAdd(&counters[8], (unsigned long long)cnt.t_nodes);
+            atomicAdd(&counters[9], (unsigned long long)cnt.t_leaves);
+        }
+    }
+}
+
+// Per pixel: chunk sums of consecutive samples (chunk order, each from 0.0), added in
+// chunk order to acc (acc mode) or to 0.0 and scaled into out: the same additions, in the
+// same order, as the chunk schedule's lane sums + reduce_chunks.
+template <typename T, bool ACC>
+__global__ void __launch_bounds__(256) reduce_samples(const double* __restrict__ samples, double* __restrict__ acc,
+                                                      T* __restrict__ out, long long n_px, int n_samples, int chunk,
+                                                      double scale)
+{
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n_px) return;
+    double r = 0.0, g = 0.0, b = 0.0;
+    if (ACC) {
+        r = acc[3 * i + 0];
+        g = acc[3 * i + 1];
+        b = acc[3 * i + 2];
+    }
+    for (int c0 = 0; c0 < n_samples; c0 += chunk) {
+        const int c1 = min(n_samples, c0 + chunk);
+        double cr = 0.0, cg = 0.0, cb = 0.0;
+        for (int j = c0; j < c1; ++j) {
+            const double* p = samples + ((size_t)j * n_px + i) * 3;
+            cr = cr + p[0];
+            cg = cg + p[1];
+            cb = cb + p[2];
+        }
+        r = r + cr;
+        g = g + cg;
+        b = b + cb;
+    }
+    if (ACC) {
+        acc[3 * i + 0] = r;
+        acc[3 * i + 1] = g;
+        acc[3 * i + 2] = b;
+    } else {
+        out[3 * i + 0] = (T)(r * scale);
+        out[3 * i + 1] = (T)(g * scale);
+        out[3 * i + 2] = (T)(b * scale);
     }
 }
 
@@ -1127,32 +1315,67 @@ __global__ void eval_numerics(int fn, const double* x, const double* y, const do
 // ---------------------------------------------------------------------------
 // host-side launchers
 // ---------------------------------------------------------------------------
-template <uint32_t F, bool S32, bool LDS, bool COUNT>
-static void launch_one(unsigned blocks, hipStream_t stream, const SceneDev& S, const KParams* P, double* partial,
-                       unsigned long long* counters, bool nall)
+struct Launch {
+    const SceneDev* S;
+    const KParams* P;
+    double* out;                   // chunk partials (chunk schedule) or per-sample radiance (pool)
+    unsigned long long* counters;
+    unsigned* work;                // pool: work-block counter
+    int pool;
+    unsigned long long n_blocks;   // 8x8 tiles x chunks
+};
+
+// Persistent grid for the pool schedule: as many blocks as fit on the device at once.
+template <class K>
+static unsigned resident_blocks(K kernel, size_t lds)
 {
+    static int cus = 0;
+    if (!cus) {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+    }
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, 256, lds) != hipSuccess || per_cu <= 0) per_cu = 1;
+    return (unsigned)(cus * per_cu);
+}
+
+template <uint32_t F, bool S32, bool LDS, bool COUNT>
+static void launch_one(const Launch& L, hipStream_t stream, bool nall)
+{
+    const SceneDev& S = *L.S;
     const size_t lds = (LDS ? (size_t)S.stack_entries * 256 * sizeof(int) : 0) + (size_t)S.n_lds_nodes * 64;
+    if (L.pool) {
+        auto go = [&](auto kernel) {
+            const unsigned nb = std::min<unsigned long long>(resident_blocks(kernel, lds), (L.n_blocks + 3) / 4);
+            hipLaunchKernelGGL(kernel, dim3(nb), dim3(256), lds, stream, S, L.P, L.out, L.counters, L.work);
+        };
+        if (nall) go(trace_pool<Cfg<F, S32, LDS, true, COUNT>>);
+        else go(trace_pool<Cfg<F, S32, LDS, false, COUNT>>);
+        return;
+    }
+    const unsigned nb = (unsigned)((L.n_blocks + 3) / 4);
     if (nall)
-        hipLaunchKernelGGL((trace_chunks<Cfg<F, S32, LDS, true, COUNT>>), dim3(blocks), dim3(256), lds, stream, S,
-                           P, partial, counters);
+        hipLaunchKernelGGL((trace_chunks<Cfg<F, S32, LDS, true, COUNT>>), dim3(nb), dim3(256), lds, stream, S,
+                           L.P, L.out, L.counters);
     else
-        hipLaunchKernelGGL((trace_chunks<Cfg<F, S32, LDS, false, COUNT>>), dim3(blocks), dim3(256), lds, stream, S,
-                           P, partial, counters);
+        hipLaunchKernelGGL((trace_chunks<Cfg<F, S32, LDS, false, COUNT>>), dim3(nb), dim3(256), lds, stream, S,
+                           L.P, L.out, L.counters);
 }
 
 // Variant table: feature set x slab precision x loop form. The launcher takes the
 // smallest feature set covering the scene.
 template <uint32_t F, bool COUNT>
-static void launch_f(int slab32, int lds, unsigned blocks, hipStream_t stream, const SceneDev& S, const KParams* P,
-                     double* partial, unsigned long long* counters)
+static void launch_f(const Launch& L, int slab32, int lds, hipStream_t stream)
 {
+    const SceneDev& S = *L.S;
     const bool nall = S.n_lds_nodes > 0 && S.n_lds_nodes == S.n_tlas_nodes;
     if (slab32) {
-        if (lds) launch_one<F, true, true, COUNT>(blocks, stream, S, P, partial, counters, nall);
-        else launch_one<F, true, false, COUNT>(blocks, stream, S, P, partial, counters, nall);
+        if (lds) launch_one<F, true, true, COUNT>(L, stream, nall);
+        else launch_one<F, true, false, COUNT>(L, stream, nall);
     } else {
-        if (lds) launch_one<F, false, true, COUNT>(blocks, stream, S, P, partial, counters, nall);
-        else launch_one<F, false, false, COUNT>(blocks, stream, S, P, partial, counters, nall);
+        if (lds) launch_one<F, false, true, COUNT>(L, stream, nall);
+        else launch_one<F, false, false, COUNT>(L, stream, nall);
     }
 }
 
@@ -1163,24 +1386,50 @@ uint32_t variant_features(uint32_t scene_features)
     return FEAT_ALL;
 }
 
-hipError_t launch_trace(const SceneDev& S, const KParams& Ph, const KParams* P, double* partial,
-                        unsigned long long* counters, const LaunchOpts& o, hipStream_t stream)
+hipError_t launch_trace(const SceneDev& S, const KParams& Ph, const KParams* P, double* out,
+                        unsigned long long* counters, unsigned* work, const LaunchOpts& o, hipStream_t stream)
 {
-    const long long waves = (long long)Ph.tiles_x * Ph.tiles_y * Ph.n_chunks;
-    const long long blocks = (waves + 3) / 4;
-    if (blocks <= 0) return hipSuccess;
-    if (blocks > 0x7fffffffLL) return hipErrorInvalidValue;
-    const unsigned nb = (unsigned)blocks;
+    Launch L;
+    L.S = &S;
+    L.P = P;
+    L.out = out;
+    L.counters = counters;
+    L.work = work;
+    L.pool = o.pool;
+    L.n_blocks = (unsigned long long)Ph.tiles_x * Ph.tiles_y * Ph.n_chunks;  // waves of the chunk schedule
+    if (L.n_blocks == 0) return hipSuccess;
+    if (L.n_blocks > 0xfffffff0ULL) return hipErrorInvalidValue;
+    if (o.pool) {
+        const hipError_t e = hipMemsetAsync(work, 0, sizeof(unsigned), stream);
+        if (e != hipSuccess) return e;
+    }
     const uint32_t f = variant_features(o.features);
     if (o.count) {
-        if (f == FEAT_SET_SPHERES) launch_f<FEAT_SET_SPHERES, true>(o.slab32, o.lds_stack, nb, stream, S, P, partial, counters);
-        else if (f == FEAT_SET_RECTINST) launch_f<FEAT_SET_RECTINST, true>(o.slab32, o.lds_stack, nb, stream, S, P, partial, counters);
-        else launch_f<FEAT_ALL, true>(o.slab32, o.lds_stack, nb, stream, S, P, partial, counters);
+        if (f == FEAT_SET_SPHERES) launch_f<FEAT_SET_SPHERES, true>(L, o.slab32, o.lds_stack, stream);
+        else if (f == FEAT_SET_RECTINST) launch_f<FEAT_SET_RECTINST, true>(L, o.slab32, o.lds_stack, stream);
+        else launch_f<FEAT_ALL, true>(L, o.slab32, o.lds_stack, stream);
     } else {
-        if (f == FEAT_SET_SPHERES) launch_f<FEAT_SET_SPHERES, false>(o.slab32, o.lds_stack, nb, stream, S, P, partial, counters);
-        else if (f == FEAT_SET_RECTINST) launch_f<FEAT_SET_RECTINST, false>(o.slab32, o.lds_stack, nb, stream, S, P, partial, counters);
-        else launch_f<FEAT_ALL, false>(o.slab32, o.lds_stack, nb, stream, S, P, partial, counters);
+        if (f == FEAT_SET_SPHERES) launch_f<FEAT_SET_SPHERES, false>(L, o.slab32, o.lds_stack, stream);
+        else if (f == FEAT_SET_RECTINST) launch_f<FEAT_SET_RECTINST, false>(L, o.slab32, o.lds_stack, stream);
+        else launch_f<FEAT_ALL, false>(L, o.slab32, o.lds_stack, stream);
     }
+    return hipGetLastError();
+}
+
+hipError_t launch_reduce_samples(const double* samples, double* acc, void* out, bool f64, long long n_px,
+                                 int n_samples, int chunk, double scale, hipStream_t stream)
+{
+    const long long blocks = (n_px + 255) / 256;
+    if (blocks <= 0) return hipSuccess;
+    if (acc)
+        hipLaunchKernelGGL((reduce_samples<double, true>), dim3((unsigned)blocks), dim3(256), 0, stream, samples, acc,
+                           (double*)nullptr, n_px, n_samples, chunk, scale);
+    else if (f64)
+        hipLaunchKernelGGL((reduce_samples<double, false>), dim3((unsigned)blocks), dim3(256), 0, stream, samples,
+                           (double*)nullptr, (double*)out, n_px, n_samples, chunk, scale);
+    else
+        hipLaunchKernelGGL((reduce_samples<float, false>), dim3((unsigned)blocks), dim3(256), 0, stream, samples,
+                           (double*)nullptr, (float*)out, n_px, n_samples, chunk, scale);
     return hipGetLastError();
 }
 

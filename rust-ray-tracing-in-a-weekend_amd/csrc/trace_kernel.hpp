@@ -56,12 +56,19 @@ struct LaunchOpts {
     int slab32;         // conservative f32 slab tests
     int lds_stack;      // traversal stack in LDS (1) or scratch (0)
     int count;          // count_work variant
+    int pool;           // 1: sample-pool schedule (per-sample output), 0: chunk schedule (partials)
 };
 
 uint32_t variant_features(uint32_t scene_features);
 // Ph: host copy of the params (grid size); P: the same params in device memory
-hipError_t launch_trace(const SceneDev& S, const KParams& Ph, const KParams* P, double* partial,
-                        unsigned long long* counters, const LaunchOpts& o, hipStream_t stream);
+// chunk schedule: out = chunk partials [n_chunks][n_px][3]; pool schedule: out = per-sample
+// radiance [spp - sample_begin][n_px][3], work = one device counter
+hipError_t launch_trace(const SceneDev& S, const KParams& Ph, const KParams* P, double* out,
+                        unsigned long long* counters, unsigned* work, const LaunchOpts& o, hipStream_t stream);
+// pool schedule: per pixel, chunk sums of its samples (sample order) added to acc, or (acc
+// null) to 0.0 and written scaled to out
+hipError_t launch_reduce_samples(const double* samples, double* acc, void* out, bool f64, long long n_px,
+                                 int n_samples, int chunk, double scale, hipStream_t stream);
 hipError_t launch_reduce(const double* partial, void* out, bool f64, long long n_px, int n_chunks, double scale,
                          hipStream_t stream);
 // acc[i] += chunk partials in chunk order (progressive accumulation, rt_accum_add)

@@ -32,6 +32,8 @@ SCENES = {"random": 0, "two_spheres": 1, "two_perlin": 2, "earth": 3, "simple_li
 SCENES_NEEDING_IMAGE = (3, 7)
 
 RT_OUT_F32, RT_OUT_F64 = 0, 1
+RT_SCHED_CHUNKS = 0
+RT_SCHED_POOL = 1
 RT_ACCEL_SAH = 0
 RT_ACCEL_LINEAR = 1     # hit_hittables linear scan (hittable.rs:31-41)
 RT_ACCEL_MEDIAN = 2     # the reference BvhNode hierarchy (hittable.rs:77-130)
@@ -48,7 +50,7 @@ EXPORTED = [
     "rt_scene_preset_get", "rt_scene_camera", "rt_world_flatten", "rt_ctx_upload_soa",
     "rt_ctx_upload_world", "rt_render", "rt_rows_in_shard", "rt_last_stats", "rt_write_ppm",
     "rt_ctx_set_variant", "rt_device_eval", "rt_accum_create", "rt_accum_destroy", "rt_accum_add",
-    "rt_accum_get", "rt_accum_set", "rt_accum_resolve", "rt_render_progressive",
+    "rt_accum_get", "rt_accum_set", "rt_accum_resolve", "rt_render_progressive", "rt_ctx_set_schedule",
 ]
 
 # int (*rt_progress_fn)(void* user, int64_t samples_done, int64_t samples_total)
@@ -112,7 +114,9 @@ class Stats(ctypes.Structure):
                 ("slab32", ctypes.c_int32), ("lds_stack", ctypes.c_int32), ("lds_nodes", ctypes.c_int32),
                 ("cycles_camera", ctypes.c_uint64),
                 ("cycles_trace", ctypes.c_uint64), ("cycles_shade", ctypes.c_uint64),
-                ("wave_steps", ctypes.c_uint64), ("wave_node_steps", ctypes.c_uint64)]
+                ("wave_steps", ctypes.c_uint64), ("wave_node_steps", ctypes.c_uint64),
+                ("cycles_nodes", ctypes.c_uint64), ("cycles_leaves", ctypes.c_uint64),
+                ("schedule", ctypes.c_int32), ("n_batches", ctypes.c_int32)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -158,6 +162,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "rt_write_ppm": ([P, I, I, ctypes.c_char_p], I),
         "rt_device_eval": ([P, I, P, P, P, P, I], I), "rt_ctx_set_variant": ([P, I, I, I], I),
         "rt_accum_create": ([P, ctypes.POINTER(RenderParams), ctypes.POINTER(P)], I),
+        "rt_ctx_set_schedule": ([P, I], I),
         "rt_accum_destroy": ([P], None),
         "rt_accum_add": ([P, P, ctypes.POINTER(Camera), ctypes.POINTER(RenderParams), I], I),
         "rt_accum_get": ([P, P, ctypes.POINTER(ctypes.c_int64)], I),
@@ -400,6 +405,9 @@ class Renderer:
 
     def accumulator(self, params: RenderParams) -> "Accumulator":
         return Accumulator(self, params)
+
+    def set_schedule(self, schedule: int):
+        _check(self.lib.rt_ctx_set_schedule(self.h, schedule), "rt_ctx_set_schedule")
 
     def set_variant(self, slab32: int = 1, lds_stack: int = 1, lds_nodes: int = 1):
         _check(self.lib.rt_ctx_set_variant(self.h, slab32, lds_stack, lds_nodes), "rt_ctx_set_variant")

@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--depth", type=int, default=50)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--variants", default="1:1:1,1:1:0", help="slab32:lds_stack:lds_nodes tuples")
+    ap.add_argument("--sched", default="", help="comma list of schedules to A/B: 0 chunks, 1 pool")
     ap.add_argument("--chunks", default="", help="comma list of spp_chunk values to A/B")
     ap.add_argument("--accel", default="", help="comma list of accel modes to A/B: 0 SAH, 1 LINEAR, 2 MEDIAN")
     ap.add_argument("--bvh", default="", help="comma list of CI:MAXLEAF[:LEAFN] BVH builds to A/B (default variant)")
@@ -64,6 +65,31 @@ def main():
         print(f"variant {v}: median {ms:.2f} ms  min {min(t):.2f} ms  "
               f"-> {W * H * args.spp / ms / 1e3:.1f} Msamples/s")
     print("last variant features/slab32/lds_stack:", used)
+    if args.sched:
+        scheds = [int(x) for x in args.sched.split(",")]
+        r.set_variant(*variants[0])
+        st_t, st_img, occ = {m: [] for m in scheds}, {}, {}
+        for m in scheds:
+            r.set_schedule(m)
+            st_img[m] = r.render(cam, rt.Renderer.params(W, H, 4, args.depth, bg, 1, row_stride=8,
+                                                         out_format=rt.RT_OUT_F64))
+            ck = max(1, (args.spp + 15) // 16)
+            r.render(cam, rt.Renderer.params(W, H, min(args.spp, 2 * ck), args.depth, bg, 1, spp_chunk=ck,
+                                             count_work=1))
+            q = r.stats()
+            occ[m] = q.casts / max(64 * q.wave_steps, 1)
+        for rnd in range(args.rounds + 1):
+            for m in scheds:
+                r.set_schedule(m)
+                r.render(cam, p, out)
+                if rnd > 0:
+                    st_t[m].append(r.stats().kernel_ms)
+        for m in scheds:
+            ms = float(np.median(st_t[m]))
+            print(f"schedule {m}: median {ms:.2f} ms -> {W * H * args.spp / ms / 1e3:.1f} Msamples/s  "
+                  f"bounce-loop occupancy {occ[m]:.3f}  image == schedule {scheds[0]}: "
+                  f"{np.array_equal(st_img[m], st_img[scheds[0]])}")
+        r.set_schedule(1)
     if args.accel:
         modes = [int(x) for x in args.accel.split(",")]
         names = {0: "SAH", 1: "LINEAR", 2: "MEDIAN"}
@@ -109,16 +135,20 @@ def main():
                   f"median {float(np.median(bt[b])):.2f} ms")
         os.environ.pop("RT_BVH_CI"); os.environ.pop("RT_BVH_MAXLEAF")
         r.upload(world)
-    # phase shares from the diagnostic count_work variant (first variant's knobs)
+    # phase shares from the diagnostic count_work variant (first variant's knobs), at the
+    # timed run's chunk size so the lane-occupancy figures describe the same waves
     r.set_variant(*variants[0])
-    r.render(cam, rt.Renderer.params(W, H, min(args.spp, 16), args.depth, bg, 1, count_work=1))
+    chunk = max(1, (args.spp + 15) // 16)
+    r.render(cam, rt.Renderer.params(W, H, min(args.spp, 2 * chunk), args.depth, bg, 1, spp_chunk=chunk,
+                                     count_work=1))
     st = r.stats()
     tot = st.cycles_camera + st.cycles_trace + st.cycles_shade
     if tot:
-        print(f"phase shares (wave-cycles): camera {st.cycles_camera / tot:.3f}  trace {st.cycles_trace / tot:.3f}  "
+        print(f"phase shares (wave-cycles): camera {st.cycles_camera / tot:.3f}  trace {st.cycles_trace / tot:.3f} "
+              f"(node loops {st.cycles_nodes / tot:.3f}, leaves {st.cycles_leaves / tot:.3f})  "
               f"shade {st.cycles_shade / tot:.3f};  casts/sample {st.casts / st.samples:.3f}  "
               f"nodes/cast {st.node_visits / max(st.casts, 1):.2f}  prims/cast {st.prim_tests / max(st.casts, 1):.2f}")
-        print(f"lane occupancy: bounce loop {st.casts / max(64 * st.wave_steps, 1):.3f}  "
+        print(f"lane occupancy (spp_chunk {chunk}): bounce loop {st.casts / max(64 * st.wave_steps, 1):.3f}  "
               f"node-visit loop {st.node_visits / max(64 * st.wave_node_steps, 1):.3f}")
     if args.chunks:
         cks = [int(x) for x in args.chunks.split(",")]

@@ -293,3 +293,31 @@ def test_progressive_early_stop_and_divisor(rt, renderer):
     q = rt.Renderer.params(W, H, 32, 50, bg, 1, row_begin=1, out_format=rt.RT_OUT_F64)
     with pytest.raises(rt.RTError):
         acc.add(cam, q, 2)                          # another shard
+
+
+@pytest.mark.parametrize("scene_id,W,H,spp", [(0, 40, 24, 8), (5, 24, 24, 8), (6, 24, 24, 8), (7, 32, 18, 8)])
+def test_schedules_render_identically(rt, scene_id, W, H, spp):
+    """The sample-pool schedule (persistent waves, per-lane refill, [sample][pixel] buffer)
+    and the chunk schedule give the same bits; so does the pool split into many buffer
+    batches (RT_SAMPLE_BUF_MB), at ragged sizes and with row shards."""
+    import os
+    world = rt.World(1).build_scene(scene_id)
+    cam, bg = rt.scene_camera(scene_id, W, H)
+    imgs = []
+    os.environ["RT_SAMPLE_BUF_MB"] = "1"
+    try:
+        small = rt.Renderer(0)                       # reads the buffer bound at creation
+    finally:
+        os.environ.pop("RT_SAMPLE_BUF_MB")
+    r = rt.Renderer(0)
+    for rr, sched in [(r, rt.RT_SCHED_CHUNKS), (r, rt.RT_SCHED_POOL), (small, rt.RT_SCHED_POOL)]:
+        rr.set_schedule(sched)
+        rr.upload(world)
+        imgs.append(rr.render(cam, rt.Renderer.params(W, H, spp, 50, bg, 1, row_begin=1, row_stride=2,
+                                                      out_format=rt.RT_OUT_F64)))
+        assert rr.stats().schedule == sched
+    assert np.array_equal(imgs[0], imgs[1]) and np.array_equal(imgs[0], imgs[2])
+    big = 64 * 48
+    small.render(cam, rt.Renderer.params(64, 48, 40, 50, bg, 1))
+    assert small.stats().n_batches > 1 and big * 40 * 24 > (1 << 20)
+    assert_parity(imgs[1], ob.render(scene_id, W, H, spp, row_begin=1, row_stride=2), f"pool scene {scene_id}")
