@@ -564,9 +564,9 @@ struct Sink {
 // Traces samples [s_begin, s_end) of the shard in chunks of `chunk` and reduces them into
 // the sink. Events: ev[0] before the first trace launch, ev[1] after the last one, ev[2]
 // after the last reduction. Chunk schedule: one launch into chunk partials. Pool schedule:
-// per-sample radiance in batches of whole chunks that fit sample_buf_cap; with more than
-// one batch the sums run through acc (the sink's, or acc_tmp), which keeps the additions
-// in the one-batch order.
+// per-sample radiance in batches that fit sample_buf_cap; with more than one batch (or an
+// acc sink) the sums run through acc (the sink's, or acc_tmp) plus the open chunk's sum
+// (carried across batches), which keeps the additions in the one-batch order.
 static int run_range(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, int s_begin, int s_end, int chunk,
                      hipStream_t stream, const Sink& sink)
 {
@@ -608,21 +608,20 @@ static int run_range(rt_ctx* c, const rt_camera* cam, const rt_render_params* p,
     rtk::SceneDev S = c->S;
     S.n_lds_nodes = c->opt_lds_nodes ? std::min(c->n_tlas_nodes, kMaxLdsNodes) : 0;
 
-    // batches of whole chunks
     const long long total = s_end - s_begin;
     long long batch = total;
-    if (o.pool) {
-        const long long fit = (long long)(c->sample_buf_cap / (px * 3 * sizeof(double)));
-        batch = std::max<long long>(chunk, fit / chunk * chunk);
-        batch = std::min(batch, total);
-    }
+    if (o.pool) batch = std::min<long long>(total, std::max<size_t>(1, c->sample_buf_cap / (px * 3 * sizeof(double))));
     const int n_batches = (int)((total + batch - 1) / batch);
     double* acc = sink.acc;
-    if (o.pool && n_batches > 1 && !acc) {
-        int rc = grow(c, stream, c->acc_tmp, c->acc_tmp_cap, px * 3 * sizeof(double));
+    double* open = nullptr;
+    if (o.pool && (n_batches > 1 || acc)) {  // acc_tmp = [open chunk sums | running total (no acc sink)]
+        int rc = grow(c, stream, c->acc_tmp, c->acc_tmp_cap, 2 * px * 3 * sizeof(double));
         if (rc) return rc;
-        HIP_TRY(hipMemsetAsync(c->acc_tmp, 0, px * 3 * sizeof(double), stream));
-        acc = c->acc_tmp;
+        open = c->acc_tmp;
+        if (!acc) {
+            acc = c->acc_tmp + px * 3;
+            HIP_TRY(hipMemsetAsync(acc, 0, px * 3 * sizeof(double), stream));
+        }
     }
     const int max_chunks = (int)((batch + chunk - 1) / chunk);
     const size_t need = o.pool ? (size_t)batch * px * 3 * sizeof(double) : (size_t)max_chunks * px * 3 * sizeof(double);
@@ -644,12 +643,15 @@ static int run_range(rt_ctx* c, const rt_camera* cam, const rt_render_params* p,
         if (!o.pool) {
             if (sink.acc) HIP_TRY(rtk::launch_accumulate(c->partial, sink.acc, n_px, K.n_chunks, stream));
             else HIP_TRY(rtk::launch_reduce(c->partial, sink.out, sink.f64, n_px, K.n_chunks, sink.scale, stream));
+        } else if (!open) {
+            HIP_TRY(rtk::launch_reduce_samples(c->partial, sink.out, sink.f64, n_px, b1 - b0, chunk, sink.scale, stream));
         } else {
-            HIP_TRY(rtk::launch_reduce_samples(c->partial, acc, sink.out, sink.f64, n_px, b1 - b0, chunk, sink.scale,
-                                               stream));
+            HIP_TRY(rtk::launch_reduce_samples_carry(c->partial, acc, open, n_px, b1 - b0, chunk,
+                                                     (int)(((long long)b0 - s_begin) % chunk), bi == n_batches - 1,
+                                                     stream));
         }
     }
-    if (o.pool && acc && !sink.acc)  // resolve the running sums: 0.0 + sum, times scale, as one batch does
+    if (open && !sink.acc)  // resolve the running sums: 0.0 + sum, times scale, as one batch does
         HIP_TRY(rtk::launch_reduce(acc, sink.out, sink.f64, n_px, 1, sink.scale, stream));
     HIP_TRY(hipEventRecord(c->ev[2], stream));
 

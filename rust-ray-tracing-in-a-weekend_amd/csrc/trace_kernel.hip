@@ -1205,21 +1205,15 @@ __global__ void __launch_bounds__(256, min_waves<C>()) trace_pool(SceneDev S, co
 }
 
 // Per pixel: chunk sums of consecutive samples (chunk order, each from 0.0), added in
-// chunk order to acc (acc mode) or to 0.0 and scaled into out: the same additions, in the
-// same order, as the chunk schedule's lane sums + reduce_chunks.
-template <typename T, bool ACC>
-__global__ void __launch_bounds__(256) reduce_samples(const double* __restrict__ samples, double* __restrict__ acc,
-                                                      T* __restrict__ out, long long n_px, int n_samples, int chunk,
-                                                      double scale)
+// chunk order to 0.0 and scaled into out: the same additions, in the same order, as the
+// chunk schedule's lane sums + reduce_chunks.
+template <typename T>
+__global__ void __launch_bounds__(256) reduce_samples(const double* __restrict__ samples, T* __restrict__ out,
+                                                      long long n_px, int n_samples, int chunk, double scale)
 {
     const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n_px) return;
     double r = 0.0, g = 0.0, b = 0.0;
-    if (ACC) {
-        r = acc[3 * i + 0];
-        g = acc[3 * i + 1];
-        b = acc[3 * i + 2];
-    }
     for (int c0 = 0; c0 < n_samples; c0 += chunk) {
         const int c1 = min(n_samples, c0 + chunk);
         double cr = 0.0, cg = 0.0, cb = 0.0;
@@ -1233,15 +1227,52 @@ __global__ void __launch_bounds__(256) reduce_samples(const double* __restrict__
         g = g + cg;
         b = b + cb;
     }
-    if (ACC) {
-        acc[3 * i + 0] = r;
-        acc[3 * i + 1] = g;
-        acc[3 * i + 2] = b;
-    } else {
-        out[3 * i + 0] = (T)(r * scale);
-        out[3 * i + 1] = (T)(g * scale);
-        out[3 * i + 2] = (T)(b * scale);
+    out[3 * i + 0] = (T)(r * scale);
+    out[3 * i + 1] = (T)(g * scale);
+    out[3 * i + 2] = (T)(b * scale);
+}
+
+// The same sums over a render split into buffer batches that need not end on a chunk
+// boundary: acc holds the closed chunks' total, open the chunk in progress (pos samples
+// in at batch start, uniform); `close` ends the render's last chunk.
+__global__ void __launch_bounds__(256) reduce_samples_carry(const double* __restrict__ samples,
+                                                            double* __restrict__ acc, double* __restrict__ open,
+                                                            long long n_px, int n_samples, int chunk, int pos,
+                                                            int close)
+{
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n_px) return;
+    double r = acc[3 * i + 0], g = acc[3 * i + 1], b = acc[3 * i + 2];
+    double cr = 0.0, cg = 0.0, cb = 0.0;
+    if (pos > 0) {
+        cr = open[3 * i + 0];
+        cg = open[3 * i + 1];
+        cb = open[3 * i + 2];
     }
+    for (int j = 0; j < n_samples; ++j) {
+        const double* p = samples + ((size_t)j * n_px + i) * 3;
+        cr = cr + p[0];
+        cg = cg + p[1];
+        cb = cb + p[2];
+        if (++pos == chunk) {
+            r = r + cr;
+            g = g + cg;
+            b = b + cb;
+            cr = cg = cb = 0.0;
+            pos = 0;
+        }
+    }
+    if (close && pos > 0) {
+        r = r + cr;
+        g = g + cg;
+        b = b + cb;
+    }
+    acc[3 * i + 0] = r;
+    acc[3 * i + 1] = g;
+    acc[3 * i + 2] = b;
+    open[3 * i + 0] = cr;
+    open[3 * i + 1] = cg;
+    open[3 * i + 2] = cb;
 }
 
 // sum of partials in chunk order, times 1/spp (math.rs:120-125 before sqrt).
@@ -1416,20 +1447,27 @@ hipError_t launch_trace(const SceneDev& S, const KParams& Ph, const KParams* P, 
     return hipGetLastError();
 }
 
-hipError_t launch_reduce_samples(const double* samples, double* acc, void* out, bool f64, long long n_px,
-                                 int n_samples, int chunk, double scale, hipStream_t stream)
+hipError_t launch_reduce_samples(const double* samples, void* out, bool f64, long long n_px, int n_samples,
+                                 int chunk, double scale, hipStream_t stream)
 {
     const long long blocks = (n_px + 255) / 256;
     if (blocks <= 0) return hipSuccess;
-    if (acc)
-        hipLaunchKernelGGL((reduce_samples<double, true>), dim3((unsigned)blocks), dim3(256), 0, stream, samples, acc,
-                           (double*)nullptr, n_px, n_samples, chunk, scale);
-    else if (f64)
-        hipLaunchKernelGGL((reduce_samples<double, false>), dim3((unsigned)blocks), dim3(256), 0, stream, samples,
-                           (double*)nullptr, (double*)out, n_px, n_samples, chunk, scale);
+    if (f64)
+        hipLaunchKernelGGL(reduce_samples<double>, dim3((unsigned)blocks), dim3(256), 0, stream, samples, (double*)out,
+                           n_px, n_samples, chunk, scale);
     else
-        hipLaunchKernelGGL((reduce_samples<float, false>), dim3((unsigned)blocks), dim3(256), 0, stream, samples,
-                           (double*)nullptr, (float*)out, n_px, n_samples, chunk, scale);
+        hipLaunchKernelGGL(reduce_samples<float>, dim3((unsigned)blocks), dim3(256), 0, stream, samples, (float*)out,
+                           n_px, n_samples, chunk, scale);
+    return hipGetLastError();
+}
+
+hipError_t launch_reduce_samples_carry(const double* samples, double* acc, double* open, long long n_px,
+                                       int n_samples, int chunk, int pos, bool close, hipStream_t stream)
+{
+    const long long blocks = (n_px + 255) / 256;
+    if (blocks <= 0) return hipSuccess;
+    hipLaunchKernelGGL(reduce_samples_carry, dim3((unsigned)blocks), dim3(256), 0, stream, samples, acc, open, n_px,
+                       n_samples, chunk, pos, (int)close);
     return hipGetLastError();
 }
 

@@ -65,10 +65,13 @@ uint32_t variant_features(uint32_t scene_features);
 // radiance [spp - sample_begin][n_px][3], work = one device counter
 hipError_t launch_trace(const SceneDev& S, const KParams& Ph, const KParams* P, double* out,
                         unsigned long long* counters, unsigned* work, const LaunchOpts& o, hipStream_t stream);
-// pool schedule: per pixel, chunk sums of its samples (sample order) added to acc, or (acc
-// null) to 0.0 and written scaled to out
-hipError_t launch_reduce_samples(const double* samples, double* acc, void* out, bool f64, long long n_px,
-                                 int n_samples, int chunk, double scale, hipStream_t stream);
+// pool schedule: per pixel, chunk sums of its samples (sample order) added to 0.0, scaled to out
+hipError_t launch_reduce_samples(const double* samples, void* out, bool f64, long long n_px, int n_samples,
+                                 int chunk, double scale, hipStream_t stream);
+// the same across buffer batches: acc = closed chunks' total, open = the chunk in progress
+// (pos of its samples seen before this batch); close ends the last chunk
+hipError_t launch_reduce_samples_carry(const double* samples, double* acc, double* open, long long n_px,
+                                       int n_samples, int chunk, int pos, bool close, hipStream_t stream);
 hipError_t launch_reduce(const double* partial, void* out, bool f64, long long n_px, int n_chunks, double scale,
                          hipStream_t stream);
 // acc[i] += chunk partials in chunk order (progressive accumulation, rt_accum_add)

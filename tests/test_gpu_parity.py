@@ -317,7 +317,13 @@ def test_schedules_render_identically(rt, scene_id, W, H, spp):
                                                       out_format=rt.RT_OUT_F64)))
         assert rr.stats().schedule == sched
     assert np.array_equal(imgs[0], imgs[1]) and np.array_equal(imgs[0], imgs[2])
-    big = 64 * 48
-    small.render(cam, rt.Renderer.params(64, 48, 40, 50, bg, 1))
-    assert small.stats().n_batches > 1 and big * 40 * 24 > (1 << 20)
+    q = rt.Renderer.params(64, 48, 40, 50, bg, 1, out_format=rt.RT_OUT_F64)   # 73.7 KB per sample
+    batched = small.render(cam, q)
+    assert small.stats().n_batches == 3              # 14 + 14 + 12 samples; chunks of 3 straddle batches
+    assert np.array_equal(batched, r.render(cam, q)) and r.stats().n_batches == 1
+    acc = small.accumulator(q)                       # an accumulator batch straddling buffer batches
+    acc.add(cam, q, 21)
+    acc.add(cam, q, 19)
+    one = r.render(cam, rt.Renderer.params(64, 48, 40, 50, bg, 1, spp_chunk=3, out_format=rt.RT_OUT_F64))
+    assert np.array_equal(acc.resolve(out_format=rt.RT_OUT_F64), one)
     assert_parity(imgs[1], ob.render(scene_id, W, H, spp, row_begin=1, row_stride=2), f"pool scene {scene_id}")
