@@ -153,7 +153,10 @@ def main():
                         cs.casts * cs.material_bytes) / max(cs.samples, 1)
     samples_per_launch = rows * W * spp
     items_per_launch = last.n_items
-    alg_bytes_launch = bytes_per_sample * samples_per_launch + items_per_launch * 24
+    # radiance written per launch: one f64 triple per sample (pool schedule) or per
+    # (pixel, chunk) partial (chunk schedule)
+    out_units = samples_per_launch if last.schedule == rt.RT_SCHED_POOL else items_per_launch
+    alg_bytes_launch = bytes_per_sample * samples_per_launch + out_units * 24
     k_ms = float(np.mean(kernel_ms)) if kernel_ms else float("nan")
     achieved = alg_bytes_launch / (k_ms * 1e-3) / 1e9
     # HBM traffic per launch from the committed rocprofv3 PMC pass of this workload
@@ -161,9 +164,9 @@ def main():
     traffic, traffic_src = None, None
     pmc = os.environ.get("RT_PMC_TRAFFIC_JSON", os.path.join(REPO, "profiles", "pmc_traffic.json"))
     if os.path.exists(pmc):
-        pj = json.load(open(pmc))
-        if pj.get("workload") == [args.scene, W, H, spp, depth, world]:
-            traffic, traffic_src = pj.get("hbm_bytes_per_launch"), pj.get("tag")
+        for e in json.load(open(pmc)).get("entries", []):
+            if e.get("workload") == [args.scene, W, H, spp, depth, world] and e.get("schedule") == last.schedule:
+                traffic, traffic_src = e.get("hbm_bytes_per_launch"), e.get("tag")
 
     if args.ppm and rank == 0:
         rt.write_ppm(frame.cpu().numpy(), args.ppm)

@@ -966,10 +966,12 @@ __device__ __forceinline__ bool lane_work(const KParams& P, LaneWork& w)
 #define RT_MIN_WAVES_SPHERES 1
 #endif
 #ifndef RT_MIN_WAVES_RECTINST
-#define RT_MIN_WAVES_RECTINST 4   // measured: Cornell 202 -> 190 ms (800x800x200)
+#define RT_MIN_WAVES_RECTINST 4   // measured: Cornell 202 -> 190 ms (800x800x200); pool: 4 80.7, 3 81.0
 #endif
 #ifndef RT_MIN_WAVES_ALL
-#define RT_MIN_WAVES_ALL 4        // measured: final scene 255 -> 169 ms (960x540x200); 2: 239, 3: 176
+// measured, pool schedule: final scene 960x540x200 4: 112.0 ms (scratch spills: 0.7 TB of HBM
+// writes per launch), 3: 102.8, 2: 131.5; cornell smoke 600x600x200 4: 74.1, 3: 62.3, 2: 79.7
+#define RT_MIN_WAVES_ALL 3
 #endif
 // minimum waves per SIMD requested from the register allocator, per feature set
 template <class C>

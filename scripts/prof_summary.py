@@ -18,8 +18,8 @@ import statistics
 import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-PROF = os.path.join(REPO, "gpurun_out", "prof")
-KERNEL = "trace_chunks"   # the timed variant (COUNT = false)
+PROF = os.path.join(REPO, "gpurun_out", os.environ.get("PROF_DIR", "prof"))
+KERNEL = os.environ.get("PROF_KERNEL", "trace_pool")   # the timed variant (COUNT = false)
 
 
 def per_launch(path, kernel=KERNEL):
@@ -71,11 +71,20 @@ def main():
                      f"{counters['SQ_THREAD_CYCLES_VALU'] / (64 * counters['SQ_ACTIVE_INST_VALU']):.3f}")
     open(os.path.join(out, f"{tag}_pmc.md"), "w").write("\n".join(lines) + "\n")
     workload = [int(x) for x in os.environ.get("PROF_WORKLOAD", "0,1200,800,500,50,1").split(",")]
-    json.dump({"tag": tag, "config": config, "workload": workload, "kernel": KERNEL,
-               "hbm_bytes_per_launch": traffic,
-               "fetch_size_kib": counters.get("FETCH_SIZE"), "write_size_kib": counters.get("WRITE_SIZE"),
-               "kernel_avg_ns": avg_ns},
-              open(os.path.join(out, "pmc_traffic.json"), "w"), indent=1)
+    schedule = 1 if KERNEL == "trace_pool" else 0
+    path = os.path.join(out, "pmc_traffic.json")
+    entries = []
+    if os.path.exists(path):
+        entries = [e for e in json.load(open(path)).get("entries", [])
+                   if not (e.get("workload") == workload and e.get("schedule") == schedule)]
+    entries.append({"tag": tag, "config": config, "workload": workload, "kernel": KERNEL, "schedule": schedule,
+                    "hbm_bytes_per_launch": traffic,
+                    "fetch_size_kib": counters.get("FETCH_SIZE"), "write_size_kib": counters.get("WRITE_SIZE"),
+                    "kernel_avg_ns": avg_ns})
+    json.dump({"note": "HBM bytes per trace-kernel launch (2*FETCH_SIZE + WRITE_SIZE, KiB*1024), "
+                       "from scripts/profile.sh + scripts/prof_summary.py; bench.py matches workload "
+                       "[scene, W, H, spp, depth, n_gpus] and schedule",
+               "entries": entries}, open(path, "w"), indent=1)
     print("\n".join(lines))
 
 
