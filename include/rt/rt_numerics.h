@@ -113,6 +113,30 @@ RT_HD uint64_t rt_stream_next_u64(rt_stream* s)
     return ((uint64_t)r.v[1] << 32) | r.v[0];
 }
 
+/* Render-stream discipline (every draw of a path): each draw event
+ * takes whole Philox blocks, so lanes of a wave never diverge on whether a cached half is
+ * left. Events: (u, v) jitter = one pair; a unit-disk candidate = one pair; the ray time =
+ * the first half of a fresh block; a unit-sphere candidate = one pair (x, y) + the first
+ * half of the next block (z); the dielectric draw = the first half of a fresh block.
+ * (The scene-construction stream keeps rt_stream_next_u64's consecutive halves.) */
+RT_HD void rt_stream_pair(rt_stream* s, uint64_t* a, uint64_t* b)
+{
+    rt_u32x4 c; c.v[0] = s->c0; c.v[1] = s->c1; c.v[2] = s->blk; c.v[3] = s->c3;
+    rt_u32x4 r = rt_philox4x32_10(c, s->k0, s->k1);
+    s->blk += 1;
+    s->have = 0;
+    *a = ((uint64_t)r.v[1] << 32) | r.v[0];
+    *b = ((uint64_t)r.v[3] << 32) | r.v[2];
+}
+
+RT_HD uint64_t rt_stream_fresh_u64(rt_stream* s)
+{
+    uint64_t a, b;
+    rt_stream_pair(s, &a, &b);
+    (void)b;
+    return a;
+}
+
 /* One keyed u64 (medium draws; counter = pixel, sample, bounce, stream). */
 RT_HD uint64_t rt_keyed_u64(uint64_t seed, uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3)
 {

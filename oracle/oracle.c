@@ -87,6 +87,7 @@ static void sphere_uv(V3 p, double* u, double* v)
 /* ------------------------------------------------------------------------- */
 typedef struct {
     rt_stream s;            /* sequential stream (thread_rng replacement) */
+    int render;             /* 1: render-stream discipline (rt_numerics.h: whole blocks per draw) */
     uint64_t seed;
     uint32_t pixel, sample; /* keyed-draw coordinates */
     uint32_t bounce;
@@ -94,10 +95,14 @@ typedef struct {
 
 static __thread OrcRng* tl_rng;
 
-static inline double random_double(void) { return rt_unit53(rt_stream_next_u64(&tl_rng->s)); }
+static inline uint64_t rng_u64(void)
+{
+    return tl_rng->render ? rt_stream_fresh_u64(&tl_rng->s) : rt_stream_next_u64(&tl_rng->s);
+}
+static inline double random_double(void) { return rt_unit53(rng_u64()); }
 static inline double random_double_range(double a, double b)
 {
-    return rt_uniform_sample(rt_stream_next_u64(&tl_rng->s), a, rt_uniform_incl_scale(a, b));
+    return rt_uniform_sample(rng_u64(), a, rt_uniform_incl_scale(a, b));
 }
 static inline int random_int_range(int a, int b)                                         /* math.rs:278-280 */
 {
@@ -117,18 +122,28 @@ static inline V3 v3_random_range(double a, double b)                            
     double z = random_double_range(a, b);
     return v3(x, y, z);
 }
+/* render only: candidates as whole-block draw events (x, y pair + z fresh; x, y pair) */
 static V3 random_in_unit_sphere(void)                                                    /* math.rs:51-58 */
 {
+    const double sc = rt_uniform_incl_scale(-1.0, 1.0);
     for (;;) {
-        V3 p = v3_random_range(-1.0, 1.0);
+        uint64_t a, b;
+        rt_stream_pair(&tl_rng->s, &a, &b);
+        double x = rt_uniform_sample(a, -1.0, sc);
+        double y = rt_uniform_sample(b, -1.0, sc);
+        double z = rt_uniform_sample(rt_stream_fresh_u64(&tl_rng->s), -1.0, sc);
+        V3 p = v3(x, y, z);                                                              /* v3_random_range */
         if (vlen2(p) < 1.0) return p;
     }
 }
 static V3 random_in_unit_disk(void)                                                      /* math.rs:69-76 */
 {
+    const double sc = rt_uniform_incl_scale(-1.0, 1.0);
     for (;;) {
-        double x = random_double_range(-1.0, 1.0);
-        double y = random_double_range(-1.0, 1.0);
+        uint64_t a, b;
+        rt_stream_pair(&tl_rng->s, &a, &b);
+        double x = rt_uniform_sample(a, -1.0, sc);
+        double y = rt_uniform_sample(b, -1.0, sc);
         V3 p = v3(x, y, 0.0);
         if (vlen2(p) < 1.0) return p;
     }
@@ -1114,8 +1129,11 @@ static void render_pixel(Job* job, RenderCtx* ctx, OrcRng* rng, int x, int y, in
         rng->pixel = (uint32_t)y * (uint32_t)p->width + (uint32_t)x;
         rng->sample = (uint32_t)s;
         rt_stream_init(&rng->s, p->render_seed, rng->pixel, rng->sample, RT_STREAM_MAIN);
-        double u = ((double)x + random_double()) / ((double)p->width - 1.0);            /* main.rs:517 */
-        double v = ((double)y + random_double()) / ((double)p->height - 1.0);           /* main.rs:518 */
+        rng->render = 1;
+        uint64_t ju, jv;                                                                  /* one pair */
+        rt_stream_pair(&rng->s, &ju, &jv);
+        double u = ((double)x + rt_unit53(ju)) / ((double)p->width - 1.0);               /* main.rs:517 */
+        double v = ((double)y + rt_unit53(jv)) / ((double)p->height - 1.0);              /* main.rs:518 */
         Ray r = camera_get_ray(job->cam, u, v);                                           /* main.rs:520 */
         V3 c = ray_color(ctx, &r, p->max_depth);                                          /* main.rs:522 */
         part = vadd(part, c);

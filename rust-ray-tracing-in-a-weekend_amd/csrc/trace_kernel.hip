@@ -796,20 +796,18 @@ __device__ void tex_value(const SceneDev& S, int ti, const Hit& h, double& cr, d
     }
 }
 
-__device__ __forceinline__ double rnd01(rt_stream& st) { return rt_unit53(rt_stream_next_u64(&st)); }
-__device__ __forceinline__ double rnd_m11(rt_stream& st, double scale_m11)
-{
-    return rt_uniform_sample(rt_stream_next_u64(&st), -1.0, scale_m11);
-}
+__device__ __forceinline__ double rnd01(rt_stream& st) { return rt_unit53(rt_stream_fresh_u64(&st)); }
 
 // math.rs:51-58
 __device__ __forceinline__ void random_in_unit_sphere(rt_stream& st, double scale_m11, double& x, double& y,
                                                       double& z, double& len2)
 {
-    for (;;) {
-        x = rnd_m11(st, scale_m11);
-        y = rnd_m11(st, scale_m11);
-        z = rnd_m11(st, scale_m11);
+    for (;;) {  // one candidate = a pair (x, y) + a fresh half (z), rt_numerics.h
+        uint64_t a, b;
+        rt_stream_pair(&st, &a, &b);
+        x = rt_uniform_sample(a, -1.0, scale_m11);
+        y = rt_uniform_sample(b, -1.0, scale_m11);
+        z = rt_uniform_sample(rt_stream_fresh_u64(&st), -1.0, scale_m11);
         len2 = x * x + y * y + z * z;
         if (len2 < 1.0) return;
     }
@@ -822,12 +820,16 @@ __device__ __forceinline__ void random_in_unit_sphere(rt_stream& st, double scal
 // main.rs:517-520 + Camera::get_ray (camera.rs:58-66)
 __device__ __forceinline__ void camera_ray(const KParams& P, int x, int y, rt_stream& st, Ray& r)
 {
-    const double u = ((double)x + rnd01(st)) / ((double)P.width - 1.0);
-    const double v = ((double)y + rnd01(st)) / ((double)P.height - 1.0);
+    uint64_t ju, jv;  // draw events: rt_numerics.h render-stream discipline
+    rt_stream_pair(&st, &ju, &jv);
+    const double u = ((double)x + rt_unit53(ju)) / ((double)P.width - 1.0);
+    const double v = ((double)y + rt_unit53(jv)) / ((double)P.height - 1.0);
     double dxl, dyl;
     for (;;) {
-        dxl = rnd_m11(st, P.scale_m11);
-        dyl = rnd_m11(st, P.scale_m11);
+        uint64_t a, b;
+        rt_stream_pair(&st, &a, &b);
+        dxl = rt_uniform_sample(a, -1.0, P.scale_m11);
+        dyl = rt_uniform_sample(b, -1.0, P.scale_m11);
         if (dxl * dxl + dyl * dyl + 0.0 * 0.0 < 1.0) break;
     }
     const double rdx = dxl * P.cam.lens_radius, rdy = dyl * P.cam.lens_radius;
@@ -840,7 +842,7 @@ __device__ __forceinline__ void camera_ray(const KParams& P, int x, int y, rt_st
     r.dx = P.cam.lower_left_corner[0] + P.cam.horizontal[0] * u + P.cam.vertical[0] * v - P.cam.origin[0] - offx;
     r.dy = P.cam.lower_left_corner[1] + P.cam.horizontal[1] * u + P.cam.vertical[1] * v - P.cam.origin[1] - offy;
     r.dz = P.cam.lower_left_corner[2] + P.cam.horizontal[2] * u + P.cam.vertical[2] * v - P.cam.origin[2] - offz;
-    r.time = rt_uniform_sample(rt_stream_next_u64(&st), P.cam.time0, P.scale_time);
+    r.time = rt_uniform_sample(rt_stream_fresh_u64(&st), P.cam.time0, P.scale_time);
 }
 
 // One hit of ray_color (main.rs:25-34): emitted + attenuation * (next), with the
