@@ -265,6 +265,30 @@ RT_HD double rt_sin(double x)
     }
 }
 
+/* Sign of rt_sin(x) without the polynomial: +1 / -1, 0 for a zero, NaN or infinite
+ * result, 2 when |sin x| may be below 2^-340 (the caller then evaluates rt_sin). For
+ * |y0| <= pi/4 the kernels keep the sign of y0 (|ksin - y0| < |y0|) and kcos > 0.7, so a
+ * product of three such factors is nonzero with this sign unless a factor is tiny. */
+RT_HD int rt_sin_sign(double x)
+{
+    const double tiny = 0x1.0p-339;
+    uint32_t ix = (uint32_t)(rt_f64_bits(x) >> 32) & 0x7fffffffu;
+    if (ix <= 0x3fe921fbu) {
+        if (x == 0.0) return 0;
+        if (__builtin_fabs(x) < tiny) return 2;
+        return x < 0.0 ? -1 : 1;
+    }
+    if (ix >= 0x7ff00000u) return 0;
+    double y0, y1;
+    int n = rt__rem_pio2(x, &y0, &y1);
+    switch (n & 3) {
+    case 0: return __builtin_fabs(y0) < tiny ? 2 : (y0 < 0.0 ? -1 : 1);
+    case 1: return 1;
+    case 2: return __builtin_fabs(y0) < tiny ? 2 : (y0 < 0.0 ? 1 : -1);
+    default: return -1;
+    }
+}
+
 RT_HD double rt_cos(double x)
 {
     uint32_t ix = (uint32_t)(rt_f64_bits(x) >> 32) & 0x7fffffffu;

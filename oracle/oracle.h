@@ -73,7 +73,7 @@ int orc_scene_info(int scene_id, uint64_t scene_seed, const uint8_t* image_rgb, 
 
 /* Function-level probes used by the unit tests. fn: 0 sin, 1 cos, 2 log, 3 atan2(x, y),
  * 4 acos, 5 sphere_uv u of unit vector (x[i], y[i], z[i]), 6 sphere_uv v, 7 pow5,
- * 8 sqrt, 9 x/y, 10 unit53(bits of x), 11 uniform(-1,1) of bits of x. */
+ * 8 sqrt, 9 x/y, 10 unit53(bits of x), 11 uniform(-1,1) of bits of x, 12 rt_sin_sign. */
 int orc_eval(int fn, const double* x, const double* y, const double* z, double* out, int n);
 
 /* Philox4x32-10 of (ctr[4], key[2]) -> out[4]. */

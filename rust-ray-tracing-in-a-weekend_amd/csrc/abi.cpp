@@ -946,7 +946,7 @@ int rt_ctx_set_schedule(rt_ctx* c, int schedule)
 
 int rt_device_eval(rt_ctx* c, int fn, const double* x, const double* y, const double* z, double* out, int n)
 {
-    if (!c || !x || !out || n < 0 || fn < 0 || fn > 11) return fail(RT_ERR_INVALID, "bad argument");
+    if (!c || !x || !out || n < 0 || fn < 0 || fn > 12) return fail(RT_ERR_INVALID, "bad argument");
     if (n == 0) return RT_OK;
     HIP_TRY(hipSetDevice(c->device));
     double* d = nullptr;

@@ -746,14 +746,23 @@ __device__ void hit_uv(const Hit& h, double& u, double& v)
     }
 }
 
+// texture.rs:35-41: sin(10x)*sin(10y)*sin(10z) < 0 from the three signs (rt_sin_sign);
+// the full product only when a factor may be tiny enough to underflow it
+__device__ __forceinline__ bool checker_odd(const Hit& h)
+{
+    const double ax = 10.0 * h.px, ay = 10.0 * h.py, az = 10.0 * h.pz;
+    const int sx = rt_sin_sign(ax), sy = rt_sin_sign(ay), sz = rt_sin_sign(az);
+    if (sx == 2 || sy == 2 || sz == 2) return rt_sin(ax) * rt_sin(ay) * rt_sin(az) < 0.0;
+    return sx * sy * sz < 0;
+}
+
 template <class C>
 __device__ void tex_value(const SceneDev& S, int ti, const Hit& h, double& cr, double& cg, double& cb)
 {
     const rt_texture& t = S.textures[ti];
     if constexpr (!(C::F & (FEAT_NOISE | FEAT_IMAGE))) {
         if (t.kind == RT_TEX_CHECKER) {
-            const double sines = rt_sin(10.0 * h.px) * rt_sin(10.0 * h.py) * rt_sin(10.0 * h.pz);
-            const double* c = sines < 0.0 ? t.c1 : t.c0;
+            const double* c = checker_odd(h) ? t.c1 : t.c0;
             cr = c[0]; cg = c[1]; cb = c[2];
         } else {
             cr = t.c0[0]; cg = t.c0[1]; cb = t.c0[2];
@@ -763,8 +772,7 @@ __device__ void tex_value(const SceneDev& S, int ti, const Hit& h, double& cr, d
     switch (t.kind) {
     case RT_TEX_SOLID: cr = t.c0[0]; cg = t.c0[1]; cb = t.c0[2]; return;
     case RT_TEX_CHECKER: {
-        const double sines = rt_sin(10.0 * h.px) * rt_sin(10.0 * h.py) * rt_sin(10.0 * h.pz);
-        if (sines < 0.0) { cr = t.c1[0]; cg = t.c1[1]; cb = t.c1[2]; }
+        if (checker_odd(h)) { cr = t.c1[0]; cg = t.c1[1]; cb = t.c1[2]; }
         else { cr = t.c0[0]; cg = t.c0[1]; cb = t.c0[2]; }
         return;
     }
@@ -1342,6 +1350,7 @@ __global__ void eval_numerics(int fn, const double* x, const double* y, const do
     case 9: r = x[i] / y[i]; break;
     case 10: r = rt_unit53(rt_f64_bits(x[i])); break;
     case 11: r = rt_uniform_sample(rt_f64_bits(x[i]), -1.0, rt_uniform_incl_scale(-1.0, 1.0)); break;
+    case 12: r = (double)rt_sin_sign(x[i]); break;
     default: break;
     }
     out[i] = r;

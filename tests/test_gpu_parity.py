@@ -45,7 +45,7 @@ def test_device_numerics_bit_equal_host(rt, renderer):
     n /= np.linalg.norm(n, axis=0)
     bits = rng.integers(0, 2 ** 63, size=5000, dtype=np.int64).astype(np.uint64).view(np.float64)
     cases = {0: (x,), 1: (x,), 2: (pos,), 3: (x, y), 4: (np.clip(y / 3, -1, 1),), 5: tuple(n), 6: tuple(n),
-             7: (pos,), 8: (np.abs(x),), 9: (x, y), 10: (bits,), 11: (bits,)}
+             7: (pos,), 8: (np.abs(x),), 9: (x, y), 10: (bits,), 11: (bits,), 12: (x,)}
     for fn, args in cases.items():
         host = ob.evaluate(fn, *args)
         dev = renderer.device_eval(fn, *args)

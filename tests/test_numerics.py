@@ -109,3 +109,28 @@ def test_rand_float_mappings():
     # value0_1 = (u64 >> 12 as mantissa in [1,2)) - 1; scale s.t. max_rand*scale + low <= high
     top = ob.evaluate(11, np.array([(1 << 64) - 1], dtype=np.uint64).view(np.float64))[0]
     assert top <= 1.0 and top > 1.0 - 1e-15
+
+
+def test_sin_sign_matches_sin():
+    """rt_sin_sign (the checker texture's fast path, texture.rs:35-41) against the sign of
+    rt_sin itself, incl. arguments next to multiples of pi/2, tiny, zero, inf and NaN; and the
+    checker decision (product of three sines < 0) it feeds."""
+    rng = np.random.default_rng(5)
+    k = rng.integers(-4000, 4000, 20000).astype(np.float64)
+    near = k * (np.pi / 2)
+    near = np.concatenate([near, np.nextafter(near, np.inf), np.nextafter(near, -np.inf)])
+    x = np.concatenate([rng.uniform(-200, 200, 50000), near, 10.0 * rng.uniform(-15, 15, 20000),
+                        2.0 ** -rng.uniform(0, 1070, 2000) * rng.choice([-1, 1], 2000),
+                        [0.0, -0.0, np.inf, -np.inf, np.nan, 5e-324, -5e-324]])
+    s = ob.evaluate(0, x)
+    sg = ob.evaluate(12, x)
+    exact = np.where(np.isnan(s) | (s == 0), 0, np.sign(s))
+    known = sg != 2
+    assert np.all(sg[known] == exact[known])
+    assert np.all(np.abs(s[~known]) < 2.0 ** -300)        # "tiny" only where |sin| really is
+    a, b, c = (x[rng.permutation(x.size)] for _ in range(3))
+    sa, sb, sc = (ob.evaluate(0, v) for v in (a, b, c))
+    ga, gb, gc = (ob.evaluate(12, v) for v in (a, b, c))
+    full = sa * sb * sc < 0.0
+    ok = (ga != 2) & (gb != 2) & (gc != 2)
+    assert np.array_equal(full[ok], (ga * gb * gc)[ok] < 0)
