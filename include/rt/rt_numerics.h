@@ -116,8 +116,10 @@ RT_HD uint64_t rt_stream_next_u64(rt_stream* s)
 /* Render-stream discipline (every draw of a path): each draw event
  * takes whole Philox blocks, so lanes of a wave never diverge on whether a cached half is
  * left. Events: (u, v) jitter = one pair; a unit-disk candidate = one pair; the ray time =
- * the first half of a fresh block; a unit-sphere candidate = one pair (x, y) + the first
- * half of the next block (z); the dielectric draw = the first half of a fresh block.
+ * the first half of a fresh block; unit-sphere candidates come in pairs over three blocks
+ * (a b)(c d)(e f): candidate 0 = (a, b, c), candidate 1 = (d, e, f), and so on — the loop
+ * stops after any candidate and the next event takes a fresh block; the dielectric draw =
+ * the first half of a fresh block.
  * (The scene-construction stream keeps rt_stream_next_u64's consecutive halves.) */
 RT_HD void rt_stream_pair(rt_stream* s, uint64_t* a, uint64_t* b)
 {

@@ -122,17 +122,22 @@ static inline V3 v3_random_range(double a, double b)                            
     double z = random_double_range(a, b);
     return v3(x, y, z);
 }
-/* render only: candidates as whole-block draw events (x, y pair + z fresh; x, y pair) */
+/* render only: candidates as whole-block draw events (rt_numerics.h render discipline) */
 static V3 random_in_unit_sphere(void)                                                    /* math.rs:51-58 */
 {
     const double sc = rt_uniform_incl_scale(-1.0, 1.0);
-    for (;;) {
-        uint64_t a, b;
-        rt_stream_pair(&tl_rng->s, &a, &b);
-        double x = rt_uniform_sample(a, -1.0, sc);
-        double y = rt_uniform_sample(b, -1.0, sc);
-        double z = rt_uniform_sample(rt_stream_fresh_u64(&tl_rng->s), -1.0, sc);
-        V3 p = v3(x, y, z);                                                              /* v3_random_range */
+    uint64_t d = 0;
+    for (int k = 0;; k ^= 1) {        /* candidate pairs share three blocks: (a b)(c d)(e f) */
+        uint64_t a, b, c;
+        if (k == 0) {
+            rt_stream_pair(&tl_rng->s, &a, &b);
+            rt_stream_pair(&tl_rng->s, &c, &d);
+        } else {
+            a = d;
+            rt_stream_pair(&tl_rng->s, &b, &c);
+        }
+        V3 p = v3(rt_uniform_sample(a, -1.0, sc), rt_uniform_sample(b, -1.0, sc),
+                  rt_uniform_sample(c, -1.0, sc));                                       /* v3_random_range */
         if (vlen2(p) < 1.0) return p;
     }
 }

@@ -810,12 +810,21 @@ __device__ __forceinline__ double rnd01(rt_stream& st) { return rt_unit53(rt_str
 __device__ __forceinline__ void random_in_unit_sphere(rt_stream& st, double scale_m11, double& x, double& y,
                                                       double& z, double& len2)
 {
-    for (;;) {  // one candidate = a pair (x, y) + a fresh half (z), rt_numerics.h
-        uint64_t a, b;
-        rt_stream_pair(&st, &a, &b);
+    // candidates in pairs over three blocks (rt_numerics.h): every lane in the loop is at
+    // the same candidate, so each iteration runs one code path (2 or 1 Philox blocks)
+    uint64_t d = 0;
+    for (int k = 0;; k ^= 1) {
+        uint64_t a, b, c;
+        if (k == 0) {
+            rt_stream_pair(&st, &a, &b);
+            rt_stream_pair(&st, &c, &d);
+        } else {
+            a = d;
+            rt_stream_pair(&st, &b, &c);
+        }
         x = rt_uniform_sample(a, -1.0, scale_m11);
         y = rt_uniform_sample(b, -1.0, scale_m11);
-        z = rt_uniform_sample(rt_stream_fresh_u64(&st), -1.0, scale_m11);
+        z = rt_uniform_sample(c, -1.0, scale_m11);
         len2 = x * x + y * y + z * z;
         if (len2 < 1.0) return;
     }
