@@ -10,7 +10,9 @@
  *
  *   - Philox4x32-10 (Salmon et al., SC'11), the counter RNG that replaces the
  *     reference's unseedable `rand::thread_rng()` (math.rs:268-276). KAT-checked
- *     against Random123's published vectors and ROCm's rocrand host engine.
+ *     against Random123's published vectors and ROCm's rocrand host engine. It
+ *     drives scene construction directly and seeds one xoshiro128++ path stream per
+ *     (pixel, sample) for rendering.
  *   - The `rand` 0.8 float mappings the reference calls:
  *       random_double()            -> `Standard` f64: (u64 >> 11) * 2^-53
  *       random_double_range(a, b)  -> `gen_range(a..=b)`: UniformFloat
@@ -74,18 +76,18 @@ RT_HD rt_u32x4 rt_philox4x32_10(rt_u32x4 c, uint32_t k0, uint32_t k1)
     return c;
 }
 
-/* Counter layout of the render streams:
+/* Counter layout of the Philox streams:
  *   c0 = pixel index y*W + x (image coordinates, y = 0 at the bottom)
  *   c1 = sample index
- *   c2 = block index of the sequential stream  | bounce for keyed draws
- *   c3 = RT_STREAM_MAIN                        | RT_STREAM_MEDIUM + medium id
+ *   c2 = 0 for the path seed                  | bounce for keyed draws
+ *   c3 = RT_STREAM_PATH                       | RT_STREAM_MEDIUM + medium id
  * The scene-construction stream uses c3 = RT_STREAM_SCENE, c0/c1 = block index.
  */
-#define RT_STREAM_MAIN 0u
+#define RT_STREAM_PATH 0x9A750000u
 #define RT_STREAM_SCENE 0x5CE4E000u
 #define RT_STREAM_MEDIUM 0x10000u
 
-/* Sequential stream: 2 u64 per Philox block, consumed in order. */
+/* Sequential Philox stream (scene construction): 2 u64 per block, consumed in order. */
 typedef struct {
     uint32_t k0, k1;      /* key = seed */
     uint32_t c0, c1, c3;  /* fixed counter words */
@@ -113,30 +115,47 @@ RT_HD uint64_t rt_stream_next_u64(rt_stream* s)
     return ((uint64_t)r.v[1] << 32) | r.v[0];
 }
 
-/* Render-stream discipline (every draw of a path): each draw event
- * takes whole Philox blocks, so lanes of a wave never diverge on whether a cached half is
- * left. Events: (u, v) jitter = one pair; a unit-disk candidate = one pair; the ray time =
- * the first half of a fresh block; unit-sphere candidates come in pairs over three blocks
- * (a b)(c d)(e f): candidate 0 = (a, b, c), candidate 1 = (d, e, f), and so on — the loop
- * stops after any candidate and the next event takes a fresh block; the dielectric draw =
- * the first half of a fresh block.
- * (The scene-construction stream keeps rt_stream_next_u64's consecutive halves.) */
-RT_HD void rt_stream_pair(rt_stream* s, uint64_t* a, uint64_t* b)
+/* Path stream (every draw of one (pixel, sample) path): one
+ * Philox4x32-10 block of (pixel, sample, 0, RT_STREAM_PATH) under the render seed is the
+ * 128-bit state of a xoshiro128++ generator (Blackman & Vigna, "Scrambled linear
+ * pseudorandom number generators", 2019/2021: 32-bit state words, output
+ * rotl(s0 + s3, 7) + s0), from which the path draws in the reference's order, one u64
+ * per draw = (first output << 32) | second output. The stream is a function of
+ * (seed, pixel, sample) only, like the counter streams it replaces, at two xoshiro steps
+ * (add / shift / xor / rotate) per draw instead of half a Philox block (ten rounds of
+ * 32x32->64 products): the draws of the unit-sphere and unit-disk rejection loops are
+ * cheap enough to run at the pace of a wave's slowest lane. The all-zero state (the
+ * generator's fixed point, probability 2^-128) is replaced by s0 = 1. */
+typedef struct { uint32_t s0, s1, s2, s3; } rt_pstream;
+
+RT_HD void rt_pstream_init(rt_pstream* p, uint64_t seed, uint32_t pixel, uint32_t sample)
 {
-    rt_u32x4 c; c.v[0] = s->c0; c.v[1] = s->c1; c.v[2] = s->blk; c.v[3] = s->c3;
-    rt_u32x4 r = rt_philox4x32_10(c, s->k0, s->k1);
-    s->blk += 1;
-    s->have = 0;
-    *a = ((uint64_t)r.v[1] << 32) | r.v[0];
-    *b = ((uint64_t)r.v[3] << 32) | r.v[2];
+    rt_u32x4 c; c.v[0] = pixel; c.v[1] = sample; c.v[2] = 0; c.v[3] = RT_STREAM_PATH;
+    rt_u32x4 r = rt_philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+    p->s0 = r.v[0]; p->s1 = r.v[1]; p->s2 = r.v[2]; p->s3 = r.v[3];
+    if ((p->s0 | p->s1 | p->s2 | p->s3) == 0) p->s0 = 1;
 }
 
-RT_HD uint64_t rt_stream_fresh_u64(rt_stream* s)
+RT_HD uint32_t rt_rotl32(uint32_t x, int k) { return (x << k) | (x >> (32 - k)); }
+
+/* xoshiro128++ next() */
+RT_HD uint32_t rt_pstream_u32(rt_pstream* p)
 {
-    uint64_t a, b;
-    rt_stream_pair(s, &a, &b);
-    (void)b;
-    return a;
+    const uint32_t result = rt_rotl32(p->s0 + p->s3, 7) + p->s0;
+    const uint32_t t = p->s1 << 9;
+    p->s2 ^= p->s0;
+    p->s3 ^= p->s1;
+    p->s1 ^= p->s2;
+    p->s0 ^= p->s3;
+    p->s2 ^= t;
+    p->s3 = rt_rotl32(p->s3, 11);
+    return result;
+}
+
+RT_HD uint64_t rt_pstream_u64(rt_pstream* p)
+{
+    const uint64_t hi = rt_pstream_u32(p);
+    return (hi << 32) | rt_pstream_u32(p);
 }
 
 /* One keyed u64 (medium draws; counter = pixel, sample, bounce, stream). */

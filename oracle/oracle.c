@@ -86,8 +86,9 @@ static void sphere_uv(V3 p, double* u, double* v)
 /* RNG (math.rs:268-280 -> seeded Philox, rt_numerics.h)                      */
 /* ------------------------------------------------------------------------- */
 typedef struct {
-    rt_stream s;            /* sequential stream (thread_rng replacement) */
-    int render;             /* 1: render-stream discipline (rt_numerics.h: whole blocks per draw) */
+    rt_stream s;            /* scene construction: sequential Philox stream (thread_rng replacement) */
+    rt_pstream ps;          /* rendering: the path stream of (pixel, sample) (rt_numerics.h) */
+    int render;             /* 1: draws come from ps */
     uint64_t seed;
     uint32_t pixel, sample; /* keyed-draw coordinates */
     uint32_t bounce;
@@ -97,7 +98,7 @@ static __thread OrcRng* tl_rng;
 
 static inline uint64_t rng_u64(void)
 {
-    return tl_rng->render ? rt_stream_fresh_u64(&tl_rng->s) : rt_stream_next_u64(&tl_rng->s);
+    return tl_rng->render ? rt_pstream_u64(&tl_rng->ps) : rt_stream_next_u64(&tl_rng->s);
 }
 static inline double random_double(void) { return rt_unit53(rng_u64()); }
 static inline double random_double_range(double a, double b)
@@ -122,33 +123,18 @@ static inline V3 v3_random_range(double a, double b)                            
     double z = random_double_range(a, b);
     return v3(x, y, z);
 }
-/* render only: candidates as whole-block draw events (rt_numerics.h render discipline) */
 static V3 random_in_unit_sphere(void)                                                    /* math.rs:51-58 */
 {
-    const double sc = rt_uniform_incl_scale(-1.0, 1.0);
-    uint64_t d = 0;
-    for (int k = 0;; k ^= 1) {        /* candidate pairs share three blocks: (a b)(c d)(e f) */
-        uint64_t a, b, c;
-        if (k == 0) {
-            rt_stream_pair(&tl_rng->s, &a, &b);
-            rt_stream_pair(&tl_rng->s, &c, &d);
-        } else {
-            a = d;
-            rt_stream_pair(&tl_rng->s, &b, &c);
-        }
-        V3 p = v3(rt_uniform_sample(a, -1.0, sc), rt_uniform_sample(b, -1.0, sc),
-                  rt_uniform_sample(c, -1.0, sc));                                       /* v3_random_range */
+    for (;;) {
+        V3 p = v3_random_range(-1.0, 1.0);
         if (vlen2(p) < 1.0) return p;
     }
 }
 static V3 random_in_unit_disk(void)                                                      /* math.rs:69-76 */
 {
-    const double sc = rt_uniform_incl_scale(-1.0, 1.0);
     for (;;) {
-        uint64_t a, b;
-        rt_stream_pair(&tl_rng->s, &a, &b);
-        double x = rt_uniform_sample(a, -1.0, sc);
-        double y = rt_uniform_sample(b, -1.0, sc);
+        double x = random_double_range(-1.0, 1.0);
+        double y = random_double_range(-1.0, 1.0);
         V3 p = v3(x, y, 0.0);
         if (vlen2(p) < 1.0) return p;
     }
@@ -1133,12 +1119,10 @@ static void render_pixel(Job* job, RenderCtx* ctx, OrcRng* rng, int x, int y, in
     for (int s = s_begin; s < s_end; ++s) {
         rng->pixel = (uint32_t)y * (uint32_t)p->width + (uint32_t)x;
         rng->sample = (uint32_t)s;
-        rt_stream_init(&rng->s, p->render_seed, rng->pixel, rng->sample, RT_STREAM_MAIN);
+        rt_pstream_init(&rng->ps, p->render_seed, rng->pixel, rng->sample);
         rng->render = 1;
-        uint64_t ju, jv;                                                                  /* one pair */
-        rt_stream_pair(&rng->s, &ju, &jv);
-        double u = ((double)x + rt_unit53(ju)) / ((double)p->width - 1.0);               /* main.rs:517 */
-        double v = ((double)y + rt_unit53(jv)) / ((double)p->height - 1.0);              /* main.rs:518 */
+        double u = ((double)x + random_double()) / ((double)p->width - 1.0);              /* main.rs:517 */
+        double v = ((double)y + random_double()) / ((double)p->height - 1.0);             /* main.rs:518 */
         Ray r = camera_get_ray(job->cam, u, v);                                           /* main.rs:520 */
         V3 c = ray_color(ctx, &r, p->max_depth);                                          /* main.rs:522 */
         part = vadd(part, c);
@@ -1305,6 +1289,13 @@ void orc_philox(const uint32_t* ctr, const uint32_t* key, uint32_t* out)
     for (int i = 0; i < 4; ++i) c.v[i] = ctr[i];
     rt_u32x4 r = rt_philox4x32_10(c, key[0], key[1]);
     for (int i = 0; i < 4; ++i) out[i] = r.v[i];
+}
+
+void orc_pstream(uint64_t seed, uint32_t pixel, uint32_t sample, int n, uint64_t* out)
+{
+    rt_pstream ps;
+    rt_pstream_init(&ps, seed, pixel, sample);
+    for (int i = 0; i < n; ++i) out[i] = rt_pstream_u64(&ps);
 }
 
 int orc_camera(int scene_id, int width, int height, double* o)

@@ -79,6 +79,9 @@ int orc_eval(int fn, const double* x, const double* y, const double* z, double* 
 /* Philox4x32-10 of (ctr[4], key[2]) -> out[4]. */
 void orc_philox(const uint32_t* ctr, const uint32_t* key, uint32_t* out);
 
+/* The first n u64 draws of the path stream of (seed, pixel, sample) (rt_numerics.h rt_pstream). */
+void orc_pstream(uint64_t seed, uint32_t pixel, uint32_t sample, int n, uint64_t* out);
+
 /* Camera of scene_id at width x height (camera.rs:18-56 with main.rs parameters):
  * 24 doubles: origin, lower_left_corner, horizontal, vertical, u, v, w, lens_radius, t0, t1. */
 int orc_camera(int scene_id, int width, int height, double* out24);

@@ -16,8 +16,8 @@
 //     one f64x3 partial; a second kernel adds the partials in chunk order and
 //     scales by 1/spp (math.rs:119-126), so the image does not depend on the
 //     launch geometry or on how rows are sharded over GPUs;
-//   * RNG: Philox4x32-10 keyed by (pixel, sample) (rt_numerics.h), the medium's
-//     in-hit draw keyed by (pixel, sample, bounce, medium id).
+//   * RNG: per (pixel, sample) a Philox4x32-10 block seeds a xoshiro128++ path stream
+//     (rt_numerics.h); the medium's in-hit draw is keyed by (pixel, sample, bounce, medium id).
 // Built with -ffp-contract=off: bit-for-bit the operation order of the reference.
 #include <hip/hip_runtime.h>
 
@@ -804,27 +804,26 @@ __device__ void tex_value(const SceneDev& S, int ti, const Hit& h, double& cr, d
     }
 }
 
-__device__ __forceinline__ double rnd01(rt_stream& st) { return rt_unit53(rt_stream_fresh_u64(&st)); }
+// The path stream of rt_numerics.h (rt_pstream): one Philox block of (pixel, sample) seeds
+// a xoshiro128++ state, from which the path draws in the reference's order.
+__device__ __forceinline__ void ds_start(rt_pstream& st, uint64_t seed, uint32_t pixel, uint32_t sample)
+{
+#ifdef RT_EXPERIMENT_CHEAP_RNG  // timing probe of the seeding's share: NOT the product's stream
+    st.s0 = pixel * 0x9E3779B1u ^ sample; st.s1 = sample * 0x85EBCA77u ^ pixel; st.s2 = ~pixel; st.s3 = (uint32_t)seed;
+    return;
+#endif
+    rt_pstream_init(&st, seed, pixel, sample);
+}
+__device__ __forceinline__ uint64_t ds_u64(rt_pstream& st) { return rt_pstream_u64(&st); }
 
-// math.rs:51-58
-__device__ __forceinline__ void random_in_unit_sphere(rt_stream& st, double scale_m11, double& x, double& y,
+// math.rs:51-58: random_double_range(-1, 1) x 3 until inside
+__device__ __forceinline__ void random_in_unit_sphere(rt_pstream& st, double scale_m11, double& x, double& y,
                                                       double& z, double& len2)
 {
-    // candidates in pairs over three blocks (rt_numerics.h): every lane in the loop is at
-    // the same candidate, so each iteration runs one code path (2 or 1 Philox blocks)
-    uint64_t d = 0;
-    for (int k = 0;; k ^= 1) {
-        uint64_t a, b, c;
-        if (k == 0) {
-            rt_stream_pair(&st, &a, &b);
-            rt_stream_pair(&st, &c, &d);
-        } else {
-            a = d;
-            rt_stream_pair(&st, &b, &c);
-        }
-        x = rt_uniform_sample(a, -1.0, scale_m11);
-        y = rt_uniform_sample(b, -1.0, scale_m11);
-        z = rt_uniform_sample(c, -1.0, scale_m11);
+    for (;;) {
+        x = rt_uniform_sample(ds_u64(st), -1.0, scale_m11);
+        y = rt_uniform_sample(ds_u64(st), -1.0, scale_m11);
+        z = rt_uniform_sample(ds_u64(st), -1.0, scale_m11);
         len2 = x * x + y * y + z * z;
         if (len2 < 1.0) return;
     }
@@ -835,18 +834,14 @@ __device__ __forceinline__ void random_in_unit_sphere(rt_stream& st, double scal
 // ---------------------------------------------------------------------------
 
 // main.rs:517-520 + Camera::get_ray (camera.rs:58-66)
-__device__ __forceinline__ void camera_ray(const KParams& P, int x, int y, rt_stream& st, Ray& r)
+__device__ __forceinline__ void camera_ray(const KParams& P, int x, int y, rt_pstream& st, Ray& r)
 {
-    uint64_t ju, jv;  // draw events: rt_numerics.h render-stream discipline
-    rt_stream_pair(&st, &ju, &jv);
-    const double u = ((double)x + rt_unit53(ju)) / ((double)P.width - 1.0);
-    const double v = ((double)y + rt_unit53(jv)) / ((double)P.height - 1.0);
+    const double u = ((double)x + rt_unit53(ds_u64(st))) / ((double)P.width - 1.0);
+    const double v = ((double)y + rt_unit53(ds_u64(st))) / ((double)P.height - 1.0);
     double dxl, dyl;
     for (;;) {
-        uint64_t a, b;
-        rt_stream_pair(&st, &a, &b);
-        dxl = rt_uniform_sample(a, -1.0, P.scale_m11);
-        dyl = rt_uniform_sample(b, -1.0, P.scale_m11);
+        dxl = rt_uniform_sample(ds_u64(st), -1.0, P.scale_m11);
+        dyl = rt_uniform_sample(ds_u64(st), -1.0, P.scale_m11);
         if (dxl * dxl + dyl * dyl + 0.0 * 0.0 < 1.0) break;
     }
     const double rdx = dxl * P.cam.lens_radius, rdy = dyl * P.cam.lens_radius;
@@ -859,7 +854,7 @@ __device__ __forceinline__ void camera_ray(const KParams& P, int x, int y, rt_st
     r.dx = P.cam.lower_left_corner[0] + P.cam.horizontal[0] * u + P.cam.vertical[0] * v - P.cam.origin[0] - offx;
     r.dy = P.cam.lower_left_corner[1] + P.cam.horizontal[1] * u + P.cam.vertical[1] * v - P.cam.origin[1] - offy;
     r.dz = P.cam.lower_left_corner[2] + P.cam.horizontal[2] * u + P.cam.vertical[2] * v - P.cam.origin[2] - offz;
-    r.time = rt_uniform_sample(rt_stream_fresh_u64(&st), P.cam.time0, P.scale_time);
+    r.time = rt_uniform_sample(ds_u64(st), P.cam.time0, P.scale_time);
 }
 
 // One hit of ray_color (main.rs:25-34): emitted + attenuation * (next), with the
@@ -867,12 +862,13 @@ __device__ __forceinline__ void camera_ray(const KParams& P, int x, int y, rt_st
 // DiffuseLight ends it), so adding T*e straight into the chunk sum gives the same bits
 // as the reference's per-sample sum. Returns true if the path continues with r.
 template <class C>
-__device__ __forceinline__ bool shade(const SceneDev& S, const KParams& P, const Hit& h, Ray& r, rt_stream& st,
+__device__ __forceinline__ bool shade(const SceneDev& S, const KParams& P, const Hit& h, Ray& r, rt_pstream& st,
                                       double& Tr, double& Tg, double& Tb, double& sum_r, double& sum_g,
                                       double& sum_b)
 {
     const rt_material& m = S.materials[h.mat];
-    if (m.kind == RT_MAT_DIFFUSE_LIGHT) {  // material.rs:25-34 (emits on both faces, never scatters)
+    const int kind = m.kind;
+    if (kind == RT_MAT_DIFFUSE_LIGHT) {  // material.rs:25-34 (emits on both faces, never scatters)
         double er, eg, eb;
         tex_value<C>(S, m.tex, h, er, eg, eb);
         sum_r = sum_r + Tr * er;
@@ -880,74 +876,64 @@ __device__ __forceinline__ bool shade(const SceneDev& S, const KParams& P, const
         sum_b = sum_b + Tb * eb;
         return false;
     }
+    // The materials share their expensive steps, so a wave holding several materials runs
+    // each once: one unit-sphere loop (Lambertian, Metal, Isotropic), one 1/sqrt (of the
+    // candidate for Lambertian, of the ray direction for Metal and Dielectric), one texture
+    // lookup (Lambertian, Isotropic).
+    double qx = 0.0, qy = 0.0, qz = 0.0, l2 = 1.0;
+    if (kind != RT_MAT_DIELECTRIC) random_in_unit_sphere(st, P.scale_m11, qx, qy, qz, l2);
+    const double inv = 1.0 / __builtin_sqrt(kind == RT_MAT_LAMBERTIAN ? l2 : r.a);
     double sdx, sdy, sdz, ar = 1.0, ag = 1.0, ab = 1.0;
     bool scattered = true;
-    switch (m.kind) {
-    case RT_MAT_LAMBERTIAN: {  // material.rs:36-48
-        double qx, qy, qz, l2;
-        random_in_unit_sphere(st, P.scale_m11, qx, qy, qz, l2);
-        const double inv = 1.0 / __builtin_sqrt(l2);
+    if (kind == RT_MAT_LAMBERTIAN) {  // material.rs:36-48
         sdx = h.nx + qx * inv;
         sdy = h.ny + qy * inv;
         sdz = h.nz + qz * inv;
         if (__builtin_fabs(sdx) < 1e-8 && __builtin_fabs(sdy) < 1e-8 && __builtin_fabs(sdz) < 1e-8) {
             sdx = h.nx; sdy = h.ny; sdz = h.nz;
         }
-        tex_value<C>(S, m.tex, h, ar, ag, ab);
-        break;
-    }
-    case RT_MAT_METAL: {  // material.rs:50-60
-        const double inv = 1.0 / __builtin_sqrt(r.a);
-        const double ux = r.dx * inv, uy = r.dy * inv, uz = r.dz * inv;
-        const double k2 = 2.0 * (ux * h.nx + uy * h.ny + uz * h.nz);
-        double qx, qy, qz, l2;
-        random_in_unit_sphere(st, P.scale_m11, qx, qy, qz, l2);
-        sdx = (ux - h.nx * k2) + qx * m.fuzz;
-        sdy = (uy - h.ny * k2) + qy * m.fuzz;
-        sdz = (uz - h.nz * k2) + qz * m.fuzz;
-        scattered = sdx * h.nx + sdy * h.ny + sdz * h.nz > 0.0;
-        ar = m.albedo[0]; ag = m.albedo[1]; ab = m.albedo[2];
-        break;
-    }
-    case RT_MAT_DIELECTRIC: {  // material.rs:62-82, 89-94
-        const double ratio = h.front ? (1.0 / m.ir) : m.ir;
-        const double inv = 1.0 / __builtin_sqrt(r.a);
-        const double ux = r.dx * inv, uy = r.dy * inv, uz = r.dz * inv;
-        const double cos_theta = fmin((-ux) * h.nx + (-uy) * h.ny + (-uz) * h.nz, 1.0);
-        const double sin_theta = __builtin_sqrt(1.0 - cos_theta * cos_theta);
-        const bool cannot_refract = ratio * sin_theta > 1.0;
-        bool reflect = cannot_refract;
-        if (!reflect) {
-            double r0 = (1.0 - ratio) / (1.0 + ratio);
-            r0 = r0 * r0;
-            const double refl = r0 + (1.0 - r0) * rt_pow5(1.0 - cos_theta);
-            reflect = refl > rnd01(st);
-        }
-        if (reflect) {
+    } else if (kind == RT_MAT_METAL || kind == RT_MAT_DIELECTRIC) {
+        const double ux = r.dx * inv, uy = r.dy * inv, uz = r.dz * inv;  // normalize(r_in.direction)
+        if (kind == RT_MAT_METAL) {  // material.rs:50-60
             const double k2 = 2.0 * (ux * h.nx + uy * h.ny + uz * h.nz);
-            sdx = ux - h.nx * k2;
-            sdy = uy - h.ny * k2;
-            sdz = uz - h.nz * k2;
-        } else {  // math.rs:110-117 (cos_theta recomputed there from the same inputs)
-            const double px = (ux + h.nx * cos_theta) * ratio;
-            const double py = (uy + h.ny * cos_theta) * ratio;
-            const double pz = (uz + h.nz * cos_theta) * ratio;
-            const double pl = px * px + py * py + pz * pz;
-            const double kk = -__builtin_sqrt(__builtin_fabs(1.0 - pl));
-            sdx = px + h.nx * kk;
-            sdy = py + h.ny * kk;
-            sdz = pz + h.nz * kk;
+            sdx = (ux - h.nx * k2) + qx * m.fuzz;
+            sdy = (uy - h.ny * k2) + qy * m.fuzz;
+            sdz = (uz - h.nz * k2) + qz * m.fuzz;
+            scattered = sdx * h.nx + sdy * h.ny + sdz * h.nz > 0.0;
+            ar = m.albedo[0]; ag = m.albedo[1]; ab = m.albedo[2];
+        } else {  // material.rs:62-82, 89-94
+            const double ratio = h.front ? (1.0 / m.ir) : m.ir;
+            const double cos_theta = fmin((-ux) * h.nx + (-uy) * h.ny + (-uz) * h.nz, 1.0);
+            const double sin_theta = __builtin_sqrt(1.0 - cos_theta * cos_theta);
+            const bool cannot_refract = ratio * sin_theta > 1.0;
+            bool reflect = cannot_refract;
+            if (!reflect) {  // the draw is skipped on TIR (the || short-circuit of material.rs:72)
+                double r0 = (1.0 - ratio) / (1.0 + ratio);
+                r0 = r0 * r0;
+                const double refl = r0 + (1.0 - r0) * rt_pow5(1.0 - cos_theta);
+                reflect = refl > rt_unit53(ds_u64(st));
+            }
+            if (reflect) {
+                const double k2 = 2.0 * (ux * h.nx + uy * h.ny + uz * h.nz);
+                sdx = ux - h.nx * k2;
+                sdy = uy - h.ny * k2;
+                sdz = uz - h.nz * k2;
+            } else {  // math.rs:110-117 (cos_theta recomputed there from the same inputs)
+                const double px = (ux + h.nx * cos_theta) * ratio;
+                const double py = (uy + h.ny * cos_theta) * ratio;
+                const double pz = (uz + h.nz * cos_theta) * ratio;
+                const double pl = px * px + py * py + pz * pz;
+                const double kk = -__builtin_sqrt(__builtin_fabs(1.0 - pl));
+                sdx = px + h.nx * kk;
+                sdy = py + h.ny * kk;
+                sdz = pz + h.nz * kk;
+            }
         }
-        break;
-    }
-    default: {  // isotropic, material.rs:84-87
-        double l2;
-        random_in_unit_sphere(st, P.scale_m11, sdx, sdy, sdz, l2);
-        tex_value<C>(S, m.tex, h, ar, ag, ab);
-        break;
-    }
+    } else {  // isotropic, material.rs:84-87
+        sdx = qx; sdy = qy; sdz = qz;
     }
     if (!scattered) return false;  // emitted (0) only
+    if (kind == RT_MAT_LAMBERTIAN || kind == RT_MAT_ISOTROPIC) tex_value<C>(S, m.tex, h, ar, ag, ab);
     Tr = Tr * ar;
     Tg = Tg * ag;
     Tb = Tb * ab;
@@ -1024,7 +1010,7 @@ __global__ void __launch_bounds__(256, min_waves<C>()) trace_chunks(SceneDev S, 
     if (C::COUNT) t_prev = __builtin_amdgcn_s_memtime();
     double sum_r = 0.0, sum_g = 0.0, sum_b = 0.0;
     Keyed key{P.seed, w.pixel, 0, 0};
-    rt_stream st;
+    rt_pstream st;
     Ray r;
     double Tr = 1, Tg = 1, Tb = 1;
     int depth = 0;
@@ -1034,7 +1020,7 @@ __global__ void __launch_bounds__(256, min_waves<C>()) trace_chunks(SceneDev S, 
         if (C::COUNT && first_active_lane()) cnt.wave_steps++;
         if (new_sample) {
             new_sample = false;
-            rt_stream_init(&st, P.seed, w.pixel, (uint32_t)s, RT_STREAM_MAIN);
+            ds_start(st, P.seed, w.pixel, (uint32_t)s);
             key.sample = (uint32_t)s;
             camera_ray(P, w.x, w.y, st, r);
             finish_ray<C>(r);
@@ -1131,7 +1117,7 @@ __global__ void __launch_bounds__(256, min_waves<C>()) trace_pool(SceneDev S, co
     int x = 0, k = 0, s = 0, depth = 0;
     double cr = 0, cg = 0, cb = 0, Tr = 1, Tg = 1, Tb = 1;
     Keyed key{P.seed, 0, 0, 0};
-    rt_stream st;
+    rt_pstream st;
     Ray r;
     for (;;) {
         uint64_t need = __ballot(!active);
@@ -1175,7 +1161,7 @@ __global__ void __launch_bounds__(256, min_waves<C>()) trace_pool(SceneDev S, co
             const int y = P.row_begin + k * P.row_stride;
             key.pixel = (uint32_t)y * (uint32_t)P.width + (uint32_t)x;
             key.sample = (uint32_t)s;
-            rt_stream_init(&st, P.seed, key.pixel, (uint32_t)s, RT_STREAM_MAIN);
+            ds_start(st, P.seed, key.pixel, (uint32_t)s);
             camera_ray(P, x, y, st, r);
             finish_ray<C>(r);
             Tr = Tg = Tb = 1.0;
@@ -1457,6 +1443,12 @@ hipError_t launch_trace(const SceneDev& S, const KParams& Ph, const KParams* P, 
         if (e != hipSuccess) return e;
     }
     const uint32_t f = variant_features(o.features);
+#ifdef RT_EXPERIMENT_SPHERES_ONLY  // A/B builds of the random-spheres variant only (scripts/ab_builds.py)
+    if (f != FEAT_SET_SPHERES) return hipErrorNotSupported;
+    if (o.count) launch_f<FEAT_SET_SPHERES, true>(L, o.slab32, o.lds_stack, stream);
+    else launch_f<FEAT_SET_SPHERES, false>(L, o.slab32, o.lds_stack, stream);
+    return hipGetLastError();
+#endif
     if (o.count) {
         if (f == FEAT_SET_SPHERES) launch_f<FEAT_SET_SPHERES, true>(L, o.slab32, o.lds_stack, stream);
         else if (f == FEAT_SET_RECTINST) launch_f<FEAT_SET_RECTINST, true>(L, o.slab32, o.lds_stack, stream);

@@ -1,0 +1,81 @@
+#!/usr/bin/env python3
+"""A/B whole library builds (e.g. lib/librtiow_amd.so vs lib/librtiow_exp_*.so built with
+__graft_entry__.build_library(extra_flags=[...], name=...)) on one render config.
+
+Each build runs in its own child process (RT_LIB_PATH picks the .so); the children run
+one after another, `--rounds` times round-robin, so clock drift spreads over all builds.
+Prints per-build median kernel ms and whether the f64 test image equals the first build's.
+
+usage: python scripts/ab_builds.py lib/a.so lib/b.so [--scene 0 --width 1200 --height 800 --spp 500]
+"""
+import argparse
+import hashlib
+import json
+import os
+import subprocess
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+CHILD = r"""
+import json, os, sys, time
+sys.path.insert(0, {repo!r})
+import numpy as np
+import __graft_entry__ as ge
+rt = ge.import_binding()
+a = json.loads({args!r})
+world = rt.World(1).build_scene(a["scene"])
+cam, bg = rt.scene_camera(a["scene"], a["width"], a["height"])
+r = rt.Renderer(0)
+r.upload(world)
+img = r.render(cam, rt.Renderer.params(a["width"], a["height"], 2, a["depth"], bg, 1, row_stride=8,
+                                       out_format=rt.RT_OUT_F64))
+p = rt.Renderer.params(a["width"], a["height"], a["spp"], a["depth"], bg, 1, out_format=rt.RT_OUT_F32)
+out = np.empty((a["height"], a["width"], 3), np.float32)
+r.render(cam, p, out)
+ms = []
+for _ in range(a["reps"]):
+    r.render(cam, p, out)
+    ms.append(r.stats().kernel_ms)
+import hashlib
+print("RESULT", json.dumps({{"ms": ms, "img": hashlib.sha1(img.tobytes()).hexdigest()}}))
+"""
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("libs", nargs="+")
+    ap.add_argument("--scene", type=int, default=0)
+    ap.add_argument("--width", type=int, default=1200)
+    ap.add_argument("--height", type=int, default=800)
+    ap.add_argument("--spp", type=int, default=500)
+    ap.add_argument("--depth", type=int, default=50)
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--rounds", type=int, default=2)
+    a = ap.parse_args()
+    args = json.dumps(dict(scene=a.scene, width=a.width, height=a.height, spp=a.spp, depth=a.depth, reps=a.reps))
+    code = CHILD.format(repo=REPO, args=args)
+    res = {lib: [] for lib in a.libs}
+    imgs = {}
+    for _ in range(a.rounds):
+        for lib in a.libs:
+            env = dict(os.environ, RT_LIB_PATH=os.path.abspath(os.path.join(REPO, lib)))
+            out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=600)
+            if out.returncode != 0:
+                print(f"{lib}: child failed ({out.returncode})\n{out.stderr[-2000:]}")
+                sys.exit(out.returncode if out.returncode > 0 else 1)
+            line = [x for x in out.stdout.splitlines() if x.startswith("RESULT ")][-1]
+            d = json.loads(line[7:])
+            res[lib] += d["ms"]
+            imgs[lib] = d["img"]
+            print(f"  {lib}: {['%.2f' % m for m in d['ms']]}", flush=True)
+    base = imgs[a.libs[0]]
+    n = a.width * a.height * a.spp
+    for lib in a.libs:
+        ms = sorted(res[lib])[len(res[lib]) // 2]
+        print(f"{lib}: median {ms:.2f} ms  min {min(res[lib]):.2f}  -> {n / ms / 1e3:.1f} Msamples/s  "
+              f"image == {a.libs[0]}: {imgs[lib] == base}")
+
+
+if __name__ == "__main__":
+    main()

@@ -50,6 +50,8 @@ def lib() -> ctypes.CDLL:
     l.orc_eval.restype = ctypes.c_int
     l.orc_philox.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
     l.orc_philox.restype = None
+    l.orc_pstream.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int, ctypes.c_void_p]
+    l.orc_pstream.restype = None
     l.orc_camera.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
     l.orc_camera.restype = ctypes.c_int
     return l
@@ -114,4 +116,10 @@ def camera(scene_id: int, width: int, height: int) -> np.ndarray:
     out = np.zeros(24, dtype=np.float64)
     if lib().orc_camera(scene_id, width, height, out.ctypes.data) != 0:
         raise ValueError(scene_id)
+    return out
+
+
+def pstream(seed: int, pixel: int, sample: int, n: int) -> np.ndarray:
+    out = np.zeros(n, np.uint64)
+    lib().orc_pstream(seed, pixel, sample, n, out.ctypes.data)
     return out

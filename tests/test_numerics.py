@@ -44,6 +44,34 @@ def test_philox_random123_published():
         [0xd16cfe09, 0x94fdcceb, 0x5001e420, 0x24126ea1]
 
 
+def _xoshiro128pp(state, n):
+    """xoshiro128++ as published (Blackman & Vigna, prng.di.unimi.it/xoshiro128plusplus.c)."""
+    M = 0xFFFFFFFF
+    rotl = lambda x, k: ((x << k) | (x >> (32 - k))) & M  # noqa: E731
+    s = list(state)
+    out = []
+    for _ in range(n):
+        out.append((rotl((s[0] + s[3]) & M, 7) + s[0]) & M)
+        t = (s[1] << 9) & M
+        s[2] ^= s[0]
+        s[3] ^= s[1]
+        s[1] ^= s[2]
+        s[0] ^= s[3]
+        s[2] ^= t
+        s[3] = rotl(s[3], 11)
+    return out
+
+
+@pytest.mark.parametrize("seed,pixel,sample", [(1, 0, 0), (1, 959999, 499), (0xDEADBEEF12345678, 17, 3)])
+def test_path_stream_is_philox_seeded_xoshiro128pp(seed, pixel, sample):
+    """rt_pstream: state = Philox4x32-10((pixel, sample, 0, RT_STREAM_PATH), seed); each u64
+    draw = (xoshiro128++ output << 32) | next output."""
+    state = ob.philox([pixel, sample, 0, 0x9A750000], [seed & 0xFFFFFFFF, seed >> 32])
+    words = _xoshiro128pp([int(v) for v in state], 40)
+    want = [(words[2 * i] << 32) | words[2 * i + 1] for i in range(20)]
+    assert [int(v) for v in ob.pstream(seed, pixel, sample, 20)] == want
+
+
 @pytest.mark.parametrize("p,uv", [
     ((1, 0, 0), (0.5, 0.5)), ((-1, 0, 0), (0.0, 0.5)), ((0, 1, 0), (0.5, 1.0)),
     ((0, -1, 0), (0.5, 0.0)), ((0, 0, 1), (0.25, 0.5)), ((0, 0, -1), (0.75, 0.5)),
