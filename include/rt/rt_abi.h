@@ -187,6 +187,12 @@ typedef struct rt_stats {
     uint64_t cycles_leaves;      /* count_work only: wave-cycles in leaf primitive tests (part of trace) */
     int32_t schedule;            /* RT_SCHED_* the last render ran with */
     int32_t n_batches;           /* trace launches it took (pool: per-sample buffer batches) */
+    uint64_t wave_leaf_steps;    /* count_work only: leaf-loop iterations per wave, summed;
+                                    prim_tests / (64 * wave_leaf_steps) = its lane occupancy */
+    uint64_t camera_lanes;       /* count_work only: lanes starting a sample, summed over the */
+    uint64_t camera_steps;       /*   wave iterations in which any lane did (camera_steps) */
+    uint64_t shade_lanes;        /* count_work only: lanes shading a hit, summed over the */
+    uint64_t shade_steps;        /*   wave iterations in which any lane did (shade_steps) */
 } rt_stats;
 int rt_last_stats(rt_ctx* ctx, rt_stats* out);
 

@@ -893,11 +893,18 @@ int rt_last_stats(rt_ctx* c, rt_stats* out)
             c->stats.wave_node_steps = h[7];
             c->stats.cycles_nodes = h[8];
             c->stats.cycles_leaves = h[9];
+            c->stats.wave_leaf_steps = h[10];
+            c->stats.camera_lanes = h[11];
+            c->stats.camera_steps = h[12];
+            c->stats.shade_lanes = h[13];
+            c->stats.shade_steps = h[14];
         } else {
             c->stats.casts = c->stats.node_visits = c->stats.prim_tests = 0;
             c->stats.cycles_camera = c->stats.cycles_trace = c->stats.cycles_shade = 0;
             c->stats.wave_steps = c->stats.wave_node_steps = 0;
             c->stats.cycles_nodes = c->stats.cycles_leaves = 0;
+            c->stats.wave_leaf_steps = c->stats.camera_lanes = c->stats.camera_steps = 0;
+            c->stats.shade_lanes = c->stats.shade_steps = 0;
         }
         c->pending_stats = false;
     }

@@ -63,6 +63,9 @@ struct Keyed {                 // coordinates of the medium's keyed draw
 struct Count {
     uint32_t casts, nodes, prims;
     uint32_t wave_steps, wave_nodes;  // loop iterations the wave executed (counted by its first active lane)
+    uint32_t wave_leaves;             // leaf-loop iterations the wave executed
+    uint32_t cam_lanes, cam_steps;    // lanes starting a sample / iterations in which any did
+    uint32_t shade_lanes, shade_steps;
     uint64_t t_nodes, t_leaves;       // wave-cycles in node-visit loops / leaf tests (same in every lane)
 };
 // COUNT only: true in exactly one active lane of the wave
@@ -270,13 +273,20 @@ __device__ __forceinline__ bool box_t(const rt_prim& p, const Ray& r, double t_m
     return any;
 }
 
-// center_0 + ((time - time_0) / (time_1 - time_0)) * (center_1 - center_0)   (hittable.rs:556-558)
-__device__ __forceinline__ void moving_center(const rt_prim& p, const Ray& r, double& cx, double& cy, double& cz)
+// The centre of a Sphere, or of a MovingSphere at the ray's time: center_0 +
+// ((time - time_0) / (time_1 - time_0)) * (center_1 - center_0) (hittable.rs:556-558).
+// Both kinds go through one code path (the moving centre is a select), so a wave whose
+// lanes hold both kinds runs the sphere test once, not once per kind.
+__device__ __forceinline__ void sphere_center(const rt_prim& p, const Ray& r, double& cx, double& cy, double& cz)
 {
-    const double s = p.a ? r.time : (r.time - p.p[8]) / (p.p[9] - p.p[8]);
-    cx = p.p[0] + p.p[5] * s;
-    cy = p.p[1] + p.p[6] * s;
-    cz = p.p[2] + p.p[7] * s;
+    const double c0x = p.p[0], c0y = p.p[1], c0z = p.p[2];
+    const double vx = p.p[5], vy = p.p[6], vz = p.p[7];
+    const bool moving = p.kind == RT_PRIM_MOVING_SPHERE;
+    double s = r.time;
+    if (moving && !p.a) s = (r.time - p.p[8]) / (p.p[9] - p.p[8]);
+    cx = moving ? c0x + vx * s : c0x;
+    cy = moving ? c0y + vy * s : c0y;
+    cz = moving ? c0z + vz * s : c0z;
 }
 
 // Sphere, MovingSphere, rects, Box: t-only (hittable.rs:211-231).
@@ -285,19 +295,12 @@ __device__ __forceinline__ bool simple_t(const rt_prim& p, const Ray& r, double 
                                          int& side, Count& cnt)
 {
     if (C::COUNT) cnt.prims++;
-    if constexpr (!(C::F & FEAT_RECT)) {
-        if (p.kind == RT_PRIM_SPHERE) return sphere_t(p.p[0], p.p[1], p.p[2], p.p[3], r, t_min, t_max, t);
+    if (!(C::F & FEAT_RECT) || p.kind <= RT_PRIM_MOVING_SPHERE) {
         double cx, cy, cz;
-        moving_center(p, r, cx, cy, cz);
+        sphere_center(p, r, cx, cy, cz);
         return sphere_t(cx, cy, cz, p.p[3], r, t_min, t_max, t);
     } else {
         switch (p.kind) {
-        case RT_PRIM_SPHERE: return sphere_t(p.p[0], p.p[1], p.p[2], p.p[3], r, t_min, t_max, t);
-        case RT_PRIM_MOVING_SPHERE: {
-            double cx, cy, cz;
-            moving_center(p, r, cx, cy, cz);
-            return sphere_t(cx, cy, cz, p.p[3], r, t_min, t_max, t);
-        }
         case RT_PRIM_XY_RECT: return rect_t(0, p.p[0], p.p[1], p.p[2], p.p[3], p.p[4], r, t_min, t_max, t);
         case RT_PRIM_XZ_RECT: return rect_t(1, p.p[0], p.p[1], p.p[2], p.p[3], p.p[4], r, t_min, t_max, t);
         case RT_PRIM_YZ_RECT: return rect_t(2, p.p[0], p.p[1], p.p[2], p.p[3], p.p[4], r, t_min, t_max, t);
@@ -323,13 +326,9 @@ __device__ __forceinline__ void simple_finish(const rt_prim& p, const Ray& r, do
             return;
         }
     }
-    if (p.kind == RT_PRIM_SPHERE) {
-        sphere_finish<C>(p.p[0], p.p[1], p.p[2], p.p[4], r, t, p.mat, h);
-    } else {
-        double cx, cy, cz;
-        moving_center(p, r, cx, cy, cz);
-        sphere_finish<C>(cx, cy, cz, p.p[4], r, t, p.mat, h);
-    }
+    double cx, cy, cz;
+    sphere_center(p, r, cx, cy, cz);
+    sphere_finish<C>(cx, cy, cz, p.p[4], r, t, p.mat, h);
 }
 
 // ---------------------------------------------------------------------------
@@ -441,6 +440,7 @@ __device__ __forceinline__ bool traverse(const SceneDev& S, int root, const Ray&
         code = ~code;
         const int first = code >> 5, count = code & 31;
         for (int i = 0; i < count; ++i) {
+            if (C::COUNT && first_active_lane()) cnt.wave_leaves++;
             const int prim = S.prim_refs[first + i];
             if (leaf(prim, t_max, best)) {
                 best.prim = prim;
@@ -1005,7 +1005,7 @@ __global__ void __launch_bounds__(256, min_waves<C>()) trace_chunks(SceneDev S, 
     if (!lane_work(P, w)) return;
     StackT<C> stack;
     if constexpr (C::LDS) stack.base = rt_lds + threadIdx.x;
-    Count cnt{0, 0, 0, 0, 0, 0, 0};
+    Count cnt{};
     uint64_t t_cam = 0, t_trace = 0, t_shade = 0, t_prev = 0;
     if (C::COUNT) t_prev = __builtin_amdgcn_s_memtime();
     double sum_r = 0.0, sum_g = 0.0, sum_b = 0.0;
@@ -1061,6 +1061,11 @@ __global__ void __launch_bounds__(256, min_waves<C>()) trace_chunks(SceneDev S, 
         atomicAdd(&counters[2], (unsigned long long)cnt.prims);
         atomicAdd(&counters[6], (unsigned long long)cnt.wave_steps);
         atomicAdd(&counters[7], (unsigned long long)cnt.wave_nodes);
+        atomicAdd(&counters[10], (unsigned long long)cnt.wave_leaves);
+        atomicAdd(&counters[11], (unsigned long long)cnt.cam_lanes);
+        atomicAdd(&counters[12], (unsigned long long)cnt.cam_steps);
+        atomicAdd(&counters[13], (unsigned long long)cnt.shade_lanes);
+        atomicAdd(&counters[14], (unsigned long long)cnt.shade_steps);
         // phase times are per wave (every active lane sees the same clock): one lane adds
         if ((int)(threadIdx.x & 63) == __ffsll((long long)__ballot(1)) - 1) {
             atomicAdd(&counters[3], (unsigned long long)t_cam);
@@ -1101,7 +1106,7 @@ __global__ void __launch_bounds__(256, min_waves<C>()) trace_pool(SceneDev S, co
     }
     StackT<C> stack;
     if constexpr (C::LDS) stack.base = rt_lds + threadIdx.x;
-    Count cnt{0, 0, 0, 0, 0, 0, 0};
+    Count cnt{};
     uint64_t t_cam = 0, t_trace = 0, t_shade = 0, t_prev = 0;
     if (C::COUNT) t_prev = __builtin_amdgcn_s_memtime();
     const int lane = threadIdx.x & 63;
@@ -1157,6 +1162,10 @@ __global__ void __launch_bounds__(256, min_waves<C>()) trace_pool(SceneDev S, co
         if (C::COUNT && first_active_lane()) cnt.wave_steps++;
         if (!active) continue;
         if (new_sample) {
+            if (C::COUNT) {
+                cnt.cam_lanes++;
+                if (first_active_lane()) cnt.cam_steps++;
+            }
             new_sample = false;
             const int y = P.row_begin + k * P.row_stride;
             key.pixel = (uint32_t)y * (uint32_t)P.width + (uint32_t)x;
@@ -1181,6 +1190,10 @@ __global__ void __launch_bounds__(256, min_waves<C>()) trace_pool(SceneDev S, co
                 cg = cg + Tg * P.bg[1];
                 cb = cb + Tb * P.bg[2];
             } else {
+                if (C::COUNT) {
+                    cnt.shade_lanes++;
+                    if (first_active_lane()) cnt.shade_steps++;
+                }
                 cont = shade<C>(S, P, h, r, st, Tr, Tg, Tb, cr, cg, cb);
             }
         }
@@ -1201,6 +1214,11 @@ __global__ void __launch_bounds__(256, min_waves<C>()) trace_pool(SceneDev S, co
         atomicAdd(&counters[2], (unsigned long long)cnt.prims);
         atomicAdd(&counters[6], (unsigned long long)cnt.wave_steps);
         atomicAdd(&counters[7], (unsigned long long)cnt.wave_nodes);
+        atomicAdd(&counters[10], (unsigned long long)cnt.wave_leaves);
+        atomicAdd(&counters[11], (unsigned long long)cnt.cam_lanes);
+        atomicAdd(&counters[12], (unsigned long long)cnt.cam_steps);
+        atomicAdd(&counters[13], (unsigned long long)cnt.shade_lanes);
+        atomicAdd(&counters[14], (unsigned long long)cnt.shade_steps);
         if (lane == 0) {  // every lane stays in the loop to the end: lane 0 saw the wave's whole time
             atomicAdd(&counters[3], (unsigned long long)t_cam);
             atomicAdd(&counters[4], (unsigned long long)t_trace);

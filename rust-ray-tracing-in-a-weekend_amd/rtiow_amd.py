@@ -116,7 +116,10 @@ class Stats(ctypes.Structure):
                 ("cycles_trace", ctypes.c_uint64), ("cycles_shade", ctypes.c_uint64),
                 ("wave_steps", ctypes.c_uint64), ("wave_node_steps", ctypes.c_uint64),
                 ("cycles_nodes", ctypes.c_uint64), ("cycles_leaves", ctypes.c_uint64),
-                ("schedule", ctypes.c_int32), ("n_batches", ctypes.c_int32)]
+                ("schedule", ctypes.c_int32), ("n_batches", ctypes.c_int32),
+                ("wave_leaf_steps", ctypes.c_uint64), ("camera_lanes", ctypes.c_uint64),
+                ("camera_steps", ctypes.c_uint64), ("shade_lanes", ctypes.c_uint64),
+                ("shade_steps", ctypes.c_uint64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

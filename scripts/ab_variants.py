@@ -149,7 +149,12 @@ def main():
               f"shade {st.cycles_shade / tot:.3f};  casts/sample {st.casts / st.samples:.3f}  "
               f"nodes/cast {st.node_visits / max(st.casts, 1):.2f}  prims/cast {st.prim_tests / max(st.casts, 1):.2f}")
         print(f"lane occupancy (spp_chunk {chunk}): bounce loop {st.casts / max(64 * st.wave_steps, 1):.3f}  "
-              f"node-visit loop {st.node_visits / max(64 * st.wave_node_steps, 1):.3f}")
+              f"node-visit loop {st.node_visits / max(64 * st.wave_node_steps, 1):.3f}  "
+              f"leaf loop {st.prim_tests / max(64 * st.wave_leaf_steps, 1):.3f}  "
+              f"camera {st.camera_lanes / max(64 * st.camera_steps, 1):.3f} ({st.camera_steps / max(st.wave_steps, 1):.3f} of iterations)  "
+              f"shade {st.shade_lanes / max(64 * st.shade_steps, 1):.3f} ({st.shade_steps / max(st.wave_steps, 1):.3f} of iterations)")
+        print(f"per wave iteration: node steps {st.wave_node_steps / max(st.wave_steps, 1):.2f}  "
+              f"leaf steps {st.wave_leaf_steps / max(st.wave_steps, 1):.2f}")
     if args.chunks:
         cks = [int(x) for x in args.chunks.split(",")]
         ct = {k: [] for k in cks}
