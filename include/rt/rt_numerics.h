@@ -292,6 +292,17 @@ RT_HD double rt_sin(double x)
  * product of three such factors is nonzero with this sign unless a factor is tiny. */
 RT_HD int rt_sin_sign(double x)
 {
+    /* Fast path, no argument reduction: for |x| < 2^16, q = x * (1/pi) is within 5e-12 of
+     * x/pi, so when its fractional part lies 1e-9 or more away from an integer,
+     * floor(x/pi) = floor(q) and sin x has the sign (-1)^floor(q), with |sin x| > 3e-9,
+     * far above rt_sin's error: the same sign rt_sin gives. Otherwise (near a multiple
+     * of pi, large, inf or NaN) the reduction below decides. */
+    if (__builtin_fabs(x) < 65536.0) {
+        const double q = x * 0.31830988618379067154;
+        const double k = __builtin_floor(q);
+        const double f = q - k;
+        if (f > 1e-9 && f < 1.0 - 1e-9) return (((int64_t)k) & 1) ? -1 : 1;
+    }
     const double tiny = 0x1.0p-339;
     uint32_t ix = (uint32_t)(rt_f64_bits(x) >> 32) & 0x7fffffffu;
     if (ix <= 0x3fe921fbu) {

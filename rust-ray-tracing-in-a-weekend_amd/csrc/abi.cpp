@@ -453,15 +453,19 @@ int rt_ctx_upload_soa(rt_ctx* c, const rt_scene_soa* s)
             return fail(RT_ERR_INVALID, "bad instance child");
     }
 
-    size_t off[9], bytes[9] = {
+    // the primitive records in leaf-slot order (prims[prim_refs[j]]): the kernel's leaf
+    // loops read a record without first loading its index
+    std::vector<rt_prim> leaf_prims((size_t)s->n_prim_refs);
+    for (int j = 0; j < s->n_prim_refs; ++j) leaf_prims[(size_t)j] = s->prims[s->prim_refs[j]];
+    size_t off[10], bytes[10] = {
         (size_t)s->n_nodes * sizeof(rt_bvh_node), (size_t)s->n_prim_refs * 4, (size_t)s->n_prims * sizeof(rt_prim),
         (size_t)s->n_instances * sizeof(rt_instance), (size_t)s->n_materials * sizeof(rt_material),
         (size_t)s->n_textures * sizeof(rt_texture), (size_t)s->n_perlin * 768 * 8, (size_t)s->n_perlin * 768 * 4,
-        (size_t)s->image_bytes};
-    const void* src[9] = {s->nodes, s->prim_refs, s->prims, s->instances, s->materials, s->textures,
-                          s->perlin_ranvec, s->perlin_perm, s->image_data};
+        (size_t)s->image_bytes, (size_t)s->n_prim_refs * sizeof(rt_prim)};
+    const void* src[10] = {s->nodes, s->prim_refs, s->prims, s->instances, s->materials, s->textures,
+                           s->perlin_ranvec, s->perlin_perm, s->image_data, leaf_prims.data()};
     size_t total = 0;
-    for (int i = 0; i < 9; ++i) {
+    for (int i = 0; i < 10; ++i) {
         off[i] = total;
         total = align_up(total + bytes[i], 256);
     }
@@ -476,7 +480,7 @@ int rt_ctx_upload_soa(rt_ctx* c, const rt_scene_soa* s)
         c->scene_bytes = total;
     }
     char* base = (char*)c->scene_buf;
-    for (int i = 0; i < 9; ++i)
+    for (int i = 0; i < 10; ++i)
         if (bytes[i]) HIP_TRY(hipMemcpy(base + off[i], src[i], bytes[i], hipMemcpyHostToDevice));
     c->S.nodes = (const rt_bvh_node*)(base + off[0]);
     c->S.prim_refs = (const int32_t*)(base + off[1]);
@@ -487,6 +491,7 @@ int rt_ctx_upload_soa(rt_ctx* c, const rt_scene_soa* s)
     c->S.perlin_ranvec = (const double*)(base + off[6]);
     c->S.perlin_perm = (const int32_t*)(base + off[7]);
     c->S.image = (const uint8_t*)(base + off[8]);
+    c->S.leaf_prims = (const rt_prim*)(base + off[9]);
     c->S.tlas_root = s->tlas_root;
     c->S.n_lds_nodes = 0;
     // traversal stack: TLAS walk, then a nested BLAS walk (instances) above it

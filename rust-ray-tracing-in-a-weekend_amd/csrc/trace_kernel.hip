@@ -166,10 +166,18 @@ __device__ __forceinline__ bool sphere_t(double cx, double cy, double cz, double
     const double c = (ocx * ocx + ocy * ocy + ocz * ocz) - radius * radius;
     const double disc = half_b * half_b - r.a * c;
     if (disc < 0.0) return false;
+#ifdef RT_PROBE_FAST_SPHERE  // timing probe (inexact sqrt / division): NOT the product
+    const double sqrtd = __builtin_amdgcn_sqrt(disc);
+    const double ia = __builtin_amdgcn_rcp(r.a);
+    double root = (-half_b - sqrtd) * ia;
+    if (root < t_min || t_max < root) {
+        root = (-half_b + sqrtd) * ia;
+#else
     const double sqrtd = __builtin_sqrt(disc);
     double root = (-half_b - sqrtd) / r.a;
     if (root < t_min || t_max < root) {
         root = (-half_b + sqrtd) / r.a;
+#endif
         if (root < t_min || t_max < root) return false;
     }
     t = root;
@@ -393,8 +401,9 @@ __device__ __forceinline__ Node load_node(const rt_bvh_node* base, int i)
     return n;
 }
 
-// Closest hit in a BVH (nodes + leaf ranges of prim_refs). `leaf(prim, t_max, best)`
-// tests one primitive; on a closer hit it fills best (t and sub ids) and returns true.
+// Closest hit in a BVH (nodes + leaf ranges of slots j, whose records are leaf_prims[j]).
+// `leaf(slot, t_max, best)` tests one primitive; on a closer hit it fills best (t and sub
+// ids) and returns true; best.prim is then the slot.
 template <class C, bool NL = false, class LeafFn>
 __device__ __forceinline__ bool traverse(const SceneDev& S, int root, const Ray& r, double t_min, double t_max,
                                          HitRef& best, StackT<C>& stack, int sp0, Count& cnt, LeafFn&& leaf)
@@ -441,9 +450,9 @@ __device__ __forceinline__ bool traverse(const SceneDev& S, int root, const Ray&
         const int first = code >> 5, count = code & 31;
         for (int i = 0; i < count; ++i) {
             if (C::COUNT && first_active_lane()) cnt.wave_leaves++;
-            const int prim = S.prim_refs[first + i];
-            if (leaf(prim, t_max, best)) {
-                best.prim = prim;
+            const int slot = first + i;
+            if (leaf(slot, t_max, best)) {
+                best.prim = slot;
                 t_max = best.t;
                 any = true;
                 if constexpr (C::S32) tmax_f = f32_up(t_max);
@@ -548,8 +557,8 @@ __device__ bool instance_t(const SceneDev& S, const rt_instance& in, const Ray& 
     }
     HitRef inner;
     if (!traverse<C>(S, in.child, r, t_min, t_max, inner, stack, sp0, cnt,
-                     [&](int prim, double tmax, HitRef& b) {
-                         return simple_t<C>(S.prims[prim], r, t_min, tmax, b.t, b.side, cnt);
+                     [&](int slot, double tmax, HitRef& b) {
+                         return simple_t<C>(S.leaf_prims[slot], r, t_min, tmax, b.t, b.side, cnt);
                      }))
         return false;
     ref.t = inner.t;
@@ -564,7 +573,9 @@ __device__ void instance_finish(const SceneDev& S, const rt_instance& in, const 
     Ray r = ray;
     double dirx[4], diry[4], dirz[4];
     instance_ray(in, r, dirx, diry, dirz);
-    simple_finish<C>(S.prims[ref.sub], r, ref.t, ref.side, h);
+    // ref.sub: the child prim (RT_CHILD_PRIM) or the BLAS leaf slot
+    simple_finish<C>(in.child_kind == RT_CHILD_PRIM ? S.prims[ref.sub] : S.leaf_prims[ref.sub], r, ref.t, ref.side,
+                     h);
     const int n = in.n_ops;
 #pragma unroll
     for (int i = 3; i >= 0; --i) {
@@ -648,8 +659,8 @@ __device__ bool trace_world(const SceneDev& S, const Ray& r, Hit& h, StackT<C>& 
     HitRef best;
     best.sub = 0;
     best.side = 0;
-    auto leaf = [&](int prim, double tmax, HitRef& b) {
-        const rt_prim& p = S.prims[prim];
+    auto leaf = [&](int slot, double tmax, HitRef& b) {
+        const rt_prim& p = S.leaf_prims[slot];
         if constexpr ((C::F & FEAT_INST) != 0)
             if (p.kind == RT_PRIM_INSTANCE)
                 return instance_t<C>(S, S.instances[p.a], r, t_min, tmax, b, stack, S.blas_base, cnt);
@@ -659,7 +670,7 @@ __device__ bool trace_world(const SceneDev& S, const Ray& r, Hit& h, StackT<C>& 
     };
     const bool hit = traverse<C, true>(S, S.tlas_root, r, t_min, RT_INF, best, stack, 0, cnt, leaf);
     if (!hit) return false;
-    const rt_prim& p = S.prims[best.prim];
+    const rt_prim& p = S.leaf_prims[best.prim];
     if constexpr ((C::F & FEAT_INST) != 0) {
         if (p.kind == RT_PRIM_INSTANCE) {
             instance_finish<C>(S, S.instances[p.a], r, best, h);
@@ -750,6 +761,9 @@ __device__ void hit_uv(const Hit& h, double& u, double& v)
 // the full product only when a factor may be tiny enough to underflow it
 __device__ __forceinline__ bool checker_odd(const Hit& h)
 {
+#ifdef RT_PROBE_NO_CHECKER  // timing probe: NOT the product
+    return h.px * h.pz < 0.0;
+#endif
     const double ax = 10.0 * h.px, ay = 10.0 * h.py, az = 10.0 * h.pz;
     const int sx = rt_sin_sign(ax), sy = rt_sin_sign(ay), sz = rt_sin_sign(az);
     if (sx == 2 || sy == 2 || sz == 2) return rt_sin(ax) * rt_sin(ay) * rt_sin(az) < 0.0;
@@ -836,8 +850,13 @@ __device__ __forceinline__ void random_in_unit_sphere(rt_pstream& st, double sca
 // main.rs:517-520 + Camera::get_ray (camera.rs:58-66)
 __device__ __forceinline__ void camera_ray(const KParams& P, int x, int y, rt_pstream& st, Ray& r)
 {
+#ifdef RT_PROBE_FAST_CAMERA  // timing probe: NOT the product
+    const double u = ((double)x + rt_unit53(ds_u64(st))) * __builtin_amdgcn_rcp((double)P.width - 1.0);
+    const double v = ((double)y + rt_unit53(ds_u64(st))) * __builtin_amdgcn_rcp((double)P.height - 1.0);
+#else
     const double u = ((double)x + rt_unit53(ds_u64(st))) / ((double)P.width - 1.0);
     const double v = ((double)y + rt_unit53(ds_u64(st))) / ((double)P.height - 1.0);
+#endif
     double dxl, dyl;
     for (;;) {
         dxl = rt_uniform_sample(ds_u64(st), -1.0, P.scale_m11);
@@ -882,7 +901,11 @@ __device__ __forceinline__ bool shade(const SceneDev& S, const KParams& P, const
     // lookup (Lambertian, Isotropic).
     double qx = 0.0, qy = 0.0, qz = 0.0, l2 = 1.0;
     if (kind != RT_MAT_DIELECTRIC) random_in_unit_sphere(st, P.scale_m11, qx, qy, qz, l2);
+#ifdef RT_PROBE_FAST_SHADE  // timing probe: NOT the product
+    const double inv = __builtin_amdgcn_rsq(kind == RT_MAT_LAMBERTIAN ? l2 : r.a);
+#else
     const double inv = 1.0 / __builtin_sqrt(kind == RT_MAT_LAMBERTIAN ? l2 : r.a);
+#endif
     double sdx, sdy, sdz, ar = 1.0, ag = 1.0, ab = 1.0;
     bool scattered = true;
     if (kind == RT_MAT_LAMBERTIAN) {  // material.rs:36-48
@@ -1148,9 +1171,17 @@ __global__ void __launch_bounds__(256, min_waves<C>()) trace_pool(SceneDev S, co
             const unsigned take = min((unsigned)__popcll(need), blk_units - blk_next);
             if (!active && rank < take) {
                 const unsigned u = blk_next + rank;
-                const unsigned si = u / nvalid, p = u - si * nvalid;
-                x = tx0 + (int)(p % (unsigned)vw);
-                k = tk0 + (int)(p / (unsigned)vw);
+                unsigned si;
+                if (nvalid == 64u) {  // a full 8x8 tile (wave-uniform): shifts, not divisions
+                    si = u >> 6;
+                    x = tx0 + (int)(u & 7u);
+                    k = tk0 + (int)((u >> 3) & 7u);
+                } else {
+                    si = u / nvalid;
+                    const unsigned p = u - si * nvalid;
+                    x = tx0 + (int)(p % (unsigned)vw);
+                    k = tk0 + (int)(p / (unsigned)vw);
+                }
                 s = s0 + (int)si;
                 active = true;
                 new_sample = true;

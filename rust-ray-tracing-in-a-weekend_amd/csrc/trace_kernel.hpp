@@ -11,6 +11,8 @@ namespace rtk {
 struct SceneDev {
     const rt_prim* prims;
     const int32_t* prim_refs;
+    const rt_prim* leaf_prims;  // prims[prim_refs[j]] for every leaf slot j (copied at upload):
+                                // a primitive test reads its record directly, not through prim_refs
     const rt_bvh_node* nodes;
     const rt_instance* instances;
     const rt_material* materials;
