@@ -117,16 +117,23 @@ def main():
         else:
             frame[:] = slab[:H]
 
-    for _ in range(args.warmup):
+    def progress(msg):   # stderr, one line per step: long configs (C5) keep the run visibly alive
+        if rank == 0:
+            print(f"bench: {msg}", file=sys.stderr, flush=True)
+
+    for i in range(args.warmup):
         step()
+        torch.cuda.synchronize(device)
+        progress(f"warmup {i + 1}/{args.warmup}")
     torch.cuda.synchronize(device)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(device)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for i in range(args.steps):
         step()
         kernel_ms.append(renderer.stats().kernel_ms)   # HIP events around the trace kernel on `stream`
+        progress(f"step {i + 1}/{args.steps}: kernel {kernel_ms[-1]:.1f} ms")
     torch.cuda.synchronize(device)
     if world > 1:
         dist.barrier()
@@ -171,6 +178,7 @@ def main():
     if args.ppm and rank == 0:
         rt.write_ppm(frame.cpu().numpy(), args.ppm)
 
+    progress("timed steps done; count pass and CPU baseline")
     # ---- CPU baseline (rank 0, N = 1 only)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -182,15 +190,21 @@ def main():
         _, st1 = ob.render(args.scene, W, H, min(spp, 16), depth, args.seed, args.seed, row_begin=0,
                            row_stride=cal_stride, threads=cores, return_stats=True)
         rate = st1.samples / max(st1.seconds, 1e-9)
-        n_rows = int(args.cpu_seconds * rate / (W * spp))
+        target = args.cpu_seconds * rate            # samples worth ~cpu_seconds
+        n_rows = int(target / (W * spp))
         n_rows = max(cores, min(H, n_rows // cores * cores))
         stride = max(1, H // n_rows)
-        _, st = ob.render(args.scene, W, H, spp, depth, args.seed, args.seed, row_begin=0, row_stride=stride,
+        n_rows = len(range(0, H, stride))
+        # a frame too large for even `cores` full rows (C5) takes the first spp_cpu samples
+        # of every pixel of those rows: the per-sample work is the same
+        spp_cpu = int(min(spp, max(1, target // (n_rows * W))))
+        _, st = ob.render(args.scene, W, H, spp_cpu, depth, args.seed, args.seed, row_begin=0, row_stride=stride,
                           threads=cores, return_stats=True)
+        spp_note = "" if spp_cpu == spp else f", samples 0..{spp_cpu - 1} of each pixel"
         cpu = {"value": st.samples / st.seconds / 1e6, "unit": "Msamples/s", "cores": cores, "kind": "port",
                "sample": f"oracle (C, f64, recursive ray_color, linear hit_hittables scan) on rows y % {stride} == 0 "
-                         f"of the same {W}x{H}x{spp} depth-{depth} frame: {st.samples} samples in {st.seconds:.1f} s "
-                         f"on {cores} threads"}
+                         f"of the same {W}x{H}x{spp} depth-{depth} frame{spp_note}: {st.samples} samples in "
+                         f"{st.seconds:.1f} s on {cores} threads"}
 
     if rank == 0:
         out = {

@@ -37,6 +37,7 @@ struct Ray {
     double ix, iy, iz;        // 1 / direction (f64 slab tests only)
     float fix, fiy, fiz;      // f32 1 / direction (f32 slab tests only)
     float fox, foy, foz;      // -origin * (1 / direction) in f32
+    uint32_t onx, ony, onz;   // byte offsets in a node of child 0's near planes (by direction sign)
 };
 
 // The HitRecord of hittable.rs:6-27 (uv deferred to texture lookup: uvkind 1 keeps the
@@ -135,6 +136,10 @@ __device__ __forceinline__ void finish_ray(Ray& r)
         r.fox = -(float)r.ox * r.fix;
         r.foy = -(float)r.oy * r.fiy;
         r.foz = -(float)r.oz * r.fiz;
+        // rt_bvh_node: lo0 at bytes 0/4/8, hi0 at 12/16/20 (x/y/z); child 1's box 24 bytes on
+        r.onx = r.fix >= 0.0f ? 0u : 12u;
+        r.ony = r.fiy >= 0.0f ? 4u : 16u;
+        r.onz = r.fiz >= 0.0f ? 8u : 20u;
     } else {
         r.ix = 1.0 / r.dx;
         r.iy = 1.0 / r.dy;
@@ -420,9 +425,45 @@ __device__ __forceinline__ bool traverse(const SceneDev& S, int root, const Ray&
         tmin_f = f32_down(t_min);
         tmax_f = f32_up(t_max);
     }
+    // TLAS entirely in LDS, f32 slabs: each plane is read at the offset the ray's
+    // direction signs select (near plane first), so the slab test needs no min/max pair
+    // per axis: t_near = max(near planes), t_far = min(far planes)
+    constexpr bool OCT = NL && C::NALL && C::S32;
+    const char* const lb = reinterpret_cast<const char*>(lds_nodes);
+    const char *pnx = lb, *pny = lb, *pnz = lb, *pfx = lb, *pfy = lb, *pfz = lb;
+    if constexpr (OCT) {
+        pnx = lb + r.onx; pfx = lb + (r.onx ^ 12u);
+        pny = lb + r.ony; pfy = lb + (r.ony ^ 20u);
+        pnz = lb + r.onz; pfz = lb + (r.onz ^ 28u);
+    }
     // one node visit: test both children, continue with the nearer, push the farther
     auto visit = [&](int node) -> int {
         if (C::COUNT) cnt.nodes++;
+        if constexpr (OCT) {
+            const int o = node * 64;
+            auto plane = [&](const char* p, int child) { return *reinterpret_cast<const float*>(p + o + 24 * child); };
+            const int2 ch = *reinterpret_cast<const int2*>(lb + o + 48);
+            float tn[2], tf[2];
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+                const float nx = __builtin_fmaf(plane(pnx, c), r.fix, r.fox);
+                const float ny = __builtin_fmaf(plane(pny, c), r.fiy, r.foy);
+                const float nz = __builtin_fmaf(plane(pnz, c), r.fiz, r.foz);
+                const float fx = __builtin_fmaf(plane(pfx, c), r.fix, r.fox);
+                const float fy = __builtin_fmaf(plane(pfy, c), r.fiy, r.foy);
+                const float fz = __builtin_fmaf(plane(pfz, c), r.fiz, r.foz);
+                tn[c] = fmaxf(fmaxf(nx, ny), fmaxf(nz, tmin_f));
+                tf[c] = fminf(fminf(fx, fy), fminf(fz, tmax_f));
+            }
+            const bool h0 = tn[0] <= tf[0], h1 = tn[1] <= tf[1], near0 = tn[0] <= tn[1];
+            if (h0 && h1) {
+                stack[sp++] = near0 ? ch.y : ch.x;
+                return near0 ? ch.x : ch.y;
+            }
+            if (h0) return ch.x;
+            if (h1) return ch.y;
+            return sp == sp0 ? RT_DONE : stack[--sp];
+        }
         const Node nd = (NL && (C::NALL || node < S.n_lds_nodes)) ? load_node(lds_nodes, node)
                                                                   : load_node(S.nodes, node);
         bool h0, h1, near0;
