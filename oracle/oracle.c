@@ -1277,6 +1277,7 @@ int orc_eval(int fn, const double* x, const double* y, const double* z, double* 
         case 10: out[i] = rt_unit53(rt_f64_bits(x[i])); break;
         case 11: out[i] = rt_uniform_sample(rt_f64_bits(x[i]), -1.0, rt_uniform_incl_scale(-1.0, 1.0)); break;
         case 12: out[i] = (double)rt_sin_sign(x[i]); break;
+        case 13: out[i] = x[i] / y[i]; break;   /* the kernel's reciprocal division (div_rcp) */
         default: return -1;
         }
     }

@@ -585,6 +585,10 @@ static int run_range(rt_ctx* c, const rt_camera* cam, const rt_render_params* p,
     for (int i = 0; i < 3; ++i) K.bg[i] = p->background[i];
     K.scale_m11 = rt_uniform_incl_scale(-1.0, 1.0);
     K.scale_time = rt_uniform_incl_scale(cam->time0, cam->time1);
+    K.wm1 = (double)p->width - 1.0;
+    K.hm1 = (double)p->height - 1.0;
+    K.inv_wm1 = 1.0 / K.wm1;
+    K.inv_hm1 = 1.0 / K.hm1;
     K.seed = p->render_seed;
     K.width = p->width;
     K.height = p->height;
@@ -958,7 +962,7 @@ int rt_ctx_set_schedule(rt_ctx* c, int schedule)
 
 int rt_device_eval(rt_ctx* c, int fn, const double* x, const double* y, const double* z, double* out, int n)
 {
-    if (!c || !x || !out || n < 0 || fn < 0 || fn > 12) return fail(RT_ERR_INVALID, "bad argument");
+    if (!c || !x || !out || n < 0 || fn < 0 || fn > 13) return fail(RT_ERR_INVALID, "bad argument");
     if (n == 0) return RT_OK;
     HIP_TRY(hipSetDevice(c->device));
     double* d = nullptr;

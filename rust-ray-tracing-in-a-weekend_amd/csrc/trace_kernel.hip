@@ -34,6 +34,7 @@ struct Ray {
     double dx, dy, dz;
     double time;
     double a;                 // length_squared(direction)
+    double ya;                // 1 / a correctly rounded (NaN outside [2^-900, 2^900]: see div_rcp)
     double ix, iy, iz;        // 1 / direction (f64 slab tests only)
     float fix, fiy, fiz;      // f32 1 / direction (f32 slab tests only)
     float fox, foy, foz;      // -origin * (1 / direction) in f32
@@ -116,6 +117,28 @@ template <class C>
 using StackT = Stack<C::LDS>;
 extern __shared__ int rt_lds[];  // [stack entries x 256 lanes] [cached TLAS nodes]
 
+// Division by a value b used many times, through its correctly rounded reciprocal
+// y = RN(1/b): q0 = RN(q*y), then one correction q1 = RN(q0 + RN-exact(q - b*q0) * y).
+// With y correctly rounded this is Markstein's theorem (IBM J. R&D 34(1), 1990): q1 =
+// RN(q/b), bit for bit what `q / b` gives, barring overflow / underflow in the products,
+// which the range guard on b excludes (y is NaN outside it, and the division runs then);
+// checked on 8e8 random and adversarial pairs on the host (all-ones / power-of-two
+// significands, both signs, exponents -20..20). A zero q may come out as -0 where q / b
+// gives +0 or the reverse; every caller compares the quotient with t_min > 0 first or
+// has q, b >= 0, so the sign of a zero quotient changes nothing.
+__device__ __forceinline__ double rcp_for_div(double b)
+{
+    const double m = __builtin_fabs(b);
+    return (m >= 0x1.0p-900 && m <= 0x1.0p+900) ? 1.0 / b : __builtin_nan("");
+}
+__device__ __forceinline__ double div_rcp(double q, double b, double y)
+{
+    const double q0 = q * y;
+    const double q1 = __builtin_fma(__builtin_fma(-b, q0, q), y, q0);
+    if (__builtin_expect(q1 != q1, 0)) return q / b;  // y outside the guard (or q not finite)
+    return q1;
+}
+
 __device__ __forceinline__ float f32_inv_dir(double d)
 {
     // an exact 0 would give inf * 0 = NaN in the slab products; a 1e-30 component keeps the
@@ -129,6 +152,7 @@ template <class C>
 __device__ __forceinline__ void finish_ray(Ray& r)
 {
     r.a = r.dx * r.dx + r.dy * r.dy + r.dz * r.dz;
+    r.ya = rcp_for_div(r.a);
     if constexpr (C::S32) {
         r.fix = f32_inv_dir(r.dx);
         r.fiy = f32_inv_dir(r.dy);
@@ -179,9 +203,9 @@ __device__ __forceinline__ bool sphere_t(double cx, double cy, double cz, double
         root = (-half_b + sqrtd) * ia;
 #else
     const double sqrtd = __builtin_sqrt(disc);
-    double root = (-half_b - sqrtd) / r.a;
+    double root = div_rcp(-half_b - sqrtd, r.a, r.ya);
     if (root < t_min || t_max < root) {
-        root = (-half_b + sqrtd) / r.a;
+        root = div_rcp(-half_b + sqrtd, r.a, r.ya);
 #endif
         if (root < t_min || t_max < root) return false;
     }
@@ -895,8 +919,8 @@ __device__ __forceinline__ void camera_ray(const KParams& P, int x, int y, rt_ps
     const double u = ((double)x + rt_unit53(ds_u64(st))) * __builtin_amdgcn_rcp((double)P.width - 1.0);
     const double v = ((double)y + rt_unit53(ds_u64(st))) * __builtin_amdgcn_rcp((double)P.height - 1.0);
 #else
-    const double u = ((double)x + rt_unit53(ds_u64(st))) / ((double)P.width - 1.0);
-    const double v = ((double)y + rt_unit53(ds_u64(st))) / ((double)P.height - 1.0);
+    const double u = div_rcp((double)x + rt_unit53(ds_u64(st)), P.wm1, P.inv_wm1);
+    const double v = div_rcp((double)y + rt_unit53(ds_u64(st)), P.hm1, P.inv_hm1);
 #endif
     double dxl, dyl;
     for (;;) {
@@ -1436,6 +1460,7 @@ __global__ void eval_numerics(int fn, const double* x, const double* y, const do
     case 10: r = rt_unit53(rt_f64_bits(x[i])); break;
     case 11: r = rt_uniform_sample(rt_f64_bits(x[i]), -1.0, rt_uniform_incl_scale(-1.0, 1.0)); break;
     case 12: r = (double)rt_sin_sign(x[i]); break;
+    case 13: r = div_rcp(x[i], y[i], rcp_for_div(y[i])); break;   // must equal x / y bit for bit
     default: break;
     }
     out[i] = r;

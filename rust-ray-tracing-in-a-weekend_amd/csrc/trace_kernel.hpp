@@ -33,6 +33,8 @@ struct KParams {
     double bg[3];
     double scale_m11;   // rand UniformFloat::new_inclusive(-1, 1) scale
     double scale_time;  // rand UniformFloat::new_inclusive(time0, time1) scale
+    double wm1, hm1;    // width - 1, height - 1 (the jitter divisors of main.rs:517-518)
+    double inv_wm1, inv_hm1;  // 1 / (width - 1), 1 / (height - 1), correctly rounded
     uint64_t seed;
     int32_t width, height, spp, max_depth;
     int32_t spp_chunk, n_chunks;

@@ -44,12 +44,21 @@ def test_device_numerics_bit_equal_host(rt, renderer):
     n = rng.normal(size=(3, 3000))
     n /= np.linalg.norm(n, axis=0)
     bits = rng.integers(0, 2 ** 63, size=5000, dtype=np.int64).astype(np.uint64).view(np.float64)
+    # fn 13: the kernel's division through a correctly rounded reciprocal (div_rcp) against
+    # IEEE division, incl. significands of all ones / powers of two, zeros and infinities
+    ones = np.frombuffer(np.array([0x3FFFFFFFFFFFFFFF, 0x400FFFFFFFFFFFFF, 0x3FF0000000000000],
+                                  dtype=np.uint64).tobytes(), dtype=np.float64)
+    den = np.concatenate([y, rng.uniform(0.5, 3, 3000) * 2.0 ** rng.integers(-30, 30, 3000),
+                          np.repeat(ones, 100) * 2.0 ** rng.integers(-20, 20, 300), [0.0, -0.0, np.inf, 1e-310]])
+    num = np.concatenate([x, rng.uniform(-1e4, 1e4, 3000), rng.uniform(-10, 10, 300), [1.0, 0.0, 2.0, 3.0]])
     cases = {0: (x,), 1: (x,), 2: (pos,), 3: (x, y), 4: (np.clip(y / 3, -1, 1),), 5: tuple(n), 6: tuple(n),
-             7: (pos,), 8: (np.abs(x),), 9: (x, y), 10: (bits,), 11: (bits,), 12: (x,)}
+             7: (pos,), 8: (np.abs(x),), 9: (x, y), 10: (bits,), 11: (bits,), 12: (x,), 13: (num, den)}
     for fn, args in cases.items():
         host = ob.evaluate(fn, *args)
         dev = renderer.device_eval(fn, *args)
         same = (host.view(np.uint64) == dev.view(np.uint64)) | (np.isnan(host) & np.isnan(dev))
+        if fn == 13:  # a zero quotient may differ in sign (div_rcp's comment); any other value bit for bit
+            same |= (host == 0.0) & (dev == 0.0)
         assert same.all(), f"fn {fn}: {int((~same).sum())} mismatches, e.g. {args[0][~same][:3]}"
 
 
