@@ -583,7 +583,7 @@ __device__ __forceinline__ bool traverse(const SceneDev& S, int root, const Ray&
 // ---------------------------------------------------------------------------
 // Translate / RotateY instances (hittable.rs:232-244, 386-415), outermost op first
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ void instance_ray(const rt_instance& in, Ray& r, double* dirx, double* diry, double* dirz)
+__device__ __forceinline__ void instance_ray(const rt_instance& in, Ray& r)
 {
     const int n = in.n_ops;
 #pragma unroll
@@ -599,7 +599,6 @@ __device__ __forceinline__ void instance_ray(const rt_instance& in, Ray& r, doub
                 const double dx = c * r.dx - s * r.dz, dz = s * r.dx + c * r.dz;
                 r.ox = ox; r.oz = oz; r.dx = dx; r.dz = dz;
             }
-            if (dirx) { dirx[i] = r.dx; diry[i] = r.dy; dirz[i] = r.dz; }
         }
     }
 }
@@ -611,7 +610,7 @@ __device__ bool instance_t(const SceneDev& S, const rt_instance& in, const Ray& 
                            HitRef& ref, StackT<C>& stack, int sp0, Count& cnt)
 {
     Ray r = ray;
-    instance_ray(in, r, nullptr, nullptr, nullptr);
+    instance_ray(in, r);
     finish_ray<C>(r);
     if (in.child_kind == RT_CHILD_PRIM) {
         int side = 0;
@@ -632,12 +631,29 @@ __device__ bool instance_t(const SceneDev& S, const rt_instance& in, const Ray& 
     return true;
 }
 
+// The ray direction after ops 0..i (only RotateY changes it; y never changes): recomputed
+// per op on the way back instead of kept in arrays through the child's finisher, which
+// held 8 f64 registers live and pushed the instance variants into scratch spills.
+__device__ __forceinline__ void dir_after(const rt_instance& in, const Ray& ray, int i, double& dx, double& dz)
+{
+    dx = ray.dx;
+    dz = ray.dz;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        if (j <= i && j < in.n_ops && in.op_kind[j] != RT_OP_TRANSLATE) {
+            const double s = in.op[j][0], c = in.op[j][1];
+            const double x = c * dx - s * dz, z = s * dx + c * dz;
+            dx = x;
+            dz = z;
+        }
+    }
+}
+
 template <class C>
 __device__ void instance_finish(const SceneDev& S, const rt_instance& in, const Ray& ray, const HitRef& ref, Hit& h)
 {
     Ray r = ray;
-    double dirx[4], diry[4], dirz[4];
-    instance_ray(in, r, dirx, diry, dirz);
+    instance_ray(in, r);
     // ref.sub: the child prim (RT_CHILD_PRIM) or the BLAS leaf slot
     simple_finish<C>(in.child_kind == RT_CHILD_PRIM ? S.prims[ref.sub] : S.leaf_prims[ref.sub], r, ref.t, ref.side,
                      h);
@@ -645,17 +661,19 @@ __device__ void instance_finish(const SceneDev& S, const rt_instance& in, const 
 #pragma unroll
     for (int i = 3; i >= 0; --i) {
         if (i < n) {
+            double dx, dz;
+            dir_after(in, ray, i, dx, dz);
             if (in.op_kind[i] == RT_OP_TRANSLATE) {  // rec.point += offset; set_face_normal(moved_ray, normal)
                 h.px = h.px + in.op[i][0];
                 h.py = h.py + in.op[i][1];
                 h.pz = h.pz + in.op[i][2];
-                set_face_normal(h, dirx[i], diry[i], dirz[i], h.nx, h.ny, h.nz);
+                set_face_normal(h, dx, ray.dy, dz, h.nx, h.ny, h.nz);
             } else {                                  // rotate back; set_face_normal(rotated_ray, normal)
                 const double s = in.op[i][0], c = in.op[i][1];
                 const double px = c * h.px + s * h.pz, pz = -s * h.px + c * h.pz;
                 const double nx = c * h.nx + s * h.nz, nz = -s * h.nx + c * h.nz;
                 h.px = px; h.pz = pz;
-                set_face_normal(h, dirx[i], diry[i], dirz[i], nx, h.ny, nz);
+                set_face_normal(h, dx, ray.dy, dz, nx, h.ny, nz);
             }
         }
     }
@@ -1059,7 +1077,10 @@ __device__ __forceinline__ bool lane_work(const KParams& P, LaneWork& w)
 #define RT_MIN_WAVES_SPHERES 1
 #endif
 #ifndef RT_MIN_WAVES_RECTINST
-#define RT_MIN_WAVES_RECTINST 4   // measured: Cornell 202 -> 190 ms (800x800x200); pool: 4 80.7, 3 81.0
+// measured (Cornell 800x800x200): chunk schedule 4 waves 190 vs 202 ms; pool schedule 4: 80.7,
+// 3: 81.0; after the reciprocal divisions (more live state, 4 waves spilled to scratch):
+// 4: 66.6, 3: 58.6
+#define RT_MIN_WAVES_RECTINST 3
 #endif
 #ifndef RT_MIN_WAVES_ALL
 // measured, pool schedule: final scene 960x540x200 4: 112.0 ms (scratch spills: 0.7 TB of HBM
