@@ -517,6 +517,9 @@ int rt_ctx_upload_soa(rt_ctx* c, const rt_scene_soa* s)
         if (s->textures[i].kind == RT_TEX_IMAGE) feat |= rtk::FEAT_IMAGE;
     }
     c->features = feat;
+    c->S.has_spheres = 0;
+    for (int i = 0; i < s->n_prims; ++i)
+        if (s->prims[i].kind == RT_PRIM_SPHERE || s->prims[i].kind == RT_PRIM_MOVING_SPHERE) c->S.has_spheres = 1;
     c->pad_extent = s->pad_extent > 0.0 && std::isfinite(s->pad_extent) ? s->pad_extent : 0.0;
     c->stats.scene_bytes = (int64_t)total;
     return RT_OK;

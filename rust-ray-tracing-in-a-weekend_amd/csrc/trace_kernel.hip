@@ -148,11 +148,12 @@ __device__ __forceinline__ float f32_inv_dir(double d)
     return __builtin_amdgcn_rcpf(f);
 }
 
+// spheres: the scene has spheres (wave-uniform); otherwise no root division needs 1/a
 template <class C>
-__device__ __forceinline__ void finish_ray(Ray& r)
+__device__ __forceinline__ void finish_ray(Ray& r, bool spheres)
 {
     r.a = r.dx * r.dx + r.dy * r.dy + r.dz * r.dz;
-    r.ya = rcp_for_div(r.a);
+    r.ya = (C::F == FEAT_SET_SPHERES || spheres) ? rcp_for_div(r.a) : __builtin_nan("");
     if constexpr (C::S32) {
         r.fix = f32_inv_dir(r.dx);
         r.fiy = f32_inv_dir(r.dy);
@@ -611,7 +612,7 @@ __device__ bool instance_t(const SceneDev& S, const rt_instance& in, const Ray& 
 {
     Ray r = ray;
     instance_ray(in, r);
-    finish_ray<C>(r);
+    finish_ray<C>(r, S.has_spheres != 0);
     if (in.child_kind == RT_CHILD_PRIM) {
         int side = 0;
         if (!simple_t<C>(S.prims[in.child], r, t_min, t_max, ref.t, side, cnt)) return false;
@@ -1045,7 +1046,7 @@ __device__ __forceinline__ bool shade(const SceneDev& S, const KParams& P, const
     Tb = Tb * ab;
     r.ox = h.px; r.oy = h.py; r.oz = h.pz;
     r.dx = sdx; r.dy = sdy; r.dz = sdz;
-    finish_ray<C>(r);
+    finish_ray<C>(r, S.has_spheres != 0);
     return true;
 }
 
@@ -1132,7 +1133,7 @@ __global__ void __launch_bounds__(256, min_waves<C>()) trace_chunks(SceneDev S, 
             ds_start(st, P.seed, w.pixel, (uint32_t)s);
             key.sample = (uint32_t)s;
             camera_ray(P, w.x, w.y, st, r);
-            finish_ray<C>(r);
+            finish_ray<C>(r, S.has_spheres != 0);
             Tr = Tg = Tb = 1.0;
             depth = P.max_depth;
         }
@@ -1289,7 +1290,7 @@ __global__ void __launch_bounds__(256, min_waves<C>()) trace_pool(SceneDev S, co
             key.sample = (uint32_t)s;
             ds_start(st, P.seed, key.pixel, (uint32_t)s);
             camera_ray(P, x, y, st, r);
-            finish_ray<C>(r);
+            finish_ray<C>(r, S.has_spheres != 0);
             Tr = Tg = Tb = 1.0;
             cr = cg = cb = 0.0;
             depth = P.max_depth;

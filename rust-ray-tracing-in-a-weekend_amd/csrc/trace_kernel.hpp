@@ -25,7 +25,7 @@ struct SceneDev {
     int32_t stack_entries;  // traversal stack entries per lane (TLAS + BLAS walk)
     int32_t n_lds_nodes;    // the first n TLAS nodes (BFS order, nodes[0, n)) are copied into LDS
     int32_t n_tlas_nodes;   // TLAS size (its nodes are nodes[0, n_tlas_nodes))
-    int32_t pad2;
+    int32_t has_spheres;    // any Sphere / MovingSphere: rays need 1/|d|^2 for the root divisions
 };
 
 struct KParams {
