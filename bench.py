@@ -57,7 +57,7 @@ def parse():
     ap.add_argument("--depth", type=int, default=None)
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--cpu-seconds", type=float, default=25.0)
     ap.add_argument("--count-spp", type=int, default=16, help="spp of the untimed count_work pass")
     ap.add_argument("--no-count", action="store_true", help="skip the count_work pass (profiling runs)")
     ap.add_argument("--ppm", default="", help="write the rendered frame (rank 0) as a P3 PPM")
