@@ -9,10 +9,13 @@
  *
  * Deliberate, documented departures from the reference:
  *   - RNG: `rand::thread_rng()` (ChaCha12 from OS entropy, math.rs:268-276) is
- *     replaced by Philox4x32-10 streams keyed per (pixel, sample); the medium's
- *     in-`hit` draw (hittable.rs:446) is keyed per (pixel, sample, bounce,
- *     medium id) so the outcome is independent of traversal order. The `rand`
- *     0.8 float mappings (Standard, UniformFloat inclusive) are restated.
+ *     replaced by one stream per (pixel, sample) path — a Philox4x32-10 block of
+ *     (pixel, sample) seeding xoshiro128++ (rt_numerics.h rt_pstream) — drawn in
+ *     the reference's order; the medium's in-`hit` draw (hittable.rs:446) is keyed
+ *     per (pixel, sample, bounce, medium id) through Philox so the outcome is
+ *     independent of traversal order; scene construction uses a sequential Philox
+ *     stream. The `rand` 0.8 float mappings (Standard, UniformFloat inclusive) are
+ *     restated.
  *   - libm: sin/log/atan2/acos/pow come from rt_numerics.h (fdlibm algorithms)
  *     so that host and device agree bit-for-bit; host-only set-up math (tan in
  *     Camera::new, sin/cos in new_rotate_y) uses the platform libm, as Rust does.
