@@ -103,19 +103,24 @@ def main():
     slab = torch.zeros((rows_max, W, 3), dtype=torch.float32, device=device)
     gathered = [torch.empty_like(slab) for _ in range(world)] if (world > 1 and rank == 0) else None
     frame = torch.empty((H, W, 3), dtype=torch.float32, device=device) if rank == 0 else None
-    stream = torch.cuda.current_stream(device)
+    # A stream of our own: torch's default stream has the null handle, which the C ABI reads
+    # as "the context's stream" (a non-blocking stream the default stream does not wait
+    # for), so the frame copy / RCCL gather would not be ordered after the render. Every
+    # op of a step runs under this stream; NCCL orders its gather after it.
+    stream = torch.cuda.Stream(device)
     params = rt.Renderer.params(W, H, spp, depth, bg, args.seed, row_begin=rank, row_stride=world,
                                 out_format=rt.RT_OUT_F32)
     kernel_ms = []
 
     def step():
-        renderer.render_device(cam, params, slab.data_ptr(), stream.cuda_stream)
-        if world > 1:
-            dist.gather(slab, gathered if rank == 0 else None, dst=0)
-            if rank == 0:
-                rt.assemble_rows(gathered, H, world, out=frame)   # rows y = r + k*world
-        else:
-            frame[:] = slab[:H]
+        with torch.cuda.stream(stream):
+            renderer.render_device(cam, params, slab.data_ptr(), stream.cuda_stream)
+            if world > 1:
+                dist.gather(slab, gathered if rank == 0 else None, dst=0)
+                if rank == 0:
+                    rt.assemble_rows(gathered, H, world, out=frame)   # rows y = r + k*world
+            else:
+                frame[:] = slab[:H]
 
     def progress(msg):   # stderr, one line per step: long configs (C5) keep the run visibly alive
         if rank == 0:
@@ -168,12 +173,13 @@ def main():
     achieved = alg_bytes_launch / (k_ms * 1e-3) / 1e9
     # HBM traffic per launch from the committed rocprofv3 PMC pass of this workload
     # (scripts/profile.sh + scripts/prof_summary.py); null if none matches.
-    traffic, traffic_src = None, None
+    traffic, traffic_src, valu_busy = None, None, None
     pmc = os.environ.get("RT_PMC_TRAFFIC_JSON", os.path.join(REPO, "profiles", "pmc_traffic.json"))
     if os.path.exists(pmc):
         for e in json.load(open(pmc)).get("entries", []):
             if e.get("workload") == [args.scene, W, H, spp, depth, world] and e.get("schedule") == last.schedule:
                 traffic, traffic_src = e.get("hbm_bytes_per_launch"), e.get("tag")
+                valu_busy = e.get("valu_busy")
 
     if args.ppm and rank == 0:
         rt.write_ppm(frame.cpu().numpy(), args.ppm)
@@ -239,6 +245,8 @@ def main():
                        "spp_chunk": last.spp_chunk, "scene_bytes": int(last.scene_bytes),
                        "scene_build_upload_s": round(t_build, 3),
                        "traffic_source": traffic_src,
+                       # the binding resource (same PMC pass): VALU issue cycles / SIMD-cycles
+                       "valu_busy": None if valu_busy is None else round(valu_busy, 3),
                        "traffic_gbs": None if traffic is None else round(traffic / (k_ms * 1e-3) / 1e9, 2)},
         }
         print(json.dumps(out), flush=True)

@@ -66,6 +66,12 @@ def main():
               f"(fetch {fetch_b / 1e6:.2f} MB raw, write {write_b / 1e6:.1f} MB)"]
     if "GRBM_GUI_ACTIVE" in counters and avg_ns:
         lines.append(f"effective clock ~ GRBM_GUI_ACTIVE/8/t = {counters['GRBM_GUI_ACTIVE'] / 8 / (avg_ns * 1e-9) / 1e9:.2f} GHz")
+    valu_busy = None
+    if "SQ_ACTIVE_INST_VALU" in counters and counters.get("GRBM_GUI_ACTIVE"):
+        # quad-cycles of VALU issue summed over waves, x4 -> cycles, over the SIMD-cycles of
+        # the launch (1024 SIMDs x GRBM_GUI_ACTIVE / 8 XCDs): ~1 means VALU-issue bound
+        valu_busy = 4.0 * counters["SQ_ACTIVE_INST_VALU"] / (1024.0 * counters["GRBM_GUI_ACTIVE"] / 8.0)
+        lines.append(f"VALU issue busy ~ 4*SQ_ACTIVE_INST_VALU / (1024 SIMDs * GRBM_GUI_ACTIVE/8) = {valu_busy:.3f}")
     if "SQ_THREAD_CYCLES_VALU" in counters and "SQ_ACTIVE_INST_VALU" in counters:
         lines.append(f"VALU lane utilisation ~ SQ_THREAD_CYCLES_VALU / (64*SQ_ACTIVE_INST_VALU) = "
                      f"{counters['SQ_THREAD_CYCLES_VALU'] / (64 * counters['SQ_ACTIVE_INST_VALU']):.3f}")
@@ -80,7 +86,7 @@ def main():
     entries.append({"tag": tag, "config": config, "workload": workload, "kernel": KERNEL, "schedule": schedule,
                     "hbm_bytes_per_launch": traffic,
                     "fetch_size_kib": counters.get("FETCH_SIZE"), "write_size_kib": counters.get("WRITE_SIZE"),
-                    "kernel_avg_ns": avg_ns})
+                    "kernel_avg_ns": avg_ns, "valu_busy": valu_busy})
     json.dump({"note": "HBM bytes per trace-kernel launch (2*FETCH_SIZE + WRITE_SIZE, KiB*1024), "
                        "from scripts/profile.sh + scripts/prof_summary.py; bench.py matches workload "
                        "[scene, W, H, spp, depth, n_gpus] and schedule",

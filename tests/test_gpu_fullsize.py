@@ -78,3 +78,22 @@ def test_independent_seeds_agree_statistically(rt, renderer):
     assert int(np.sum(t > 6.0)) <= 2, int(np.sum(t > 6.0))    # P(|t_7| > 6) ~ 5e-4 per block
     # and the global mean agrees to well within 1 %
     assert abs(float(imgs[0].mean()) / float(np.mean(imgs[2:])) - 1.0) < 0.01
+
+
+def test_device_output_on_a_torch_stream_matches_host_render(rt, renderer):
+    """bench.py's step: render_device into a torch tensor on a torch stream, then a torch
+    copy on that stream, must see the finished frame (same bits as the host-output render)."""
+    import torch
+    W, H, spp = 96, 64, 8
+    world = rt.World(1).build_scene(0)
+    cam, bg = rt.scene_camera(0, W, H)
+    renderer.upload(world)
+    stream = torch.cuda.Stream(torch.device("cuda", 0))
+    slab = torch.zeros((H, W, 3), dtype=torch.float32, device="cuda:0")
+    with torch.cuda.stream(stream):
+        renderer.render_device(cam, rt.Renderer.params(W, H, spp, 50, bg, 1, out_format=rt.RT_OUT_F32),
+                               slab.data_ptr(), stream.cuda_stream)
+        frame = slab.clone()
+    torch.cuda.synchronize()
+    host = renderer.render(cam, rt.Renderer.params(W, H, spp, 50, bg, 1, out_format=rt.RT_OUT_F32))
+    assert np.array_equal(frame.cpu().numpy(), host)
