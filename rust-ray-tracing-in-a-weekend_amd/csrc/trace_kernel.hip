@@ -3,19 +3,22 @@
 // everything below it (hittable.rs, material.rs, texture.rs, perlin.rs), in f64
 // like the reference (math.rs:13-17).
 //
-// Execution model (DESIGN.md §Kernels):
-//   * one work item = (pixel, chunk of spp_chunk samples); a wave64 owns an 8x8
-//     pixel tile of one chunk, so neighbouring lanes trace coherent rays;
-//   * the depth-50 recursion is an iterative bounce loop; a lane whose path ends
-//     starts its next sample in the same loop iteration (path regeneration), so a
-//     wave stays busy until every lane has finished its chunk;
-//   * traversal carries only (t, primitive ids); the full HitRecord (point, normal,
-//     face, uv; hittable.rs:6-27) is rebuilt once per cast for the winning primitive
-//     by re-running its test with t_max = t — same inputs, same arithmetic, same bits;
-//   * the lane sums its chunk's samples in sample order (deterministic), writes
-//     one f64x3 partial; a second kernel adds the partials in chunk order and
-//     scales by 1/spp (math.rs:119-126), so the image does not depend on the
-//     launch geometry or on how rows are sharded over GPUs;
+// Execution model (DESIGN.md §5):
+//   * work unit = one (pixel, sample) path; work block = one 8x8 pixel tile x one chunk
+//     of spp_chunk samples (a function of spp only);
+//   * trace_pool (default): persistent waves take blocks from a device counter, and a
+//     lane whose path ended takes the block's next unit in the same bounce-loop
+//     iteration (ballot + mbcnt), so lanes do not idle until the last blocks run out;
+//     each sample's radiance goes to its slot of a [sample][pixel] buffer and
+//     reduce_samples sums every pixel's samples in sample order, chunk by chunk — the
+//     image does not depend on which lane computed a sample, on the launch geometry or
+//     on how rows are sharded over GPUs; trace_chunks (the first schedule, kept for A/B)
+//     gives a lane one pixel's chunk and adds the same partial sums;
+//   * the depth-50 recursion is an iterative bounce loop; traversal carries only
+//     (t, primitive slot); the HitRecord (hittable.rs:6-27) is built once per cast;
+//   * TLAS nodes and the traversal stack in LDS, conservative f32 slab tests, f64
+//     primitive tests; materials share their expensive steps so a wave holding several
+//     kinds runs each step once;
 //   * RNG: per (pixel, sample) a Philox4x32-10 block seeds a xoshiro128++ path stream
 //     (rt_numerics.h); the medium's in-hit draw is keyed by (pixel, sample, bounce, medium id).
 // Built with -ffp-contract=off: bit-for-bit the operation order of the reference.
