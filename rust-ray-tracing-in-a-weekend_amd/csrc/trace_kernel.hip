@@ -1091,12 +1091,16 @@ __device__ __forceinline__ bool lane_work(const KParams& P, LaneWork& w)
 // writes per launch), 3: 102.8, 2: 131.5; cornell smoke 600x600x200 4: 74.1, 3: 62.3, 2: 79.7
 #define RT_MIN_WAVES_ALL 3
 #endif
+#ifndef RT_MIN_WAVES_MEDIA
+#define RT_MIN_WAVES_MEDIA 3
+#endif
 // minimum waves per SIMD requested from the register allocator, per feature set
 template <class C>
 constexpr int min_waves()
 {
     return C::F == FEAT_SET_SPHERES ? RT_MIN_WAVES_SPHERES
-           : C::F == FEAT_SET_RECTINST ? RT_MIN_WAVES_RECTINST : RT_MIN_WAVES_ALL;
+           : C::F == FEAT_SET_RECTINST ? RT_MIN_WAVES_RECTINST
+           : C::F == FEAT_SET_MEDIA    ? RT_MIN_WAVES_MEDIA : RT_MIN_WAVES_ALL;
 }
 
 // KParams comes by pointer: read where used (scalar loads) instead of pinning ~70 SGPRs
@@ -1562,6 +1566,7 @@ uint32_t variant_features(uint32_t scene_features)
 {
     if ((scene_features & ~FEAT_SET_SPHERES) == 0) return FEAT_SET_SPHERES;
     if ((scene_features & ~FEAT_SET_RECTINST) == 0) return FEAT_SET_RECTINST;
+    if ((scene_features & ~FEAT_SET_MEDIA) == 0) return FEAT_SET_MEDIA;
     return FEAT_ALL;
 }
 
@@ -1592,10 +1597,12 @@ hipError_t launch_trace(const SceneDev& S, const KParams& Ph, const KParams* P, 
     if (o.count) {
         if (f == FEAT_SET_SPHERES) launch_f<FEAT_SET_SPHERES, true>(L, o.slab32, o.lds_stack, stream);
         else if (f == FEAT_SET_RECTINST) launch_f<FEAT_SET_RECTINST, true>(L, o.slab32, o.lds_stack, stream);
+        else if (f == FEAT_SET_MEDIA) launch_f<FEAT_SET_MEDIA, true>(L, o.slab32, o.lds_stack, stream);
         else launch_f<FEAT_ALL, true>(L, o.slab32, o.lds_stack, stream);
     } else {
         if (f == FEAT_SET_SPHERES) launch_f<FEAT_SET_SPHERES, false>(L, o.slab32, o.lds_stack, stream);
         else if (f == FEAT_SET_RECTINST) launch_f<FEAT_SET_RECTINST, false>(L, o.slab32, o.lds_stack, stream);
+        else if (f == FEAT_SET_MEDIA) launch_f<FEAT_SET_MEDIA, false>(L, o.slab32, o.lds_stack, stream);
         else launch_f<FEAT_ALL, false>(L, o.slab32, o.lds_stack, stream);
     }
     return hipGetLastError();

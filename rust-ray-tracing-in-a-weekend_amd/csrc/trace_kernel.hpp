@@ -52,7 +52,8 @@ enum : uint32_t {
     FEAT_IMAGE = 16,    // image texture
     FEAT_ALL = 31,
     FEAT_SET_SPHERES = 0,                      // compiled variant: spheres + solid/checker
-    FEAT_SET_RECTINST = FEAT_RECT | FEAT_INST  // compiled variant: + rects, boxes, instances
+    FEAT_SET_RECTINST = FEAT_RECT | FEAT_INST,  // compiled variant: + rects, boxes, instances
+    FEAT_SET_MEDIA = FEAT_SET_RECTINST | FEAT_MEDIUM  // compiled variant: + constant media
 };
 
 struct LaunchOpts {
