@@ -540,7 +540,10 @@ int rt_rows_in_shard(int height, int row_begin, int row_stride)
     return (height - row_begin + row_stride - 1) / row_stride;
 }
 
-static int auto_chunk(int spp) { return std::max(1, (spp + 15) / 16); }
+// ceil(spp/16), at most 16 samples per work block (measured, pool schedule: C2 16 vs 32
+// 99.4 / 100.4 ms, C4 16 vs 63 1565 / 1636 ms, C3 flat); a function of spp only, so the
+// summation order (and the image) does not depend on launch geometry or sharding
+static int auto_chunk(int spp) { return std::min(16, std::max(1, (spp + 15) / 16)); }
 
 static bool bad_geometry(const rt_render_params* p)
 {

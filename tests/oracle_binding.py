@@ -72,7 +72,7 @@ def render(scene_id: int, width: int, height: int, spp: int, max_depth: int = 50
         threads = min(8, os.cpu_count() or 1)
     n_rows = 0 if row_begin >= height else (height - row_begin + row_stride - 1) // row_stride
     if spp_chunk <= 0:
-        spp_chunk = max(1, (spp + 15) // 16)   # the product's automatic chunking (abi.cpp auto_chunk)
+        spp_chunk = min(16, max(1, (spp + 15) // 16))   # the product's automatic chunking (abi.cpp auto_chunk)
     p = Params(scene_id, scene_seed, render_seed, width, height, spp, max_depth, spp_chunk, row_begin, row_stride,
                threads, split, img.ctypes.data, img.shape[1], img.shape[0])
     out = np.zeros((n_rows, width, 3), dtype=np.float64)
