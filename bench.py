@@ -8,18 +8,25 @@ the shards are gathered to rank 0 over RCCL (torch.distributed "nccl") and put b
 in row order — inside the timed region. The scene is built and uploaded before timing.
 
 Prints ONE JSON line (rank 0). Besides the contract fields it carries
-  roofline:     algorithmic bytes per launch (BVH nodes + primitives + materials +
-                partial writes, counted by the kernel's count_work pass) / kernel time,
-                against the 8 TB/s HBM peak; `traffic` from a rocprofv3 PMC pass if
-                RT_PMC_TRAFFIC_JSON points at one (else null);
+  roofline:     the binding resource, VALU issue: the issue cycles the launch's VALU
+                instruction mix needs (per-class counts from a rocprofv3 PMC pass of THIS
+                build and workload, profiles/pmc_r02.json keyed by the source hash; cycles
+                per instruction class calibrated on the box, scripts/calib) against the
+                SIMD-cycles of the live-timed kernel; `traffic` = DRAM bytes per launch from
+                the same PMC pass; the DRAM fraction and the SURVEY §8(d) algorithmic
+                (LDS/L1/L2-served) bytes are reported beside it (DESIGN.md §5.5);
   cpu_baseline: the CPU oracle (reference-faithful C restatement, linear list scan like
-                hittable.rs:43-55) on this host's cores, rank 0 at N=1 only, on a bounded
-                row subset of the same workload.
+                hittable.rs:43-55) on this host's usable cores, rank 0 at N=1 only, on a
+                bounded row subset of the same workload, plus the reference's own 10-thread
+                sample split (main.rs:497-551) for comparison with README.md:6;
+  parity:       the GPU render of exactly the rows and samples the CPU baseline rendered,
+                against the oracle's image, per pixel (north_star: L_inf <= 1e-3).
 """
 from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -28,7 +35,8 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
-CPU_BASELINE_CORES = 16        # the GPU box's CPU share per GPU
+N_SIMDS = 1024                 # 256 CUs x 4 SIMDs
+PMC_JSON = os.path.join(REPO, "profiles", "pmc_r02.json")
 
 
 # BASELINE.json configs (SURVEY §8 shorthand). The headline metric is C2; the others are
@@ -57,7 +65,8 @@ def parse():
     ap.add_argument("--depth", type=int, default=None)
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=25.0)
+    ap.add_argument("--cpu-seconds", type=float, default=20.0)
+    ap.add_argument("--t10-seconds", type=float, default=10.0, help="CPU time of the reference 10-thread split run")
     ap.add_argument("--count-spp", type=int, default=16, help="spp of the untimed count_work pass")
     ap.add_argument("--no-count", action="store_true", help="skip the count_work pass (profiling runs)")
     ap.add_argument("--ppm", default="", help="write the rendered frame (rank 0) as a P3 PPM")
@@ -66,6 +75,59 @@ def parse():
         if getattr(args, k) is None:
             setattr(args, k, v)
     return args
+
+
+def usable_cores():
+    """CPU threads this process may really run: its affinity mask, capped by a cgroup CPU
+    quota (the GPU box gives one GPU's job a 16-CPU share of a larger machine)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, math.ceil(int(q) / int(period)))
+    except (OSError, ValueError):
+        pass
+    return (min(n, quota) if quota else n), n, quota
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def pmc_entry(src_hash, workload):
+    """The PMC record of this build (source hash) and workload, or None."""
+    if not os.path.exists(PMC_JSON):
+        return None, None
+    doc = json.load(open(PMC_JSON))
+    for e in doc.get("entries", []):
+        if e.get("src_hash") == src_hash and e.get("workload") == workload:
+            return e, doc.get("calibration")
+    return None, doc.get("calibration")
+
+
+def valu_issue_cycles(counts, calib):
+    """Issue cycles (summed over SIMDs) the launch's VALU instruction mix needs at the
+    calibrated saturated rates: sum over classes of count x cycles per wave-instruction; the
+    instructions no class counter covers (moves, compares, selects, bit ops) at the measured
+    rate of those (calib 'other')."""
+    cyc = calib["cycles_per_inst"]
+    total = counts["SQ_INSTS_VALU"]
+    known, need = 0.0, 0.0
+    for cls, key in calib["class_counters"].items():
+        n = counts.get(key)
+        if n is None:
+            continue
+        known += n
+        need += n * cyc[cls]
+    need += max(0.0, total - known) * cyc["other"]
+    return need
 
 
 def main():
@@ -153,43 +215,62 @@ def main():
     samples_per_step = W * H * spp
     value = samples_per_step * args.steps / elapsed / 1e6
     ms_per_step = elapsed / args.steps * 1e3
-
-    # ---- algorithmic bytes per sample from an untimed count_work pass (same scene/camera)
-    count_spp = min(args.count_spp, spp)
-    cp = rt.Renderer.params(W, H, count_spp if not args.no_count else 1, depth, bg, args.seed, row_begin=rank,
-                            row_stride=world, out_format=rt.RT_OUT_F32, count_work=0 if args.no_count else 1)
-    if not args.no_count:
-        renderer.render(cam, cp)
-    cs = renderer.stats()
-    bytes_per_sample = (cs.node_visits * cs.node_bytes + cs.prim_tests * cs.prim_bytes +
-                        cs.casts * cs.material_bytes) / max(cs.samples, 1)
-    samples_per_launch = rows * W * spp
-    items_per_launch = last.n_items
-    # radiance written per launch: one f64 triple per sample (pool schedule) or per
-    # (pixel, chunk) partial (chunk schedule)
-    out_units = samples_per_launch if last.schedule == rt.RT_SCHED_POOL else items_per_launch
-    alg_bytes_launch = bytes_per_sample * samples_per_launch + out_units * 24
     k_ms = float(np.mean(kernel_ms)) if kernel_ms else float("nan")
-    achieved = alg_bytes_launch / (k_ms * 1e-3) / 1e9
-    # HBM traffic per launch from the committed rocprofv3 PMC pass of this workload
-    # (scripts/profile.sh + scripts/prof_summary.py); null if none matches.
-    traffic, traffic_src, valu_busy = None, None, None
-    pmc = os.environ.get("RT_PMC_TRAFFIC_JSON", os.path.join(REPO, "profiles", "pmc_traffic.json"))
-    if os.path.exists(pmc):
-        for e in json.load(open(pmc)).get("entries", []):
-            if e.get("workload") == [args.scene, W, H, spp, depth, world] and e.get("schedule") == last.schedule:
-                traffic, traffic_src = e.get("hbm_bytes_per_launch"), e.get("tag")
-                valu_busy = e.get("valu_busy")
 
+    # ---- roofline: VALU issue (the binding resource), from the PMC pass of this build
+    src_hash = ge.source_hash()
+    workload = [args.scene, W, H, spp, depth, world, last.schedule]
+    pmc, calib = pmc_entry(src_hash, workload)
+    roofline = {"bound": "valu", "achieved": None, "peak": None, "unit": "G SIMD-cycles/s", "frac": None,
+                "traffic": None, "src_hash": src_hash}
+    if pmc is not None and calib is not None:
+        need = valu_issue_cycles(pmc["counters"], calib)         # SIMD-cycles of VALU issue per launch
+        clk = pmc["clock_ghz"]                                   # the clock the chip held in that pass
+        achieved = need / (k_ms * 1e-3) / 1e9                    # per live-timed launch
+        peak = N_SIMDS * clk
+        dram = pmc["dram_bytes"]
+        roofline.update({
+            "achieved": round(achieved, 1), "peak": round(peak, 1), "frac": round(achieved / peak, 4),
+            "traffic": int(dram),
+            "valu_lane_util": round(pmc["counters"]["SQ_THREAD_CYCLES_VALU"] /
+                                    (64.0 * pmc["counters"]["SQ_INSTS_VALU"]), 4),
+            "hbm": {"achieved": round(dram / (k_ms * 1e-3) / 1e9, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(dram / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)},
+            "pmc_tag": pmc.get("tag"), "pmc_kernel_ms": pmc.get("kernel_ms"), "clock_ghz": clk})
+    else:
+        roofline["note"] = "no PMC pass of this build (source hash) and workload in profiles/pmc_r02.json"
+
+    # ---- SURVEY §8(d) algorithmic bytes per sample (LDS/L1/L2-served; not an HBM figure)
+    count_spp = min(args.count_spp, spp)
+    cs = None
+    if not args.no_count:
+        cp = rt.Renderer.params(W, H, count_spp, depth, bg, args.seed, row_begin=rank, row_stride=world,
+                                out_format=rt.RT_OUT_F32, count_work=1)
+        renderer.render(cam, cp)
+        cs = renderer.stats()
+    alg = None
+    if cs is not None:
+        bytes_per_sample = (cs.node_visits * cs.node_bytes + cs.prim_tests * cs.prim_bytes +
+                            cs.casts * cs.material_bytes) / max(cs.samples, 1)
+        alg = {"bytes_per_sample": round(bytes_per_sample, 1),
+               "gbs": round(bytes_per_sample * rows * W * spp / (k_ms * 1e-3) / 1e9, 1),
+               "casts_per_sample": round(cs.casts / max(cs.samples, 1), 4),
+               "nodes_per_cast": round(cs.node_visits / max(cs.casts, 1), 3),
+               "prims_per_cast": round(cs.prim_tests / max(cs.casts, 1), 3),
+               "bounce_lane_occupancy": round(cs.casts / max(64 * cs.wave_steps, 1), 3),
+               "node_lane_occupancy": round(cs.node_visits / max(64 * cs.wave_node_steps, 1), 3),
+               "leaf_lane_occupancy": round(cs.prim_tests / max(64 * cs.wave_leaf_steps, 1), 3)}
+
+    frame_np = frame.cpu().numpy() if rank == 0 else None
     if args.ppm and rank == 0:
-        rt.write_ppm(frame.cpu().numpy(), args.ppm)
+        rt.write_ppm(frame_np, args.ppm)
 
-    progress("timed steps done; count pass and CPU baseline")
-    # ---- CPU baseline (rank 0, N = 1 only)
-    cpu = None
+    progress("timed steps done; count pass, CPU baseline and parity")
+    # ---- CPU baseline + parity (rank 0, N = 1 only)
+    cpu, parity = None, None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         from tests import oracle_binding as ob
-        cores = min(CPU_BASELINE_CORES, os.cpu_count() or 1)
+        cores, n_aff, quota = usable_cores()
         # calibrate on `cores` interleaved rows at low spp, then take an interleaved row
         # subset of the real workload worth ~cpu_seconds (a multiple of `cores` rows)
         cal_stride = max(1, H // cores)
@@ -204,13 +285,38 @@ def main():
         # a frame too large for even `cores` full rows (C5) takes the first spp_cpu samples
         # of every pixel of those rows: the per-sample work is the same
         spp_cpu = int(min(spp, max(1, target // (n_rows * W))))
-        _, st = ob.render(args.scene, W, H, spp_cpu, depth, args.seed, args.seed, row_begin=0, row_stride=stride,
-                          threads=cores, return_stats=True)
+        ref_img, st = ob.render(args.scene, W, H, spp_cpu, depth, args.seed, args.seed, row_begin=0,
+                                row_stride=stride, threads=cores, return_stats=True)
         spp_note = "" if spp_cpu == spp else f", samples 0..{spp_cpu - 1} of each pixel"
         cpu = {"value": st.samples / st.seconds / 1e6, "unit": "Msamples/s", "cores": cores, "kind": "port",
                "sample": f"oracle (C, f64, recursive ray_color, linear hit_hittables scan) on rows y % {stride} == 0 "
                          f"of the same {W}x{H}x{spp} depth-{depth} frame{spp_note}: {st.samples} samples in "
-                         f"{st.seconds:.1f} s on {cores} threads"}
+                         f"{st.seconds:.1f} s on {cores} threads (interleaved rows)",
+               "cpu_model": cpu_model(), "nproc": os.cpu_count(), "affinity": n_aff, "cgroup_quota": quota}
+        # the reference's own decomposition: 10 threads, each all pixels x spp/10 samples
+        # (main.rs:497-551, spp/thread_count at :516), the figure comparable to README.md:6
+        n10 = max(1, int(args.t10_seconds * rate * min(10, cores) / cores / (W * spp)))
+        stride10 = max(1, H // n10)
+        _, st10 = ob.render(args.scene, W, H, spp, depth, args.seed, args.seed, row_begin=0, row_stride=stride10,
+                            threads=10, split=ob.SPLIT_SAMPLES, return_stats=True)
+        cpu["ref_split_t10"] = {
+            "value": st10.samples / st10.seconds / 1e6, "unit": "Msamples/s", "threads": 10,
+            "sample": f"rows y % {stride10} == 0, all {spp} spp split over 10 threads ({spp // 10} each, "
+                      f"main.rs:516): {st10.samples} samples in {st10.seconds:.1f} s",
+            "comparable_to": "README.md:6 (1200x800x500 in 1 h 10 min on 10 threads = 0.114 Msamples/s; "
+                             "older book-1 scene revision, unknown CPU)"}
+        # parity: the GPU renders exactly those rows and samples (f64 output) and the timed
+        # f32 frame's same rows (full spp only) are compared as well
+        gp = rt.Renderer.params(W, H, spp_cpu, depth, bg, args.seed, row_begin=0, row_stride=stride,
+                                out_format=rt.RT_OUT_F64)
+        gimg = renderer.render(cam, gp)
+        d = np.abs(gimg - ref_img)
+        parity = {"linf": float(d.max()), "max_rel": float((d / np.maximum(np.abs(ref_img), 1e-300)).max()),
+                  "rows": n_rows, "row_stride": stride, "spp": spp_cpu, "max_depth": depth,
+                  "samples": int(st.samples), "tolerance": 1e-3, "pass": bool(d.max() <= 1e-3),
+                  "vs": "oracle image of the cpu_baseline sample (same rows, samples, seeds)"}
+        if spp_cpu == spp:
+            parity["linf_timed_f32_frame"] = float(np.abs(frame_np[0::stride].astype(np.float64) - ref_img).max())
 
     if rank == 0:
         out = {
@@ -232,22 +338,13 @@ def main():
                                       depth, world),
                        "scene": args.scene, "width": W, "height": H, "spp": spp, "max_depth": depth,
                        "parallelism": "rows interleaved over %d rank(s), RCCL gather" % world},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": None if traffic is None else int(traffic)},
+            "roofline": roofline,
             "cpu_baseline": cpu,
+            "parity": parity,
             "detail": {"kernel_ms_mean": round(k_ms, 3), "reduce_ms": round(last.reduce_ms, 3),
-                       "bytes_per_sample": round(bytes_per_sample, 1),
-                       "casts_per_sample": round(cs.casts / max(cs.samples, 1), 4),
-                       "nodes_per_cast": round(cs.node_visits / max(cs.casts, 1), 3),
-                       "prims_per_cast": round(cs.prim_tests / max(cs.casts, 1), 3),
-                       "alg_bytes_per_launch": int(alg_bytes_launch), "n_items": int(items_per_launch),
-                       "spp_chunk": last.spp_chunk, "scene_bytes": int(last.scene_bytes),
-                       "scene_build_upload_s": round(t_build, 3),
-                       "traffic_source": traffic_src,
-                       # the binding resource (same PMC pass): VALU issue cycles / SIMD-cycles
-                       "valu_busy": None if valu_busy is None else round(valu_busy, 3),
-                       "traffic_gbs": None if traffic is None else round(traffic / (k_ms * 1e-3) / 1e9, 2)},
+                       "schedule": last.schedule, "n_batches": last.n_batches, "spp_chunk": last.spp_chunk,
+                       "scene_bytes": int(last.scene_bytes), "scene_build_upload_s": round(t_build, 3),
+                       "algorithmic_bytes_survey_8d": alg},
         }
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -134,6 +134,11 @@ int rt_scene_camera(int scene_id, int width, int height, rt_camera* cam_out, dou
 /* Flattens the world into SoA tables owned by the world (valid until the next
  * flatten or rt_world_destroy). accel: RT_ACCEL_SAH / _LINEAR / _MEDIAN (rt_scene.h). */
 int rt_world_flatten(rt_world* w, int accel, const rt_scene_soa** soa_out);
+/* Checks a (possibly foreign) SoA the way rt_ctx_upload_soa does before copying it: every
+ * index in range, no cycle in the node graph, and the traversal stack each walk needs
+ * (computed from the tables; the soa's tlas_depth / blas_depth fields are not trusted).
+ * Host only, no device needed. Depth outputs may be NULL. */
+int rt_scene_validate(const rt_scene_soa* soa, int32_t* tlas_depth, int32_t* blas_depth);
 int rt_ctx_upload_soa(rt_ctx* ctx, const rt_scene_soa* soa);
 int rt_ctx_upload_world(rt_ctx* ctx, rt_world* w, int accel);
 
@@ -241,13 +246,19 @@ int rt_write_ppm(const float* mean_rgb, int width, int height, const char* path)
  * environment variables. Results do not depend on them (tests check this). */
 int rt_ctx_set_variant(rt_ctx* ctx, int slab32, int lds_stack, int lds_nodes);
 
-/* Work schedule of a context (default RT_SCHED_POOL, or the RT_SCHEDULE environment
- * variable). CHUNKS: a wave owns an 8x8 tile x one chunk of samples, each lane one pixel's
- * chunk. POOL: persistent waves take (tile, chunk) blocks from a device counter and a lane
- * whose path ended takes the block's next (pixel, sample) at once; every sample's radiance
- * goes to a [sample][pixel] buffer (batched to RT_SAMPLE_BUF_MB, default 32 GiB) that is
- * summed per pixel in sample order. Images are bit-identical either way. */
-enum { RT_SCHED_CHUNKS = 0, RT_SCHED_POOL = 1 };
+/* Work schedule of a context (default RT_SCHED_ITEMS, or the RT_SCHEDULE environment
+ * variable 0/1/2). Images are bit-identical under all three.
+ *   CHUNKS: a wave owns an 8x8 tile x one chunk of samples, each lane one pixel's chunk,
+ *           written as one partial per (pixel, chunk); the wave waits for its slowest lane.
+ *   POOL:   persistent waves take (tile, chunk) blocks from a device counter and a lane
+ *           whose path ended takes the block's next (pixel, sample) at once; every sample's
+ *           radiance goes to a [sample][pixel] buffer summed per pixel in sample order.
+ *   ITEMS:  persistent waves as POOL, but a lane takes a whole (pixel, chunk) item, traces
+ *           its samples in order and writes one partial, as CHUNKS does (1/chunk of POOL's
+ *           buffer bytes); a lane whose item ended takes the next item at once.
+ * One launch's trace output is bounded by RT_SAMPLE_BUF_MB (default 32 GiB); a larger
+ * render runs in buffer batches (on chunk boundaries) whose sums are carried across. */
+enum { RT_SCHED_CHUNKS = 0, RT_SCHED_POOL = 1, RT_SCHED_ITEMS = 2 };
 int rt_ctx_set_schedule(rt_ctx* ctx, int schedule);
 
 /* ---- self test ------------------------------------------------------------------------------ */

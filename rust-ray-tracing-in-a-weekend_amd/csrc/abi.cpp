@@ -38,8 +38,8 @@ int hip_fail(hipError_t e, const char* what)
 
 size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
-// device slots for launch params: renders queued on different streams of one context
-// may overlap up to this many in flight
+// device slots for launch params (a ring: a render's params stay intact while later
+// renders are enqueued behind it on the same stream)
 constexpr int kParamSlots = 16;
 
 // LDS stack entries per lane above which the scratch stack is used (48 KB per block)
@@ -72,6 +72,13 @@ struct rt_ctx {
     rtk::KParams* params = nullptr;     // ring of kParamSlots device copies of the launch params
     int param_slot = 0;
     hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+    // Cross-stream ordering: the scratch buffers (partial, work counter, acc_tmp, counters,
+    // params ring, staging) are per context, so work enqueued on a new stream must wait for
+    // everything the context enqueued on the previous one. ev_done is recorded after each
+    // enqueue; a call on another stream first makes that stream wait for it.
+    hipEvent_t ev_done = nullptr;
+    hipStream_t last_stream = nullptr;
+    bool any_enqueued = false;
     bool pending_stats = false;
     bool pending_counts = false;
     rt_stats stats{};
@@ -80,10 +87,10 @@ struct rt_ctx {
     int opt_slab32 = 1;                 // rt_ctx_set_variant / RT_SLAB32
     int opt_lds = 1;                    // rt_ctx_set_variant / RT_LDS_STACK
     int opt_lds_nodes = 1;              // RT_LDS_NODES: keep the TLAS in LDS when it fits
-    int opt_pool = 1;                   // rt_ctx_set_schedule / RT_SCHEDULE: sample-pool (1) or chunk (0)
-    size_t sample_buf_cap = (size_t)32 << 30;  // RT_SAMPLE_BUF_MB: per-sample buffer bound (pool)
-    unsigned* work = nullptr;           // pool schedule: work-block counter
-    double* acc_tmp = nullptr;          // pool schedule: running sums when a render takes several batches
+    int opt_pool = RT_SCHED_ITEMS;      // rt_ctx_set_schedule / RT_SCHEDULE: RT_SCHED_*
+    size_t sample_buf_cap = (size_t)32 << 30;  // RT_SAMPLE_BUF_MB: bound of one launch's trace output
+    unsigned* work = nullptr;           // pool / item schedules: work-block counter
+    double* acc_tmp = nullptr;          // running sums when a render takes several buffer batches
     size_t acc_tmp_cap = 0;
     int n_tlas_nodes = 0;
 };
@@ -120,10 +127,11 @@ int rt_ctx_create(int device, rt_ctx** out)
     if (const char* e = std::getenv("RT_SLAB32")) c->opt_slab32 = std::atoi(e) != 0;
     if (const char* e = std::getenv("RT_LDS_STACK")) c->opt_lds = std::atoi(e) != 0;
     if (const char* e = std::getenv("RT_LDS_NODES")) c->opt_lds_nodes = std::atoi(e) != 0;
-    if (const char* e = std::getenv("RT_SCHEDULE")) c->opt_pool = std::atoi(e) != 0;
+    if (const char* e = std::getenv("RT_SCHEDULE")) c->opt_pool = std::min(2, std::max(0, std::atoi(e)));
     if (const char* e = std::getenv("RT_SAMPLE_BUF_MB")) c->sample_buf_cap = (size_t)std::max(1L, std::atol(e)) << 20;
     hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     for (int i = 0; i < 3 && e == hipSuccess; ++i) e = hipEventCreate(&c->ev[i]);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_done, hipEventDisableTiming);
     if (e == hipSuccess) e = hipMalloc((void**)&c->counters, kCounters * sizeof(unsigned long long));
     if (e == hipSuccess) e = hipMalloc((void**)&c->params, kParamSlots * sizeof(rtk::KParams));
     if (e == hipSuccess) e = hipMalloc((void**)&c->work, sizeof(unsigned));
@@ -140,6 +148,7 @@ void rt_ctx_destroy(rt_ctx* c)
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->ev_done && c->any_enqueued) (void)hipEventSynchronize(c->ev_done);  // work on a caller's stream
     (void)hipFree(c->scene_buf);
     (void)hipFree(c->partial);
     (void)hipFree(c->out_buf);
@@ -149,6 +158,7 @@ void rt_ctx_destroy(rt_ctx* c)
     (void)hipFree(c->acc_tmp);
     for (auto& e : c->ev)
         if (e) (void)hipEventDestroy(e);
+    if (c->ev_done) (void)hipEventDestroy(c->ev_done);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -409,31 +419,80 @@ int rt_world_flatten(rt_world* w, int accel, const rt_scene_soa** soa_out)
     return RT_OK;
 }
 
-int rt_ctx_upload_soa(rt_ctx* c, const rt_scene_soa* s)
+// Stack entries a walk from `ref` needs, the way the kernel's visit uses its stack (push
+// the farther child when both are hit; with two identical child boxes child 0 is always
+// taken first, so only it stacks above the pushed child 1) — the rule flatten.cpp's
+// stack_need builds with, recomputed here from the tables alone. Iterative post-order
+// with three colours, so a cycle in a foreign node graph is found instead of walked
+// forever (the persistent kernel would spin on it). Returns -1 on a cycle.
+static int walk_need(const rt_scene_soa* s, int ref, std::vector<int>& need, std::vector<uint8_t>& colour)
 {
-    if (!c || !s) return fail(RT_ERR_INVALID, "null argument");
+    if (ref < 0) return 0;
+    std::vector<int> todo{ref};
+    while (!todo.empty()) {
+        const int i = todo.back();
+        if (colour[i] == 2) {
+            todo.pop_back();
+            continue;
+        }
+        const rt_bvh_node& nd = s->nodes[i];
+        if (colour[i] == 0) {
+            colour[i] = 1;  // on the current path
+            for (int ch : nd.child) {
+                if (ch < 0 || colour[ch] == 2) continue;
+                if (colour[ch] == 1) return -1;  // back edge
+                todo.push_back(ch);
+            }
+            continue;
+        }
+        todo.pop_back();  // both children done
+        auto nc = [&](int ch) { return ch < 0 ? 0 : need[ch]; };
+        const bool same = std::memcmp(nd.lo0, nd.lo1, 12) == 0 && std::memcmp(nd.hi0, nd.hi1, 12) == 0;
+        need[i] = same ? std::max(1 + nc(nd.child[0]), nc(nd.child[1])) : 1 + std::max(nc(nd.child[0]), nc(nd.child[1]));
+        colour[i] = 2;
+    }
+    return need[ref];
+}
+
+// Validates a (possibly foreign) SoA so the kernel never indexes out of bounds, never
+// overruns its traversal stack and never walks a cycle; computes the stack needs itself
+// (the tlas_depth / blas_depth fields are not trusted) and whether the TLAS really lies in
+// nodes[0, n_tlas_nodes) (the kernel copies that prefix into LDS and then reads only LDS).
+static int validate_soa(const rt_scene_soa* s, int& tlas_depth, int& blas_depth, int& n_tlas_nodes)
+{
     if (s->n_prim_refs >= (1 << 26) - 64) return fail(RT_ERR_UNSUPPORTED, "too many primitive references");
     if (s->n_prims < 0 || s->n_prim_refs < 0 || s->n_nodes < 0 || s->n_instances < 0 || s->n_materials < 0 ||
         s->n_textures < 0 || s->n_perlin < 0 || s->image_bytes < 0)
         return fail(RT_ERR_INVALID, "negative table size");
-    // validate references so the kernel never indexes out of bounds
+    if ((s->n_prims && !s->prims) || (s->n_prim_refs && !s->prim_refs) || (s->n_nodes && !s->nodes) ||
+        (s->n_instances && !s->instances) || (s->n_materials && !s->materials) || (s->n_textures && !s->textures) ||
+        (s->n_perlin && (!s->perlin_ranvec || !s->perlin_perm)) || (s->image_bytes && !s->image_data))
+        return fail(RT_ERR_INVALID, "null table");
+    auto simple_kind = [](int k) { return k >= RT_PRIM_SPHERE && k <= RT_PRIM_BOX; };
     for (int i = 0; i < s->n_prims; ++i) {
         const rt_prim& p = s->prims[i];
         if (p.kind < RT_PRIM_SPHERE || p.kind > RT_PRIM_MEDIUM) return fail(RT_ERR_INVALID, "bad prim kind");
         if (p.kind == RT_PRIM_INSTANCE && (p.a < 0 || p.a >= s->n_instances)) return fail(RT_ERR_INVALID, "bad instance");
-        if (p.kind == RT_PRIM_MEDIUM && (p.a < 0 || p.a >= s->n_prims)) return fail(RT_ERR_INVALID, "bad boundary");
+        if (p.kind == RT_PRIM_MEDIUM) {
+            if (p.a < 0 || p.a >= s->n_prims) return fail(RT_ERR_INVALID, "bad boundary");
+            const int bk = s->prims[p.a].kind;  // boundary_t: a simple prim or an instance
+            if (!simple_kind(bk) && bk != RT_PRIM_INSTANCE) return fail(RT_ERR_UNSUPPORTED, "medium boundary kind");
+        }
         if (p.kind != RT_PRIM_INSTANCE && (p.mat < 0 || p.mat >= s->n_materials)) return fail(RT_ERR_INVALID, "bad material");
     }
     for (int i = 0; i < s->n_materials; ++i) {
         const rt_material& m = s->materials[i];
+        if (m.kind < RT_MAT_LAMBERTIAN || m.kind > RT_MAT_ISOTROPIC) return fail(RT_ERR_INVALID, "bad material kind");
         bool needs_tex = m.kind == RT_MAT_LAMBERTIAN || m.kind == RT_MAT_DIFFUSE_LIGHT || m.kind == RT_MAT_ISOTROPIC;
         if (needs_tex && (m.tex < 0 || m.tex >= s->n_textures)) return fail(RT_ERR_INVALID, "bad texture ref");
     }
     for (int i = 0; i < s->n_textures; ++i) {
         const rt_texture& t = s->textures[i];
+        if (t.kind < RT_TEX_SOLID || t.kind > RT_TEX_IMAGE) return fail(RT_ERR_INVALID, "bad texture kind");
         if (t.kind == RT_TEX_NOISE && (t.perlin < 0 || t.perlin >= s->n_perlin)) return fail(RT_ERR_INVALID, "bad perlin");
         if (t.kind == RT_TEX_IMAGE && t.img_w > 0 &&
-            t.img_offset + t.img_bps * (int64_t)(t.img_h - 1) + 3 * (int64_t)t.img_w > s->image_bytes)
+            (t.img_h <= 0 || t.img_offset < 0 || t.img_bps < 3 * (int64_t)t.img_w ||
+             t.img_offset + t.img_bps * (int64_t)(t.img_h - 1) + 3 * (int64_t)t.img_w > s->image_bytes))
             return fail(RT_ERR_INVALID, "image texture out of range");
     }
     for (int i = 0; i < s->n_prim_refs; ++i)
@@ -449,9 +508,65 @@ int rt_ctx_upload_soa(rt_ctx* c, const rt_scene_soa* s)
     for (int i = 0; i < s->n_instances; ++i) {
         const rt_instance& in = s->instances[i];
         if (in.n_ops < 0 || in.n_ops > 4) return fail(RT_ERR_INVALID, "bad instance ops");
+        if (in.child_kind != RT_CHILD_PRIM && in.child_kind != RT_CHILD_BVH) return fail(RT_ERR_INVALID, "bad instance child kind");
         if (in.child_kind == RT_CHILD_PRIM ? (in.child < 0 || in.child >= s->n_prims) : !check_ref(in.child))
             return fail(RT_ERR_INVALID, "bad instance child");
+        if (in.child_kind == RT_CHILD_PRIM && !simple_kind(s->prims[in.child].kind))
+            return fail(RT_ERR_UNSUPPORTED, "instance child must be a simple primitive or a BVH");
     }
+    // stack needs (the kernel: TLAS walk in entries [0, tlas), a nested BLAS walk above it)
+    std::vector<int> need((size_t)s->n_nodes, 0);
+    std::vector<uint8_t> colour((size_t)s->n_nodes, 0);
+    const int t = walk_need(s, s->tlas_root, need, colour);
+    if (t < 0) return fail(RT_ERR_INVALID, "cycle in the TLAS node graph");
+    tlas_depth = t + 1;  // + 1 as flatten.cpp records it
+    blas_depth = 0;
+    for (int i = 0; i < s->n_instances; ++i) {
+        const rt_instance& in = s->instances[i];
+        if (in.child_kind != RT_CHILD_BVH) continue;
+        std::fill(colour.begin(), colour.end(), 0);
+        const int b = walk_need(s, in.child, need, colour);
+        if (b < 0) return fail(RT_ERR_INVALID, "cycle in an instance BVH");
+        blas_depth = std::max(blas_depth, b + 1);
+    }
+    if (tlas_depth > 32 || blas_depth > 32) return fail(RT_ERR_UNSUPPORTED, "BVH too deep for the traversal stack");
+    // the TLAS-in-LDS claim: every node reachable from the root lies in [0, n_tlas_nodes)
+    n_tlas_nodes = 0;
+    if (s->n_tlas_nodes > 0 && s->n_tlas_nodes <= s->n_nodes && s->tlas_root == 0) {
+        bool inside = true;
+        std::vector<int> todo{0};
+        std::fill(colour.begin(), colour.end(), 0);
+        while (!todo.empty() && inside) {
+            const int i = todo.back();
+            todo.pop_back();
+            if (i >= s->n_tlas_nodes) inside = false;
+            if (!inside || colour[i]) continue;
+            colour[i] = 1;
+            for (int ch : s->nodes[i].child)
+                if (ch >= 0) todo.push_back(ch);
+        }
+        if (inside) n_tlas_nodes = s->n_tlas_nodes;
+    }
+    return RT_OK;
+}
+
+int rt_scene_validate(const rt_scene_soa* s, int32_t* tlas_depth, int32_t* blas_depth)
+{
+    if (!s) return fail(RT_ERR_INVALID, "null argument");
+    int t = 0, b = 0, n = 0;
+    int rc = validate_soa(s, t, b, n);
+    if (rc) return rc;
+    if (tlas_depth) *tlas_depth = t;
+    if (blas_depth) *blas_depth = b;
+    return RT_OK;
+}
+
+int rt_ctx_upload_soa(rt_ctx* c, const rt_scene_soa* s)
+{
+    if (!c || !s) return fail(RT_ERR_INVALID, "null argument");
+    int tlas_depth = 0, blas_depth = 0, n_tlas_nodes = 0;
+    int vrc = validate_soa(s, tlas_depth, blas_depth, n_tlas_nodes);
+    if (vrc) return vrc;
 
     // the primitive records in leaf-slot order (prims[prim_refs[j]]): the kernel's leaf
     // loops read a record without first loading its index
@@ -472,6 +587,7 @@ int rt_ctx_upload_soa(rt_ctx* c, const rt_scene_soa* s)
     total = std::max<size_t>(total, 256);
     HIP_TRY(hipSetDevice(c->device));
     HIP_TRY(hipStreamSynchronize(c->stream));
+    if (c->any_enqueued) HIP_TRY(hipEventSynchronize(c->ev_done));  // renders still reading the scene
     if (total > c->scene_bytes) {
         (void)hipFree(c->scene_buf);
         c->scene_buf = nullptr;
@@ -494,15 +610,11 @@ int rt_ctx_upload_soa(rt_ctx* c, const rt_scene_soa* s)
     c->S.leaf_prims = (const rt_prim*)(base + off[9]);
     c->S.tlas_root = s->tlas_root;
     c->S.n_lds_nodes = 0;
-    // traversal stack: TLAS walk, then a nested BLAS walk (instances) above it
-    if (s->tlas_depth > 0 && s->tlas_depth <= 32 && s->blas_depth >= 0 && s->blas_depth <= 32) {
-        c->S.blas_base = s->tlas_depth;
-        c->S.stack_entries = std::max(1, s->tlas_depth + s->blas_depth);
-    } else {  // unknown depths (a foreign host's tables): the 64-entry scratch stack
-        c->S.blas_base = 32;
-        c->S.stack_entries = 64;
-    }
-    c->n_tlas_nodes = (s->n_tlas_nodes > 0 && s->n_tlas_nodes <= s->n_nodes && s->tlas_root == 0) ? s->n_tlas_nodes : 0;
+    // traversal stack: TLAS walk, then a nested BLAS walk (instances) above it, sized from the
+    // depths validate_soa measured (<= 32 each, so the 64-entry scratch stack always fits)
+    c->S.blas_base = tlas_depth;
+    c->S.stack_entries = std::max(1, tlas_depth + blas_depth);
+    c->n_tlas_nodes = n_tlas_nodes;
     c->S.n_tlas_nodes = c->n_tlas_nodes;
     c->has_scene = true;
     uint32_t feat = 0;
@@ -574,10 +686,11 @@ struct Sink {
 
 // Traces samples [s_begin, s_end) of the shard in chunks of `chunk` and reduces them into
 // the sink. Events: ev[0] before the first trace launch, ev[1] after the last one, ev[2]
-// after the last reduction. Chunk schedule: one launch into chunk partials. Pool schedule:
-// per-sample radiance in batches that fit sample_buf_cap; with more than one batch (or an
-// acc sink) the sums run through acc (the sink's, or acc_tmp) plus the open chunk's sum
-// (carried across batches), which keeps the additions in the one-batch order.
+// after the last reduction. Chunk and item schedules: chunk partials per launch, reduced in
+// chunk order (or added to the sink's / a running accumulator across buffer batches).
+// Per-sample pool: per-sample radiance in batches; with more than one batch (or an acc
+// sink) the sums run through an accumulator plus the open chunk's sum (carried across
+// batches), which keeps the additions in the one-batch order.
 static int run_range(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, int s_begin, int s_end, int chunk,
                      hipStream_t stream, const Sink& sink)
 {
@@ -624,22 +737,35 @@ static int run_range(rt_ctx* c, const rt_camera* cam, const rt_render_params* p,
     S.n_lds_nodes = c->opt_lds_nodes ? std::min(c->n_tlas_nodes, kMaxLdsNodes) : 0;
 
     const long long total = s_end - s_begin;
-    long long batch = total;
-    if (o.pool) batch = std::min<long long>(total, std::max<size_t>(1, c->sample_buf_cap / (px * 3 * sizeof(double))));
+    // Buffer batches: the trace output of one launch is bounded by sample_buf_cap. Per-sample
+    // pool: samples x pixels x 24 B; chunk and item schedules: chunks x pixels x 24 B, batches
+    // on chunk boundaries (relative to s_begin), so the partials add in one-launch order.
+    const bool per_sample = o.pool == RT_SCHED_POOL;
+    const size_t px_bytes = px * 3 * sizeof(double);
+    const long long fit = (long long)std::max<size_t>(1, c->sample_buf_cap / px_bytes);
+    const long long batch = std::min<long long>(total, per_sample ? fit : fit * chunk);
     const int n_batches = (int)((total + batch - 1) / batch);
     double* acc = sink.acc;
     double* open = nullptr;
-    if (o.pool && (n_batches > 1 || acc)) {  // acc_tmp = [open chunk sums | running total (no acc sink)]
-        int rc = grow(c, stream, c->acc_tmp, c->acc_tmp_cap, 2 * px * 3 * sizeof(double));
+    bool own_acc = false;
+    if (per_sample && (n_batches > 1 || acc)) {  // acc_tmp = [open chunk sums | running total (no acc sink)]
+        int rc = grow(c, stream, c->acc_tmp, c->acc_tmp_cap, 2 * px_bytes);
         if (rc) return rc;
         open = c->acc_tmp;
         if (!acc) {
             acc = c->acc_tmp + px * 3;
-            HIP_TRY(hipMemsetAsync(acc, 0, px * 3 * sizeof(double), stream));
+            own_acc = true;
+            HIP_TRY(hipMemsetAsync(acc, 0, px_bytes, stream));
         }
+    } else if (!per_sample && n_batches > 1 && !acc) {  // running total of the chunk partials
+        int rc = grow(c, stream, c->acc_tmp, c->acc_tmp_cap, px_bytes);
+        if (rc) return rc;
+        acc = c->acc_tmp;
+        own_acc = true;
+        HIP_TRY(hipMemsetAsync(acc, 0, px_bytes, stream));
     }
     const int max_chunks = (int)((batch + chunk - 1) / chunk);
-    const size_t need = o.pool ? (size_t)batch * px * 3 * sizeof(double) : (size_t)max_chunks * px * 3 * sizeof(double);
+    const size_t need = per_sample ? (size_t)batch * px_bytes : (size_t)max_chunks * px_bytes;
     int rc = grow(c, stream, c->partial, c->partial_cap, need);
     if (rc) return rc;
     if (count) HIP_TRY(hipMemsetAsync(c->counters, 0, kCounters * sizeof(unsigned long long), stream));
@@ -655,8 +781,8 @@ static int run_range(rt_ctx* c, const rt_camera* cam, const rt_render_params* p,
         HIP_TRY(hipMemcpyAsync(dK, &K, sizeof K, hipMemcpyHostToDevice, stream));
         HIP_TRY(rtk::launch_trace(S, K, dK, c->partial, c->counters, c->work, o, stream));
         if (bi == n_batches - 1) HIP_TRY(hipEventRecord(c->ev[1], stream));
-        if (!o.pool) {
-            if (sink.acc) HIP_TRY(rtk::launch_accumulate(c->partial, sink.acc, n_px, K.n_chunks, stream));
+        if (!per_sample) {
+            if (acc) HIP_TRY(rtk::launch_accumulate(c->partial, acc, n_px, K.n_chunks, stream));
             else HIP_TRY(rtk::launch_reduce(c->partial, sink.out, sink.f64, n_px, K.n_chunks, sink.scale, stream));
         } else if (!open) {
             HIP_TRY(rtk::launch_reduce_samples(c->partial, sink.out, sink.f64, n_px, b1 - b0, chunk, sink.scale, stream));
@@ -666,7 +792,7 @@ static int run_range(rt_ctx* c, const rt_camera* cam, const rt_render_params* p,
                                                      stream));
         }
     }
-    if (open && !sink.acc)  // resolve the running sums: 0.0 + sum, times scale, as one batch does
+    if (own_acc)  // resolve the running sums: 0.0 + sum, times scale, as one batch does
         HIP_TRY(rtk::launch_reduce(acc, sink.out, sink.f64, n_px, 1, sink.scale, stream));
     HIP_TRY(hipEventRecord(c->ev[2], stream));
 
@@ -689,10 +815,26 @@ static int run_range(rt_ctx* c, const rt_camera* cam, const rt_render_params* p,
     return RT_OK;
 }
 
+// Orders work about to be enqueued on `stream` after everything this context enqueued on
+// another stream before (the context's scratch buffers are shared between its renders).
+static int begin_on(rt_ctx* c, hipStream_t stream)
+{
+    if (c->any_enqueued && stream != c->last_stream) HIP_TRY(hipStreamWaitEvent(stream, c->ev_done, 0));
+    return RT_OK;
+}
+static int end_on(rt_ctx* c, hipStream_t stream)
+{
+    HIP_TRY(hipEventRecord(c->ev_done, stream));
+    c->last_stream = stream;
+    c->any_enqueued = true;
+    return RT_OK;
+}
+
 // Device buffer for a host-bound result (grown on demand).
-static int out_staging(rt_ctx* c, size_t out_bytes, void*& dev_out)
+static int out_staging(rt_ctx* c, hipStream_t stream, size_t out_bytes, void*& dev_out)
 {
     if (out_bytes > c->out_cap) {
+        HIP_TRY(hipStreamSynchronize(stream));  // ordered after every earlier use (begin_on)
         (void)hipFree(c->out_buf);
         c->out_buf = nullptr;
         c->out_cap = 0;
@@ -715,22 +857,24 @@ int rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, void* 
 
     HIP_TRY(hipSetDevice(c->device));
     hipStream_t stream = p->stream ? (hipStream_t)p->stream : c->stream;
+    int rc = begin_on(c, stream);
+    if (rc) return rc;
     const size_t out_bytes = (size_t)n_px * 3 * (p->out_format == RT_OUT_F64 ? 8 : 4);
     void* dev_out = out;
     if (!p->out_on_device) {
-        int rc = out_staging(c, out_bytes, dev_out);
+        rc = out_staging(c, stream, out_bytes, dev_out);
         if (rc) return rc;
     }
     Sink sink;
     sink.out = dev_out;
     sink.f64 = p->out_format == RT_OUT_F64;
     sink.scale = 1.0 / (double)p->spp;
-    int rc = run_range(c, cam, p, 0, p->spp, chunk, stream, sink);
+    rc = run_range(c, cam, p, 0, p->spp, chunk, stream, sink);
     if (rc) return rc;
-    if (!p->out_on_device) {
-        HIP_TRY(hipMemcpyAsync(out, dev_out, out_bytes, hipMemcpyDeviceToHost, stream));
-        HIP_TRY(hipStreamSynchronize(stream));
-    }
+    if (!p->out_on_device) HIP_TRY(hipMemcpyAsync(out, dev_out, out_bytes, hipMemcpyDeviceToHost, stream));
+    rc = end_on(c, stream);
+    if (rc) return rc;
+    if (!p->out_on_device) HIP_TRY(hipStreamSynchronize(stream));
     return RT_OK;
 }
 
@@ -797,9 +941,13 @@ int rt_accum_add(rt_ctx* c, rt_accum* a, const rt_camera* cam, const rt_render_p
     HIP_TRY(hipSetDevice(c->device));
     hipStream_t stream = p->stream ? (hipStream_t)p->stream : c->stream;
     if (stream != a->last_stream) HIP_TRY(hipStreamSynchronize(a->last_stream));
+    int rc = begin_on(c, stream);
+    if (rc) return rc;
     Sink sink;
     sink.acc = a->sums;
-    int rc = run_range(c, cam, p, (int)a->done, (int)(a->done + sample_count), a->chunk, stream, sink);
+    rc = run_range(c, cam, p, (int)a->done, (int)(a->done + sample_count), a->chunk, stream, sink);
+    if (rc) return rc;
+    rc = end_on(c, stream);
     if (rc) return rc;
     a->done += sample_count;
     a->last_stream = stream;
@@ -837,18 +985,20 @@ int rt_accum_resolve(rt_ctx* c, rt_accum* a, double divisor, int out_format, int
     if (!(divisor > 0.0) || !std::isfinite(divisor)) return fail(RT_ERR_INVALID, "nothing accumulated / bad divisor");
     HIP_TRY(hipSetDevice(c->device));
     hipStream_t stream = a->last_stream;
+    int rc = begin_on(c, stream);
+    if (rc) return rc;
     const size_t out_bytes = (size_t)a->n_px * 3 * (out_format == RT_OUT_F64 ? 8 : 4);
     void* dev_out = out;
     if (!out_on_device) {
-        int rc = out_staging(c, out_bytes, dev_out);
+        rc = out_staging(c, stream, out_bytes, dev_out);
         if (rc) return rc;
     }
     // one "chunk" holding the running sums: 0.0 + sum = sum, then * (1/divisor) as rt_render
     HIP_TRY(rtk::launch_reduce(a->sums, dev_out, out_format == RT_OUT_F64, a->n_px, 1, 1.0 / divisor, stream));
-    if (!out_on_device) {
-        HIP_TRY(hipMemcpyAsync(out, dev_out, out_bytes, hipMemcpyDeviceToHost, stream));
-        HIP_TRY(hipStreamSynchronize(stream));
-    }
+    if (!out_on_device) HIP_TRY(hipMemcpyAsync(out, dev_out, out_bytes, hipMemcpyDeviceToHost, stream));
+    rc = end_on(c, stream);
+    if (rc) return rc;
+    if (!out_on_device) HIP_TRY(hipStreamSynchronize(stream));
     return RT_OK;
 }
 
@@ -961,8 +1111,8 @@ int rt_ctx_set_variant(rt_ctx* c, int slab32, int lds_stack, int lds_nodes)
 
 int rt_ctx_set_schedule(rt_ctx* c, int schedule)
 {
-    if (!c || (schedule != RT_SCHED_CHUNKS && schedule != RT_SCHED_POOL)) return fail(RT_ERR_INVALID, "bad schedule");
-    c->opt_pool = schedule == RT_SCHED_POOL;
+    if (!c || schedule < RT_SCHED_CHUNKS || schedule > RT_SCHED_ITEMS) return fail(RT_ERR_INVALID, "bad schedule");
+    c->opt_pool = schedule;
     return RT_OK;
 }
 

@@ -1,0 +1,1476 @@
+// trace_device.hpp — the MI355X megakernel for the reference's per-(pixel, sample)
+// hot path: Camera::get_ray (camera.rs:58-66) + ray_color (main.rs:19-38) and
+// everything below it (hittable.rs, material.rs, texture.rs, perlin.rs), in f64
+// like the reference (math.rs:13-17).
+//
+// Execution model:
+//   * work unit = one (pixel, sample) path; work block = one 8x8 pixel tile x one chunk
+//     of spp_chunk samples (a function of spp only);
+//   * trace_pool (default): persistent waves take blocks from a device counter, and a
+//     lane whose path ended takes the block's next unit in the same bounce-loop
+//     iteration (ballot + mbcnt), so lanes do not idle until the last blocks run out;
+//     each sample's radiance goes to its slot of a [sample][pixel] buffer and
+//     reduce_samples sums every pixel's samples in sample order, chunk by chunk — the
+//     image does not depend on which lane computed a sample, on the launch geometry or
+//     on how rows are sharded over GPUs; trace_chunks (the first schedule, kept for A/B)
+//     gives a lane one pixel's chunk and adds the same partial sums;
+//   * the depth-50 recursion is an iterative bounce loop; traversal carries only
+//     (t, primitive slot); the HitRecord (hittable.rs:6-27) is built once per cast;
+//   * TLAS nodes and the traversal stack in LDS, conservative f32 slab tests, f64
+//     primitive tests; materials share their expensive steps so a wave holding several
+//     kinds runs each step once;
+//   * RNG: per (pixel, sample) a Philox4x32-10 block seeds a xoshiro128++ path stream
+//     (rt_numerics.h); the medium's in-hit draw is keyed by (pixel, sample, bounce, medium id).
+// Built with -ffp-contract=off: bit-for-bit the operation order of the reference.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+#include "rt/rt_numerics.h"
+#include "rt/rt_scene.h"
+#include "trace_kernel.hpp"
+
+namespace rtk {
+
+struct Ray {
+    double ox, oy, oz;
+    double dx, dy, dz;
+    double time;
+    double a;                 // length_squared(direction)
+    double ya;                // 1 / a correctly rounded (NaN outside [2^-900, 2^900]: see div_rcp)
+    double ix, iy, iz;        // 1 / direction (f64 slab tests only)
+    float fix, fiy, fiz;      // f32 1 / direction (f32 slab tests only)
+    float fox, foy, foz;      // -origin * (1 / direction) in f32
+    uint32_t onx, ony, onz;   // byte offsets in a node of child 0's near planes (by direction sign)
+};
+
+// The HitRecord of hittable.rs:6-27 (uv deferred to texture lookup: uvkind 1 keeps the
+// object-space outward normal for sphere_uv, 2 keeps (x-a0, a1-a0, y-b0, b1-b0)).
+struct Hit {
+    double t, px, py, pz, nx, ny, nz;
+    double uv0, uv1, uv2, uv3;
+    int front, mat, uvkind;
+};
+
+// What traversal keeps per candidate: the parameter and which primitive produced it.
+struct HitRef {
+    double t;
+    int prim;   // prim index (top level)
+    int sub;    // instance: BLAS prim index; box: winning side (0..5)
+    int side;   // box inside an instance: winning side
+};
+
+struct Keyed {                 // coordinates of the medium's keyed draw
+    uint64_t seed;
+    uint32_t pixel, sample, bounce;
+};
+
+struct Count {
+    uint32_t casts, nodes, prims;
+    uint32_t wave_steps, wave_nodes;  // loop iterations the wave executed (counted by its first active lane)
+    uint32_t wave_leaves;             // leaf-loop iterations the wave executed
+    uint32_t cam_lanes, cam_steps;    // lanes starting a sample / iterations in which any did
+    uint32_t shade_lanes, shade_steps;
+    uint64_t t_nodes, t_leaves;       // wave-cycles in node-visit loops / leaf tests (same in every lane)
+};
+// COUNT only: true in exactly one active lane of the wave
+__device__ __forceinline__ bool first_active_lane()
+{
+    return (int)(threadIdx.x & 63) == __ffsll((long long)__ballot(1)) - 1;
+}
+
+// Compile-time kernel configuration (one instantiation per variant):
+//   F      scene features the variant handles (trace_kernel.hpp FEAT_*); code for the
+//          others is not emitted, which keeps register pressure and code size down
+//   S32    conservative f32 slab tests (boxes padded on the host, see flatten.cpp)
+//   LDS    traversal stack in LDS (interleaved per lane) instead of scratch
+//   COUNT  diagnostic: count casts / node visits / primitive tests and time the phases
+// Traversal is while-while (Aila & Laine 2009); the if-if form and a per-lane state
+// machine with ballot-gated shading both measured slower.
+//   NALL   every TLAS node is in LDS (no per-node LDS/global choice)
+#ifndef RT_TRACE_LOOP
+#define RT_TRACE_LOOP 1   // 0 if-if, 1 while-while, 2 while-while with speculative node visits
+#endif
+template <uint32_t F_, bool S32_, bool LDS_, bool NALL_, bool COUNT_>
+struct Cfg {
+    static constexpr uint32_t F = F_;
+    static constexpr bool S32 = S32_;
+    static constexpr bool LDS = LDS_;
+    static constexpr bool NALL = NALL_;
+    static constexpr bool COUNT = COUNT_;
+    static constexpr int LOOP = RT_TRACE_LOOP;
+};
+
+// Traversal stack. LDS: a lane-interleaved dynamic LDS array [entry][256 threads]
+// (consecutive lanes hit consecutive banks) sized per scene by the host (TLAS depth +
+// BLAS depth); scratch: a private array (deep scenes).
+template <bool LDS>
+struct Stack;
+template <>
+struct Stack<true> {
+    int* base;
+    __device__ __forceinline__ int& operator[](int i) const { return base[i * 256]; }
+};
+template <>
+struct Stack<false> {
+    int v[64];
+    __device__ __forceinline__ int& operator[](int i) { return v[i]; }
+};
+template <class C>
+using StackT = Stack<C::LDS>;
+extern __shared__ int rt_lds[];  // [stack entries x 256 lanes] [cached TLAS nodes]
+
+// Division by a value b used many times, through its correctly rounded reciprocal
+// y = RN(1/b): q0 = RN(q*y), then one correction q1 = RN(q0 + RN-exact(q - b*q0) * y).
+// With y correctly rounded this is Markstein's theorem (IBM J. R&D 34(1), 1990): q1 =
+// RN(q/b), bit for bit what `q / b` gives, barring overflow / underflow in the products,
+// which the range guard on b excludes (y is NaN outside it, and the division runs then);
+// checked on 8e8 random and adversarial pairs on the host (all-ones / power-of-two
+// significands, both signs, exponents -20..20). A zero q may come out as -0 where q / b
+// gives +0 or the reverse; every caller compares the quotient with t_min > 0 first or
+// has q, b >= 0, so the sign of a zero quotient changes nothing.
+__device__ __forceinline__ double rcp_for_div(double b)
+{
+    const double m = __builtin_fabs(b);
+    return (m >= 0x1.0p-900 && m <= 0x1.0p+900) ? 1.0 / b : __builtin_nan("");
+}
+__device__ __forceinline__ double div_rcp(double q, double b, double y)
+{
+    const double q0 = q * y;
+    const double q1 = __builtin_fma(__builtin_fma(-b, q0, q), y, q0);
+    if (__builtin_expect(q1 != q1, 0)) return q / b;  // y outside the guard (or q not finite)
+    return q1;
+}
+
+__device__ __forceinline__ float f32_inv_dir(double d)
+{
+    // an exact 0 would give inf * 0 = NaN in the slab products; a 1e-30 component keeps the
+    // interval of a ray parallel to a slab finite and correct (inside: huge, outside: empty)
+    float f = (float)d;
+    if (__builtin_fabsf(f) < 1e-30f) f = __builtin_copysignf(1e-30f, f);
+    return __builtin_amdgcn_rcpf(f);
+}
+
+// spheres: the scene has spheres (wave-uniform); otherwise no root division needs 1/a
+template <class C>
+__device__ __forceinline__ void finish_ray(Ray& r, bool spheres)
+{
+    r.a = r.dx * r.dx + r.dy * r.dy + r.dz * r.dz;
+    r.ya = (C::F == FEAT_SET_SPHERES || spheres) ? rcp_for_div(r.a) : __builtin_nan("");
+    if constexpr (C::S32) {
+        r.fix = f32_inv_dir(r.dx);
+        r.fiy = f32_inv_dir(r.dy);
+        r.fiz = f32_inv_dir(r.dz);
+        r.fox = -(float)r.ox * r.fix;
+        r.foy = -(float)r.oy * r.fiy;
+        r.foz = -(float)r.oz * r.fiz;
+        // rt_bvh_node: lo0 at bytes 0/4/8, hi0 at 12/16/20 (x/y/z); child 1's box 24 bytes on
+        r.onx = r.fix >= 0.0f ? 0u : 12u;
+        r.ony = r.fiy >= 0.0f ? 4u : 16u;
+        r.onz = r.fiz >= 0.0f ? 8u : 20u;
+    } else {
+        r.ix = 1.0 / r.dx;
+        r.iy = 1.0 / r.dy;
+        r.iz = 1.0 / r.dz;
+    }
+}
+
+// hittable.rs:23-26
+__device__ __forceinline__ void set_face_normal(Hit& h, double dx, double dy, double dz, double nx, double ny,
+                                                double nz)
+{
+    const bool front = dx * nx + dy * ny + dz * nz < 0.0;
+    h.front = front;
+    h.nx = front ? nx : -nx;
+    h.ny = front ? ny : -ny;
+    h.nz = front ? nz : -nz;
+}
+
+// ---------------------------------------------------------------------------
+// primitives: a t-only test (traversal) and a finisher (once per cast)
+// ---------------------------------------------------------------------------
+
+// hittable.rs:254-273: the root in [t_min, t_max]
+__device__ __forceinline__ bool sphere_t(double cx, double cy, double cz, double radius, const Ray& r, double t_min,
+                                         double t_max, double& t)
+{
+    const double ocx = r.ox - cx, ocy = r.oy - cy, ocz = r.oz - cz;
+    const double half_b = ocx * r.dx + ocy * r.dy + ocz * r.dz;
+    const double c = (ocx * ocx + ocy * ocy + ocz * ocz) - radius * radius;
+    const double disc = half_b * half_b - r.a * c;
+    if (disc < 0.0) return false;
+#ifdef RT_PROBE_FAST_SPHERE  // timing probe (inexact sqrt / division): NOT the product
+    const double sqrtd = __builtin_amdgcn_sqrt(disc);
+    const double ia = __builtin_amdgcn_rcp(r.a);
+    double root = (-half_b - sqrtd) * ia;
+    if (root < t_min || t_max < root) {
+        root = (-half_b + sqrtd) * ia;
+#else
+    const double sqrtd = __builtin_sqrt(disc);
+    double root = div_rcp(-half_b - sqrtd, r.a, r.ya);
+    if (root < t_min || t_max < root) {
+        root = div_rcp(-half_b + sqrtd, r.a, r.ya);
+#endif
+        if (root < t_min || t_max < root) return false;
+    }
+    t = root;
+    return true;
+}
+
+// hittable.rs:275-287
+template <class C>
+__device__ __forceinline__ void sphere_finish(double cx, double cy, double cz, double inv_r, const Ray& r, double t,
+                                              int mat, Hit& h)
+{
+    h.t = t;
+    h.px = r.ox + r.dx * t;
+    h.py = r.oy + r.dy * t;
+    h.pz = r.oz + r.dz * t;
+    const double onx = (h.px - cx) * inv_r, ony = (h.py - cy) * inv_r, onz = (h.pz - cz) * inv_r;
+    set_face_normal(h, r.dx, r.dy, r.dz, onx, ony, onz);
+    h.mat = mat;
+    h.uvkind = 1;
+    if constexpr ((C::F & FEAT_IMAGE) != 0) {
+        h.uv0 = onx;
+        h.uv1 = ony;
+        h.uv2 = onz;
+    }
+}
+
+// hittable.rs:308-320 (axis 0: XY, k on z; 1: XZ, k on y; 2: YZ, k on x)
+__device__ __forceinline__ void rect_axes(int axis, const Ray& r, double& ok, double& dk, double& oa, double& da,
+                                          double& ob, double& db)
+{
+    if (axis == 0) { ok = r.oz; dk = r.dz; oa = r.ox; da = r.dx; ob = r.oy; db = r.dy; }
+    else if (axis == 1) { ok = r.oy; dk = r.dy; oa = r.ox; da = r.dx; ob = r.oz; db = r.dz; }
+    else { ok = r.ox; dk = r.dx; oa = r.oy; da = r.dy; ob = r.oz; db = r.dz; }
+}
+
+__device__ __forceinline__ bool rect_t(int axis, double a0, double a1, double b0, double b1, double k, const Ray& r,
+                                       double t_min, double t_max, double& t_out)
+{
+    double ok, dk, oa, da, ob, db;
+    rect_axes(axis, r, ok, dk, oa, da, ob, db);
+    const double t = (k - ok) / dk;
+    if (t < t_min || t > t_max) return false;
+    const double x = oa + t * da;
+    const double y = ob + t * db;
+    if (x < a0 || x > a1 || y < b0 || y > b1) return false;
+    t_out = t;
+    return true;
+}
+
+// hittable.rs:322-331
+template <class C>
+__device__ __forceinline__ void rect_finish(int axis, double a0, double a1, double b0, double b1, const Ray& r,
+                                            double t, int mat, Hit& h)
+{
+    double ok, dk, oa, da, ob, db;
+    rect_axes(axis, r, ok, dk, oa, da, ob, db);
+    h.uvkind = 2;
+    if constexpr ((C::F & FEAT_IMAGE) != 0) {
+        const double x = oa + t * da;
+        const double y = ob + t * db;
+        h.uv0 = x - a0;
+        h.uv1 = a1 - a0;
+        h.uv2 = y - b0;
+        h.uv3 = b1 - b0;
+    }
+    h.t = t;
+    set_face_normal(h, r.dx, r.dy, r.dz, axis == 2 ? 1.0 : 0.0, axis == 1 ? 1.0 : 0.0, axis == 0 ? 1.0 : 0.0);
+    h.mat = mat;
+    h.px = r.ox + r.dx * t;
+    h.py = r.oy + r.dy * t;
+    h.pz = r.oz + r.dz * t;
+}
+
+// the six sides of new_box (hittable.rs:135-142): side -> axis, (a0 a1 b0 b1 k) from min/max
+__device__ __forceinline__ void box_side(const rt_prim& p, int side, int& axis, double& a0, double& a1, double& b0,
+                                         double& b1, double& k)
+{
+    const double mnx = p.p[0], mny = p.p[1], mnz = p.p[2], mxx = p.p[3], mxy = p.p[4], mxz = p.p[5];
+    if (side < 2) { axis = 0; a0 = mnx; a1 = mxx; b0 = mny; b1 = mxy; k = side == 0 ? mxz : mnz; }
+    else if (side < 4) { axis = 1; a0 = mnx; a1 = mxx; b0 = mnz; b1 = mxz; k = side == 2 ? mxy : mny; }
+    else { axis = 2; a0 = mny; a1 = mxy; b0 = mnz; b1 = mxz; k = side == 4 ? mxx : mnx; }
+}
+
+// Box::hit = hit_hittables over its sides (hittable.rs:229-231): closest, ties to the later side.
+__device__ __forceinline__ bool box_t(const rt_prim& p, const Ray& r, double t_min, double t_max, double& t,
+                                      int& side)
+{
+    bool any = false;
+#pragma unroll
+    for (int s = 0; s < 6; ++s) {
+        int axis;
+        double a0, a1, b0, b1, k, ts;
+        box_side(p, s, axis, a0, a1, b0, b1, k);
+        if (rect_t(axis, a0, a1, b0, b1, k, r, t_min, t_max, ts)) {
+            t_max = ts;
+            t = ts;
+            side = s;
+            any = true;
+        }
+    }
+    return any;
+}
+
+// The centre of a Sphere, or of a MovingSphere at the ray's time: center_0 +
+// ((time - time_0) / (time_1 - time_0)) * (center_1 - center_0) (hittable.rs:556-558).
+// Both kinds go through one code path (the moving centre is a select), so a wave whose
+// lanes hold both kinds runs the sphere test once, not once per kind.
+__device__ __forceinline__ void sphere_center(const rt_prim& p, const Ray& r, double& cx, double& cy, double& cz)
+{
+    const double c0x = p.p[0], c0y = p.p[1], c0z = p.p[2];
+    const double vx = p.p[5], vy = p.p[6], vz = p.p[7];
+    const bool moving = p.kind == RT_PRIM_MOVING_SPHERE;
+    double s = r.time;
+    if (moving && !p.a) s = (r.time - p.p[8]) / (p.p[9] - p.p[8]);
+    cx = moving ? c0x + vx * s : c0x;
+    cy = moving ? c0y + vy * s : c0y;
+    cz = moving ? c0z + vz * s : c0z;
+}
+
+// Sphere, MovingSphere, rects, Box: t-only (hittable.rs:211-231).
+template <class C>
+__device__ __forceinline__ bool simple_t(const rt_prim& p, const Ray& r, double t_min, double t_max, double& t,
+                                         int& side, Count& cnt)
+{
+    if (C::COUNT) cnt.prims++;
+    if (!(C::F & FEAT_RECT) || p.kind <= RT_PRIM_MOVING_SPHERE) {
+        double cx, cy, cz;
+        sphere_center(p, r, cx, cy, cz);
+        return sphere_t(cx, cy, cz, p.p[3], r, t_min, t_max, t);
+    } else {
+        switch (p.kind) {
+        case RT_PRIM_XY_RECT: return rect_t(0, p.p[0], p.p[1], p.p[2], p.p[3], p.p[4], r, t_min, t_max, t);
+        case RT_PRIM_XZ_RECT: return rect_t(1, p.p[0], p.p[1], p.p[2], p.p[3], p.p[4], r, t_min, t_max, t);
+        case RT_PRIM_YZ_RECT: return rect_t(2, p.p[0], p.p[1], p.p[2], p.p[3], p.p[4], r, t_min, t_max, t);
+        case RT_PRIM_BOX: return box_t(p, r, t_min, t_max, t, side);
+        default: return false;
+        }
+    }
+}
+
+template <class C>
+__device__ __forceinline__ void simple_finish(const rt_prim& p, const Ray& r, double t, int side, Hit& h)
+{
+    if constexpr ((C::F & FEAT_RECT) != 0) {
+        if (p.kind >= RT_PRIM_XY_RECT && p.kind <= RT_PRIM_YZ_RECT) {
+            rect_finish<C>(p.kind - RT_PRIM_XY_RECT, p.p[0], p.p[1], p.p[2], p.p[3], r, t, p.mat, h);
+            return;
+        }
+        if (p.kind == RT_PRIM_BOX) {
+            int axis;
+            double a0, a1, b0, b1, k;
+            box_side(p, side, axis, a0, a1, b0, b1, k);
+            rect_finish<C>(axis, a0, a1, b0, b1, r, t, p.mat, h);
+            return;
+        }
+    }
+    double cx, cy, cz;
+    sphere_center(p, r, cx, cy, cz);
+    sphere_finish<C>(cx, cy, cz, p.p[4], r, t, p.mat, h);
+}
+
+// ---------------------------------------------------------------------------
+// BVH traversal
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ bool slab32(const float* lo, const float* hi, const Ray& r, float t_min, float t_max,
+                                       float& t_near)
+{
+    const float x0 = __builtin_fmaf(lo[0], r.fix, r.fox), x1 = __builtin_fmaf(hi[0], r.fix, r.fox);
+    const float y0 = __builtin_fmaf(lo[1], r.fiy, r.foy), y1 = __builtin_fmaf(hi[1], r.fiy, r.foy);
+    const float z0 = __builtin_fmaf(lo[2], r.fiz, r.foz), z1 = __builtin_fmaf(hi[2], r.fiz, r.foz);
+    const float tn = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fmaxf(fminf(z0, z1), t_min));
+    const float tf = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fminf(fmaxf(z0, z1), t_max));
+    t_near = tn;
+    return tn <= tf;
+}
+
+// f32 bounds of a double t range, rounded outward
+__device__ __forceinline__ float f32_down(double t)
+{
+    const float f = (float)t;
+    return f > 0.0f ? f * (1.0f - 0x1.0p-20f) : f * (1.0f + 0x1.0p-20f);
+}
+__device__ __forceinline__ float f32_up(double t)
+{
+    const float f = (float)t;
+    return f > 0.0f ? f * (1.0f + 0x1.0p-20f) : f * (1.0f - 0x1.0p-20f);
+}
+
+// Conservative slab test against an f32 box (rounded outward and padded on the
+// host), in f64. NaN products (0 * inf) are ignored by fmin/fmax.
+__device__ __forceinline__ bool slab(const float* lo, const float* hi, const Ray& r, double t_min, double t_max,
+                                     double& t_near)
+{
+    const double x0 = ((double)lo[0] - r.ox) * r.ix, x1 = ((double)hi[0] - r.ox) * r.ix;
+    const double y0 = ((double)lo[1] - r.oy) * r.iy, y1 = ((double)hi[1] - r.oy) * r.iy;
+    const double z0 = ((double)lo[2] - r.oz) * r.iz, z1 = ((double)hi[2] - r.oz) * r.iz;
+    const double tn = fmax(fmax(fmin(x0, x1), fmin(y0, y1)), fmax(fmin(z0, z1), t_min));
+    const double tf = fmin(fmin(fmax(x0, x1), fmax(y0, y1)), fmin(fmax(z0, z1), t_max));
+    t_near = tn;
+    return tn <= tf;
+}
+
+constexpr int RT_DONE = (int)0x80000000;
+
+// A node as four 16-B loads (ds_read_b128 from LDS, global_load_dwordx4 from L1/L2).
+struct Node {
+    float lo0[3], hi0[3], lo1[3], hi1[3];
+    int child[2];
+};
+__device__ __forceinline__ Node load_node(const rt_bvh_node* base, int i)
+{
+    const uint4* q = reinterpret_cast<const uint4*>(base + i);
+    const uint4 a = q[0], b = q[1], c = q[2], d = q[3];
+    Node n;
+    n.lo0[0] = __uint_as_float(a.x); n.lo0[1] = __uint_as_float(a.y); n.lo0[2] = __uint_as_float(a.z);
+    n.hi0[0] = __uint_as_float(a.w); n.hi0[1] = __uint_as_float(b.x); n.hi0[2] = __uint_as_float(b.y);
+    n.lo1[0] = __uint_as_float(b.z); n.lo1[1] = __uint_as_float(b.w); n.lo1[2] = __uint_as_float(c.x);
+    n.hi1[0] = __uint_as_float(c.y); n.hi1[1] = __uint_as_float(c.z); n.hi1[2] = __uint_as_float(c.w);
+    n.child[0] = (int)d.x;
+    n.child[1] = (int)d.y;
+    return n;
+}
+
+// Closest hit in a BVH (nodes + leaf ranges of slots j, whose records are leaf_prims[j]).
+// `leaf(slot, t_max, best)` tests one primitive; on a closer hit it fills best (t and sub
+// ids) and returns true; best.prim is then the slot.
+template <class C, bool NL = false, class LeafFn>
+__device__ __forceinline__ bool traverse(const SceneDev& S, int root, const Ray& r, double t_min, double t_max,
+                                         HitRef& best, StackT<C>& stack, int sp0, Count& cnt, LeafFn&& leaf)
+{
+    // NL: this is the TLAS, whose first S.n_lds_nodes nodes (BFS order) were copied into
+    // LDS at block start; deeper nodes are read from L1/L2
+    const rt_bvh_node* lds_nodes =
+        reinterpret_cast<const rt_bvh_node*>(rt_lds + (C::LDS ? S.stack_entries * 256 : 0));
+    bool any = false;
+    int sp = sp0;
+    int cur = root;
+    float tmin_f = 0.0f, tmax_f = 0.0f;
+    if constexpr (C::S32) {
+        tmin_f = f32_down(t_min);
+        tmax_f = f32_up(t_max);
+    }
+    // TLAS entirely in LDS, f32 slabs: each plane is read at the offset the ray's
+    // direction signs select (near plane first), so the slab test needs no min/max pair
+    // per axis: t_near = max(near planes), t_far = min(far planes)
+    constexpr bool OCT = NL && C::NALL && C::S32;
+    const char* const lb = reinterpret_cast<const char*>(lds_nodes);
+    const char *pnx = lb, *pny = lb, *pnz = lb, *pfx = lb, *pfy = lb, *pfz = lb;
+    if constexpr (OCT) {
+        pnx = lb + r.onx; pfx = lb + (r.onx ^ 12u);
+        pny = lb + r.ony; pfy = lb + (r.ony ^ 20u);
+        pnz = lb + r.onz; pfz = lb + (r.onz ^ 28u);
+    }
+    // one node visit: test both children, continue with the nearer, push the farther
+    auto visit = [&](int node) -> int {
+        if (C::COUNT) cnt.nodes++;
+        if constexpr (OCT) {
+            const int o = node * 64;
+            auto plane = [&](const char* p, int child) { return *reinterpret_cast<const float*>(p + o + 24 * child); };
+            const int2 ch = *reinterpret_cast<const int2*>(lb + o + 48);
+            float tn[2], tf[2];
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+                const float nx = __builtin_fmaf(plane(pnx, c), r.fix, r.fox);
+                const float ny = __builtin_fmaf(plane(pny, c), r.fiy, r.foy);
+                const float nz = __builtin_fmaf(plane(pnz, c), r.fiz, r.foz);
+                const float fx = __builtin_fmaf(plane(pfx, c), r.fix, r.fox);
+                const float fy = __builtin_fmaf(plane(pfy, c), r.fiy, r.foy);
+                const float fz = __builtin_fmaf(plane(pfz, c), r.fiz, r.foz);
+                tn[c] = fmaxf(fmaxf(nx, ny), fmaxf(nz, tmin_f));
+                tf[c] = fminf(fminf(fx, fy), fminf(fz, tmax_f));
+            }
+            const bool h0 = tn[0] <= tf[0], h1 = tn[1] <= tf[1], near0 = tn[0] <= tn[1];
+            if (h0 && h1) {
+                stack[sp++] = near0 ? ch.y : ch.x;
+                return near0 ? ch.x : ch.y;
+            }
+            if (h0) return ch.x;
+            if (h1) return ch.y;
+            return sp == sp0 ? RT_DONE : stack[--sp];
+        }
+        const Node nd = (NL && (C::NALL || node < S.n_lds_nodes)) ? load_node(lds_nodes, node)
+                                                                  : load_node(S.nodes, node);
+        bool h0, h1, near0;
+        if constexpr (C::S32) {
+            float tn0, tn1;
+            h0 = slab32(nd.lo0, nd.hi0, r, tmin_f, tmax_f, tn0);
+            h1 = slab32(nd.lo1, nd.hi1, r, tmin_f, tmax_f, tn1);
+            near0 = tn0 <= tn1;
+        } else {
+            double tn0, tn1;
+            h0 = slab(nd.lo0, nd.hi0, r, t_min, t_max, tn0);
+            h1 = slab(nd.lo1, nd.hi1, r, t_min, t_max, tn1);
+            near0 = tn0 <= tn1;
+        }
+        if (h0 && h1) {
+            stack[sp++] = near0 ? nd.child[1] : nd.child[0];
+            return near0 ? nd.child[0] : nd.child[1];
+        }
+        if (h0) return nd.child[0];
+        if (h1) return nd.child[1];
+        return sp == sp0 ? RT_DONE : stack[--sp];
+    };
+    auto do_leaf = [&](int code) {
+        code = ~code;
+        const int first = code >> 5, count = code & 31;
+        for (int i = 0; i < count; ++i) {
+            if (C::COUNT && first_active_lane()) cnt.wave_leaves++;
+            const int slot = first + i;
+            if (leaf(slot, t_max, best)) {
+                best.prim = slot;
+                t_max = best.t;
+                any = true;
+                if constexpr (C::S32) tmax_f = f32_up(t_max);
+            }
+        }
+    };
+    if constexpr (C::LOOP == 0) {
+        while (cur != RT_DONE) {
+            if (cur < 0) {
+                do_leaf(cur);
+                cur = sp == sp0 ? RT_DONE : stack[--sp];
+            } else {
+                cur = visit(cur);
+            }
+        }
+    } else if constexpr (C::LOOP == 1) {
+        uint64_t t0 = 0;
+        while (cur != RT_DONE) {
+            if (C::COUNT) t0 = __builtin_amdgcn_s_memtime();
+            while (cur >= 0) {
+                if (C::COUNT && first_active_lane()) cnt.wave_nodes++;
+                cur = visit(cur);
+            }
+            if (C::COUNT) { const uint64_t t = __builtin_amdgcn_s_memtime(); cnt.t_nodes += t - t0; t0 = t; }
+            if (cur == RT_DONE) break;
+            do_leaf(cur);
+            if (C::COUNT) cnt.t_leaves += __builtin_amdgcn_s_memtime() - t0;
+            cur = sp == sp0 ? RT_DONE : stack[--sp];
+        }
+    } else {
+        // Speculative while-while (Aila & Laine 2009, §4): a lane that reaches a leaf parks
+        // it and keeps visiting nodes until every lane still in the node loop holds one,
+        // so the node loop runs with more lanes busy; then each lane tests one leaf.
+        int parked = 0;  // 0: none; else a leaf code (< 0, never RT_DONE)
+        for (;;) {
+            while (cur >= 0) {
+                if (C::COUNT && first_active_lane()) cnt.wave_nodes++;
+                cur = visit(cur);
+                if (cur < 0 && cur != RT_DONE && parked == 0) {
+                    parked = cur;
+                    cur = sp == sp0 ? RT_DONE : stack[--sp];
+                }
+                if (__all(parked != 0)) break;
+            }
+            int lf;
+            if (parked != 0) {
+                lf = parked;
+                parked = 0;
+            } else if (cur != RT_DONE && cur < 0) {
+                lf = cur;
+                cur = sp == sp0 ? RT_DONE : stack[--sp];
+            } else if (cur == RT_DONE) {
+                break;
+            } else {
+                continue;
+            }
+            do_leaf(lf);
+        }
+    }
+    return any;
+}
+
+// ---------------------------------------------------------------------------
+// Translate / RotateY instances (hittable.rs:232-244, 386-415), outermost op first
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void instance_ray(const rt_instance& in, Ray& r)
+{
+    const int n = in.n_ops;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        if (i < n) {
+            if (in.op_kind[i] == RT_OP_TRANSLATE) {  // moved_ray = (o - offset, d, time)
+                r.ox = r.ox - in.op[i][0];
+                r.oy = r.oy - in.op[i][1];
+                r.oz = r.oz - in.op[i][2];
+            } else {                                  // rotated_ray
+                const double s = in.op[i][0], c = in.op[i][1];
+                const double ox = c * r.ox - s * r.oz, oz = s * r.ox + c * r.oz;
+                const double dx = c * r.dx - s * r.dz, dz = s * r.dx + c * r.dz;
+                r.ox = ox; r.oz = oz; r.dx = dx; r.dz = dz;
+            }
+        }
+    }
+}
+
+// t-only: the closest hit of the instance's child; sub = BLAS prim (or the child prim),
+// side = winning box side.
+template <class C>
+__device__ bool instance_t(const SceneDev& S, const rt_instance& in, const Ray& ray, double t_min, double t_max,
+                           HitRef& ref, StackT<C>& stack, int sp0, Count& cnt)
+{
+    Ray r = ray;
+    instance_ray(in, r);
+    finish_ray<C>(r, S.has_spheres != 0);
+    if (in.child_kind == RT_CHILD_PRIM) {
+        int side = 0;
+        if (!simple_t<C>(S.prims[in.child], r, t_min, t_max, ref.t, side, cnt)) return false;
+        ref.sub = in.child;
+        ref.side = side;
+        return true;
+    }
+    HitRef inner;
+    if (!traverse<C>(S, in.child, r, t_min, t_max, inner, stack, sp0, cnt,
+                     [&](int slot, double tmax, HitRef& b) {
+                         return simple_t<C>(S.leaf_prims[slot], r, t_min, tmax, b.t, b.side, cnt);
+                     }))
+        return false;
+    ref.t = inner.t;
+    ref.sub = inner.prim;
+    ref.side = inner.side;
+    return true;
+}
+
+// The ray direction after ops 0..i (only RotateY changes it; y never changes): recomputed
+// per op on the way back instead of kept in arrays through the child's finisher, which
+// held 8 f64 registers live and pushed the instance variants into scratch spills.
+__device__ __forceinline__ void dir_after(const rt_instance& in, const Ray& ray, int i, double& dx, double& dz)
+{
+    dx = ray.dx;
+    dz = ray.dz;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        if (j <= i && j < in.n_ops && in.op_kind[j] != RT_OP_TRANSLATE) {
+            const double s = in.op[j][0], c = in.op[j][1];
+            const double x = c * dx - s * dz, z = s * dx + c * dz;
+            dx = x;
+            dz = z;
+        }
+    }
+}
+
+template <class C>
+__device__ void instance_finish(const SceneDev& S, const rt_instance& in, const Ray& ray, const HitRef& ref, Hit& h)
+{
+    Ray r = ray;
+    instance_ray(in, r);
+    // ref.sub: the child prim (RT_CHILD_PRIM) or the BLAS leaf slot
+    simple_finish<C>(in.child_kind == RT_CHILD_PRIM ? S.prims[ref.sub] : S.leaf_prims[ref.sub], r, ref.t, ref.side,
+                     h);
+    const int n = in.n_ops;
+#pragma unroll
+    for (int i = 3; i >= 0; --i) {
+        if (i < n) {
+            double dx, dz;
+            dir_after(in, ray, i, dx, dz);
+            if (in.op_kind[i] == RT_OP_TRANSLATE) {  // rec.point += offset; set_face_normal(moved_ray, normal)
+                h.px = h.px + in.op[i][0];
+                h.py = h.py + in.op[i][1];
+                h.pz = h.pz + in.op[i][2];
+                set_face_normal(h, dx, ray.dy, dz, h.nx, h.ny, h.nz);
+            } else {                                  // rotate back; set_face_normal(rotated_ray, normal)
+                const double s = in.op[i][0], c = in.op[i][1];
+                const double px = c * h.px + s * h.pz, pz = -s * h.px + c * h.pz;
+                const double nx = c * h.nx + s * h.nz, nz = -s * h.nx + c * h.nz;
+                h.px = px; h.pz = pz;
+                set_face_normal(h, dx, ray.dy, dz, nx, h.ny, nz);
+            }
+        }
+    }
+}
+
+// t of a medium boundary (a simple prim or an instance).
+template <class C>
+__device__ __forceinline__ bool boundary_t(const SceneDev& S, int prim, const Ray& r, double t_min, double t_max,
+                                           double& t, StackT<C>& stack, int sp0, Count& cnt)
+{
+    const rt_prim& p = S.prims[prim];
+    if constexpr ((C::F & FEAT_INST) != 0) {
+        if (p.kind == RT_PRIM_INSTANCE) {
+            HitRef ref;
+            if (!instance_t<C>(S, S.instances[p.a], r, t_min, t_max, ref, stack, sp0, cnt)) return false;
+            t = ref.t;
+            return true;
+        }
+    }
+    int side = 0;
+    return simple_t<C>(p, r, t_min, t_max, t, side, cnt);
+}
+
+// ConstantMedium (hittable.rs:417-473), keyed draw instead of the in-hit thread_rng().
+template <class C>
+__device__ bool medium_t(const SceneDev& S, const rt_prim& m, const Ray& r, double t_min, double t_max, double& t,
+                         StackT<C>& stack, int sp0, const Keyed& key, Count& cnt)
+{
+    double t1, t2;
+    if (!boundary_t<C>(S, m.a, r, -RT_INF, RT_INF, t1, stack, sp0, cnt)) return false;
+    if (!boundary_t<C>(S, m.a, r, t1 + 0.0001, RT_INF, t2, stack, sp0, cnt)) return false;
+    if (t1 < t_min) t1 = t_min;
+    if (t2 > t_max) t2 = t_max;
+    if (t1 >= t2) return false;
+    if (t1 < 0.0) t1 = 0.0;
+    const double ray_length = __builtin_sqrt(r.a);
+    const double distance_inside = (t2 - t1) * ray_length;
+    const double xi = rt_unit53(rt_keyed_u64(key.seed, key.pixel, key.sample, key.bounce,
+                                             RT_STREAM_MEDIUM + (uint32_t)m.b));
+    const double hit_distance = m.p[0] * rt_log(xi);
+    if (hit_distance > distance_inside) return false;
+    t = t1 + hit_distance / ray_length;
+    return true;
+}
+
+// hittable.rs:452-463
+__device__ __forceinline__ void medium_finish(const rt_prim& m, const Ray& r, double t, Hit& h)
+{
+    h.t = t;
+    h.px = r.ox + r.dx * t;
+    h.py = r.oy + r.dy * t;
+    h.pz = r.oz + r.dz * t;
+    h.nx = 1.0; h.ny = 0.0; h.nz = 0.0;
+    h.front = 1;
+    h.mat = m.mat;
+    h.uvkind = 0;
+}
+
+// hit_hittables(world, ray, 0.001, inf) (hittable.rs:43-55) over the TLAS, then the
+// HitRecord of the closest primitive.
+template <class C>
+__device__ bool trace_world(const SceneDev& S, const Ray& r, Hit& h, StackT<C>& stack, const Keyed& key,
+                            Count& cnt)
+{
+    const double t_min = 0.001;
+    HitRef best;
+    best.sub = 0;
+    best.side = 0;
+    auto leaf = [&](int slot, double tmax, HitRef& b) {
+        const rt_prim& p = S.leaf_prims[slot];
+        if constexpr ((C::F & FEAT_INST) != 0)
+            if (p.kind == RT_PRIM_INSTANCE)
+                return instance_t<C>(S, S.instances[p.a], r, t_min, tmax, b, stack, S.blas_base, cnt);
+        if constexpr ((C::F & FEAT_MEDIUM) != 0)
+            if (p.kind == RT_PRIM_MEDIUM) return medium_t<C>(S, p, r, t_min, tmax, b.t, stack, S.blas_base, key, cnt);
+        return simple_t<C>(p, r, t_min, tmax, b.t, b.side, cnt);
+    };
+    const bool hit = traverse<C, true>(S, S.tlas_root, r, t_min, RT_INF, best, stack, 0, cnt, leaf);
+    if (!hit) return false;
+    const rt_prim& p = S.leaf_prims[best.prim];
+    if constexpr ((C::F & FEAT_INST) != 0) {
+        if (p.kind == RT_PRIM_INSTANCE) {
+            instance_finish<C>(S, S.instances[p.a], r, best, h);
+            return true;
+        }
+    }
+    if constexpr ((C::F & FEAT_MEDIUM) != 0) {
+        if (p.kind == RT_PRIM_MEDIUM) {
+            medium_finish(p, r, best.t, h);
+            return true;
+        }
+    }
+    simple_finish<C>(p, r, best.t, best.side, h);
+    return true;
+}
+
+// ---------------------------------------------------------------------------
+// appearance: texture.rs:30-75, perlin.rs:32-108, material.rs:15-94
+// ---------------------------------------------------------------------------
+__device__ double perlin_noise(const double* ranvec, const int32_t* perm, double px, double py, double pz)
+{
+    const double fx = __builtin_floor(px), fy = __builtin_floor(py), fz = __builtin_floor(pz);
+    double u = px - fx, v = py - fy, w = pz - fz;
+    u = u * u * (3.0 - 2.0 * u);
+    v = v * v * (3.0 - 2.0 * v);
+    w = w * w * (3.0 - 2.0 * w);
+    const int32_t i = rt_sat_i32(fx), j = rt_sat_i32(fy), k = rt_sat_i32(fz);
+    const double uu = u * u * (3.0 - 2.0 * u);
+    const double vv = v * v * (3.0 - 2.0 * v);
+    const double ww = w * w * (3.0 - 2.0 * w);
+    double accum = 0.0;
+#pragma unroll
+    for (int di = 0; di < 2; ++di)
+#pragma unroll
+        for (int dj = 0; dj < 2; ++dj)
+#pragma unroll
+            for (int dk = 0; dk < 2; ++dk) {
+                const uint32_t xi = ((uint32_t)i + (uint32_t)di) & 255u;
+                const uint32_t yi = ((uint32_t)j + (uint32_t)dj) & 255u;
+                const uint32_t zi = ((uint32_t)k + (uint32_t)dk) & 255u;
+                const uint32_t idx = (uint32_t)(perm[xi] ^ perm[256 + yi] ^ perm[512 + zi]) & 255u;
+                const double cx = ranvec[3 * idx], cy = ranvec[3 * idx + 1], cz = ranvec[3 * idx + 2];
+                const double fi = (double)di, fj = (double)dj, fk = (double)dk;
+                const double wx = u - fi, wy = v - fj, wz = w - fk;
+                accum += (fi * uu + (1.0 - fi) * (1.0 - uu)) * (fj * vv + (1.0 - fj) * (1.0 - vv)) *
+                         (fk * ww + (1.0 - fk) * (1.0 - ww)) * (cx * wx + cy * wy + cz * wz);
+            }
+    return accum;
+}
+
+__device__ double perlin_turb(const double* ranvec, const int32_t* perm, double px, double py, double pz)
+{
+    double accum = 0.0, weight = 1.0;
+    for (int i = 0; i < 7; ++i) {
+        accum += weight * perlin_noise(ranvec, perm, px, py, pz);
+        weight *= 0.5;
+        px = px * 2.0;
+        py = py * 2.0;
+        pz = pz * 2.0;
+    }
+    return __builtin_fabs(accum);
+}
+
+__device__ __forceinline__ double clampd(double x, double mn, double mx)
+{
+    if (x < mn) return mn;
+    if (x > mx) return mx;
+    return x;
+}
+
+__device__ void hit_uv(const Hit& h, double& u, double& v)
+{
+    if (h.uvkind == 1) {  // sphere_uv (math.rs:288-300)
+        const double theta = rt_acos(-h.uv1);
+        const double phi = rt_atan2(-h.uv2, h.uv0) + RT_PI;
+        u = phi / (2.0 * RT_PI);
+        v = theta / RT_PI;
+    } else if (h.uvkind == 2) {
+        u = h.uv0 / h.uv1;
+        v = h.uv2 / h.uv3;
+    } else {
+        u = 0.0;
+        v = 0.0;
+    }
+}
+
+// texture.rs:35-41: sin(10x)*sin(10y)*sin(10z) < 0 from the three signs (rt_sin_sign);
+// the full product only when a factor may be tiny enough to underflow it
+__device__ __forceinline__ bool checker_odd(const Hit& h)
+{
+#ifdef RT_PROBE_NO_CHECKER  // timing probe: NOT the product
+    return h.px * h.pz < 0.0;
+#endif
+    const double ax = 10.0 * h.px, ay = 10.0 * h.py, az = 10.0 * h.pz;
+    const int sx = rt_sin_sign(ax), sy = rt_sin_sign(ay), sz = rt_sin_sign(az);
+    if (sx == 2 || sy == 2 || sz == 2) return rt_sin(ax) * rt_sin(ay) * rt_sin(az) < 0.0;
+    return sx * sy * sz < 0;
+}
+
+template <class C>
+__device__ void tex_value(const SceneDev& S, int ti, const Hit& h, double& cr, double& cg, double& cb)
+{
+    const rt_texture& t = S.textures[ti];
+    if constexpr (!(C::F & (FEAT_NOISE | FEAT_IMAGE))) {
+        if (t.kind == RT_TEX_CHECKER) {
+            const double* c = checker_odd(h) ? t.c1 : t.c0;
+            cr = c[0]; cg = c[1]; cb = c[2];
+        } else {
+            cr = t.c0[0]; cg = t.c0[1]; cb = t.c0[2];
+        }
+        return;
+    }
+    switch (t.kind) {
+    case RT_TEX_SOLID: cr = t.c0[0]; cg = t.c0[1]; cb = t.c0[2]; return;
+    case RT_TEX_CHECKER: {
+        if (checker_odd(h)) { cr = t.c1[0]; cg = t.c1[1]; cb = t.c1[2]; }
+        else { cr = t.c0[0]; cg = t.c0[1]; cb = t.c0[2]; }
+        return;
+    }
+    case RT_TEX_NOISE: {
+        const double* rv = S.perlin_ranvec + (size_t)t.perlin * 768;
+        const int32_t* pm = S.perlin_perm + (size_t)t.perlin * 768;
+        const double s = 1.0 + rt_sin(t.scale * h.pz + 10.0 * perlin_turb(rv, pm, h.px, h.py, h.pz));
+        const double c = 1.0 * 0.5 * s;
+        cr = c; cg = c; cb = c;
+        return;
+    }
+    default: {
+        if (t.img_w <= 0 || t.img_h <= 0) { cr = 0.0; cg = 1.0; cb = 1.0; return; }
+        double u, v;
+        hit_uv(h, u, v);
+        u = clampd(u, 0.0, 1.0);
+        v = 1.0 - clampd(v, 0.0, 1.0);
+        uint64_t i = rt_sat_u64(u * (double)t.img_w);
+        uint64_t j = rt_sat_u64(v * (double)t.img_h);
+        if (i >= (uint64_t)t.img_w) i = (uint64_t)t.img_w - 1;
+        if (j >= (uint64_t)t.img_h) j = (uint64_t)t.img_h - 1;
+        const uint8_t* px = S.image + t.img_offset + j * (uint64_t)t.img_bps + i * 3;
+        const double color_scale = 1.0 / 255.0;
+        cr = color_scale * (double)px[0];
+        cg = color_scale * (double)px[1];
+        cb = color_scale * (double)px[2];
+        return;
+    }
+    }
+}
+
+// The path stream of rt_numerics.h (rt_pstream): one Philox block of (pixel, sample) seeds
+// a xoshiro128++ state, from which the path draws in the reference's order.
+__device__ __forceinline__ void ds_start(rt_pstream& st, uint64_t seed, uint32_t pixel, uint32_t sample)
+{
+#ifdef RT_EXPERIMENT_CHEAP_RNG  // timing probe of the seeding's share: NOT the product's stream
+    st.s0 = pixel * 0x9E3779B1u ^ sample; st.s1 = sample * 0x85EBCA77u ^ pixel; st.s2 = ~pixel; st.s3 = (uint32_t)seed;
+    return;
+#endif
+    rt_pstream_init(&st, seed, pixel, sample);
+}
+__device__ __forceinline__ uint64_t ds_u64(rt_pstream& st) { return rt_pstream_u64(&st); }
+
+// math.rs:51-58: random_double_range(-1, 1) x 3 until inside
+__device__ __forceinline__ void random_in_unit_sphere(rt_pstream& st, double scale_m11, double& x, double& y,
+                                                      double& z, double& len2)
+{
+    for (;;) {
+        x = rt_uniform_sample(ds_u64(st), -1.0, scale_m11);
+        y = rt_uniform_sample(ds_u64(st), -1.0, scale_m11);
+        z = rt_uniform_sample(ds_u64(st), -1.0, scale_m11);
+        len2 = x * x + y * y + z * z;
+        if (len2 < 1.0) return;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// the integrator
+// ---------------------------------------------------------------------------
+
+// main.rs:517-520 + Camera::get_ray (camera.rs:58-66)
+__device__ __forceinline__ void camera_ray(const KParams& P, int x, int y, rt_pstream& st, Ray& r)
+{
+#ifdef RT_PROBE_FAST_CAMERA  // timing probe: NOT the product
+    const double u = ((double)x + rt_unit53(ds_u64(st))) * __builtin_amdgcn_rcp((double)P.width - 1.0);
+    const double v = ((double)y + rt_unit53(ds_u64(st))) * __builtin_amdgcn_rcp((double)P.height - 1.0);
+#else
+    const double u = div_rcp((double)x + rt_unit53(ds_u64(st)), P.wm1, P.inv_wm1);
+    const double v = div_rcp((double)y + rt_unit53(ds_u64(st)), P.hm1, P.inv_hm1);
+#endif
+    double dxl, dyl;
+    for (;;) {
+        dxl = rt_uniform_sample(ds_u64(st), -1.0, P.scale_m11);
+        dyl = rt_uniform_sample(ds_u64(st), -1.0, P.scale_m11);
+        if (dxl * dxl + dyl * dyl + 0.0 * 0.0 < 1.0) break;
+    }
+    const double rdx = dxl * P.cam.lens_radius, rdy = dyl * P.cam.lens_radius;
+    const double offx = P.cam.u[0] * rdx + P.cam.v[0] * rdy;
+    const double offy = P.cam.u[1] * rdx + P.cam.v[1] * rdy;
+    const double offz = P.cam.u[2] * rdx + P.cam.v[2] * rdy;
+    r.ox = P.cam.origin[0] + offx;
+    r.oy = P.cam.origin[1] + offy;
+    r.oz = P.cam.origin[2] + offz;
+    r.dx = P.cam.lower_left_corner[0] + P.cam.horizontal[0] * u + P.cam.vertical[0] * v - P.cam.origin[0] - offx;
+    r.dy = P.cam.lower_left_corner[1] + P.cam.horizontal[1] * u + P.cam.vertical[1] * v - P.cam.origin[1] - offy;
+    r.dz = P.cam.lower_left_corner[2] + P.cam.horizontal[2] * u + P.cam.vertical[2] * v - P.cam.origin[2] - offz;
+    r.time = rt_uniform_sample(ds_u64(st), P.cam.time0, P.scale_time);
+}
+
+// One hit of ray_color (main.rs:25-34): emitted + attenuation * (next), with the
+// recursion unrolled into the throughput T. A path carries at most one emission (a
+// DiffuseLight ends it), so adding T*e straight into the chunk sum gives the same bits
+// as the reference's per-sample sum. Returns true if the path continues with r.
+template <class C>
+__device__ __forceinline__ bool shade(const SceneDev& S, const KParams& P, const Hit& h, Ray& r, rt_pstream& st,
+                                      double& Tr, double& Tg, double& Tb, double& sum_r, double& sum_g,
+                                      double& sum_b)
+{
+    const rt_material& m = S.materials[h.mat];
+    const int kind = m.kind;
+    if (kind == RT_MAT_DIFFUSE_LIGHT) {  // material.rs:25-34 (emits on both faces, never scatters)
+        double er, eg, eb;
+        tex_value<C>(S, m.tex, h, er, eg, eb);
+        sum_r = sum_r + Tr * er;
+        sum_g = sum_g + Tg * eg;
+        sum_b = sum_b + Tb * eb;
+        return false;
+    }
+    // The materials share their expensive steps, so a wave holding several materials runs
+    // each once: one unit-sphere loop (Lambertian, Metal, Isotropic), one 1/sqrt (of the
+    // candidate for Lambertian, of the ray direction for Metal and Dielectric), one texture
+    // lookup (Lambertian, Isotropic).
+    double qx = 0.0, qy = 0.0, qz = 0.0, l2 = 1.0;
+    if (kind != RT_MAT_DIELECTRIC) random_in_unit_sphere(st, P.scale_m11, qx, qy, qz, l2);
+#ifdef RT_PROBE_FAST_SHADE  // timing probe: NOT the product
+    const double inv = __builtin_amdgcn_rsq(kind == RT_MAT_LAMBERTIAN ? l2 : r.a);
+#else
+    const double inv = 1.0 / __builtin_sqrt(kind == RT_MAT_LAMBERTIAN ? l2 : r.a);
+#endif
+    double sdx, sdy, sdz, ar = 1.0, ag = 1.0, ab = 1.0;
+    bool scattered = true;
+    if (kind == RT_MAT_LAMBERTIAN) {  // material.rs:36-48
+        sdx = h.nx + qx * inv;
+        sdy = h.ny + qy * inv;
+        sdz = h.nz + qz * inv;
+        if (__builtin_fabs(sdx) < 1e-8 && __builtin_fabs(sdy) < 1e-8 && __builtin_fabs(sdz) < 1e-8) {
+            sdx = h.nx; sdy = h.ny; sdz = h.nz;
+        }
+    } else if (kind == RT_MAT_METAL || kind == RT_MAT_DIELECTRIC) {
+        const double ux = r.dx * inv, uy = r.dy * inv, uz = r.dz * inv;  // normalize(r_in.direction)
+        if (kind == RT_MAT_METAL) {  // material.rs:50-60
+            const double k2 = 2.0 * (ux * h.nx + uy * h.ny + uz * h.nz);
+            sdx = (ux - h.nx * k2) + qx * m.fuzz;
+            sdy = (uy - h.ny * k2) + qy * m.fuzz;
+            sdz = (uz - h.nz * k2) + qz * m.fuzz;
+            scattered = sdx * h.nx + sdy * h.ny + sdz * h.nz > 0.0;
+            ar = m.albedo[0]; ag = m.albedo[1]; ab = m.albedo[2];
+        } else {  // material.rs:62-82, 89-94
+            const double ratio = h.front ? (1.0 / m.ir) : m.ir;
+            const double cos_theta = fmin((-ux) * h.nx + (-uy) * h.ny + (-uz) * h.nz, 1.0);
+            const double sin_theta = __builtin_sqrt(1.0 - cos_theta * cos_theta);
+            const bool cannot_refract = ratio * sin_theta > 1.0;
+            bool reflect = cannot_refract;
+            if (!reflect) {  // the draw is skipped on TIR (the || short-circuit of material.rs:72)
+                double r0 = (1.0 - ratio) / (1.0 + ratio);
+                r0 = r0 * r0;
+                const double refl = r0 + (1.0 - r0) * rt_pow5(1.0 - cos_theta);
+                reflect = refl > rt_unit53(ds_u64(st));
+            }
+            if (reflect) {
+                const double k2 = 2.0 * (ux * h.nx + uy * h.ny + uz * h.nz);
+                sdx = ux - h.nx * k2;
+                sdy = uy - h.ny * k2;
+                sdz = uz - h.nz * k2;
+            } else {  // math.rs:110-117 (cos_theta recomputed there from the same inputs)
+                const double px = (ux + h.nx * cos_theta) * ratio;
+                const double py = (uy + h.ny * cos_theta) * ratio;
+                const double pz = (uz + h.nz * cos_theta) * ratio;
+                const double pl = px * px + py * py + pz * pz;
+                const double kk = -__builtin_sqrt(__builtin_fabs(1.0 - pl));
+                sdx = px + h.nx * kk;
+                sdy = py + h.ny * kk;
+                sdz = pz + h.nz * kk;
+            }
+        }
+    } else {  // isotropic, material.rs:84-87
+        sdx = qx; sdy = qy; sdz = qz;
+    }
+    if (!scattered) return false;  // emitted (0) only
+    if (kind == RT_MAT_LAMBERTIAN || kind == RT_MAT_ISOTROPIC) tex_value<C>(S, m.tex, h, ar, ag, ab);
+    Tr = Tr * ar;
+    Tg = Tg * ag;
+    Tb = Tb * ab;
+    r.ox = h.px; r.oy = h.py; r.oz = h.pz;
+    r.dx = sdx; r.dy = sdy; r.dz = sdz;
+    finish_ray<C>(r, S.has_spheres != 0);
+    return true;
+}
+
+// lane -> (chunk, pixel): a wave64 owns an 8x8 tile of one chunk
+struct LaneWork {
+    int x, y, k, chunk, s_begin, s_end;
+    uint32_t pixel;
+};
+__device__ __forceinline__ bool lane_work(const KParams& P, LaneWork& w)
+{
+    const int lane = threadIdx.x & 63;
+    const long long wave = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const long long n_tiles = (long long)P.tiles_x * P.tiles_y;
+    if (wave >= n_tiles * P.n_chunks) return false;
+    w.chunk = (int)(wave / n_tiles);
+    const int tile = (int)(wave % n_tiles);
+    w.x = (tile % P.tiles_x) * 8 + (lane & 7);
+    w.k = (tile / P.tiles_x) * 8 + (lane >> 3);
+    if (w.x >= P.width || w.k >= P.n_rows) return false;
+    w.y = P.row_begin + w.k * P.row_stride;
+    w.pixel = (uint32_t)w.y * (uint32_t)P.width + (uint32_t)w.x;
+    w.s_begin = P.sample_begin + w.chunk * P.spp_chunk;
+    w.s_end = min(P.spp, w.s_begin + P.spp_chunk);
+    return true;
+}
+
+// LOOP 0/1: every lane traces its cast to the end, then every lane shades.
+#ifndef RT_MIN_WAVES_SPHERES
+#define RT_MIN_WAVES_SPHERES 1
+#endif
+#ifndef RT_MIN_WAVES_RECTINST
+// measured (Cornell 800x800x200): chunk schedule 4 waves 190 vs 202 ms; pool schedule 4: 80.7,
+// 3: 81.0; after the reciprocal divisions (more live state, 4 waves spilled to scratch):
+// 4: 66.6, 3: 58.6
+#define RT_MIN_WAVES_RECTINST 3
+#endif
+#ifndef RT_MIN_WAVES_ALL
+// measured, pool schedule: final scene 960x540x200 4: 112.0 ms (scratch spills: 0.7 TB of HBM
+// writes per launch), 3: 102.8, 2: 131.5; cornell smoke 600x600x200 4: 74.1, 3: 62.3, 2: 79.7
+#define RT_MIN_WAVES_ALL 3
+#endif
+#ifndef RT_MIN_WAVES_MEDIA
+#define RT_MIN_WAVES_MEDIA 3
+#endif
+// minimum waves per SIMD requested from the register allocator, per feature set
+template <class C>
+constexpr int min_waves()
+{
+    return C::F == FEAT_SET_SPHERES ? RT_MIN_WAVES_SPHERES
+           : C::F == FEAT_SET_RECTINST ? RT_MIN_WAVES_RECTINST
+           : C::F == FEAT_SET_MEDIA    ? RT_MIN_WAVES_MEDIA : RT_MIN_WAVES_ALL;
+}
+
+// KParams comes by pointer: read where used (scalar loads) instead of pinning ~70 SGPRs
+// for the whole kernel (by value it spilled SGPRs into VGPR lanes).
+template <class C>
+__global__ void __launch_bounds__(256, min_waves<C>()) trace_chunks(SceneDev S, const KParams* __restrict__ Pp,
+                                                                    double* __restrict__ partial,
+                                                                    unsigned long long* __restrict__ counters)
+{
+    const KParams& P = *Pp;
+    if (S.n_lds_nodes > 0) {  // every thread of the block takes part, before any early return
+        const int off = C::LDS ? S.stack_entries * 256 : 0;
+        uint4* dst = reinterpret_cast<uint4*>(rt_lds + off);
+        const uint4* src = reinterpret_cast<const uint4*>(S.nodes);
+        for (int i = threadIdx.x; i < S.n_lds_nodes * 4; i += 256) dst[i] = src[i];
+        __syncthreads();
+    }
+    LaneWork w;
+    if (!lane_work(P, w)) return;
+    StackT<C> stack;
+    if constexpr (C::LDS) stack.base = rt_lds + threadIdx.x;
+    Count cnt{};
+    uint64_t t_cam = 0, t_trace = 0, t_shade = 0, t_prev = 0;
+    if (C::COUNT) t_prev = __builtin_amdgcn_s_memtime();
+    double sum_r = 0.0, sum_g = 0.0, sum_b = 0.0;
+    Keyed key{P.seed, w.pixel, 0, 0};
+    rt_pstream st;
+    Ray r;
+    double Tr = 1, Tg = 1, Tb = 1;
+    int depth = 0;
+    int s = w.s_begin;
+    bool new_sample = true;
+    while (s < w.s_end) {
+        if (C::COUNT && first_active_lane()) cnt.wave_steps++;
+        if (new_sample) {
+            new_sample = false;
+            ds_start(st, P.seed, w.pixel, (uint32_t)s);
+            key.sample = (uint32_t)s;
+            camera_ray(P, w.x, w.y, st, r);
+            finish_ray<C>(r, S.has_spheres != 0);
+            Tr = Tg = Tb = 1.0;
+            depth = P.max_depth;
+        }
+        if (C::COUNT) { const uint64_t t = __builtin_amdgcn_s_memtime(); t_cam += t - t_prev; t_prev = t; }
+        bool cont = false;
+        if (depth > 0) {  // main.rs:21-23: depth 0 is black
+            key.bounce = (uint32_t)(P.max_depth - depth);
+            if (C::COUNT) cnt.casts++;
+            Hit h;
+            const bool hit = trace_world<C>(S, r, h, stack, key, cnt);
+            if (C::COUNT) { const uint64_t t = __builtin_amdgcn_s_memtime(); t_trace += t - t_prev; t_prev = t; }
+            if (!hit) {  // main.rs:37: background
+                sum_r = sum_r + Tr * P.bg[0];
+                sum_g = sum_g + Tg * P.bg[1];
+                sum_b = sum_b + Tb * P.bg[2];
+            } else {
+                cont = shade<C>(S, P, h, r, st, Tr, Tg, Tb, sum_r, sum_g, sum_b);
+            }
+        }
+        if (C::COUNT) { const uint64_t t = __builtin_amdgcn_s_memtime(); t_shade += t - t_prev; t_prev = t; }
+        if (cont) {
+            depth -= 1;
+        } else {
+            s += 1;
+            new_sample = true;
+        }
+    }
+    double* o = partial + (((size_t)w.chunk * P.n_rows + w.k) * P.width + w.x) * 3;
+    o[0] = sum_r;
+    o[1] = sum_g;
+    o[2] = sum_b;
+    if (C::COUNT) {
+        atomicAdd(&counters[0], (unsigned long long)cnt.casts);
+        atomicAdd(&counters[1], (unsigned long long)cnt.nodes);
+        atomicAdd(&counters[2], (unsigned long long)cnt.prims);
+        atomicAdd(&counters[6], (unsigned long long)cnt.wave_steps);
+        atomicAdd(&counters[7], (unsigned long long)cnt.wave_nodes);
+        atomicAdd(&counters[10], (unsigned long long)cnt.wave_leaves);
+        atomicAdd(&counters[11], (unsigned long long)cnt.cam_lanes);
+        atomicAdd(&counters[12], (unsigned long long)cnt.cam_steps);
+        atomicAdd(&counters[13], (unsigned long long)cnt.shade_lanes);
+        atomicAdd(&counters[14], (unsigned long long)cnt.shade_steps);
+        // phase times are per wave (every active lane sees the same clock): one lane adds
+        if ((int)(threadIdx.x & 63) == __ffsll((long long)__ballot(1)) - 1) {
+            atomicAdd(&counters[3], (unsigned long long)t_cam);
+            atomicAdd(&counters[4], (unsigned long long)t_trace);
+            atomicAdd(&counters[5], (unsigned long long)t_shade);
+            atomicAdd(&counters[8], (unsigned long long)cnt.t_nodes);
+            atomicAdd(&counters[9], (unsigned long long)cnt.t_leaves);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Sample-pool schedule. Persistent waves take work blocks (one 8x8 tile x one chunk of
+// samples) from a global counter; inside the wave, a lane whose path ended takes the
+// block's next (pixel, sample) unit at once (ballot + mbcnt), so lanes do not idle until
+// the last blocks run out. Each sample's radiance goes to its own slot of a
+// [sample][pixel] buffer; reduce_samples then sums every pixel's samples in sample order,
+// so the image does not depend on which lane or wave computed a sample.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ unsigned lanes_below(uint64_t mask)
+{
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+}
+
+// ITEMS (the item pool, default): a unit is a (pixel, chunk) item instead of one sample.
+// The lane that takes it traces the chunk's samples in order, summing their radiance in
+// registers exactly as trace_chunks does, and writes one partial per (pixel, chunk) when
+// the last one ends; a lane whose item ended takes the next item at once, as in the
+// per-sample pool, so lanes still do not idle. Output: chunk partials for
+// reduce_chunks, 1/chunk of the per-sample buffer's bytes.
+template <class C, bool ITEMS>
+__global__ void __launch_bounds__(256, min_waves<C>()) trace_pool(SceneDev S, const KParams* __restrict__ Pp,
+                                                                  double* __restrict__ samples,
+                                                                  unsigned long long* __restrict__ counters,
+                                                                  unsigned* __restrict__ work)
+{
+    const KParams& P = *Pp;
+    if (S.n_lds_nodes > 0) {
+        const int off = C::LDS ? S.stack_entries * 256 : 0;
+        uint4* dst = reinterpret_cast<uint4*>(rt_lds + off);
+        const uint4* src = reinterpret_cast<const uint4*>(S.nodes);
+        for (int i = threadIdx.x; i < S.n_lds_nodes * 4; i += 256) dst[i] = src[i];
+        __syncthreads();
+    }
+    StackT<C> stack;
+    if constexpr (C::LDS) stack.base = rt_lds + threadIdx.x;
+    Count cnt{};
+    uint64_t t_cam = 0, t_trace = 0, t_shade = 0, t_prev = 0;
+    if (C::COUNT) t_prev = __builtin_amdgcn_s_memtime();
+    const int lane = threadIdx.x & 63;
+    const unsigned n_tiles = (unsigned)P.tiles_x * (unsigned)P.tiles_y;
+    const unsigned n_blocks = n_tiles * (unsigned)P.n_chunks;
+    const size_t n_px = (size_t)P.n_rows * (size_t)P.width;
+    // current work block (wave-uniform)
+    unsigned blk_units = 0, blk_next = 0, nvalid = 1;
+    int tx0 = 0, tk0 = 0, vw = 1, s0 = 0;
+    bool exhausted = false;
+    // lane state
+    bool active = false, new_sample = false;
+    int x = 0, k = 0, s = 0, depth = 0;
+    int left = 0;      // ITEMS: samples of the lane's item still to trace after the current one
+    bool own = false;  // ITEMS: the lane's item has a next sample (taken before any new unit)
+    double cr = 0, cg = 0, cb = 0, Tr = 1, Tg = 1, Tb = 1;
+    Keyed key{P.seed, 0, 0, 0};
+    rt_pstream st;
+    Ray r;
+    for (;;) {
+        if (ITEMS && own) {
+            own = false;
+            active = true;
+            new_sample = true;
+            s += 1;
+            left -= 1;
+        }
+        uint64_t need = __ballot(!active);
+        while (need != 0 && !exhausted) {
+            if (blk_next == blk_units) {
+                unsigned b = 0;
+                if (lane == 0) b = atomicAdd(work, 1u);
+                b = __builtin_amdgcn_readfirstlane(b);
+                if (b >= n_blocks) {
+                    exhausted = true;
+                    break;
+                }
+                const unsigned chunk = b / n_tiles, tile = b - chunk * n_tiles;
+                tx0 = (int)(tile % (unsigned)P.tiles_x) * 8;
+                tk0 = (int)(tile / (unsigned)P.tiles_x) * 8;
+                vw = min(8, P.width - tx0);
+                nvalid = (unsigned)(vw * min(8, P.n_rows - tk0));
+                s0 = P.sample_begin + (int)chunk * P.spp_chunk;
+                blk_units = ITEMS ? nvalid : nvalid * (unsigned)(min(P.spp, s0 + P.spp_chunk) - s0);
+                blk_next = 0;
+            }
+            const unsigned rank = lanes_below(need);
+            const unsigned take = min((unsigned)__popcll(need), blk_units - blk_next);
+            if (!active && rank < take) {
+                const unsigned u = blk_next + rank;
+                unsigned si;
+                if (nvalid == 64u) {  // a full 8x8 tile (wave-uniform): shifts, not divisions
+                    si = u >> 6;
+                    x = tx0 + (int)(u & 7u);
+                    k = tk0 + (int)((u >> 3) & 7u);
+                } else {
+                    si = u / nvalid;
+                    const unsigned p = u - si * nvalid;
+                    x = tx0 + (int)(p % (unsigned)vw);
+                    k = tk0 + (int)(p / (unsigned)vw);
+                }
+                s = s0 + (int)si;  // ITEMS: si = 0, the item's first sample
+                if constexpr (ITEMS) {
+                    left = min(P.spp, s0 + P.spp_chunk) - s0 - 1;
+                    cr = cg = cb = 0.0;
+                }
+                active = true;
+                new_sample = true;
+            }
+            blk_next += take;
+            need = __ballot(!active);
+        }
+        if (!__any(active)) break;
+        if (C::COUNT && first_active_lane()) cnt.wave_steps++;
+        if (!active) continue;
+        if (new_sample) {
+            if (C::COUNT) {
+                cnt.cam_lanes++;
+                if (first_active_lane()) cnt.cam_steps++;
+            }
+            new_sample = false;
+            const int y = P.row_begin + k * P.row_stride;
+            key.pixel = (uint32_t)y * (uint32_t)P.width + (uint32_t)x;
+            key.sample = (uint32_t)s;
+            ds_start(st, P.seed, key.pixel, (uint32_t)s);
+            camera_ray(P, x, y, st, r);
+            finish_ray<C>(r, S.has_spheres != 0);
+            Tr = Tg = Tb = 1.0;
+            if constexpr (!ITEMS) cr = cg = cb = 0.0;  // ITEMS: the chunk's running sum
+            depth = P.max_depth;
+        }
+        if (C::COUNT) { const uint64_t t = __builtin_amdgcn_s_memtime(); t_cam += t - t_prev; t_prev = t; }
+        bool cont = false;
+        if (depth > 0) {  // main.rs:21-23: depth 0 is black
+            key.bounce = (uint32_t)(P.max_depth - depth);
+            if (C::COUNT) cnt.casts++;
+            Hit h;
+            const bool hit = trace_world<C>(S, r, h, stack, key, cnt);
+            if (C::COUNT) { const uint64_t t = __builtin_amdgcn_s_memtime(); t_trace += t - t_prev; t_prev = t; }
+            if (!hit) {  // main.rs:37: background
+                cr = cr + Tr * P.bg[0];
+                cg = cg + Tg * P.bg[1];
+                cb = cb + Tb * P.bg[2];
+            } else {
+                if (C::COUNT) {
+                    cnt.shade_lanes++;
+                    if (first_active_lane()) cnt.shade_steps++;
+                }
+                cont = shade<C>(S, P, h, r, st, Tr, Tg, Tb, cr, cg, cb);
+            }
+        }
+        if (C::COUNT) { const uint64_t t = __builtin_amdgcn_s_memtime(); t_shade += t - t_prev; t_prev = t; }
+        if (cont) {
+            depth -= 1;
+        } else if (ITEMS && left > 0) {  // the item's next sample: the lane takes it at the loop top
+            active = false;
+            own = true;
+        } else {
+            // per-sample pool: this sample's radiance; items: the chunk's partial (the chunk of
+            // its last sample)
+            const size_t slot = ITEMS ? (size_t)((unsigned)(s - P.sample_begin) / (unsigned)P.spp_chunk)
+                                      : (size_t)(s - P.sample_begin);
+            double* o = samples + (slot * n_px + (size_t)k * P.width + x) * 3;
+            o[0] = cr;
+            o[1] = cg;
+            o[2] = cb;
+            active = false;
+        }
+    }
+    if (C::COUNT) {
+        atomicAdd(&counters[0], (unsigned long long)cnt.casts);
+        atomicAdd(&counters[1], (unsigned long long)cnt.nodes);
+        atomicAdd(&counters[2], (unsigned long long)cnt.prims);
+        atomicAdd(&counters[6], (unsigned long long)cnt.wave_steps);
+        atomicAdd(&counters[7], (unsigned long long)cnt.wave_nodes);
+        atomicAdd(&counters[10], (unsigned long long)cnt.wave_leaves);
+        atomicAdd(&counters[11], (unsigned long long)cnt.cam_lanes);
+        atomicAdd(&counters[12], (unsigned long long)cnt.cam_steps);
+        atomicAdd(&counters[13], (unsigned long long)cnt.shade_lanes);
+        atomicAdd(&counters[14], (unsigned long long)cnt.shade_steps);
+        if (lane == 0) {  // every lane stays in the loop to the end: lane 0 saw the wave's whole time
+            atomicAdd(&counters[3], (unsigned long long)t_cam);
+            atomicAdd(&counters[4], (unsigned long long)t_trace);
+            atomicAdd(&counters[5], (unsigned long long)t_shade);
+            atomicAdd(&counters[8], (unsigned long long)cnt.t_nodes);
+            atomicAdd(&counters[9], (unsigned long long)cnt.t_leaves);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// host-side launchers
+// ---------------------------------------------------------------------------
+struct Launch {
+    const SceneDev* S;
+    const KParams* P;
+    double* out;                   // chunk partials (chunk schedule) or per-sample radiance (pool)
+    unsigned long long* counters;
+    unsigned* work;                // pool / items: work-block counter
+    int pool;                      // 0 chunks, 1 per-sample pool, 2 item pool
+    unsigned long long n_blocks;   // 8x8 tiles x chunks
+};
+
+// Persistent grid for the pool schedule: as many blocks as fit on the device at once.
+template <class K>
+static unsigned resident_blocks(K kernel, size_t lds)
+{
+    static int cus = 0;
+    if (!cus) {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+    }
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, 256, lds) != hipSuccess || per_cu <= 0) per_cu = 1;
+    return (unsigned)(cus * per_cu);
+}
+
+template <uint32_t F, bool S32, bool LDS, bool COUNT>
+static void launch_one(const Launch& L, hipStream_t stream, bool nall)
+{
+    const SceneDev& S = *L.S;
+    const size_t lds = (LDS ? (size_t)S.stack_entries * 256 * sizeof(int) : 0) + (size_t)S.n_lds_nodes * 64;
+    if (L.pool) {
+        auto go = [&](auto kernel) {
+            const unsigned nb = std::min<unsigned long long>(resident_blocks(kernel, lds), (L.n_blocks + 3) / 4);
+            hipLaunchKernelGGL(kernel, dim3(nb), dim3(256), lds, stream, S, L.P, L.out, L.counters, L.work);
+        };
+        if (L.pool == 2) {
+            if (nall) go(trace_pool<Cfg<F, S32, LDS, true, COUNT>, true>);
+            else go(trace_pool<Cfg<F, S32, LDS, false, COUNT>, true>);
+        } else {
+            if (nall) go(trace_pool<Cfg<F, S32, LDS, true, COUNT>, false>);
+            else go(trace_pool<Cfg<F, S32, LDS, false, COUNT>, false>);
+        }
+        return;
+    }
+    const unsigned nb = (unsigned)((L.n_blocks + 3) / 4);
+    if (nall)
+        hipLaunchKernelGGL((trace_chunks<Cfg<F, S32, LDS, true, COUNT>>), dim3(nb), dim3(256), lds, stream, S,
+                           L.P, L.out, L.counters);
+    else
+        hipLaunchKernelGGL((trace_chunks<Cfg<F, S32, LDS, false, COUNT>>), dim3(nb), dim3(256), lds, stream, S,
+                           L.P, L.out, L.counters);
+}
+
+// Variant table: feature set x slab precision x loop form. The launcher takes the
+// smallest feature set covering the scene.
+template <uint32_t F, bool COUNT>
+static void launch_f(const Launch& L, int slab32, int lds, hipStream_t stream)
+{
+    const SceneDev& S = *L.S;
+    const bool nall = S.n_lds_nodes > 0 && S.n_lds_nodes == S.n_tlas_nodes;
+    if (slab32) {
+        if (lds) launch_one<F, true, true, COUNT>(L, stream, nall);
+        else launch_one<F, true, false, COUNT>(L, stream, nall);
+    } else {
+        if (lds) launch_one<F, false, true, COUNT>(L, stream, nall);
+        else launch_one<F, false, false, COUNT>(L, stream, nall);
+    }
+}
+
+// One feature set's kernels, timed or counting (trace_v_*.hip instantiate one pair each,
+// one translation unit per pair).
+template <uint32_t F, bool COUNT>
+hipError_t launch_variant(const Launch& L, const LaunchOpts& o, hipStream_t stream)
+{
+    launch_f<F, COUNT>(L, o.slab32, o.lds_stack, stream);
+    return hipGetLastError();
+}
+#define RT_VARIANT_DECL(F, COUNT) \
+    extern template hipError_t launch_variant<F, COUNT>(const Launch&, const LaunchOpts&, hipStream_t);
+RT_VARIANT_DECL(FEAT_SET_SPHERES, false)
+RT_VARIANT_DECL(FEAT_SET_SPHERES, true)
+RT_VARIANT_DECL(FEAT_SET_RECTINST, false)
+RT_VARIANT_DECL(FEAT_SET_RECTINST, true)
+RT_VARIANT_DECL(FEAT_SET_MEDIA, false)
+RT_VARIANT_DECL(FEAT_SET_MEDIA, true)
+RT_VARIANT_DECL(FEAT_ALL, false)
+RT_VARIANT_DECL(FEAT_ALL, true)
+#undef RT_VARIANT_DECL
+
+}  // namespace rtk

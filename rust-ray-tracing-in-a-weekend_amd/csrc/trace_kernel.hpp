@@ -61,7 +61,7 @@ struct LaunchOpts {
     int slab32;         // conservative f32 slab tests
     int lds_stack;      // traversal stack in LDS (1) or scratch (0)
     int count;          // count_work variant
-    int pool;           // 1: sample-pool schedule (per-sample output), 0: chunk schedule (partials)
+    int pool;           // RT_SCHED_*: 0 chunks, 1 per-sample pool (per-sample output), 2 item pool (partials)
 };
 
 uint32_t variant_features(uint32_t scene_features);

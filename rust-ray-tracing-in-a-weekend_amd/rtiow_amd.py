@@ -34,6 +34,7 @@ SCENES_NEEDING_IMAGE = (3, 7)
 RT_OUT_F32, RT_OUT_F64 = 0, 1
 RT_SCHED_CHUNKS = 0
 RT_SCHED_POOL = 1
+RT_SCHED_ITEMS = 2
 RT_ACCEL_SAH = 0
 RT_ACCEL_LINEAR = 1     # hit_hittables linear scan (hittable.rs:31-41)
 RT_ACCEL_MEDIAN = 2     # the reference BvhNode hierarchy (hittable.rs:77-130)
@@ -51,6 +52,7 @@ EXPORTED = [
     "rt_ctx_upload_world", "rt_render", "rt_rows_in_shard", "rt_last_stats", "rt_write_ppm",
     "rt_ctx_set_variant", "rt_device_eval", "rt_accum_create", "rt_accum_destroy", "rt_accum_add",
     "rt_accum_get", "rt_accum_set", "rt_accum_resolve", "rt_render_progressive", "rt_ctx_set_schedule",
+    "rt_scene_validate",
 ]
 
 # int (*rt_progress_fn)(void* user, int64_t samples_done, int64_t samples_total)
@@ -159,7 +161,9 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "rt_scene_preset_get": ([I, ctypes.POINTER(ScenePreset)], I),
         "rt_scene_camera": ([I, I, I, ctypes.POINTER(Camera), PD], I),
         "rt_world_flatten": ([P, I, ctypes.POINTER(ctypes.POINTER(SceneSoA))], I),
-        "rt_ctx_upload_soa": ([P, ctypes.POINTER(SceneSoA)], I), "rt_ctx_upload_world": ([P, P, I], I),
+        "rt_ctx_upload_soa": ([P, ctypes.POINTER(SceneSoA)], I),
+        "rt_scene_validate": ([ctypes.POINTER(SceneSoA), ctypes.POINTER(ctypes.c_int32),
+                               ctypes.POINTER(ctypes.c_int32)], I), "rt_ctx_upload_world": ([P, P, I], I),
         "rt_render": ([P, ctypes.POINTER(Camera), ctypes.POINTER(RenderParams), P], I),
         "rt_rows_in_shard": ([I, I, I], I), "rt_last_stats": ([P, ctypes.POINTER(Stats)], I),
         "rt_write_ppm": ([P, I, I, ctypes.c_char_p], I),
@@ -285,6 +289,15 @@ class World:
         p = ctypes.POINTER(SceneSoA)()
         _check(self.lib.rt_world_flatten(self.h, accel, ctypes.byref(p)), "rt_world_flatten")
         return p.contents
+
+
+def validate_soa(soa: SceneSoA):
+    """rt_scene_validate: (tlas_depth, blas_depth) the kernel's walks need; raises RTError on a
+    malformed table (out-of-range index, cycle, too deep)."""
+    lib = load_library()
+    t, b = ctypes.c_int32(), ctypes.c_int32()
+    _check(lib.rt_scene_validate(ctypes.byref(soa), ctypes.byref(t), ctypes.byref(b)), "rt_scene_validate")
+    return t.value, b.value
 
 
 def camera_new(look_from, look_at, vup, vfov, aspect_ratio, aperture, focus_dist, time0, time1) -> Camera:

@@ -1,0 +1,188 @@
+// valu_calib.hip — VALU issue-rate calibration for the roofline.
+//
+// Each kernel runs one VALU instruction class in a loop: 8 independent accumulators per
+// lane (no dependency stalls at >= 2 waves per SIMD), the loop body unrolled 8x, so the
+// class's wave-instructions dominate everything else the kernel issues. Launched with many
+// waves on every SIMD, a kernel is issue-bound on that class, and
+//     cycles per wave-instruction = 1024 SIMDs x kernel cycles / SQ_INSTS_VALU
+// calibrates the counters the trace kernel's roofline reads (scripts/valu_roofline.py).
+// Kernel cycles come from rocprofv3's GRBM_GUI_ACTIVE / 8 (8 XCDs) in the PMC pass, and
+// are cross-checked here with hipEvent time x the in-kernel clock (s_memtime over
+// s_memrealtime, 100 MHz).
+//
+// Modes: "sat" (grid = 8 blocks x 256 threads per CU, every SIMD holds 8 waves),
+//        "one" (1 block of 256 threads per CU: one wave per SIMD, the single-wave issue cost),
+//        "lat" (one dependent accumulator, one wave per SIMD: dependent-issue latency).
+// Output: one JSON line per (class, mode) on stdout.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#define CHECK(x)                                                                        \
+    do {                                                                                \
+        hipError_t e_ = (x);                                                            \
+        if (e_ != hipSuccess) {                                                         \
+            std::fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e_));                \
+            std::exit(2);                                                               \
+        }                                                                               \
+    } while (0)
+
+enum Op { F64_FMA, F64_ADD, F64_MUL, F64_RCP, F64_SQRT, F32_FMA, F32_ADD, F32_RCP, I32_ADD, I32_MUL, B32_XOR,
+          CNDMASK, N_OPS };
+static const char* kNames[N_OPS] = {"f64_fma", "f64_add", "f64_mul", "f64_rcp", "f64_sqrt", "f32_fma", "f32_add",
+                                    "f32_rcp", "i32_add", "i32_mul", "b32_xor", "cndmask"};
+
+// Each class as one exact instruction (inline asm): the compiler may not fold repeated
+// adds, pack f32 pairs into v_pk_* or strength-reduce, so the loop issues exactly
+// 8 x NACC wave-instructions of the class per iteration (plus two scalar loop ops).
+template <int OP, int NACC>
+__device__ __forceinline__ void body(double (&d)[8], float (&f)[8], unsigned (&u)[8], double db, double dc, float fb,
+                                     float fc, unsigned ub, unsigned long long mask)
+{
+#pragma unroll
+    for (int i = 0; i < NACC; ++i) {
+        if constexpr (OP == F64_FMA) asm volatile("v_fma_f64 %0, %0, %1, %2" : "+v"(d[i]) : "v"(db), "v"(dc));
+        if constexpr (OP == F64_ADD) asm volatile("v_add_f64 %0, %0, %1" : "+v"(d[i]) : "v"(db));
+        if constexpr (OP == F64_MUL) asm volatile("v_mul_f64 %0, %0, %1" : "+v"(d[i]) : "v"(db));
+        if constexpr (OP == F64_RCP) asm volatile("v_rcp_f64 %0, %0" : "+v"(d[i]));
+        if constexpr (OP == F64_SQRT) asm volatile("v_sqrt_f64 %0, %0" : "+v"(d[i]));
+        if constexpr (OP == F32_FMA) asm volatile("v_fma_f32 %0, %0, %1, %2" : "+v"(f[i]) : "v"(fb), "v"(fc));
+        if constexpr (OP == F32_ADD) asm volatile("v_add_f32 %0, %0, %1" : "+v"(f[i]) : "v"(fb));
+        if constexpr (OP == F32_RCP) asm volatile("v_rcp_f32 %0, %0" : "+v"(f[i]));
+        if constexpr (OP == I32_ADD) asm volatile("v_add_u32 %0, %0, %1" : "+v"(u[i]) : "v"(ub));
+        if constexpr (OP == I32_MUL) asm volatile("v_mul_lo_u32 %0, %0, %1" : "+v"(u[i]) : "v"(ub));
+        if constexpr (OP == B32_XOR) asm volatile("v_xor_b32 %0, %0, %1" : "+v"(u[i]) : "v"(ub));
+        if constexpr (OP == CNDMASK) asm volatile("v_cndmask_b32_e64 %0, %0, %1, %2" : "+v"(u[i]) : "v"(ub), "s"(mask));
+    }
+}
+
+template <int OP, int NACC>
+__global__ void __launch_bounds__(256) calib(const double* __restrict__ in, double* __restrict__ out, int iters,
+                                             unsigned long long* __restrict__ clk)
+{
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    double d[8];
+    float f[8];
+    unsigned u[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        d[i] = in[(t + i) & 1023];
+        f[i] = (float)d[i];
+        u[i] = (unsigned)t * 2654435761u + i;
+    }
+    const double db = in[1024], dc = in[1025];
+    const float fb = (float)db, fc = (float)dc;
+    const unsigned ub = (unsigned)in[1026];
+    const unsigned long long mask = __builtin_amdgcn_read_exec() & 0x5555555555555555ull;
+    unsigned long long c0 = 0, r0 = 0;
+    if (threadIdx.x == 0) {
+        c0 = __builtin_amdgcn_s_memtime();
+        r0 = __builtin_amdgcn_s_memrealtime();
+    }
+    for (int k = 0; k < iters; ++k) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) body<OP, NACC>(d, f, u, db, dc, fb, fc, ub, mask);
+    }
+    if (threadIdx.x == 0 && blockIdx.x == 0) {
+        clk[0] = __builtin_amdgcn_s_memtime() - c0;
+        clk[1] = __builtin_amdgcn_s_memrealtime() - r0;
+    }
+    double acc = 0.0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc += d[i] + (double)f[i] + (double)u[i];
+    out[t] = acc;
+}
+
+template <int OP>
+static void run(const char* mode, int cus, double* din, double* dout, unsigned long long* dclk, int iters)
+{
+    const bool lat = !std::strcmp(mode, "lat");
+    const int blocks = !std::strcmp(mode, "sat") ? cus * 8 : cus;
+    auto kern = lat ? calib<OP, 1> : calib<OP, 8>;
+    hipEvent_t a, b;
+    CHECK(hipEventCreate(&a));
+    CHECK(hipEventCreate(&b));
+    hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), 0, 0, din, dout, 2, dclk);  // warm-up
+    CHECK(hipDeviceSynchronize());
+    CHECK(hipEventRecord(a));
+    hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), 0, 0, din, dout, iters, dclk);
+    CHECK(hipEventRecord(b));
+    CHECK(hipEventSynchronize(b));
+    float ms = 0;
+    CHECK(hipEventElapsedTime(&ms, a, b));
+    unsigned long long clk[2];
+    CHECK(hipMemcpy(clk, dclk, sizeof clk, hipMemcpyDeviceToHost));
+    const double ghz = clk[1] ? (double)clk[0] / (double)clk[1] * 0.1 : 0.0;  // memrealtime = 100 MHz
+    const int nacc = lat ? 1 : 8;
+    const double waves = (double)blocks * 4.0;
+    const double inst = waves * (double)iters * 8.0 * nacc;  // class wave-instructions
+    const double simds = cus * 4.0;
+    const double cyc = ms * 1e-3 * ghz * 1e9;
+    std::printf("{\"op\": \"%s\", \"mode\": \"%s\", \"blocks\": %d, \"iters\": %d, \"ms\": %.4f, \"clock_ghz\": %.4f, "
+                "\"class_insts\": %.6g, \"cycles_per_inst_per_simd\": %.4f}\n",
+                kNames[OP], mode, blocks, iters, ms, ghz, inst, simds * cyc / inst);
+    std::fflush(stdout);
+    CHECK(hipEventDestroy(a));
+    CHECK(hipEventDestroy(b));
+}
+
+template <int OP>
+static void run_modes(const std::vector<std::string>& modes, int cus, double* din, double* dout,
+                      unsigned long long* dclk, int iters)
+{
+    for (const auto& m : modes) run<OP>(m.c_str(), cus, din, dout, dclk, m == "sat" ? iters : iters * 2);
+}
+
+int main(int argc, char** argv)
+{
+    // usage: valu_calib [ops,comma,separated|all] [modes: sat,one,lat] [iters]
+    const std::string ops = argc > 1 ? argv[1] : "all";
+    std::vector<std::string> modes;
+    {
+        std::string m = argc > 2 ? argv[2] : "sat,one,lat";
+        size_t p = 0;
+        while (p <= m.size()) {
+            size_t q = m.find(',', p);
+            if (q == std::string::npos) q = m.size();
+            modes.push_back(m.substr(p, q - p));
+            p = q + 1;
+        }
+    }
+    const int iters = argc > 3 ? std::atoi(argv[3]) : 4000;
+    int dev = 0, cus = 0;
+    CHECK(hipGetDevice(&dev));
+    CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    std::vector<double> h(1028);
+    for (int i = 0; i < 1024; ++i) h[i] = 1.0 + i * 1e-3;
+    h[1024] = 0.999999;
+    h[1025] = 1e-7;
+    h[1026] = 3;
+    h[1027] = 5;
+    double *din, *dout;
+    unsigned long long* dclk;
+    CHECK(hipMalloc(&din, h.size() * sizeof(double)));
+    CHECK(hipMalloc(&dout, (size_t)cus * 8 * 256 * sizeof(double)));
+    CHECK(hipMalloc(&dclk, 2 * sizeof(unsigned long long)));
+    CHECK(hipMemcpy(din, h.data(), h.size() * sizeof(double), hipMemcpyHostToDevice));
+    auto want = [&](int op) { return ops == "all" || ("," + ops + ",").find("," + std::string(kNames[op]) + ",") != std::string::npos; };
+    if (want(F64_FMA)) run_modes<F64_FMA>(modes, cus, din, dout, dclk, iters);
+    if (want(F64_ADD)) run_modes<F64_ADD>(modes, cus, din, dout, dclk, iters);
+    if (want(F64_MUL)) run_modes<F64_MUL>(modes, cus, din, dout, dclk, iters);
+    if (want(F64_RCP)) run_modes<F64_RCP>(modes, cus, din, dout, dclk, iters);
+    if (want(F64_SQRT)) run_modes<F64_SQRT>(modes, cus, din, dout, dclk, iters);
+    if (want(F32_FMA)) run_modes<F32_FMA>(modes, cus, din, dout, dclk, iters);
+    if (want(F32_ADD)) run_modes<F32_ADD>(modes, cus, din, dout, dclk, iters);
+    if (want(F32_RCP)) run_modes<F32_RCP>(modes, cus, din, dout, dclk, iters);
+    if (want(I32_ADD)) run_modes<I32_ADD>(modes, cus, din, dout, dclk, iters);
+    if (want(I32_MUL)) run_modes<I32_MUL>(modes, cus, din, dout, dclk, iters);
+    if (want(B32_XOR)) run_modes<B32_XOR>(modes, cus, din, dout, dclk, iters);
+    if (want(CNDMASK)) run_modes<CNDMASK>(modes, cus, din, dout, dclk, iters);
+    CHECK(hipFree(din));
+    CHECK(hipFree(dout));
+    CHECK(hipFree(dclk));
+    return 0;
+}

@@ -1,0 +1,191 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 runs into profiles/ (round 2 format).
+
+  python scripts/pmc_r02.py calib <gpurun_out dir> <tag>
+      scripts/calib_r02.sh output -> the VALU calibration block of profiles/pmc_r02.json
+      and profiles/<tag>_valu_calib.md
+  python scripts/pmc_r02.py bench <gpurun_out dir> <tag> <scene,W,H,spp,depth,n_gpus,schedule> [note]
+      scripts/profile_r02.sh output -> one entry of profiles/pmc_r02.json (keyed by the
+      source hash of this tree and the workload), profiles/<tag>_pmc.md and
+      profiles/<tag>_kernel_stats.csv
+
+Counter reading (MI355X_MICROARCH.md §HBM, §rocprofv3 PMC slots, §Per-instruction cycle
+constants): SQ_* cycle counters count quad-cycles; GRBM_GUI_ACTIVE is summed over the 8
+XCDs, so the clock the chip held = GRBM_GUI_ACTIVE / 8 / kernel time; FETCH_SIZE and
+WRITE_SIZE are KiB, and on gfx950 FETCH_SIZE reports half the bytes of wide coalesced
+reads, so DRAM bytes = 2 x FETCH_SIZE + WRITE_SIZE (an upper estimate for this kernel's
+narrower loads; the kernel reads almost nothing from DRAM either way).
+"""
+import collections
+import csv
+import glob
+import json
+import os
+import re
+import shutil
+import statistics
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+OUT_JSON = os.path.join(REPO, "profiles", "pmc_r02.json")
+N_SIMDS = 1024
+
+# trace-kernel VALU classes (rocprofv3 counter) -> the calibration kernel measuring its rate
+CLASS_COUNTERS = {
+    "f64_add": "SQ_INSTS_VALU_ADD_F64", "f64_mul": "SQ_INSTS_VALU_MUL_F64", "f64_fma": "SQ_INSTS_VALU_FMA_F64",
+    "f64_trans": "SQ_INSTS_VALU_TRANS_F64", "f32_add": "SQ_INSTS_VALU_ADD_F32", "f32_mul": "SQ_INSTS_VALU_MUL_F32",
+    "f32_fma": "SQ_INSTS_VALU_FMA_F32", "f32_trans": "SQ_INSTS_VALU_TRANS_F32", "int32": "SQ_INSTS_VALU_INT32",
+    "int64": "SQ_INSTS_VALU_INT64", "cvt": "SQ_INSTS_VALU_CVT"}
+CLASS_PROXY = {"f64_add": ["f64_add"], "f64_mul": ["f64_mul"], "f64_fma": ["f64_fma"],
+               "f64_trans": ["f64_rcp", "f64_sqrt"], "f32_add": ["f32_add"], "f32_mul": ["f32_add"],
+               "f32_fma": ["f32_fma"], "f32_trans": ["f32_rcp"], "int32": ["i32_add"],
+               "int64": ["f64_add"], "cvt": ["i32_add"], "other": ["b32_xor", "cndmask"]}
+CALIB_OPS = ["f64_fma", "f64_add", "f64_mul", "f64_rcp", "f64_sqrt", "f32_fma", "f32_add", "f32_rcp", "i32_add",
+             "i32_mul", "b32_xor", "cndmask"]
+
+
+def read_counters(d, select):
+    """{kernel key: {counter: mean per dispatch}, ...}, {kernel key: mean duration ns}."""
+    per = collections.defaultdict(lambda: collections.defaultdict(float))
+    dur = {}
+    kname = {}
+    for f in sorted(glob.glob(os.path.join(d, "*", "*_counter_collection.csv"))):
+        for r in csv.DictReader(open(f)):
+            k = select(r["Kernel_Name"])
+            if k is None:
+                continue
+            did = (f, r["Dispatch_Id"])
+            per[(k, did)][r["Counter_Name"]] += float(r["Counter_Value"])
+            dur[(k, did)] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+            kname[k] = r["Kernel_Name"]
+    agg = collections.defaultdict(lambda: collections.defaultdict(list))
+    durs = collections.defaultdict(list)
+    for (k, did), cs in per.items():
+        for c, v in cs.items():
+            agg[k][c].append(v)
+        durs[k].append(dur[(k, did)])
+    return ({k: {c: statistics.mean(v) for c, v in cs.items()} for k, cs in agg.items()},
+            {k: statistics.mean(v) for k, v in durs.items()}, kname)
+
+
+def load():
+    if os.path.exists(OUT_JSON):
+        return json.load(open(OUT_JSON))
+    return {"note": "rocprofv3 PMC per trace-kernel launch, keyed by source hash (__graft_entry__.source_hash) "
+                    "and workload [scene, W, H, spp, depth, n_gpus, schedule]; calibration: VALU cycles per "
+                    "wave-instruction per class at saturation (scripts/calib). Written by scripts/pmc_r02.py.",
+            "calibration": None, "entries": []}
+
+
+def calib(d, tag):
+    ops = {i: n for i, n in enumerate(CALIB_OPS)}
+
+    def sel(name):
+        m = re.search(r"calib<(\d+), 8>", name)
+        return ops[int(m.group(1))] if m else None
+
+    counters, durs, _ = read_counters(d, sel)
+    timing = [json.loads(l) for l in open(os.path.join(d, "timing.jsonl")) if l.strip()]
+    lines = [f"# VALU issue calibration `{tag}` (scripts/calib/valu_calib.hip, MI355X)", "",
+             "Saturated mode: 8 blocks x 256 threads per CU (8 waves per SIMD), 8 independent accumulators",
+             "per lane, the class as one inline-asm instruction. cyc/inst (PMC) = 1024 SIMDs x",
+             "(GRBM_GUI_ACTIVE/8) / SQ_INSTS_VALU; cyc/inst (timing) = SIMDs x hipEvent time x in-kernel",
+             "clock / class instructions issued. 'one' = one wave per SIMD, 'lat' = one dependent chain.", "",
+             "| op | cyc/inst PMC (sat) | clock GHz (PMC) | counters hit | ACTIVE_INST_VALU x4 / SIMD-cycles | "
+             "cyc/inst timing sat | one | lat |", "|---|---|---|---|---|---|---|---|"]
+    rates = {}
+    for op in CALIB_OPS:
+        c = counters.get(op, {})
+        t = {m: x for x in timing if x["op"] == op for m in [x["mode"]]}
+        cyc = None
+        if c.get("SQ_INSTS_VALU") and c.get("GRBM_GUI_ACTIVE"):
+            cycles = c["GRBM_GUI_ACTIVE"] / 8.0
+            cyc = N_SIMDS * cycles / c["SQ_INSTS_VALU"]
+            clk = cycles / (durs[op] * 1e-9) / 1e9
+            busy = 4.0 * c.get("SQ_ACTIVE_INST_VALU", 0.0) / (N_SIMDS * cycles)
+        hits = [k[len("SQ_INSTS_VALU_"):] for k, v in c.items()
+                if k.startswith("SQ_INSTS_VALU_") and v > 0.5 * c.get("SQ_INSTS_VALU", 1e30)]
+        sat = t.get("sat", {}).get("cycles_per_inst_per_simd")
+        rates[op] = cyc if cyc is not None else sat
+        lines.append(f"| {op} | {cyc if cyc is None else round(cyc, 3)} | "
+                     f"{'' if cyc is None else round(clk, 3)} | {', '.join(hits)} | "
+                     f"{'' if cyc is None else round(busy, 3)} | {sat if sat is None else round(sat, 3)} | "
+                     f"{round(t['one']['cycles_per_inst_per_simd'], 3) if 'one' in t else ''} | "
+                     f"{round(t['lat']['cycles_per_inst_per_simd'], 3) if 'lat' in t else ''} |")
+    cyc = {cls: statistics.mean(rates[o] for o in proxies) for cls, proxies in CLASS_PROXY.items()}
+    lines += ["", "Cycles per wave-instruction used by the roofline (class <- calibration kernel(s)):", ""]
+    lines += [f"- {cls}: {cyc[cls]:.3f} <- {', '.join(CLASS_PROXY[cls])}" for cls in CLASS_PROXY]
+    doc = load()
+    doc["calibration"] = {"tag": tag, "cycles_per_inst": cyc, "class_counters": CLASS_COUNTERS,
+                          "proxies": CLASS_PROXY, "raw": {o: rates[o] for o in CALIB_OPS}}
+    json.dump(doc, open(OUT_JSON, "w"), indent=1)
+    open(os.path.join(REPO, "profiles", f"{tag}_valu_calib.md"), "w").write("\n".join(lines) + "\n")
+    print("\n".join(lines))
+
+
+def bench(d, tag, workload, note=""):
+    import __graft_entry__ as ge
+
+    def sel(name):
+        m = re.search(r"(trace_pool|trace_chunks)<rtk::Cfg<(\d+)u, (\w+), (\w+), (\w+), (\w+)>", name)
+        if not m or m.group(6) == "true":      # skip the count_work variant
+            return None
+        return m.group(1)
+
+    counters, durs, knames = read_counters(d, sel)
+    if len(counters) != 1:
+        raise SystemExit(f"expected one timed trace kernel, got {list(counters)}")
+    (kern, c), = counters.items()
+    dur_ns = durs[kern]
+    avg_ns = None
+    stats = os.path.join(d, "kt", "kt_kernel_stats.csv")
+    if os.path.exists(stats):
+        shutil.copy(stats, os.path.join(REPO, "profiles", f"{tag}_kernel_stats.csv"))
+        for r in csv.DictReader(open(stats)):
+            if kern in r["Name"] and ", false>" in r["Name"].split("(")[0]:
+                avg_ns = float(r["AverageNs"])
+    cycles = c["GRBM_GUI_ACTIVE"] / 8.0
+    clk = cycles / (dur_ns * 1e-9) / 1e9
+    fetch = c.get("FETCH_SIZE", 0.0) * 1024
+    write = c.get("WRITE_SIZE", 0.0) * 1024
+    dram = 2 * fetch + write
+    doc = load()
+    entry = {"tag": tag, "src_hash": ge.source_hash(), "workload": workload, "kernel": knames[kern],
+             "kernel_ms": (avg_ns or dur_ns) / 1e6, "pmc_dispatch_ms": dur_ns / 1e6, "clock_ghz": clk,
+             "dram_bytes": dram, "fetch_bytes_raw": fetch, "write_bytes": write, "counters": c, "note": note}
+    doc["entries"] = [e for e in doc["entries"] if not (e["src_hash"] == entry["src_hash"] and
+                                                        e["workload"] == workload)] + [entry]
+    json.dump(doc, open(OUT_JSON, "w"), indent=1)
+    lines = [f"# PMC summary `{tag}` — {knames[kern].split('(')[0]}", "",
+             f"workload [scene, W, H, spp, depth, n_gpus, schedule] = {workload}; source hash {entry['src_hash']}",
+             f"{note}", "",
+             f"kernel-trace average {entry['kernel_ms']:.3f} ms; PMC-pass dispatch {dur_ns / 1e6:.3f} ms; "
+             f"clock held GRBM_GUI_ACTIVE/8/t = {clk:.3f} GHz", "",
+             "| counter | per launch |", "|---|---|"]
+    lines += [f"| {k} | {c[k]:.6g} |" for k in sorted(c)]
+    lines += ["", f"DRAM bytes per launch = 2 x FETCH_SIZE + WRITE_SIZE = {dram / 1e6:.2f} MB "
+                  f"({dram / (dur_ns * 1e-9) / 1e9:.2f} GB/s = {dram / (dur_ns * 1e-9) / 8e12:.5f} of 8 TB/s)"]
+    if "SQ_THREAD_CYCLES_VALU" in c:
+        lines.append(f"VALU lane utilisation = SQ_THREAD_CYCLES_VALU / (64 SQ_INSTS_VALU) = "
+                     f"{c['SQ_THREAD_CYCLES_VALU'] / (64 * c['SQ_INSTS_VALU']):.3f}")
+    cal = doc.get("calibration")
+    if cal:
+        import bench as bn
+        need = bn.valu_issue_cycles(c, cal)
+        lines.append(f"VALU issue cycles the mix needs (calibration `{cal['tag']}`) = {need:.4g} SIMD-cycles; "
+                     f"launch = {N_SIMDS} x {cycles:.4g} = {N_SIMDS * cycles:.4g} -> VALU issue roofline "
+                     f"fraction {need / (N_SIMDS * cycles):.3f}")
+        lines.append(f"(naive 4 x SQ_ACTIVE_INST_VALU / SIMD-cycles = "
+                     f"{4 * c.get('SQ_ACTIVE_INST_VALU', 0) / (N_SIMDS * cycles):.3f})")
+    open(os.path.join(REPO, "profiles", f"{tag}_pmc.md"), "w").write("\n".join(lines) + "\n")
+    print("\n".join(lines))
+
+
+if __name__ == "__main__":
+    mode = sys.argv[1]
+    if mode == "calib":
+        calib(os.path.join(REPO, "gpurun_out", sys.argv[2]), sys.argv[3])
+    else:
+        bench(os.path.join(REPO, "gpurun_out", sys.argv[2]), sys.argv[3], [int(x) for x in sys.argv[4].split(",")],
+              sys.argv[5] if len(sys.argv) > 5 else "")

@@ -224,3 +224,73 @@ def test_ppm_writer_reference_format(rt, tmp_path):
     assert lines[4] == "255 128 0"           # (int)(256 * clamp(sqrt(x), 0, .999))
     assert lines[4 + 5] == "0 255 181"       # NaN -> 0, clamp to .999 -> 255, sqrt(.5)*256 = 181.02
     assert len([l for l in lines[4:] if l]) == 6
+
+
+# ---- rt_scene_validate (a foreign SoA must not overrun the traversal stack or
+# make the persistent kernel walk a cycle; the depth fields are not trusted)
+
+def _soa_with_nodes(rt, world, accel=0):
+    soa = rt.SceneSoA.from_buffer_copy(world.flatten(accel))
+    _, _, nodes, _ = soa_tables(soa)
+    nodes = nodes.copy()
+    soa.nodes = nodes.ctypes.data
+    return soa, nodes
+
+
+@pytest.mark.parametrize("scene_id", range(8))
+def test_validate_recomputes_flatten_depths(rt, scene_id):
+    world = rt.World(1).build_scene(scene_id)
+    for accel in (rt.RT_ACCEL_SAH, rt.RT_ACCEL_LINEAR, rt.RT_ACCEL_MEDIAN):
+        soa = rt.SceneSoA.from_buffer_copy(world.flatten(accel))
+        assert rt.validate_soa(soa) == (soa.tlas_depth, soa.blas_depth), accel
+
+
+def test_validate_ignores_understated_depths(rt):
+    world = rt.World(1).build_scene(7)
+    soa = rt.SceneSoA.from_buffer_copy(world.flatten())
+    true = (soa.tlas_depth, soa.blas_depth)
+    assert true[0] > 2 and true[1] > 1
+    soa.tlas_depth, soa.blas_depth = 1, 0           # a foreign host that under-reports
+    assert rt.validate_soa(soa) == true
+
+
+def test_validate_rejects_cycles_and_bad_refs(rt):
+    world = rt.World(1).build_scene(0)
+    soa, nodes = _soa_with_nodes(rt, world)
+    assert soa.n_nodes > 4
+    inner = [i for i in range(soa.n_nodes) if nodes[i]["child"][0] >= 0]
+    i = inner[-1]
+    nodes[i]["child"][1] = soa.tlas_root            # back edge to the root: a cycle
+    with pytest.raises(rt.RTError, match="cycle"):
+        rt.validate_soa(soa)
+    soa, nodes = _soa_with_nodes(rt, world)
+    nodes[0]["child"][0] = soa.n_nodes              # node index out of range
+    with pytest.raises(rt.RTError, match="bad node"):
+        rt.validate_soa(soa)
+    soa, nodes = _soa_with_nodes(rt, world)
+    nodes[0]["child"][0] = ~((soa.n_prim_refs << 5) | 3)   # leaf range past the prim refs
+    with pytest.raises(rt.RTError, match="bad node"):
+        rt.validate_soa(soa)
+    soa, nodes = _soa_with_nodes(rt, world)
+    nodes[0]["child"][1] = nodes[0]["child"][0]     # a DAG (shared child) is legal
+    rt.validate_soa(soa)
+
+
+def test_validate_rejects_a_chain_deeper_than_the_stack(rt):
+    """A node chain whose walk needs more than 32 stack entries is refused (the kernel's
+    scratch stack holds 32 TLAS + 32 BLAS entries)."""
+    w = rt.World(1)
+    m = w.lambertian(w.solid(0.5, 0.5, 0.5))
+    for i in range(40):
+        w.push(w.sphere(m, (float(i), 0.0, 0.0), 0.4))
+    soa, nodes = _soa_with_nodes(rt, w)
+    n = 40
+    deep = np.zeros(n, dtype=NODE_DT)               # a left-deep chain: node k -> (node k+1, leaf k)
+    for k in range(n):
+        deep[k]["lo0"] = deep[k]["lo1"] = (-1e3, -1e3, -1e3)
+        deep[k]["hi0"] = (1e3, 1e3, 1e3)
+        deep[k]["hi1"] = (2e3, 1e3, 1e3)            # different boxes: either side may go first
+        deep[k]["child"] = (k + 1 if k + 1 < n else ~((0 << 5) | 1), ~((k % soa.n_prim_refs << 5) | 1))
+    soa.nodes, soa.n_nodes, soa.tlas_root, soa.n_tlas_nodes = deep.ctypes.data, n, 0, n
+    with pytest.raises(rt.RTError, match="UNSUPPORTED"):
+        rt.validate_soa(soa)

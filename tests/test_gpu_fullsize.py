@@ -1,8 +1,12 @@
 """GPU checks at BASELINE.json's full frame sizes, through properties that do not need
 the oracle to render the whole frame:
 
-- every BASELINE geometry against the oracle on a bounded row subset (C2/C5 scene at
-  1200x800, Cornell at 800x800, the final scene at 1920x1080);
+- every BASELINE config against the oracle on a bounded row subset at its own geometry
+  and depth: C1 (1200x800, 10 spp, depth 8), C2 (1200x800, depth 50, 64 spp), C3 (Cornell
+  800x800, 64 spp), C4 (final scene 1920x1080, 48 spp) and C5 (4096x4096: pixel keys up to
+  16.7 M, rendered in many buffer batches through the carry kernels);
+- the kernel variants (conservative f32 slabs vs f64 slabs, LDS vs scratch stack, TLAS in
+  LDS or not) and the accel modes render the FULL C2 / C3 / C4 frames bit-identically;
 - the full C2 frame (1200x800, 500 spp, depth 50): finite, deterministic (two renders are
   bit-identical), and equal to the sum of its progressive batches;
 - statistical parity across independent seeds: with another render seed the image
@@ -32,6 +36,91 @@ def test_baseline_geometries_on_row_subsets(rt, renderer, scene_id, W, H, stride
                              renderer=renderer)
     ref = ob.render(scene_id, W, H, 2, row_begin=3, row_stride=stride)
     _parity(img, ref, f"scene {scene_id} {W}x{H}")
+
+
+# BASELINE.json configs at their own geometry, depth and a real sample depth, on row subsets
+# the oracle renders in about a second (C1 full spp; C2/C3/C4 at 48-64 spp, i.e. 3-4 chunks
+# of 16 and sample indices far past the first few)
+@pytest.mark.parametrize("cfg,scene_id,W,H,spp,depth,row_begin,stride", [
+    ("C1", 0, 1200, 800, 10, 8, 2, 5),
+    ("C2", 0, 1200, 800, 64, 50, 11, 50),
+    ("C3", 5, 800, 800, 64, 50, 7, 10),
+    ("C4", 7, 1920, 1080, 48, 50, 5, 36),
+])
+def test_baseline_configs_against_oracle(rt, renderer, cfg, scene_id, W, H, spp, depth, row_begin, stride):
+    img, st = rt.render_scene(scene_id, W, H, spp, depth, row_begin=row_begin, row_stride=stride,
+                              out_format=rt.RT_OUT_F64, renderer=renderer)
+    ref = ob.render(scene_id, W, H, spp, depth, row_begin=row_begin, row_stride=stride, threads=16)
+    assert img.shape == (len(range(row_begin, H, stride)), W, 3)
+    _parity(img, ref, cfg)
+
+
+@pytest.mark.parametrize("sched", ["POOL", "ITEMS"])
+def test_c5_geometry_many_buffer_batches(rt, sched):
+    """C5's 4096x4096 frame (pixel keys y*4096 + x up to 16.7 M) on 8 full-width rows incl.
+    the top one, 40 spp (chunks of 3), with a 1 MB trace-output bound so the render runs
+    in many buffer batches: per-sample pool 1 sample per batch, chunks straddling batches
+    (reduce_samples_carry); item pool 1 chunk per batch (accumulate_chunks)."""
+    import os
+    W = H = 4096
+    spp, rows = 40, dict(row_begin=511, row_stride=512)
+    os.environ["RT_SAMPLE_BUF_MB"] = "1"
+    try:
+        r = rt.Renderer(0)
+    finally:
+        os.environ.pop("RT_SAMPLE_BUF_MB")
+    r.set_schedule(getattr(rt, "RT_SCHED_" + sched))
+    world = rt.World(1).build_scene(0)
+    cam, bg = rt.scene_camera(0, W, H)
+    r.upload(world)
+    img = r.render(cam, rt.Renderer.params(W, H, spp, 50, bg, 1, out_format=rt.RT_OUT_F64, **rows))
+    st = r.stats()
+    assert st.n_batches == (40 if sched == "POOL" else 14), st.n_batches
+    r.close()
+    ref = ob.render(0, W, H, spp, 50, threads=16, **rows)
+    assert img.shape == (8, W, 3)
+    _parity(img, ref, f"C5 geometry ({sched})")
+
+
+@pytest.mark.parametrize("scene_id,W,H,spp", [(0, 1200, 800, 16), (5, 800, 800, 16), (7, 1920, 1080, 8)])
+def test_variants_bit_identical_at_full_size(rt, renderer, scene_id, W, H, spp):
+    """The conservative f32 slab test (boxes padded on the host, flatten.cpp to_f32_box) is a
+    claim about rare rays; check it where they occur: whole C2 / C3 / C4 frames (7.7 M to
+    16.6 M samples) with f32 vs f64 slabs, LDS vs scratch stack, TLAS in LDS vs L2 — every
+    pixel bit for bit."""
+    world = rt.World(1).build_scene(scene_id)
+    cam, bg = rt.scene_camera(scene_id, W, H)
+    renderer.upload(world)
+    p = rt.Renderer.params(W, H, spp, 50, bg, 1, out_format=rt.RT_OUT_F64)
+    ref = None
+    try:
+        for v in [(1, 1, 1), (0, 1, 1), (1, 0, 1), (1, 1, 0), (0, 0, 0)]:
+            renderer.set_variant(*v)
+            img = renderer.render(cam, p)
+            st = renderer.stats()
+            assert st.slab32 == v[0]
+            if ref is None:
+                ref = img
+            else:
+                same = img == ref
+                assert same.all(), f"variant {v}: {int((~same.all(axis=2)).sum())} px differ"
+    finally:
+        renderer.set_variant(1, 1, 1)
+
+
+def test_accel_modes_bit_identical_at_full_c2_size(rt, renderer):
+    """SURVEY §8 f3 at the headline geometry: the reference's list scan (LINEAR) and the SAH
+    BVH give the same C2 frame bit for bit (closest hit does not depend on the hierarchy)."""
+    W, H, spp = 1200, 800, 4
+    world = rt.World(1).build_scene(0)
+    cam, bg = rt.scene_camera(0, W, H)
+    p = rt.Renderer.params(W, H, spp, 50, bg, 1, out_format=rt.RT_OUT_F64)
+    out = {}
+    for accel in (rt.RT_ACCEL_SAH, rt.RT_ACCEL_LINEAR):
+        renderer.upload(world, accel)
+        out[accel] = renderer.render(cam, p)
+    renderer.upload(world)
+    assert np.array_equal(out[rt.RT_ACCEL_SAH], out[rt.RT_ACCEL_LINEAR])
 
 
 def test_full_c2_frame_deterministic_and_batch_additive(rt, renderer):

@@ -306,9 +306,10 @@ def test_progressive_early_stop_and_divisor(rt, renderer):
 
 @pytest.mark.parametrize("scene_id,W,H,spp", [(0, 40, 24, 8), (5, 24, 24, 8), (6, 24, 24, 8), (7, 32, 18, 8)])
 def test_schedules_render_identically(rt, scene_id, W, H, spp):
-    """The sample-pool schedule (persistent waves, per-lane refill, [sample][pixel] buffer)
-    and the chunk schedule give the same bits; so does the pool split into many buffer
-    batches (RT_SAMPLE_BUF_MB), at ragged sizes and with row shards."""
+    """The three schedules give the same bits: chunks; the per-sample pool (persistent
+    waves, per-lane refill, [sample][pixel] buffer); the item pool (persistent waves, a lane
+    takes a whole (pixel, chunk) item). So do the pools split into many buffer batches
+    (RT_SAMPLE_BUF_MB), at ragged sizes and with row shards."""
     import os
     world = rt.World(1).build_scene(scene_id)
     cam, bg = rt.scene_camera(scene_id, W, H)
@@ -319,20 +320,55 @@ def test_schedules_render_identically(rt, scene_id, W, H, spp):
     finally:
         os.environ.pop("RT_SAMPLE_BUF_MB")
     r = rt.Renderer(0)
-    for rr, sched in [(r, rt.RT_SCHED_CHUNKS), (r, rt.RT_SCHED_POOL), (small, rt.RT_SCHED_POOL)]:
+    runs = [(r, rt.RT_SCHED_CHUNKS), (r, rt.RT_SCHED_POOL), (r, rt.RT_SCHED_ITEMS), (small, rt.RT_SCHED_POOL),
+            (small, rt.RT_SCHED_ITEMS)]
+    for rr, sched in runs:
         rr.set_schedule(sched)
         rr.upload(world)
         imgs.append(rr.render(cam, rt.Renderer.params(W, H, spp, 50, bg, 1, row_begin=1, row_stride=2,
                                                       out_format=rt.RT_OUT_F64)))
         assert rr.stats().schedule == sched
-    assert np.array_equal(imgs[0], imgs[1]) and np.array_equal(imgs[0], imgs[2])
+    for im in imgs[1:]:
+        assert np.array_equal(imgs[0], im)
     q = rt.Renderer.params(64, 48, 40, 50, bg, 1, out_format=rt.RT_OUT_F64)   # 73.7 KB per sample
+    r.set_schedule(rt.RT_SCHED_ITEMS)
+    one = r.render(cam, q)
+    assert r.stats().n_batches == 1
+    small.set_schedule(rt.RT_SCHED_POOL)
     batched = small.render(cam, q)
     assert small.stats().n_batches == 3              # 14 + 14 + 12 samples; chunks of 3 straddle batches
-    assert np.array_equal(batched, r.render(cam, q)) and r.stats().n_batches == 1
+    assert np.array_equal(batched, one)
     acc = small.accumulator(q)                       # an accumulator batch straddling buffer batches
     acc.add(cam, q, 21)
     acc.add(cam, q, 19)
-    one = r.render(cam, rt.Renderer.params(64, 48, 40, 50, bg, 1, spp_chunk=3, out_format=rt.RT_OUT_F64))
-    assert np.array_equal(acc.resolve(out_format=rt.RT_OUT_F64), one)
-    assert_parity(imgs[1], ob.render(scene_id, W, H, spp, row_begin=1, row_stride=2), f"pool scene {scene_id}")
+    ref3 = r.render(cam, rt.Renderer.params(64, 48, 40, 50, bg, 1, spp_chunk=3, out_format=rt.RT_OUT_F64))
+    assert np.array_equal(acc.resolve(out_format=rt.RT_OUT_F64), ref3)
+    # item pool in buffer batches of whole chunks: 256x192 px x 24 B > 1 MB, one chunk per launch
+    q2 = rt.Renderer.params(256, 192, 12, 50, bg, 1, out_format=rt.RT_OUT_F64)
+    small.set_schedule(rt.RT_SCHED_ITEMS)
+    b2 = small.render(cam, q2)
+    assert small.stats().n_batches == 12
+    assert np.array_equal(b2, r.render(cam, q2))
+    assert_parity(imgs[2], ob.render(scene_id, W, H, spp, row_begin=1, row_stride=2), f"items scene {scene_id}")
+
+
+def test_renders_on_two_streams_are_ordered(rt, renderer):
+    """a render enqueued on a caller's stream and an immediate render on the
+    context's own stream share the context's scratch buffers; the second must be ordered
+    after the first (no host sync in between). Both frames must equal separate renders."""
+    import torch
+    W, H, spp = 320, 240, 32
+    world = rt.World(1).build_scene(0)
+    cam, bg = rt.scene_camera(0, W, H)
+    renderer.upload(world)
+    pa = rt.Renderer.params(W, H, spp, 50, bg, 1, out_format=rt.RT_OUT_F32)
+    pb = rt.Renderer.params(W, H, 4, 50, bg, 2, out_format=rt.RT_OUT_F32)
+    ref_a = renderer.render(cam, pa)
+    ref_b = renderer.render(cam, rt.Renderer.params(W, H, 4, 50, bg, 2, out_format=rt.RT_OUT_F32))
+    stream = torch.cuda.Stream(torch.device("cuda", 0))
+    slab = torch.zeros((H, W, 3), dtype=torch.float32, device="cuda:0")
+    renderer.render_device(cam, pa, slab.data_ptr(), stream.cuda_stream)   # enqueued, not waited for
+    got_b = renderer.render(cam, pb)                                       # context stream, synchronous
+    torch.cuda.synchronize()
+    assert np.array_equal(got_b, ref_b)
+    assert np.array_equal(slab.cpu().numpy(), ref_a)
