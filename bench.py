@@ -112,12 +112,14 @@ def pmc_entry(src_hash, workload):
     return None, doc.get("calibration")
 
 
-def valu_issue_cycles(counts, calib):
+def valu_issue_cycles(counts, calib, other=None):
     """Issue cycles (summed over SIMDs) the launch's VALU instruction mix needs at the
     calibrated saturated rates: sum over classes of count x cycles per wave-instruction; the
     instructions no class counter covers (moves, compares, selects, bit ops) at the measured
-    rate of those (calib 'other')."""
-    cyc = calib["cycles_per_inst"]
+    rate of those (calib 'other', or `other` to price the bounds)."""
+    cyc = dict(calib["cycles_per_inst"])
+    if other is not None:
+        cyc["other"] = other
     total = counts["SQ_INSTS_VALU"]
     known, need = 0.0, 0.0
     for cls, key in calib["class_counters"].items():
@@ -229,6 +231,8 @@ def main():
         achieved = need / (k_ms * 1e-3) / 1e9                    # per live-timed launch
         peak = N_SIMDS * clk
         dram = pmc["dram_bytes"]
+        lo, hi = (valu_issue_cycles(pmc["counters"], calib, o) / (k_ms * 1e-3) / 1e9 / peak
+                  for o in calib.get("other_range", [calib["cycles_per_inst"]["other"]] * 2))
         roofline.update({
             "achieved": round(achieved, 1), "peak": round(peak, 1), "frac": round(achieved / peak, 4),
             "traffic": int(dram),
@@ -236,6 +240,7 @@ def main():
                                     (64.0 * pmc["counters"]["SQ_INSTS_VALU"]), 4),
             "hbm": {"achieved": round(dram / (k_ms * 1e-3) / 1e9, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(dram / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)},
+            "frac_range": [round(lo, 4), round(hi, 4)],
             "pmc_tag": pmc.get("tag"), "pmc_kernel_ms": pmc.get("kernel_ms"), "clock_ghz": clk})
     else:
         roofline["note"] = "no PMC pass of this build (source hash) and workload in profiles/pmc_r02.json"

@@ -32,16 +32,19 @@
     } while (0)
 
 enum Op { F64_FMA, F64_ADD, F64_MUL, F64_RCP, F64_SQRT, F32_FMA, F32_ADD, F32_RCP, I32_ADD, I32_MUL, B32_XOR,
-          CNDMASK, N_OPS };
+          CNDMASK, MOV_B32, CNDMASK_VCC, CMP_F64, CMP_F32, MAX_F64, MIN_F32, LSHL_B64, CVT_F64_U32, BFE_U32,
+          N_OPS };
 static const char* kNames[N_OPS] = {"f64_fma", "f64_add", "f64_mul", "f64_rcp", "f64_sqrt", "f32_fma", "f32_add",
-                                    "f32_rcp", "i32_add", "i32_mul", "b32_xor", "cndmask"};
+                                    "f32_rcp", "i32_add", "i32_mul", "b32_xor", "cndmask", "mov_b32", "cndmask_vcc",
+                                    "cmp_f64", "cmp_f32", "max_f64", "min_f32", "lshl_b64", "cvt_f64_u32",
+                                    "bfe_u32"};
 
 // Each class as one exact instruction (inline asm): the compiler may not fold repeated
 // adds, pack f32 pairs into v_pk_* or strength-reduce, so the loop issues exactly
 // 8 x NACC wave-instructions of the class per iteration (plus two scalar loop ops).
 template <int OP, int NACC>
-__device__ __forceinline__ void body(double (&d)[8], float (&f)[8], unsigned (&u)[8], double db, double dc, float fb,
-                                     float fc, unsigned ub, unsigned long long mask)
+__device__ __forceinline__ void body(double (&d)[8], float (&f)[8], unsigned (&u)[8], unsigned long long (&cm)[8],
+                                     double db, double dc, float fb, float fc, unsigned ub, unsigned long long mask)
 {
 #pragma unroll
     for (int i = 0; i < NACC; ++i) {
@@ -57,6 +60,15 @@ __device__ __forceinline__ void body(double (&d)[8], float (&f)[8], unsigned (&u
         if constexpr (OP == I32_MUL) asm volatile("v_mul_lo_u32 %0, %0, %1" : "+v"(u[i]) : "v"(ub));
         if constexpr (OP == B32_XOR) asm volatile("v_xor_b32 %0, %0, %1" : "+v"(u[i]) : "v"(ub));
         if constexpr (OP == CNDMASK) asm volatile("v_cndmask_b32_e64 %0, %0, %1, %2" : "+v"(u[i]) : "v"(ub), "s"(mask));
+        if constexpr (OP == MOV_B32) asm volatile("v_mov_b32 %0, %1" : "=v"(u[i]) : "v"(u[(i + 1) & 7]));
+        if constexpr (OP == CNDMASK_VCC) asm volatile("v_cndmask_b32_e32 %0, %0, %1, vcc" : "+v"(u[i]) : "v"(ub));
+        if constexpr (OP == CMP_F64) asm volatile("v_cmp_gt_f64 %0, %1, %2" : "=s"(cm[i]) : "v"(d[i]), "v"(db));
+        if constexpr (OP == CMP_F32) asm volatile("v_cmp_gt_f32 %0, %1, %2" : "=s"(cm[i]) : "v"(f[i]), "v"(fb));
+        if constexpr (OP == MAX_F64) asm volatile("v_max_f64 %0, %0, %1" : "+v"(d[i]) : "v"(db));
+        if constexpr (OP == MIN_F32) asm volatile("v_min_f32 %0, %0, %1" : "+v"(f[i]) : "v"(fb));
+        if constexpr (OP == LSHL_B64) asm volatile("v_lshlrev_b64 %0, 1, %0" : "+v"(d[i]));
+        if constexpr (OP == CVT_F64_U32) asm volatile("v_cvt_f64_u32 %0, %1" : "=v"(d[i]) : "v"(u[i]));
+        if constexpr (OP == BFE_U32) asm volatile("v_bfe_u32 %0, %0, 3, 7" : "+v"(u[i]));
     }
 }
 
@@ -68,8 +80,10 @@ __global__ void __launch_bounds__(256) calib(const double* __restrict__ in, doub
     double d[8];
     float f[8];
     unsigned u[8];
+    unsigned long long cm[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
+        cm[i] = 0;
         d[i] = in[(t + i) & 1023];
         f[i] = (float)d[i];
         u[i] = (unsigned)t * 2654435761u + i;
@@ -85,7 +99,7 @@ __global__ void __launch_bounds__(256) calib(const double* __restrict__ in, doub
     }
     for (int k = 0; k < iters; ++k) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) body<OP, NACC>(d, f, u, db, dc, fb, fc, ub, mask);
+        for (int j = 0; j < 8; ++j) body<OP, NACC>(d, f, u, cm, db, dc, fb, fc, ub, mask);
     }
     if (threadIdx.x == 0 && blockIdx.x == 0) {
         clk[0] = __builtin_amdgcn_s_memtime() - c0;
@@ -93,7 +107,7 @@ __global__ void __launch_bounds__(256) calib(const double* __restrict__ in, doub
     }
     double acc = 0.0;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) acc += d[i] + (double)f[i] + (double)u[i];
+    for (int i = 0; i < 8; ++i) acc += d[i] + (double)f[i] + (double)u[i] + (double)(cm[i] & 1u);
     out[t] = acc;
 }
 
@@ -181,6 +195,15 @@ int main(int argc, char** argv)
     if (want(I32_MUL)) run_modes<I32_MUL>(modes, cus, din, dout, dclk, iters);
     if (want(B32_XOR)) run_modes<B32_XOR>(modes, cus, din, dout, dclk, iters);
     if (want(CNDMASK)) run_modes<CNDMASK>(modes, cus, din, dout, dclk, iters);
+    if (want(MOV_B32)) run_modes<MOV_B32>(modes, cus, din, dout, dclk, iters);
+    if (want(CNDMASK_VCC)) run_modes<CNDMASK_VCC>(modes, cus, din, dout, dclk, iters);
+    if (want(CMP_F64)) run_modes<CMP_F64>(modes, cus, din, dout, dclk, iters);
+    if (want(CMP_F32)) run_modes<CMP_F32>(modes, cus, din, dout, dclk, iters);
+    if (want(MAX_F64)) run_modes<MAX_F64>(modes, cus, din, dout, dclk, iters);
+    if (want(MIN_F32)) run_modes<MIN_F32>(modes, cus, din, dout, dclk, iters);
+    if (want(LSHL_B64)) run_modes<LSHL_B64>(modes, cus, din, dout, dclk, iters);
+    if (want(CVT_F64_U32)) run_modes<CVT_F64_U32>(modes, cus, din, dout, dclk, iters);
+    if (want(BFE_U32)) run_modes<BFE_U32>(modes, cus, din, dout, dclk, iters);
     CHECK(hipFree(din));
     CHECK(hipFree(dout));
     CHECK(hipFree(dclk));

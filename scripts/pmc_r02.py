@@ -40,9 +40,12 @@ CLASS_COUNTERS = {
 CLASS_PROXY = {"f64_add": ["f64_add"], "f64_mul": ["f64_mul"], "f64_fma": ["f64_fma"],
                "f64_trans": ["f64_rcp", "f64_sqrt"], "f32_add": ["f32_add"], "f32_mul": ["f32_add"],
                "f32_fma": ["f32_fma"], "f32_trans": ["f32_rcp"], "int32": ["i32_add"],
-               "int64": ["f64_add"], "cvt": ["i32_add"], "other": ["b32_xor", "cndmask"]}
+               "int64": ["lshl_b64"], "cvt": ["cvt_f64_u32"], "other": None}
+# 'other' (instructions no class counter counts: moves, selects, compares, bit ops) is priced at
+# the mean of the calibration ops that hit no class counter; bounds from their min / max
 CALIB_OPS = ["f64_fma", "f64_add", "f64_mul", "f64_rcp", "f64_sqrt", "f32_fma", "f32_add", "f32_rcp", "i32_add",
-             "i32_mul", "b32_xor", "cndmask"]
+             "i32_mul", "b32_xor", "cndmask", "mov_b32", "cndmask_vcc", "cmp_f64", "cmp_f32", "max_f64", "min_f32",
+             "lshl_b64", "cvt_f64_u32", "bfe_u32"]
 
 
 def read_counters(d, select):
@@ -94,7 +97,7 @@ def calib(d, tag):
              "clock / class instructions issued. 'one' = one wave per SIMD, 'lat' = one dependent chain.", "",
              "| op | cyc/inst PMC (sat) | clock GHz (PMC) | counters hit | ACTIVE_INST_VALU x4 / SIMD-cycles | "
              "cyc/inst timing sat | one | lat |", "|---|---|---|---|---|---|---|---|"]
-    rates = {}
+    rates, unclassed = {}, []
     for op in CALIB_OPS:
         c = counters.get(op, {})
         t = {m: x for x in timing if x["op"] == op for m in [x["mode"]]}
@@ -108,17 +111,23 @@ def calib(d, tag):
                 if k.startswith("SQ_INSTS_VALU_") and v > 0.5 * c.get("SQ_INSTS_VALU", 1e30)]
         sat = t.get("sat", {}).get("cycles_per_inst_per_simd")
         rates[op] = cyc if cyc is not None else sat
+        if c and not hits:
+            unclassed.append(op)
         lines.append(f"| {op} | {cyc if cyc is None else round(cyc, 3)} | "
                      f"{'' if cyc is None else round(clk, 3)} | {', '.join(hits)} | "
                      f"{'' if cyc is None else round(busy, 3)} | {sat if sat is None else round(sat, 3)} | "
                      f"{round(t['one']['cycles_per_inst_per_simd'], 3) if 'one' in t else ''} | "
                      f"{round(t['lat']['cycles_per_inst_per_simd'], 3) if 'lat' in t else ''} |")
-    cyc = {cls: statistics.mean(rates[o] for o in proxies) for cls, proxies in CLASS_PROXY.items()}
+    proxies = dict(CLASS_PROXY, other=unclassed)
+    cyc = {cls: statistics.mean(rates[o] for o in ps) for cls, ps in proxies.items()}
+    other_range = [min(rates[o] for o in unclassed), max(rates[o] for o in unclassed)]
     lines += ["", "Cycles per wave-instruction used by the roofline (class <- calibration kernel(s)):", ""]
-    lines += [f"- {cls}: {cyc[cls]:.3f} <- {', '.join(CLASS_PROXY[cls])}" for cls in CLASS_PROXY]
+    lines += [f"- {cls}: {cyc[cls]:.3f} <- {', '.join(proxies[cls])}" for cls in proxies]
+    lines += [f"- other: range {other_range[0]:.3f} .. {other_range[1]:.3f} (bounds of the roofline fraction)"]
     doc = load()
-    doc["calibration"] = {"tag": tag, "cycles_per_inst": cyc, "class_counters": CLASS_COUNTERS,
-                          "proxies": CLASS_PROXY, "raw": {o: rates[o] for o in CALIB_OPS}}
+    doc["calibration"] = {"tag": tag, "cycles_per_inst": cyc, "other_range": other_range,
+                          "class_counters": CLASS_COUNTERS, "proxies": proxies,
+                          "raw": {o: rates[o] for o in CALIB_OPS}}
     json.dump(doc, open(OUT_JSON, "w"), indent=1)
     open(os.path.join(REPO, "profiles", f"{tag}_valu_calib.md"), "w").write("\n".join(lines) + "\n")
     print("\n".join(lines))
