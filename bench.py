@@ -68,6 +68,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--t10-seconds", type=float, default=10.0, help="CPU time of the reference 10-thread split run")
     ap.add_argument("--count-spp", type=int, default=16, help="spp of the untimed count_work pass")
+    ap.add_argument("--spp-chunk", type=int, default=0, help="samples per chunk (0: the library's automatic choice)")
     ap.add_argument("--no-count", action="store_true", help="skip the count_work pass (profiling runs)")
     ap.add_argument("--ppm", default="", help="write the rendered frame (rank 0) as a P3 PPM")
     args = ap.parse_args()
@@ -173,7 +174,7 @@ def main():
     # op of a step runs under this stream; NCCL orders its gather after it.
     stream = torch.cuda.Stream(device)
     params = rt.Renderer.params(W, H, spp, depth, bg, args.seed, row_begin=rank, row_stride=world,
-                                out_format=rt.RT_OUT_F32)
+                                spp_chunk=args.spp_chunk, out_format=rt.RT_OUT_F32)
     kernel_ms = []
 
     def step():
@@ -250,7 +251,7 @@ def main():
     cs = None
     if not args.no_count:
         cp = rt.Renderer.params(W, H, count_spp, depth, bg, args.seed, row_begin=rank, row_stride=world,
-                                out_format=rt.RT_OUT_F32, count_work=1)
+                                spp_chunk=min(args.spp_chunk, count_spp), out_format=rt.RT_OUT_F32, count_work=1)
         renderer.render(cam, cp)
         cs = renderer.stats()
     alg = None

@@ -61,7 +61,10 @@ __device__ __forceinline__ void body(double (&d)[8], float (&f)[8], unsigned (&u
         if constexpr (OP == B32_XOR) asm volatile("v_xor_b32 %0, %0, %1" : "+v"(u[i]) : "v"(ub));
         if constexpr (OP == CNDMASK) asm volatile("v_cndmask_b32_e64 %0, %0, %1, %2" : "+v"(u[i]) : "v"(ub), "s"(mask));
         if constexpr (OP == MOV_B32) asm volatile("v_mov_b32 %0, %1" : "=v"(u[i]) : "v"(u[(i + 1) & 7]));
-        if constexpr (OP == CNDMASK_VCC) asm volatile("v_cndmask_b32_e32 %0, %0, %1, vcc" : "+v"(u[i]) : "v"(ub));
+        // a compare into vcc and the select reading it: the pair the compiler emits (a select
+        // reading a vcc that nothing wrote issued at ~22 cycles in r02b: not what kernels do)
+        if constexpr (OP == CNDMASK_VCC)
+            asm volatile("v_cmp_gt_u32 vcc, %0, %1\n\tv_cndmask_b32_e32 %0, %0, %1, vcc" : "+v"(u[i]) : "v"(ub) : "vcc");
         if constexpr (OP == CMP_F64) asm volatile("v_cmp_gt_f64 %0, %1, %2" : "=s"(cm[i]) : "v"(d[i]), "v"(db));
         if constexpr (OP == CMP_F32) asm volatile("v_cmp_gt_f32 %0, %1, %2" : "=s"(cm[i]) : "v"(f[i]), "v"(fb));
         if constexpr (OP == MAX_F64) asm volatile("v_max_f64 %0, %0, %1" : "+v"(d[i]) : "v"(db));

@@ -111,7 +111,7 @@ def calib(d, tag):
                 if k.startswith("SQ_INSTS_VALU_") and v > 0.5 * c.get("SQ_INSTS_VALU", 1e30)]
         sat = t.get("sat", {}).get("cycles_per_inst_per_simd")
         rates[op] = cyc if cyc is not None else sat
-        if c and not hits:
+        if c and not hits and op != "cndmask_vcc":   # cndmask_vcc: a v_cmp + v_cndmask pair (2 instructions)
             unclassed.append(op)
         lines.append(f"| {op} | {cyc if cyc is None else round(cyc, 3)} | "
                      f"{'' if cyc is None else round(clk, 3)} | {', '.join(hits)} | "
