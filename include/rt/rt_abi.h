@@ -246,8 +246,8 @@ int rt_write_ppm(const float* mean_rgb, int width, int height, const char* path)
  * environment variables. Results do not depend on them (tests check this). */
 int rt_ctx_set_variant(rt_ctx* ctx, int slab32, int lds_stack, int lds_nodes);
 
-/* Work schedule of a context (default RT_SCHED_ITEMS, or the RT_SCHEDULE environment
- * variable 0/1/2). Images are bit-identical under all three.
+/* Work schedule of a context (default RT_SCHED_AUTO, or the RT_SCHEDULE environment
+ * variable 0/1/2/3). Images are bit-identical under all of them.
  *   CHUNKS: a wave owns an 8x8 tile x one chunk of samples, each lane one pixel's chunk,
  *           written as one partial per (pixel, chunk); the wave waits for its slowest lane.
  *   POOL:   persistent waves take (tile, chunk) blocks from a device counter and a lane
@@ -256,9 +256,12 @@ int rt_ctx_set_variant(rt_ctx* ctx, int slab32, int lds_stack, int lds_nodes);
  *   ITEMS:  persistent waves as POOL, but a lane takes a whole (pixel, chunk) item, traces
  *           its samples in order and writes one partial, as CHUNKS does (1/chunk of POOL's
  *           buffer bytes); a lane whose item ended takes the next item at once.
+ *   AUTO:   POOL when the render's [sample][pixel] buffer fits one batch (it is the faster
+ *           of the two: fewer divergent lanes), otherwise ITEMS; rt_stats.schedule
+ *           reports which ran.
  * One launch's trace output is bounded by RT_SAMPLE_BUF_MB (default 32 GiB); a larger
  * render runs in buffer batches (on chunk boundaries) whose sums are carried across. */
-enum { RT_SCHED_CHUNKS = 0, RT_SCHED_POOL = 1, RT_SCHED_ITEMS = 2 };
+enum { RT_SCHED_CHUNKS = 0, RT_SCHED_POOL = 1, RT_SCHED_ITEMS = 2, RT_SCHED_AUTO = 3 };
 int rt_ctx_set_schedule(rt_ctx* ctx, int schedule);
 
 /* ---- self test ------------------------------------------------------------------------------ */

@@ -87,7 +87,7 @@ struct rt_ctx {
     int opt_slab32 = 1;                 // rt_ctx_set_variant / RT_SLAB32
     int opt_lds = 1;                    // rt_ctx_set_variant / RT_LDS_STACK
     int opt_lds_nodes = 1;              // RT_LDS_NODES: keep the TLAS in LDS when it fits
-    int opt_pool = RT_SCHED_ITEMS;      // rt_ctx_set_schedule / RT_SCHEDULE: RT_SCHED_*
+    int opt_pool = RT_SCHED_AUTO;       // rt_ctx_set_schedule / RT_SCHEDULE: RT_SCHED_*
     size_t sample_buf_cap = (size_t)32 << 30;  // RT_SAMPLE_BUF_MB: bound of one launch's trace output
     unsigned* work = nullptr;           // pool / item schedules: work-block counter
     double* acc_tmp = nullptr;          // running sums when a render takes several buffer batches
@@ -127,7 +127,7 @@ int rt_ctx_create(int device, rt_ctx** out)
     if (const char* e = std::getenv("RT_SLAB32")) c->opt_slab32 = std::atoi(e) != 0;
     if (const char* e = std::getenv("RT_LDS_STACK")) c->opt_lds = std::atoi(e) != 0;
     if (const char* e = std::getenv("RT_LDS_NODES")) c->opt_lds_nodes = std::atoi(e) != 0;
-    if (const char* e = std::getenv("RT_SCHEDULE")) c->opt_pool = std::min(2, std::max(0, std::atoi(e)));
+    if (const char* e = std::getenv("RT_SCHEDULE")) c->opt_pool = std::min(3, std::max(0, std::atoi(e)));
     if (const char* e = std::getenv("RT_SAMPLE_BUF_MB")) c->sample_buf_cap = (size_t)std::max(1L, std::atol(e)) << 20;
     hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     for (int i = 0; i < 3 && e == hipSuccess; ++i) e = hipEventCreate(&c->ev[i]);
@@ -731,17 +731,21 @@ static int run_range(rt_ctx* c, const rt_camera* cam, const rt_render_params* p,
     o.slab32 = c->opt_slab32 && c->pad_extent > 0.0 && cam_mag <= 2.0 * c->pad_extent;
     o.lds_stack = c->opt_lds && c->S.stack_entries <= kMaxLdsStack;
     o.count = count;
-    o.pool = c->opt_pool;
+    const long long total = s_end - s_begin;
+    const size_t px_bytes = px * 3 * sizeof(double);
+    // AUTO: the per-sample pool when its [sample][pixel] buffer fits one batch (C2: 11.5 GB,
+    // 101.7 vs 106.7 ms per frame for the item pool, profiles/r02d_*), else the item pool,
+    // whose partials take 1/chunk of those bytes and need no carried batches
+    o.pool = c->opt_pool != RT_SCHED_AUTO ? c->opt_pool
+             : ((size_t)total * px_bytes <= c->sample_buf_cap ? RT_SCHED_POOL : RT_SCHED_ITEMS);
     // the TLAS in LDS (read-only, shared by the block) when it fits the per-block budget
     rtk::SceneDev S = c->S;
     S.n_lds_nodes = c->opt_lds_nodes ? std::min(c->n_tlas_nodes, kMaxLdsNodes) : 0;
 
-    const long long total = s_end - s_begin;
     // Buffer batches: the trace output of one launch is bounded by sample_buf_cap. Per-sample
     // pool: samples x pixels x 24 B; chunk and item schedules: chunks x pixels x 24 B, batches
     // on chunk boundaries (relative to s_begin), so the partials add in one-launch order.
     const bool per_sample = o.pool == RT_SCHED_POOL;
-    const size_t px_bytes = px * 3 * sizeof(double);
     const long long fit = (long long)std::max<size_t>(1, c->sample_buf_cap / px_bytes);
     const long long batch = std::min<long long>(total, per_sample ? fit : fit * chunk);
     const int n_batches = (int)((total + batch - 1) / batch);
@@ -1111,7 +1115,7 @@ int rt_ctx_set_variant(rt_ctx* c, int slab32, int lds_stack, int lds_nodes)
 
 int rt_ctx_set_schedule(rt_ctx* c, int schedule)
 {
-    if (!c || schedule < RT_SCHED_CHUNKS || schedule > RT_SCHED_ITEMS) return fail(RT_ERR_INVALID, "bad schedule");
+    if (!c || schedule < RT_SCHED_CHUNKS || schedule > RT_SCHED_AUTO) return fail(RT_ERR_INVALID, "bad schedule");
     c->opt_pool = schedule;
     return RT_OK;
 }

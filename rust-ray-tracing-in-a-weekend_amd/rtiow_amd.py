@@ -35,6 +35,7 @@ RT_OUT_F32, RT_OUT_F64 = 0, 1
 RT_SCHED_CHUNKS = 0
 RT_SCHED_POOL = 1
 RT_SCHED_ITEMS = 2
+RT_SCHED_AUTO = 3
 RT_ACCEL_SAH = 0
 RT_ACCEL_LINEAR = 1     # hit_hittables linear scan (hittable.rs:31-41)
 RT_ACCEL_MEDIAN = 2     # the reference BvhNode hierarchy (hittable.rs:77-130)

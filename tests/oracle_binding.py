@@ -14,7 +14,8 @@ import numpy as np
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ORACLE_DIR = os.path.join(REPO, "oracle")
-ORACLE_LIB = os.path.join(ORACLE_DIR, "build", "liboracle.so")
+# RT_ORACLE_LIB: another build of the same source (the sanitizer run, tests/test_sanitizers.py)
+ORACLE_LIB = os.environ.get("RT_ORACLE_LIB", os.path.join(ORACLE_DIR, "build", "liboracle.so"))
 EARTH_JPG = os.path.join(REPO, "assets", "earthmap.jpg")
 
 SPLIT_ROWS, SPLIT_SAMPLES = 0, 1
