@@ -71,6 +71,8 @@ def parse():
     ap.add_argument("--spp-chunk", type=int, default=0, help="samples per chunk (0: the library's automatic choice)")
     ap.add_argument("--no-count", action="store_true", help="skip the count_work pass (profiling runs)")
     ap.add_argument("--ppm", default="", help="write the rendered frame (rank 0) as a P3 PPM")
+    ap.add_argument("--precision", default="f64", choices=["f64", "f32"],
+                    help="f64: the reference's arithmetic (the headline); f32: the fast mode (SURVEY §8 f3)")
     args = ap.parse_args()
     for k, v in CONFIGS[args.config].items():
         if getattr(args, k) is None:
@@ -161,6 +163,9 @@ def main():
     cam, bg = rt.scene_camera(args.scene, W, H)
     renderer = rt.Renderer(local)
     renderer.upload(scene)
+    f32 = args.precision == "f32"
+    if f32:
+        renderer.set_precision(rt.RT_PREC_F32)
     t_build = time.perf_counter() - t_build
 
     rows = rt.rows_in_shard(H, rank, world)
@@ -222,7 +227,7 @@ def main():
 
     # ---- roofline: VALU issue (the binding resource), from the PMC pass of this build
     src_hash = ge.source_hash()
-    workload = [args.scene, W, H, spp, depth, world, last.schedule]
+    workload = [args.scene, W, H, spp, depth, world, last.schedule] + ([1] if f32 else [])
     pmc, calib = pmc_entry(src_hash, workload)
     roofline = {"bound": "valu", "achieved": None, "peak": None, "unit": "G SIMD-cycles/s", "frac": None,
                 "traffic": None, "src_hash": src_hash}
@@ -249,7 +254,7 @@ def main():
     # ---- SURVEY §8(d) algorithmic bytes per sample (LDS/L1/L2-served; not an HBM figure)
     count_spp = min(args.count_spp, spp)
     cs = None
-    if not args.no_count:
+    if not args.no_count and not f32:   # count_work is an f64-mode diagnostic
         cp = rt.Renderer.params(W, H, count_spp, depth, bg, args.seed, row_begin=rank, row_stride=world,
                                 spp_chunk=min(args.spp_chunk, count_spp), out_format=rt.RT_OUT_F32, count_work=1)
         renderer.render(cam, cp)
@@ -321,7 +326,11 @@ def main():
                   "rows": n_rows, "row_stride": stride, "spp": spp_cpu, "max_depth": depth,
                   "samples": int(st.samples), "tolerance": 1e-3, "pass": bool(d.max() <= 1e-3),
                   "vs": "oracle image of the cpu_baseline sample (same rows, samples, seeds)"}
-        if spp_cpu == spp:
+        if f32:   # the f32 mode's paths are its own: statistical parity (tests/test_gpu_f32.py)
+            mean_rel = abs(float(gimg.mean()) / float(ref_img.mean()) - 1.0)
+            parity.update({"mode": "statistical (f32)", "mean_rel": mean_rel, "tolerance": 0.01,
+                           "pass": bool(mean_rel < 0.01)})
+        if spp_cpu == spp and not f32:
             parity["linf_timed_f32_frame"] = float(np.abs(frame_np[0::stride].astype(np.float64) - ref_img).max())
 
     if rank == 0:
@@ -337,7 +346,7 @@ def main():
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
-            "dtype": "f64",
+            "dtype": args.precision,
             "data": "synthetic (seeded scene builders, scene_seed=render_seed=%d)" % args.seed,
             "config": {"workload": "%s %s %dx%d, %d spp, max depth %d, row-sharded over %d GPU"
                                    % (args.config, SCENE_NAMES.get(args.scene, "scene %d" % args.scene), W, H, spp,

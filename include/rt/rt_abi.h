@@ -198,6 +198,8 @@ typedef struct rt_stats {
     uint64_t camera_steps;       /*   wave iterations in which any lane did (camera_steps) */
     uint64_t shade_lanes;        /* count_work only: lanes shading a hit, summed over the */
     uint64_t shade_steps;        /*   wave iterations in which any lane did (shade_steps) */
+    int32_t precision;           /* RT_PREC_* the last render ran with */
+    int32_t pad_;
 } rt_stats;
 int rt_last_stats(rt_ctx* ctx, rt_stats* out);
 
@@ -243,7 +245,10 @@ int rt_write_ppm(const float* mean_rgb, int width, int height, const char* path)
 /* Kernel variant knobs of a context: slab32 (conservative f32 BVH slab tests),
  * lds_stack (traversal stack in LDS instead of scratch), lds_nodes (keep the TLAS in LDS
  * when it fits). Defaults 1/1/1, or the RT_SLAB32 / RT_LDS_STACK / RT_LDS_NODES
- * environment variables. Results do not depend on them (tests check this). */
+ * environment variables. Results do not depend on them (tests check this).
+ * RT_EXTRA_FEATURES (environment, read at context creation): feature bits OR-ed into the
+ * scene's, so a scene runs on a larger feature-set variant than it needs (the tests use it
+ * to run the all-features variant, which no reference scene selects). */
 int rt_ctx_set_variant(rt_ctx* ctx, int slab32, int lds_stack, int lds_nodes);
 
 /* Work schedule of a context (default RT_SCHED_AUTO, or the RT_SCHEDULE environment
@@ -256,13 +261,22 @@ int rt_ctx_set_variant(rt_ctx* ctx, int slab32, int lds_stack, int lds_nodes);
  *   ITEMS:  persistent waves as POOL, but a lane takes a whole (pixel, chunk) item, traces
  *           its samples in order and writes one partial, as CHUNKS does (1/chunk of POOL's
  *           buffer bytes); a lane whose item ended takes the next item at once.
- *   AUTO:   POOL when the render's [sample][pixel] buffer fits one batch (it is the faster
- *           of the two: fewer divergent lanes), otherwise ITEMS; rt_stats.schedule
- *           reports which ran.
+ *   AUTO:   POOL when the render's [sample][pixel] buffer takes at most 4 batches (it is
+ *           the faster of the two), otherwise ITEMS; rt_stats.schedule reports which ran.
  * One launch's trace output is bounded by RT_SAMPLE_BUF_MB (default 32 GiB); a larger
  * render runs in buffer batches (on chunk boundaries) whose sums are carried across. */
 enum { RT_SCHED_CHUNKS = 0, RT_SCHED_POOL = 1, RT_SCHED_ITEMS = 2, RT_SCHED_AUTO = 3 };
 int rt_ctx_set_schedule(rt_ctx* ctx, int schedule);
+
+/* Arithmetic of a context's renders (default RT_PREC_F64, or the RT_PRECISION
+ * environment variable 0/1).
+ *   F64: the reference's f64 everywhere (math.rs:13-17), bit-exact against the oracle.
+ *   F32: a fast mode: f32 rays, hit records, materials and textures (sphere tests keep
+ *        |oc|^2 - r^2 in f64), one 32-bit draw per uniform; per-pixel sums
+ *        stay f64. Statistically equal to F64 (independent-seed tests), not bitwise; never
+ *        the headline metric. count_work is not available in it. */
+enum { RT_PREC_F64 = 0, RT_PREC_F32 = 1 };
+int rt_ctx_set_precision(rt_ctx* ctx, int precision);
 
 /* ---- self test ------------------------------------------------------------------------------ */
 /* Evaluates rt_numerics.h functions on the device (same fn ids as the oracle's

@@ -83,11 +83,14 @@ struct rt_ctx {
     bool pending_counts = false;
     rt_stats stats{};
     uint32_t features = rtk::FEAT_ALL;  // of the uploaded scene
+    int block_chunks = 1;               // RT_BLOCK_CHUNKS: chunks per work block of the pools
+    uint32_t extra_features = 0;        // RT_EXTRA_FEATURES: a larger kernel variant than the scene needs (tests)
     double pad_extent = 0.0;
     int opt_slab32 = 1;                 // rt_ctx_set_variant / RT_SLAB32
     int opt_lds = 1;                    // rt_ctx_set_variant / RT_LDS_STACK
     int opt_lds_nodes = 1;              // RT_LDS_NODES: keep the TLAS in LDS when it fits
     int opt_pool = RT_SCHED_AUTO;       // rt_ctx_set_schedule / RT_SCHEDULE: RT_SCHED_*
+    int opt_precision = RT_PREC_F64;    // rt_ctx_set_precision / RT_PRECISION: RT_PREC_*
     size_t sample_buf_cap = (size_t)32 << 30;  // RT_SAMPLE_BUF_MB: bound of one launch's trace output
     unsigned* work = nullptr;           // pool / item schedules: work-block counter
     double* acc_tmp = nullptr;          // running sums when a render takes several buffer batches
@@ -128,6 +131,9 @@ int rt_ctx_create(int device, rt_ctx** out)
     if (const char* e = std::getenv("RT_LDS_STACK")) c->opt_lds = std::atoi(e) != 0;
     if (const char* e = std::getenv("RT_LDS_NODES")) c->opt_lds_nodes = std::atoi(e) != 0;
     if (const char* e = std::getenv("RT_SCHEDULE")) c->opt_pool = std::min(3, std::max(0, std::atoi(e)));
+    if (const char* e = std::getenv("RT_PRECISION")) c->opt_precision = std::atoi(e) == RT_PREC_F32 ? RT_PREC_F32 : RT_PREC_F64;
+    if (const char* e = std::getenv("RT_BLOCK_CHUNKS")) c->block_chunks = std::min(64, std::max(1, std::atoi(e)));
+    if (const char* e = std::getenv("RT_EXTRA_FEATURES")) c->extra_features = (uint32_t)std::atoi(e) & rtk::FEAT_ALL;
     if (const char* e = std::getenv("RT_SAMPLE_BUF_MB")) c->sample_buf_cap = (size_t)std::max(1L, std::atol(e)) << 20;
     hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     for (int i = 0; i < 3 && e == hipSuccess; ++i) e = hipEventCreate(&c->ev[i]);
@@ -624,6 +630,36 @@ int rt_ctx_upload_soa(rt_ctx* c, const rt_scene_soa* s)
         if (k == RT_PRIM_INSTANCE) feat |= rtk::FEAT_INST;
         if (k == RT_PRIM_MEDIUM) feat |= rtk::FEAT_MEDIUM;
     }
+    // what instances and medium boundaries reach (the kernel variant drops the rest there):
+    // rects / boxes under an instance, and medium boundaries other than spheres
+    auto is_rect = [](int k) {
+        return k == RT_PRIM_XY_RECT || k == RT_PRIM_XZ_RECT || k == RT_PRIM_YZ_RECT || k == RT_PRIM_BOX;
+    };
+    for (int i = 0; i < s->n_instances; ++i) {
+        const rt_instance& in = s->instances[i];
+        if (in.child_kind == RT_CHILD_PRIM) {
+            if (is_rect(s->prims[in.child].kind)) feat |= rtk::FEAT_INST_RECT;
+            continue;
+        }
+        std::vector<int> todo{in.child};   // validate_soa checked refs and acyclicity
+        while (!todo.empty() && !(feat & rtk::FEAT_INST_RECT)) {
+            const int ref = todo.back();
+            todo.pop_back();
+            if (ref >= 0) {
+                todo.push_back(s->nodes[ref].child[0]);
+                todo.push_back(s->nodes[ref].child[1]);
+                continue;
+            }
+            const int code = ~ref, first = code >> 5, count = code & 31;
+            for (int j = first; j < first + count; ++j)
+                if (is_rect(s->prims[s->prim_refs[j]].kind)) feat |= rtk::FEAT_INST_RECT;
+        }
+    }
+    for (int i = 0; i < s->n_prims; ++i)
+        if (s->prims[i].kind == RT_PRIM_MEDIUM) {
+            const int bk = s->prims[s->prims[i].a].kind;
+            if (bk != RT_PRIM_SPHERE && bk != RT_PRIM_MOVING_SPHERE) feat |= rtk::FEAT_MEDIUM_INST;
+        }
     for (int i = 0; i < s->n_textures; ++i) {
         if (s->textures[i].kind == RT_TEX_NOISE) feat |= rtk::FEAT_NOISE;
         if (s->textures[i].kind == RT_TEX_IMAGE) feat |= rtk::FEAT_IMAGE;
@@ -718,6 +754,7 @@ static int run_range(rt_ctx* c, const rt_camera* cam, const rt_render_params* p,
     K.n_rows = n_rows;
     K.tiles_x = (p->width + 7) / 8;
     K.tiles_y = (n_rows + 7) / 8;
+    K.block_chunks = c->block_chunks;
 
     const bool count = p->count_work != 0;
     // conservative f32 slab tests need every ray origin within 2M of the origin (flatten.cpp):
@@ -727,17 +764,21 @@ static int run_range(rt_ctx* c, const rt_camera* cam, const rt_render_params* p,
                            (1.0 + std::sqrt(cam->u[0] * cam->u[0] + cam->u[1] * cam->u[1] + cam->u[2] * cam->u[2]) +
                             std::sqrt(cam->v[0] * cam->v[0] + cam->v[1] * cam->v[1] + cam->v[2] * cam->v[2]));
     rtk::LaunchOpts o;
-    o.features = c->features;
+    o.features = c->features | c->extra_features;
     o.slab32 = c->opt_slab32 && c->pad_extent > 0.0 && cam_mag <= 2.0 * c->pad_extent;
     o.lds_stack = c->opt_lds && c->S.stack_entries <= kMaxLdsStack;
     o.count = count;
+    o.f32 = c->opt_precision == RT_PREC_F32;
+    if (o.f32 && count) return fail(RT_ERR_UNSUPPORTED, "count_work is an f64-mode diagnostic");
+    if (o.f32) o.slab32 = 1;   // statistical mode: f32 boxes whatever the camera
     const long long total = s_end - s_begin;
     const size_t px_bytes = px * 3 * sizeof(double);
-    // AUTO: the per-sample pool when its [sample][pixel] buffer fits one batch (C2: 11.5 GB,
-    // 101.7 vs 106.7 ms per frame for the item pool, profiles/r02d_*), else the item pool,
-    // whose partials take 1/chunk of those bytes and need no carried batches
+    // AUTO: the per-sample pool when its [sample][pixel] buffer takes at most 4 batches (C2:
+    // 11.5 GB in one, 101.6 vs 106.7 ms per frame for the item pool; C4: 49.8 GB in two,
+    // 1492 vs 1571 ms; profiles/r02d_*, r02e_*), else the item pool, whose partials take
+    // 1/chunk of those bytes and need no carried batches (C5: 1.6 TB of per-sample radiance)
     o.pool = c->opt_pool != RT_SCHED_AUTO ? c->opt_pool
-             : ((size_t)total * px_bytes <= c->sample_buf_cap ? RT_SCHED_POOL : RT_SCHED_ITEMS);
+             : ((size_t)total * px_bytes <= 4 * c->sample_buf_cap ? RT_SCHED_POOL : RT_SCHED_ITEMS);
     // the TLAS in LDS (read-only, shared by the block) when it fits the per-block budget
     rtk::SceneDev S = c->S;
     S.n_lds_nodes = c->opt_lds_nodes ? std::min(c->n_tlas_nodes, kMaxLdsNodes) : 0;
@@ -805,6 +846,7 @@ static int run_range(rt_ctx* c, const rt_camera* cam, const rt_render_params* p,
     c->stats.slab32 = o.slab32;
     c->stats.lds_stack = o.lds_stack;
     c->stats.schedule = o.pool;
+    c->stats.precision = o.f32 ? RT_PREC_F32 : RT_PREC_F64;
     c->stats.n_batches = n_batches;
     c->stats.samples = (uint64_t)n_px * (uint64_t)total;
     c->stats.n_chunks = (int32_t)((total + chunk - 1) / chunk);
@@ -1110,6 +1152,13 @@ int rt_ctx_set_variant(rt_ctx* c, int slab32, int lds_stack, int lds_nodes)
     c->opt_slab32 = slab32;
     c->opt_lds = lds_stack;
     c->opt_lds_nodes = lds_nodes;
+    return RT_OK;
+}
+
+int rt_ctx_set_precision(rt_ctx* c, int precision)
+{
+    if (!c || (precision != RT_PREC_F64 && precision != RT_PREC_F32)) return fail(RT_ERR_INVALID, "bad precision");
+    c->opt_precision = precision;
     return RT_OK;
 }
 

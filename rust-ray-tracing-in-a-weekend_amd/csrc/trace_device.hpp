@@ -26,6 +26,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <type_traits>
 
 #include "rt/rt_numerics.h"
 #include "rt/rt_scene.h"
@@ -33,13 +34,16 @@
 
 namespace rtk {
 
-struct Ray {
-    double ox, oy, oz;
-    double dx, dy, dz;
-    double time;
-    double a;                 // length_squared(direction)
-    double ya;                // 1 / a correctly rounded (NaN outside [2^-900, 2^900]: see div_rcp)
-    double ix, iy, iz;        // 1 / direction (f64 slab tests only)
+// R: the path's arithmetic type — double (the reference's f64, math.rs:13-17; bit-exact
+// against the oracle) or float (the f32 fast mode; statistically equal).
+template <class R>
+struct RayT {
+    R ox, oy, oz;
+    R dx, dy, dz;
+    R time;
+    R a;                      // length_squared(direction)
+    R ya;                     // f64: 1 / a correctly rounded (NaN outside [2^-900, 2^900]: see div_rcp)
+    R ix, iy, iz;             // 1 / direction (f64 slab tests only)
     float fix, fiy, fiz;      // f32 1 / direction (f32 slab tests only)
     float fox, foy, foz;      // -origin * (1 / direction) in f32
     uint32_t onx, ony, onz;   // byte offsets in a node of child 0's near planes (by direction sign)
@@ -47,15 +51,18 @@ struct Ray {
 
 // The HitRecord of hittable.rs:6-27 (uv deferred to texture lookup: uvkind 1 keeps the
 // object-space outward normal for sphere_uv, 2 keeps (x-a0, a1-a0, y-b0, b1-b0)).
-struct Hit {
-    double t, px, py, pz, nx, ny, nz;
-    double uv0, uv1, uv2, uv3;
+template <class R>
+struct HitT {
+    R t, px, py, pz, nx, ny, nz;
+    R uv0, uv1, uv2, uv3;
     int front, mat, uvkind;
 };
+using Hit = HitT<double>;
 
 // What traversal keeps per candidate: the parameter and which primitive produced it.
-struct HitRef {
-    double t;
+template <class R>
+struct HitRefT {
+    R t;
     int prim;   // prim index (top level)
     int sub;    // instance: BLAS prim index; box: winning side (0..5)
     int side;   // box inside an instance: winning side
@@ -92,15 +99,30 @@ __device__ __forceinline__ bool first_active_lane()
 #ifndef RT_TRACE_LOOP
 #define RT_TRACE_LOOP 1   // 0 if-if, 1 while-while, 2 while-while with speculative node visits
 #endif
-template <uint32_t F_, bool S32_, bool LDS_, bool NALL_, bool COUNT_>
+//   F32    the f32 fast mode (Real = float): statistically, not bitwise, equal
+template <uint32_t F_, bool S32_, bool LDS_, bool NALL_, bool COUNT_, bool F32_ = false>
 struct Cfg {
     static constexpr uint32_t F = F_;
     static constexpr bool S32 = S32_;
     static constexpr bool LDS = LDS_;
     static constexpr bool NALL = NALL_;
     static constexpr bool COUNT = COUNT_;
+    static constexpr bool F32 = F32_;
     static constexpr int LOOP = RT_TRACE_LOOP;
+    using Real = typename std::conditional<F32_, float, double>::type;
 };
+
+// The configuration of code reached only through an instance or a medium boundary: the
+// feature bits the scene does not need there are dropped (FEAT_INST_RECT / FEAT_MEDIUM_INST
+// clear), so e.g. the final scene's instanced BLAS of spheres compiles the sphere test only.
+template <class C, uint32_t DROP>
+struct CfgDrop : C {
+    static constexpr uint32_t F = C::F & ~DROP;
+};
+template <class C>
+using InstC = CfgDrop<C, (C::F & FEAT_INST_RECT) ? 0u : (uint32_t)FEAT_RECT>;
+template <class C>
+using BoundC = CfgDrop<C, (C::F & FEAT_MEDIUM_INST) ? 0u : (uint32_t)(FEAT_RECT | FEAT_INST)>;
 
 // Traversal stack. LDS: a lane-interleaved dynamic LDS array [entry][256 threads]
 // (consecutive lanes hit consecutive banks) sized per scene by the host (TLAS depth +
@@ -152,12 +174,37 @@ __device__ __forceinline__ float f32_inv_dir(double d)
     return __builtin_amdgcn_rcpf(f);
 }
 
+// ---- precision-generic helpers: double = the reference's libm restated (rt_numerics.h,
+// bit-identical host/device), float = the device's f32 functions (f32 mode only)
+__device__ __forceinline__ double r_sqrt(double x) { return __builtin_sqrt(x); }
+__device__ __forceinline__ float r_sqrt(float x) { return __builtin_sqrtf(x); }
+__device__ __forceinline__ double r_fabs(double x) { return __builtin_fabs(x); }
+__device__ __forceinline__ float r_fabs(float x) { return __builtin_fabsf(x); }
+__device__ __forceinline__ double r_floor(double x) { return __builtin_floor(x); }
+__device__ __forceinline__ float r_floor(float x) { return __builtin_floorf(x); }
+__device__ __forceinline__ double r_fmin(double a, double b) { return fmin(a, b); }
+__device__ __forceinline__ float r_fmin(float a, float b) { return fminf(a, b); }
+__device__ __forceinline__ double r_sin(double x) { return rt_sin(x); }
+__device__ __forceinline__ float r_sin(float x) { return sinf(x); }
+__device__ __forceinline__ double r_log(double x) { return rt_log(x); }
+__device__ __forceinline__ float r_log(float x) { return logf(x); }
+__device__ __forceinline__ double r_acos(double x) { return rt_acos(x); }
+__device__ __forceinline__ float r_acos(float x) { return acosf(x); }
+__device__ __forceinline__ double r_atan2(double y, double x) { return rt_atan2(y, x); }
+__device__ __forceinline__ float r_atan2(float y, float x) { return atan2f(y, x); }
+__device__ __forceinline__ double r_pow5(double x) { return rt_pow5(x); }
+__device__ __forceinline__ float r_pow5(float x) { const float x2 = x * x; return x2 * x2 * x; }
+template <class R>
+__device__ __forceinline__ int32_t r_sat_i32(R x) { return rt_sat_i32((double)x); }
+template <class R>
+__device__ __forceinline__ uint64_t r_sat_u64(R x) { return rt_sat_u64((double)x); }
+
 // spheres: the scene has spheres (wave-uniform); otherwise no root division needs 1/a
 template <class C>
-__device__ __forceinline__ void finish_ray(Ray& r, bool spheres)
+__device__ __forceinline__ void finish_ray(RayT<typename C::Real>& r, bool spheres)
 {
     r.a = r.dx * r.dx + r.dy * r.dy + r.dz * r.dz;
-    r.ya = (C::F == FEAT_SET_SPHERES || spheres) ? rcp_for_div(r.a) : __builtin_nan("");
+    if constexpr (!C::F32) r.ya = (C::F == FEAT_SET_SPHERES || spheres) ? rcp_for_div(r.a) : __builtin_nan("");
     if constexpr (C::S32) {
         r.fix = f32_inv_dir(r.dx);
         r.fiy = f32_inv_dir(r.dy);
@@ -170,17 +217,17 @@ __device__ __forceinline__ void finish_ray(Ray& r, bool spheres)
         r.ony = r.fiy >= 0.0f ? 4u : 16u;
         r.onz = r.fiz >= 0.0f ? 8u : 20u;
     } else {
-        r.ix = 1.0 / r.dx;
-        r.iy = 1.0 / r.dy;
-        r.iz = 1.0 / r.dz;
+        r.ix = (typename C::Real)1 / r.dx;
+        r.iy = (typename C::Real)1 / r.dy;
+        r.iz = (typename C::Real)1 / r.dz;
     }
 }
 
 // hittable.rs:23-26
-__device__ __forceinline__ void set_face_normal(Hit& h, double dx, double dy, double dz, double nx, double ny,
-                                                double nz)
+template <class R>
+__device__ __forceinline__ void set_face_normal(HitT<R>& h, R dx, R dy, R dz, R nx, R ny, R nz)
 {
-    const bool front = dx * nx + dy * ny + dz * nz < 0.0;
+    const bool front = dx * nx + dy * ny + dz * nz < (R)0;
     h.front = front;
     h.nx = front ? nx : -nx;
     h.ny = front ? ny : -ny;
@@ -192,8 +239,8 @@ __device__ __forceinline__ void set_face_normal(Hit& h, double dx, double dy, do
 // ---------------------------------------------------------------------------
 
 // hittable.rs:254-273: the root in [t_min, t_max]
-__device__ __forceinline__ bool sphere_t(double cx, double cy, double cz, double radius, const Ray& r, double t_min,
-                                         double t_max, double& t)
+__device__ __forceinline__ bool sphere_t(double cx, double cy, double cz, double radius, const RayT<double>& r,
+                                         double t_min, double t_max, double& t)
 {
     const double ocx = r.ox - cx, ocy = r.oy - cy, ocz = r.oz - cz;
     const double half_b = ocx * r.dx + ocy * r.dy + ocz * r.dz;
@@ -218,16 +265,39 @@ __device__ __forceinline__ bool sphere_t(double cx, double cy, double cz, double
     return true;
 }
 
+// f32 mode: the same roots, robust in f32 (Haines et al., Ray Tracing Gems ch. 7): c = |oc|^2
+// - r^2 is taken in f64 (an f32 c loses everything to cancellation on the r = 1000 ground
+// sphere, whose surface every bounce starts on), the near root as c / q (Vieta) instead of
+// the cancelling -b - sqrt(disc).
+__device__ __forceinline__ bool sphere_t(double cx, double cy, double cz, double radius, const RayT<float>& r,
+                                         float t_min, float t_max, float& t)
+{
+    const double ocx = (double)r.ox - cx, ocy = (double)r.oy - cy, ocz = (double)r.oz - cz;
+    const float c = (float)((ocx * ocx + ocy * ocy + ocz * ocz) - radius * radius);
+    const float half_b = (float)ocx * r.dx + (float)ocy * r.dy + (float)ocz * r.dz;
+    const float disc = half_b * half_b - r.a * c;
+    if (disc < 0.0f) return false;
+    const float q = -(half_b + __builtin_copysignf(__builtin_sqrtf(disc), half_b));
+    const float t0 = c / q, t1 = q / r.a;
+    const float tn = fminf(t0, t1), tf = fmaxf(t0, t1);
+    float root = tn;
+    if (root < t_min || t_max < root) {
+        root = tf;
+        if (root < t_min || t_max < root) return false;
+    }
+    t = root;
+    return true;
+}
+
 // hittable.rs:275-287
-template <class C>
-__device__ __forceinline__ void sphere_finish(double cx, double cy, double cz, double inv_r, const Ray& r, double t,
-                                              int mat, Hit& h)
+template <class C, class R = typename C::Real>
+__device__ __forceinline__ void sphere_finish(R cx, R cy, R cz, R inv_r, const RayT<R>& r, R t, int mat, HitT<R>& h)
 {
     h.t = t;
     h.px = r.ox + r.dx * t;
     h.py = r.oy + r.dy * t;
     h.pz = r.oz + r.dz * t;
-    const double onx = (h.px - cx) * inv_r, ony = (h.py - cy) * inv_r, onz = (h.pz - cz) * inv_r;
+    const R onx = (h.px - cx) * inv_r, ony = (h.py - cy) * inv_r, onz = (h.pz - cz) * inv_r;
     set_face_normal(h, r.dx, r.dy, r.dz, onx, ony, onz);
     h.mat = mat;
     h.uvkind = 1;
@@ -239,46 +309,47 @@ __device__ __forceinline__ void sphere_finish(double cx, double cy, double cz, d
 }
 
 // hittable.rs:308-320 (axis 0: XY, k on z; 1: XZ, k on y; 2: YZ, k on x)
-__device__ __forceinline__ void rect_axes(int axis, const Ray& r, double& ok, double& dk, double& oa, double& da,
-                                          double& ob, double& db)
+template <class R>
+__device__ __forceinline__ void rect_axes(int axis, const RayT<R>& r, R& ok, R& dk, R& oa, R& da, R& ob, R& db)
 {
     if (axis == 0) { ok = r.oz; dk = r.dz; oa = r.ox; da = r.dx; ob = r.oy; db = r.dy; }
     else if (axis == 1) { ok = r.oy; dk = r.dy; oa = r.ox; da = r.dx; ob = r.oz; db = r.dz; }
     else { ok = r.ox; dk = r.dx; oa = r.oy; da = r.dy; ob = r.oz; db = r.dz; }
 }
 
-__device__ __forceinline__ bool rect_t(int axis, double a0, double a1, double b0, double b1, double k, const Ray& r,
-                                       double t_min, double t_max, double& t_out)
+template <class R>
+__device__ __forceinline__ bool rect_t(int axis, R a0, R a1, R b0, R b1, R k, const RayT<R>& r, R t_min, R t_max,
+                                       R& t_out)
 {
-    double ok, dk, oa, da, ob, db;
+    R ok, dk, oa, da, ob, db;
     rect_axes(axis, r, ok, dk, oa, da, ob, db);
-    const double t = (k - ok) / dk;
+    const R t = (k - ok) / dk;
     if (t < t_min || t > t_max) return false;
-    const double x = oa + t * da;
-    const double y = ob + t * db;
+    const R x = oa + t * da;
+    const R y = ob + t * db;
     if (x < a0 || x > a1 || y < b0 || y > b1) return false;
     t_out = t;
     return true;
 }
 
 // hittable.rs:322-331
-template <class C>
-__device__ __forceinline__ void rect_finish(int axis, double a0, double a1, double b0, double b1, const Ray& r,
-                                            double t, int mat, Hit& h)
+template <class C, class R = typename C::Real>
+__device__ __forceinline__ void rect_finish(int axis, R a0, R a1, R b0, R b1, const RayT<R>& r, R t, int mat,
+                                            HitT<R>& h)
 {
-    double ok, dk, oa, da, ob, db;
+    R ok, dk, oa, da, ob, db;
     rect_axes(axis, r, ok, dk, oa, da, ob, db);
     h.uvkind = 2;
     if constexpr ((C::F & FEAT_IMAGE) != 0) {
-        const double x = oa + t * da;
-        const double y = ob + t * db;
+        const R x = oa + t * da;
+        const R y = ob + t * db;
         h.uv0 = x - a0;
         h.uv1 = a1 - a0;
         h.uv2 = y - b0;
         h.uv3 = b1 - b0;
     }
     h.t = t;
-    set_face_normal(h, r.dx, r.dy, r.dz, axis == 2 ? 1.0 : 0.0, axis == 1 ? 1.0 : 0.0, axis == 0 ? 1.0 : 0.0);
+    set_face_normal(h, r.dx, r.dy, r.dz, axis == 2 ? (R)1 : (R)0, axis == 1 ? (R)1 : (R)0, axis == 0 ? (R)1 : (R)0);
     h.mat = mat;
     h.px = r.ox + r.dx * t;
     h.py = r.oy + r.dy * t;
@@ -286,24 +357,24 @@ __device__ __forceinline__ void rect_finish(int axis, double a0, double a1, doub
 }
 
 // the six sides of new_box (hittable.rs:135-142): side -> axis, (a0 a1 b0 b1 k) from min/max
-__device__ __forceinline__ void box_side(const rt_prim& p, int side, int& axis, double& a0, double& a1, double& b0,
-                                         double& b1, double& k)
+template <class R>
+__device__ __forceinline__ void box_side(const rt_prim& p, int side, int& axis, R& a0, R& a1, R& b0, R& b1, R& k)
 {
-    const double mnx = p.p[0], mny = p.p[1], mnz = p.p[2], mxx = p.p[3], mxy = p.p[4], mxz = p.p[5];
+    const R mnx = (R)p.p[0], mny = (R)p.p[1], mnz = (R)p.p[2], mxx = (R)p.p[3], mxy = (R)p.p[4], mxz = (R)p.p[5];
     if (side < 2) { axis = 0; a0 = mnx; a1 = mxx; b0 = mny; b1 = mxy; k = side == 0 ? mxz : mnz; }
     else if (side < 4) { axis = 1; a0 = mnx; a1 = mxx; b0 = mnz; b1 = mxz; k = side == 2 ? mxy : mny; }
     else { axis = 2; a0 = mny; a1 = mxy; b0 = mnz; b1 = mxz; k = side == 4 ? mxx : mnx; }
 }
 
 // Box::hit = hit_hittables over its sides (hittable.rs:229-231): closest, ties to the later side.
-__device__ __forceinline__ bool box_t(const rt_prim& p, const Ray& r, double t_min, double t_max, double& t,
-                                      int& side)
+template <class R>
+__device__ __forceinline__ bool box_t(const rt_prim& p, const RayT<R>& r, R t_min, R t_max, R& t, int& side)
 {
     bool any = false;
 #pragma unroll
     for (int s = 0; s < 6; ++s) {
         int axis;
-        double a0, a1, b0, b1, k, ts;
+        R a0, a1, b0, b1, k, ts;
         box_side(p, s, axis, a0, a1, b0, b1, k);
         if (rect_t(axis, a0, a1, b0, b1, k, r, t_min, t_max, ts)) {
             t_max = ts;
@@ -319,22 +390,23 @@ __device__ __forceinline__ bool box_t(const rt_prim& p, const Ray& r, double t_m
 // ((time - time_0) / (time_1 - time_0)) * (center_1 - center_0) (hittable.rs:556-558).
 // Both kinds go through one code path (the moving centre is a select), so a wave whose
 // lanes hold both kinds runs the sphere test once, not once per kind.
-__device__ __forceinline__ void sphere_center(const rt_prim& p, const Ray& r, double& cx, double& cy, double& cz)
+template <class R>
+__device__ __forceinline__ void sphere_center(const rt_prim& p, const RayT<R>& r, double& cx, double& cy, double& cz)
 {
     const double c0x = p.p[0], c0y = p.p[1], c0z = p.p[2];
     const double vx = p.p[5], vy = p.p[6], vz = p.p[7];
     const bool moving = p.kind == RT_PRIM_MOVING_SPHERE;
-    double s = r.time;
-    if (moving && !p.a) s = (r.time - p.p[8]) / (p.p[9] - p.p[8]);
+    double s = (double)r.time;
+    if (moving && !p.a) s = ((double)r.time - p.p[8]) / (p.p[9] - p.p[8]);
     cx = moving ? c0x + vx * s : c0x;
     cy = moving ? c0y + vy * s : c0y;
     cz = moving ? c0z + vz * s : c0z;
 }
 
 // Sphere, MovingSphere, rects, Box: t-only (hittable.rs:211-231).
-template <class C>
-__device__ __forceinline__ bool simple_t(const rt_prim& p, const Ray& r, double t_min, double t_max, double& t,
-                                         int& side, Count& cnt)
+template <class C, class R = typename C::Real>
+__device__ __forceinline__ bool simple_t(const rt_prim& p, const RayT<R>& r, R t_min, R t_max, R& t, int& side,
+                                         Count& cnt)
 {
     if (C::COUNT) cnt.prims++;
     if (!(C::F & FEAT_RECT) || p.kind <= RT_PRIM_MOVING_SPHERE) {
@@ -342,27 +414,28 @@ __device__ __forceinline__ bool simple_t(const rt_prim& p, const Ray& r, double 
         sphere_center(p, r, cx, cy, cz);
         return sphere_t(cx, cy, cz, p.p[3], r, t_min, t_max, t);
     } else {
+        const R q0 = (R)p.p[0], q1 = (R)p.p[1], q2 = (R)p.p[2], q3 = (R)p.p[3], q4 = (R)p.p[4];
         switch (p.kind) {
-        case RT_PRIM_XY_RECT: return rect_t(0, p.p[0], p.p[1], p.p[2], p.p[3], p.p[4], r, t_min, t_max, t);
-        case RT_PRIM_XZ_RECT: return rect_t(1, p.p[0], p.p[1], p.p[2], p.p[3], p.p[4], r, t_min, t_max, t);
-        case RT_PRIM_YZ_RECT: return rect_t(2, p.p[0], p.p[1], p.p[2], p.p[3], p.p[4], r, t_min, t_max, t);
+        case RT_PRIM_XY_RECT: return rect_t(0, q0, q1, q2, q3, q4, r, t_min, t_max, t);
+        case RT_PRIM_XZ_RECT: return rect_t(1, q0, q1, q2, q3, q4, r, t_min, t_max, t);
+        case RT_PRIM_YZ_RECT: return rect_t(2, q0, q1, q2, q3, q4, r, t_min, t_max, t);
         case RT_PRIM_BOX: return box_t(p, r, t_min, t_max, t, side);
         default: return false;
         }
     }
 }
 
-template <class C>
-__device__ __forceinline__ void simple_finish(const rt_prim& p, const Ray& r, double t, int side, Hit& h)
+template <class C, class R = typename C::Real>
+__device__ __forceinline__ void simple_finish(const rt_prim& p, const RayT<R>& r, R t, int side, HitT<R>& h)
 {
     if constexpr ((C::F & FEAT_RECT) != 0) {
         if (p.kind >= RT_PRIM_XY_RECT && p.kind <= RT_PRIM_YZ_RECT) {
-            rect_finish<C>(p.kind - RT_PRIM_XY_RECT, p.p[0], p.p[1], p.p[2], p.p[3], r, t, p.mat, h);
+            rect_finish<C>(p.kind - RT_PRIM_XY_RECT, (R)p.p[0], (R)p.p[1], (R)p.p[2], (R)p.p[3], r, t, p.mat, h);
             return;
         }
         if (p.kind == RT_PRIM_BOX) {
             int axis;
-            double a0, a1, b0, b1, k;
+            R a0, a1, b0, b1, k;
             box_side(p, side, axis, a0, a1, b0, b1, k);
             rect_finish<C>(axis, a0, a1, b0, b1, r, t, p.mat, h);
             return;
@@ -370,13 +443,14 @@ __device__ __forceinline__ void simple_finish(const rt_prim& p, const Ray& r, do
     }
     double cx, cy, cz;
     sphere_center(p, r, cx, cy, cz);
-    sphere_finish<C>(cx, cy, cz, p.p[4], r, t, p.mat, h);
+    sphere_finish<C>((R)cx, (R)cy, (R)cz, (R)p.p[4], r, t, p.mat, h);
 }
 
 // ---------------------------------------------------------------------------
 // BVH traversal
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ bool slab32(const float* lo, const float* hi, const Ray& r, float t_min, float t_max,
+template <class RayType>
+__device__ __forceinline__ bool slab32(const float* lo, const float* hi, const RayType& r, float t_min, float t_max,
                                        float& t_near)
 {
     const float x0 = __builtin_fmaf(lo[0], r.fix, r.fox), x1 = __builtin_fmaf(hi[0], r.fix, r.fox);
@@ -389,12 +463,14 @@ __device__ __forceinline__ bool slab32(const float* lo, const float* hi, const R
 }
 
 // f32 bounds of a double t range, rounded outward
-__device__ __forceinline__ float f32_down(double t)
+template <class R>
+__device__ __forceinline__ float f32_down(R t)
 {
     const float f = (float)t;
     return f > 0.0f ? f * (1.0f - 0x1.0p-20f) : f * (1.0f + 0x1.0p-20f);
 }
-__device__ __forceinline__ float f32_up(double t)
+template <class R>
+__device__ __forceinline__ float f32_up(R t)
 {
     const float f = (float)t;
     return f > 0.0f ? f * (1.0f + 0x1.0p-20f) : f * (1.0f - 0x1.0p-20f);
@@ -402,14 +478,14 @@ __device__ __forceinline__ float f32_up(double t)
 
 // Conservative slab test against an f32 box (rounded outward and padded on the
 // host), in f64. NaN products (0 * inf) are ignored by fmin/fmax.
-__device__ __forceinline__ bool slab(const float* lo, const float* hi, const Ray& r, double t_min, double t_max,
-                                     double& t_near)
+template <class R>
+__device__ __forceinline__ bool slab(const float* lo, const float* hi, const RayT<R>& r, R t_min, R t_max, R& t_near)
 {
-    const double x0 = ((double)lo[0] - r.ox) * r.ix, x1 = ((double)hi[0] - r.ox) * r.ix;
-    const double y0 = ((double)lo[1] - r.oy) * r.iy, y1 = ((double)hi[1] - r.oy) * r.iy;
-    const double z0 = ((double)lo[2] - r.oz) * r.iz, z1 = ((double)hi[2] - r.oz) * r.iz;
-    const double tn = fmax(fmax(fmin(x0, x1), fmin(y0, y1)), fmax(fmin(z0, z1), t_min));
-    const double tf = fmin(fmin(fmax(x0, x1), fmax(y0, y1)), fmin(fmax(z0, z1), t_max));
+    const R x0 = ((R)lo[0] - r.ox) * r.ix, x1 = ((R)hi[0] - r.ox) * r.ix;
+    const R y0 = ((R)lo[1] - r.oy) * r.iy, y1 = ((R)hi[1] - r.oy) * r.iy;
+    const R z0 = ((R)lo[2] - r.oz) * r.iz, z1 = ((R)hi[2] - r.oz) * r.iz;
+    const R tn = fmax(fmax(fmin(x0, x1), fmin(y0, y1)), fmax(fmin(z0, z1), t_min));
+    const R tf = fmin(fmin(fmax(x0, x1), fmax(y0, y1)), fmin(fmax(z0, z1), t_max));
     t_near = tn;
     return tn <= tf;
 }
@@ -438,9 +514,9 @@ __device__ __forceinline__ Node load_node(const rt_bvh_node* base, int i)
 // Closest hit in a BVH (nodes + leaf ranges of slots j, whose records are leaf_prims[j]).
 // `leaf(slot, t_max, best)` tests one primitive; on a closer hit it fills best (t and sub
 // ids) and returns true; best.prim is then the slot.
-template <class C, bool NL = false, class LeafFn>
-__device__ __forceinline__ bool traverse(const SceneDev& S, int root, const Ray& r, double t_min, double t_max,
-                                         HitRef& best, StackT<C>& stack, int sp0, Count& cnt, LeafFn&& leaf)
+template <class C, bool NL = false, class LeafFn, class R = typename C::Real>
+__device__ __forceinline__ bool traverse(const SceneDev& S, int root, const RayT<R>& r, R t_min, R t_max,
+                                         HitRefT<R>& best, StackT<C>& stack, int sp0, Count& cnt, LeafFn&& leaf)
 {
     // NL: this is the TLAS, whose first S.n_lds_nodes nodes (BFS order) were copied into
     // LDS at block start; deeper nodes are read from L1/L2
@@ -502,7 +578,7 @@ __device__ __forceinline__ bool traverse(const SceneDev& S, int root, const Ray&
             h1 = slab32(nd.lo1, nd.hi1, r, tmin_f, tmax_f, tn1);
             near0 = tn0 <= tn1;
         } else {
-            double tn0, tn1;
+            R tn0, tn1;
             h0 = slab(nd.lo0, nd.hi0, r, t_min, t_max, tn0);
             h1 = slab(nd.lo1, nd.hi1, r, t_min, t_max, tn1);
             near0 = tn0 <= tn1;
@@ -588,20 +664,21 @@ __device__ __forceinline__ bool traverse(const SceneDev& S, int root, const Ray&
 // ---------------------------------------------------------------------------
 // Translate / RotateY instances (hittable.rs:232-244, 386-415), outermost op first
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ void instance_ray(const rt_instance& in, Ray& r)
+template <class R>
+__device__ __forceinline__ void instance_ray(const rt_instance& in, RayT<R>& r)
 {
     const int n = in.n_ops;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         if (i < n) {
             if (in.op_kind[i] == RT_OP_TRANSLATE) {  // moved_ray = (o - offset, d, time)
-                r.ox = r.ox - in.op[i][0];
-                r.oy = r.oy - in.op[i][1];
-                r.oz = r.oz - in.op[i][2];
+                r.ox = r.ox - (R)in.op[i][0];
+                r.oy = r.oy - (R)in.op[i][1];
+                r.oz = r.oz - (R)in.op[i][2];
             } else {                                  // rotated_ray
-                const double s = in.op[i][0], c = in.op[i][1];
-                const double ox = c * r.ox - s * r.oz, oz = s * r.ox + c * r.oz;
-                const double dx = c * r.dx - s * r.dz, dz = s * r.dx + c * r.dz;
+                const R s = (R)in.op[i][0], c = (R)in.op[i][1];
+                const R ox = c * r.ox - s * r.oz, oz = s * r.ox + c * r.oz;
+                const R dx = c * r.dx - s * r.dz, dz = s * r.dx + c * r.dz;
                 r.ox = ox; r.oz = oz; r.dx = dx; r.dz = dz;
             }
         }
@@ -610,24 +687,24 @@ __device__ __forceinline__ void instance_ray(const rt_instance& in, Ray& r)
 
 // t-only: the closest hit of the instance's child; sub = BLAS prim (or the child prim),
 // side = winning box side.
-template <class C>
-__device__ bool instance_t(const SceneDev& S, const rt_instance& in, const Ray& ray, double t_min, double t_max,
-                           HitRef& ref, StackT<C>& stack, int sp0, Count& cnt)
+template <class C, class R = typename C::Real>
+__device__ bool instance_t(const SceneDev& S, const rt_instance& in, const RayT<R>& ray, R t_min, R t_max,
+                           HitRefT<R>& ref, StackT<C>& stack, int sp0, Count& cnt)
 {
-    Ray r = ray;
+    RayT<R> r = ray;
     instance_ray(in, r);
     finish_ray<C>(r, S.has_spheres != 0);
     if (in.child_kind == RT_CHILD_PRIM) {
         int side = 0;
-        if (!simple_t<C>(S.prims[in.child], r, t_min, t_max, ref.t, side, cnt)) return false;
+        if (!simple_t<InstC<C>>(S.prims[in.child], r, t_min, t_max, ref.t, side, cnt)) return false;
         ref.sub = in.child;
         ref.side = side;
         return true;
     }
-    HitRef inner;
+    HitRefT<R> inner;
     if (!traverse<C>(S, in.child, r, t_min, t_max, inner, stack, sp0, cnt,
-                     [&](int slot, double tmax, HitRef& b) {
-                         return simple_t<C>(S.leaf_prims[slot], r, t_min, tmax, b.t, b.side, cnt);
+                     [&](int slot, R tmax, HitRefT<R>& b) {
+                         return simple_t<InstC<C>>(S.leaf_prims[slot], r, t_min, tmax, b.t, b.side, cnt);
                      }))
         return false;
     ref.t = inner.t;
@@ -639,44 +716,46 @@ __device__ bool instance_t(const SceneDev& S, const rt_instance& in, const Ray& 
 // The ray direction after ops 0..i (only RotateY changes it; y never changes): recomputed
 // per op on the way back instead of kept in arrays through the child's finisher, which
 // held 8 f64 registers live and pushed the instance variants into scratch spills.
-__device__ __forceinline__ void dir_after(const rt_instance& in, const Ray& ray, int i, double& dx, double& dz)
+template <class R>
+__device__ __forceinline__ void dir_after(const rt_instance& in, const RayT<R>& ray, int i, R& dx, R& dz)
 {
     dx = ray.dx;
     dz = ray.dz;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         if (j <= i && j < in.n_ops && in.op_kind[j] != RT_OP_TRANSLATE) {
-            const double s = in.op[j][0], c = in.op[j][1];
-            const double x = c * dx - s * dz, z = s * dx + c * dz;
+            const R s = (R)in.op[j][0], c = (R)in.op[j][1];
+            const R x = c * dx - s * dz, z = s * dx + c * dz;
             dx = x;
             dz = z;
         }
     }
 }
 
-template <class C>
-__device__ void instance_finish(const SceneDev& S, const rt_instance& in, const Ray& ray, const HitRef& ref, Hit& h)
+template <class C, class R = typename C::Real>
+__device__ void instance_finish(const SceneDev& S, const rt_instance& in, const RayT<R>& ray, const HitRefT<R>& ref,
+                                HitT<R>& h)
 {
-    Ray r = ray;
+    RayT<R> r = ray;
     instance_ray(in, r);
     // ref.sub: the child prim (RT_CHILD_PRIM) or the BLAS leaf slot
-    simple_finish<C>(in.child_kind == RT_CHILD_PRIM ? S.prims[ref.sub] : S.leaf_prims[ref.sub], r, ref.t, ref.side,
-                     h);
+    simple_finish<InstC<C>>(in.child_kind == RT_CHILD_PRIM ? S.prims[ref.sub] : S.leaf_prims[ref.sub], r, ref.t,
+                            ref.side, h);
     const int n = in.n_ops;
 #pragma unroll
     for (int i = 3; i >= 0; --i) {
         if (i < n) {
-            double dx, dz;
+            R dx, dz;
             dir_after(in, ray, i, dx, dz);
             if (in.op_kind[i] == RT_OP_TRANSLATE) {  // rec.point += offset; set_face_normal(moved_ray, normal)
-                h.px = h.px + in.op[i][0];
-                h.py = h.py + in.op[i][1];
-                h.pz = h.pz + in.op[i][2];
+                h.px = h.px + (R)in.op[i][0];
+                h.py = h.py + (R)in.op[i][1];
+                h.pz = h.pz + (R)in.op[i][2];
                 set_face_normal(h, dx, ray.dy, dz, h.nx, h.ny, h.nz);
             } else {                                  // rotate back; set_face_normal(rotated_ray, normal)
-                const double s = in.op[i][0], c = in.op[i][1];
-                const double px = c * h.px + s * h.pz, pz = -s * h.px + c * h.pz;
-                const double nx = c * h.nx + s * h.nz, nz = -s * h.nx + c * h.nz;
+                const R s = (R)in.op[i][0], c = (R)in.op[i][1];
+                const R px = c * h.px + s * h.pz, pz = -s * h.px + c * h.pz;
+                const R nx = c * h.nx + s * h.nz, nz = -s * h.nx + c * h.nz;
                 h.px = px; h.pz = pz;
                 set_face_normal(h, dx, ray.dy, dz, nx, h.ny, nz);
             }
@@ -685,53 +764,56 @@ __device__ void instance_finish(const SceneDev& S, const rt_instance& in, const 
 }
 
 // t of a medium boundary (a simple prim or an instance).
-template <class C>
-__device__ __forceinline__ bool boundary_t(const SceneDev& S, int prim, const Ray& r, double t_min, double t_max,
-                                           double& t, StackT<C>& stack, int sp0, Count& cnt)
+template <class C, class R = typename C::Real>
+__device__ __forceinline__ bool boundary_t(const SceneDev& S, int prim, const RayT<R>& r, R t_min, R t_max, R& t,
+                                           StackT<C>& stack, int sp0, Count& cnt)
 {
     const rt_prim& p = S.prims[prim];
-    if constexpr ((C::F & FEAT_INST) != 0) {
+    if constexpr ((BoundC<C>::F & FEAT_INST) != 0) {
         if (p.kind == RT_PRIM_INSTANCE) {
-            HitRef ref;
+            HitRefT<R> ref;
             if (!instance_t<C>(S, S.instances[p.a], r, t_min, t_max, ref, stack, sp0, cnt)) return false;
             t = ref.t;
             return true;
         }
     }
     int side = 0;
-    return simple_t<C>(p, r, t_min, t_max, t, side, cnt);
+    return simple_t<BoundC<C>>(p, r, t_min, t_max, t, side, cnt);
 }
 
 // ConstantMedium (hittable.rs:417-473), keyed draw instead of the in-hit thread_rng().
-template <class C>
-__device__ bool medium_t(const SceneDev& S, const rt_prim& m, const Ray& r, double t_min, double t_max, double& t,
+template <class C, class R = typename C::Real>
+__device__ bool medium_t(const SceneDev& S, const rt_prim& m, const RayT<R>& r, R t_min, R t_max, R& t,
                          StackT<C>& stack, int sp0, const Keyed& key, Count& cnt)
 {
-    double t1, t2;
-    if (!boundary_t<C>(S, m.a, r, -RT_INF, RT_INF, t1, stack, sp0, cnt)) return false;
-    if (!boundary_t<C>(S, m.a, r, t1 + 0.0001, RT_INF, t2, stack, sp0, cnt)) return false;
+    R t1, t2;
+    if (!boundary_t<C>(S, m.a, r, (R)-RT_INF, (R)RT_INF, t1, stack, sp0, cnt)) return false;
+    if (!boundary_t<C>(S, m.a, r, t1 + (R)0.0001, (R)RT_INF, t2, stack, sp0, cnt)) return false;
     if (t1 < t_min) t1 = t_min;
     if (t2 > t_max) t2 = t_max;
     if (t1 >= t2) return false;
-    if (t1 < 0.0) t1 = 0.0;
-    const double ray_length = __builtin_sqrt(r.a);
-    const double distance_inside = (t2 - t1) * ray_length;
-    const double xi = rt_unit53(rt_keyed_u64(key.seed, key.pixel, key.sample, key.bounce,
-                                             RT_STREAM_MEDIUM + (uint32_t)m.b));
-    const double hit_distance = m.p[0] * rt_log(xi);
+    if (t1 < (R)0) t1 = (R)0;
+    const R ray_length = r_sqrt(r.a);
+    const R distance_inside = (t2 - t1) * ray_length;
+    const uint64_t bits = rt_keyed_u64(key.seed, key.pixel, key.sample, key.bounce, RT_STREAM_MEDIUM + (uint32_t)m.b);
+    R xi;
+    if constexpr (C::F32) xi = (float)(bits >> 40) * 0x1.0p-24f;   // [0, 1) in 2^-24 steps
+    else xi = rt_unit53(bits);
+    const R hit_distance = (R)m.p[0] * r_log(xi);
     if (hit_distance > distance_inside) return false;
     t = t1 + hit_distance / ray_length;
     return true;
 }
 
 // hittable.rs:452-463
-__device__ __forceinline__ void medium_finish(const rt_prim& m, const Ray& r, double t, Hit& h)
+template <class R>
+__device__ __forceinline__ void medium_finish(const rt_prim& m, const RayT<R>& r, R t, HitT<R>& h)
 {
     h.t = t;
     h.px = r.ox + r.dx * t;
     h.py = r.oy + r.dy * t;
     h.pz = r.oz + r.dz * t;
-    h.nx = 1.0; h.ny = 0.0; h.nz = 0.0;
+    h.nx = (R)1; h.ny = (R)0; h.nz = (R)0;
     h.front = 1;
     h.mat = m.mat;
     h.uvkind = 0;
@@ -739,15 +821,15 @@ __device__ __forceinline__ void medium_finish(const rt_prim& m, const Ray& r, do
 
 // hit_hittables(world, ray, 0.001, inf) (hittable.rs:43-55) over the TLAS, then the
 // HitRecord of the closest primitive.
-template <class C>
-__device__ bool trace_world(const SceneDev& S, const Ray& r, Hit& h, StackT<C>& stack, const Keyed& key,
+template <class C, class R = typename C::Real>
+__device__ bool trace_world(const SceneDev& S, const RayT<R>& r, HitT<R>& h, StackT<C>& stack, const Keyed& key,
                             Count& cnt)
 {
-    const double t_min = 0.001;
-    HitRef best;
+    const R t_min = (R)0.001;
+    HitRefT<R> best;
     best.sub = 0;
     best.side = 0;
-    auto leaf = [&](int slot, double tmax, HitRef& b) {
+    auto leaf = [&](int slot, R tmax, HitRefT<R>& b) {
         const rt_prim& p = S.leaf_prims[slot];
         if constexpr ((C::F & FEAT_INST) != 0)
             if (p.kind == RT_PRIM_INSTANCE)
@@ -756,7 +838,7 @@ __device__ bool trace_world(const SceneDev& S, const Ray& r, Hit& h, StackT<C>& 
             if (p.kind == RT_PRIM_MEDIUM) return medium_t<C>(S, p, r, t_min, tmax, b.t, stack, S.blas_base, key, cnt);
         return simple_t<C>(p, r, t_min, tmax, b.t, b.side, cnt);
     };
-    const bool hit = traverse<C, true>(S, S.tlas_root, r, t_min, RT_INF, best, stack, 0, cnt, leaf);
+    const bool hit = traverse<C, true>(S, S.tlas_root, r, t_min, (R)RT_INF, best, stack, 0, cnt, leaf);
     if (!hit) return false;
     const rt_prim& p = S.leaf_prims[best.prim];
     if constexpr ((C::F & FEAT_INST) != 0) {
@@ -778,18 +860,19 @@ __device__ bool trace_world(const SceneDev& S, const Ray& r, Hit& h, StackT<C>& 
 // ---------------------------------------------------------------------------
 // appearance: texture.rs:30-75, perlin.rs:32-108, material.rs:15-94
 // ---------------------------------------------------------------------------
-__device__ double perlin_noise(const double* ranvec, const int32_t* perm, double px, double py, double pz)
+template <class R>
+__device__ R perlin_noise(const double* ranvec, const int32_t* perm, R px, R py, R pz)
 {
-    const double fx = __builtin_floor(px), fy = __builtin_floor(py), fz = __builtin_floor(pz);
-    double u = px - fx, v = py - fy, w = pz - fz;
-    u = u * u * (3.0 - 2.0 * u);
-    v = v * v * (3.0 - 2.0 * v);
-    w = w * w * (3.0 - 2.0 * w);
-    const int32_t i = rt_sat_i32(fx), j = rt_sat_i32(fy), k = rt_sat_i32(fz);
-    const double uu = u * u * (3.0 - 2.0 * u);
-    const double vv = v * v * (3.0 - 2.0 * v);
-    const double ww = w * w * (3.0 - 2.0 * w);
-    double accum = 0.0;
+    const R fx = r_floor(px), fy = r_floor(py), fz = r_floor(pz);
+    R u = px - fx, v = py - fy, w = pz - fz;
+    u = u * u * ((R)3 - (R)2 * u);
+    v = v * v * ((R)3 - (R)2 * v);
+    w = w * w * ((R)3 - (R)2 * w);
+    const int32_t i = r_sat_i32(fx), j = r_sat_i32(fy), k = r_sat_i32(fz);
+    const R uu = u * u * ((R)3 - (R)2 * u);
+    const R vv = v * v * ((R)3 - (R)2 * v);
+    const R ww = w * w * ((R)3 - (R)2 * w);
+    R accum = (R)0;
 #pragma unroll
     for (int di = 0; di < 2; ++di)
 #pragma unroll
@@ -800,54 +883,61 @@ __device__ double perlin_noise(const double* ranvec, const int32_t* perm, double
                 const uint32_t yi = ((uint32_t)j + (uint32_t)dj) & 255u;
                 const uint32_t zi = ((uint32_t)k + (uint32_t)dk) & 255u;
                 const uint32_t idx = (uint32_t)(perm[xi] ^ perm[256 + yi] ^ perm[512 + zi]) & 255u;
-                const double cx = ranvec[3 * idx], cy = ranvec[3 * idx + 1], cz = ranvec[3 * idx + 2];
-                const double fi = (double)di, fj = (double)dj, fk = (double)dk;
-                const double wx = u - fi, wy = v - fj, wz = w - fk;
-                accum += (fi * uu + (1.0 - fi) * (1.0 - uu)) * (fj * vv + (1.0 - fj) * (1.0 - vv)) *
-                         (fk * ww + (1.0 - fk) * (1.0 - ww)) * (cx * wx + cy * wy + cz * wz);
+                const R cx = (R)ranvec[3 * idx], cy = (R)ranvec[3 * idx + 1], cz = (R)ranvec[3 * idx + 2];
+                const R fi = (R)di, fj = (R)dj, fk = (R)dk;
+                const R wx = u - fi, wy = v - fj, wz = w - fk;
+                accum += (fi * uu + ((R)1 - fi) * ((R)1 - uu)) * (fj * vv + ((R)1 - fj) * ((R)1 - vv)) *
+                         (fk * ww + ((R)1 - fk) * ((R)1 - ww)) * (cx * wx + cy * wy + cz * wz);
             }
     return accum;
 }
 
-__device__ double perlin_turb(const double* ranvec, const int32_t* perm, double px, double py, double pz)
+template <class R>
+__device__ R perlin_turb(const double* ranvec, const int32_t* perm, R px, R py, R pz)
 {
-    double accum = 0.0, weight = 1.0;
+    R accum = (R)0, weight = (R)1;
     for (int i = 0; i < 7; ++i) {
         accum += weight * perlin_noise(ranvec, perm, px, py, pz);
-        weight *= 0.5;
-        px = px * 2.0;
-        py = py * 2.0;
-        pz = pz * 2.0;
+        weight *= (R)0.5;
+        px = px * (R)2;
+        py = py * (R)2;
+        pz = pz * (R)2;
     }
-    return __builtin_fabs(accum);
+    return r_fabs(accum);
 }
 
-__device__ __forceinline__ double clampd(double x, double mn, double mx)
+template <class R>
+__device__ __forceinline__ R clampd(R x, R mn, R mx)
 {
     if (x < mn) return mn;
     if (x > mx) return mx;
     return x;
 }
 
-__device__ void hit_uv(const Hit& h, double& u, double& v)
+template <class R>
+__device__ void hit_uv(const HitT<R>& h, R& u, R& v)
 {
     if (h.uvkind == 1) {  // sphere_uv (math.rs:288-300)
-        const double theta = rt_acos(-h.uv1);
-        const double phi = rt_atan2(-h.uv2, h.uv0) + RT_PI;
-        u = phi / (2.0 * RT_PI);
-        v = theta / RT_PI;
+        const R theta = r_acos(-h.uv1);
+        const R phi = r_atan2(-h.uv2, h.uv0) + (R)RT_PI;
+        u = phi / ((R)2 * (R)RT_PI);
+        v = theta / (R)RT_PI;
     } else if (h.uvkind == 2) {
         u = h.uv0 / h.uv1;
         v = h.uv2 / h.uv3;
     } else {
-        u = 0.0;
-        v = 0.0;
+        u = (R)0;
+        v = (R)0;
     }
 }
 
 // texture.rs:35-41: sin(10x)*sin(10y)*sin(10z) < 0 from the three signs (rt_sin_sign);
 // the full product only when a factor may be tiny enough to underflow it
-__device__ __forceinline__ bool checker_odd(const Hit& h)
+__device__ __forceinline__ bool checker_odd(const HitT<float>& h)   // f32 mode: the product itself
+{
+    return sinf(10.0f * h.px) * sinf(10.0f * h.py) * sinf(10.0f * h.pz) < 0.0f;
+}
+__device__ __forceinline__ bool checker_odd(const HitT<double>& h)
 {
 #ifdef RT_PROBE_NO_CHECKER  // timing probe: NOT the product
     return h.px * h.pz < 0.0;
@@ -858,49 +948,49 @@ __device__ __forceinline__ bool checker_odd(const Hit& h)
     return sx * sy * sz < 0;
 }
 
-template <class C>
-__device__ void tex_value(const SceneDev& S, int ti, const Hit& h, double& cr, double& cg, double& cb)
+template <class C, class R = typename C::Real>
+__device__ void tex_value(const SceneDev& S, int ti, const HitT<R>& h, R& cr, R& cg, R& cb)
 {
     const rt_texture& t = S.textures[ti];
     if constexpr (!(C::F & (FEAT_NOISE | FEAT_IMAGE))) {
         if (t.kind == RT_TEX_CHECKER) {
             const double* c = checker_odd(h) ? t.c1 : t.c0;
-            cr = c[0]; cg = c[1]; cb = c[2];
+            cr = (R)c[0]; cg = (R)c[1]; cb = (R)c[2];
         } else {
-            cr = t.c0[0]; cg = t.c0[1]; cb = t.c0[2];
+            cr = (R)t.c0[0]; cg = (R)t.c0[1]; cb = (R)t.c0[2];
         }
         return;
     }
     switch (t.kind) {
-    case RT_TEX_SOLID: cr = t.c0[0]; cg = t.c0[1]; cb = t.c0[2]; return;
+    case RT_TEX_SOLID: cr = (R)t.c0[0]; cg = (R)t.c0[1]; cb = (R)t.c0[2]; return;
     case RT_TEX_CHECKER: {
-        if (checker_odd(h)) { cr = t.c1[0]; cg = t.c1[1]; cb = t.c1[2]; }
-        else { cr = t.c0[0]; cg = t.c0[1]; cb = t.c0[2]; }
+        if (checker_odd(h)) { cr = (R)t.c1[0]; cg = (R)t.c1[1]; cb = (R)t.c1[2]; }
+        else { cr = (R)t.c0[0]; cg = (R)t.c0[1]; cb = (R)t.c0[2]; }
         return;
     }
     case RT_TEX_NOISE: {
         const double* rv = S.perlin_ranvec + (size_t)t.perlin * 768;
         const int32_t* pm = S.perlin_perm + (size_t)t.perlin * 768;
-        const double s = 1.0 + rt_sin(t.scale * h.pz + 10.0 * perlin_turb(rv, pm, h.px, h.py, h.pz));
-        const double c = 1.0 * 0.5 * s;
+        const R s = (R)1 + r_sin((R)t.scale * h.pz + (R)10 * perlin_turb(rv, pm, h.px, h.py, h.pz));
+        const R c = (R)1 * (R)0.5 * s;
         cr = c; cg = c; cb = c;
         return;
     }
     default: {
-        if (t.img_w <= 0 || t.img_h <= 0) { cr = 0.0; cg = 1.0; cb = 1.0; return; }
-        double u, v;
+        if (t.img_w <= 0 || t.img_h <= 0) { cr = (R)0; cg = (R)1; cb = (R)1; return; }
+        R u, v;
         hit_uv(h, u, v);
-        u = clampd(u, 0.0, 1.0);
-        v = 1.0 - clampd(v, 0.0, 1.0);
-        uint64_t i = rt_sat_u64(u * (double)t.img_w);
-        uint64_t j = rt_sat_u64(v * (double)t.img_h);
+        u = clampd(u, (R)0, (R)1);
+        v = (R)1 - clampd(v, (R)0, (R)1);
+        uint64_t i = r_sat_u64(u * (R)t.img_w);
+        uint64_t j = r_sat_u64(v * (R)t.img_h);
         if (i >= (uint64_t)t.img_w) i = (uint64_t)t.img_w - 1;
         if (j >= (uint64_t)t.img_h) j = (uint64_t)t.img_h - 1;
         const uint8_t* px = S.image + t.img_offset + j * (uint64_t)t.img_bps + i * 3;
-        const double color_scale = 1.0 / 255.0;
-        cr = color_scale * (double)px[0];
-        cg = color_scale * (double)px[1];
-        cb = color_scale * (double)px[2];
+        const R color_scale = (R)1 / (R)255;
+        cr = color_scale * (R)px[0];
+        cg = color_scale * (R)px[1];
+        cb = color_scale * (R)px[2];
         return;
     }
     }
@@ -918,16 +1008,29 @@ __device__ __forceinline__ void ds_start(rt_pstream& st, uint64_t seed, uint32_t
 }
 __device__ __forceinline__ uint64_t ds_u64(rt_pstream& st) { return rt_pstream_u64(&st); }
 
+// The path's draws. f64: rand's Standard / gen_range mappings of 64-bit draws (math.rs:268-280,
+// rt_numerics.h); f32 mode: one 32-bit draw each, 24 significant bits.
+__device__ __forceinline__ double draw_unit(rt_pstream& st, double) { return rt_unit53(ds_u64(st)); }
+__device__ __forceinline__ float draw_unit(rt_pstream& st, float)
+{
+    return (float)(rt_pstream_u32(&st) >> 8) * 0x1.0p-24f;
+}
+__device__ __forceinline__ double draw_m11(rt_pstream& st, double scale_m11) { return rt_uniform_sample(ds_u64(st), -1.0, scale_m11); }
+__device__ __forceinline__ float draw_m11(rt_pstream& st, float)
+{
+    return (float)(rt_pstream_u32(&st) >> 8) * 0x1.0p-23f - 1.0f;
+}
+
 // math.rs:51-58: random_double_range(-1, 1) x 3 until inside
-__device__ __forceinline__ void random_in_unit_sphere(rt_pstream& st, double scale_m11, double& x, double& y,
-                                                      double& z, double& len2)
+template <class R>
+__device__ __forceinline__ void random_in_unit_sphere(rt_pstream& st, R scale_m11, R& x, R& y, R& z, R& len2)
 {
     for (;;) {
-        x = rt_uniform_sample(ds_u64(st), -1.0, scale_m11);
-        y = rt_uniform_sample(ds_u64(st), -1.0, scale_m11);
-        z = rt_uniform_sample(ds_u64(st), -1.0, scale_m11);
+        x = draw_m11(st, scale_m11);
+        y = draw_m11(st, scale_m11);
+        z = draw_m11(st, scale_m11);
         len2 = x * x + y * y + z * z;
-        if (len2 < 1.0) return;
+        if (len2 < (R)1) return;
     }
 }
 
@@ -935,8 +1038,34 @@ __device__ __forceinline__ void random_in_unit_sphere(rt_pstream& st, double sca
 // the integrator
 // ---------------------------------------------------------------------------
 
+// main.rs:517-520 + Camera::get_ray (camera.rs:58-66), f32 mode
+__device__ __forceinline__ void camera_ray(const KParams& P, int x, int y, rt_pstream& st, RayT<float>& r)
+{
+    const float u = ((float)x + draw_unit(st, 0.0f)) / (float)P.wm1;
+    const float v = ((float)y + draw_unit(st, 0.0f)) / (float)P.hm1;
+    float dxl, dyl;
+    for (;;) {
+        dxl = draw_m11(st, 0.0f);
+        dyl = draw_m11(st, 0.0f);
+        if (dxl * dxl + dyl * dyl < 1.0f) break;
+    }
+    const rt_camera& c = P.cam;
+    const float rdx = dxl * (float)c.lens_radius, rdy = dyl * (float)c.lens_radius;
+    const float offx = (float)c.u[0] * rdx + (float)c.v[0] * rdy;
+    const float offy = (float)c.u[1] * rdx + (float)c.v[1] * rdy;
+    const float offz = (float)c.u[2] * rdx + (float)c.v[2] * rdy;
+    r.ox = (float)c.origin[0] + offx;
+    r.oy = (float)c.origin[1] + offy;
+    r.oz = (float)c.origin[2] + offz;
+    // lower_left_corner - origin folded in f64 on the way (one rounding instead of two)
+    r.dx = (float)(c.lower_left_corner[0] - c.origin[0]) + (float)c.horizontal[0] * u + (float)c.vertical[0] * v - offx;
+    r.dy = (float)(c.lower_left_corner[1] - c.origin[1]) + (float)c.horizontal[1] * u + (float)c.vertical[1] * v - offy;
+    r.dz = (float)(c.lower_left_corner[2] - c.origin[2]) + (float)c.horizontal[2] * u + (float)c.vertical[2] * v - offz;
+    r.time = (float)c.time0 + draw_unit(st, 0.0f) * (float)(c.time1 - c.time0);
+}
+
 // main.rs:517-520 + Camera::get_ray (camera.rs:58-66)
-__device__ __forceinline__ void camera_ray(const KParams& P, int x, int y, rt_pstream& st, Ray& r)
+__device__ __forceinline__ void camera_ray(const KParams& P, int x, int y, rt_pstream& st, RayT<double>& r)
 {
 #ifdef RT_PROBE_FAST_CAMERA  // timing probe: NOT the product
     const double u = ((double)x + rt_unit53(ds_u64(st))) * __builtin_amdgcn_rcp((double)P.width - 1.0);
@@ -968,73 +1097,75 @@ __device__ __forceinline__ void camera_ray(const KParams& P, int x, int y, rt_ps
 // recursion unrolled into the throughput T. A path carries at most one emission (a
 // DiffuseLight ends it), so adding T*e straight into the chunk sum gives the same bits
 // as the reference's per-sample sum. Returns true if the path continues with r.
-template <class C>
-__device__ __forceinline__ bool shade(const SceneDev& S, const KParams& P, const Hit& h, Ray& r, rt_pstream& st,
-                                      double& Tr, double& Tg, double& Tb, double& sum_r, double& sum_g,
+template <class C, class R = typename C::Real>
+__device__ __forceinline__ bool shade(const SceneDev& S, const KParams& P, const HitT<R>& h, RayT<R>& r,
+                                      rt_pstream& st, R& Tr, R& Tg, R& Tb, double& sum_r, double& sum_g,
                                       double& sum_b)
 {
     const rt_material& m = S.materials[h.mat];
     const int kind = m.kind;
     if (kind == RT_MAT_DIFFUSE_LIGHT) {  // material.rs:25-34 (emits on both faces, never scatters)
-        double er, eg, eb;
+        R er, eg, eb;
         tex_value<C>(S, m.tex, h, er, eg, eb);
-        sum_r = sum_r + Tr * er;
-        sum_g = sum_g + Tg * eg;
-        sum_b = sum_b + Tb * eb;
+        sum_r = sum_r + (double)(Tr * er);   // the chunk sums stay f64 in the f32 mode too
+        sum_g = sum_g + (double)(Tg * eg);
+        sum_b = sum_b + (double)(Tb * eb);
         return false;
     }
     // The materials share their expensive steps, so a wave holding several materials runs
     // each once: one unit-sphere loop (Lambertian, Metal, Isotropic), one 1/sqrt (of the
     // candidate for Lambertian, of the ray direction for Metal and Dielectric), one texture
     // lookup (Lambertian, Isotropic).
-    double qx = 0.0, qy = 0.0, qz = 0.0, l2 = 1.0;
-    if (kind != RT_MAT_DIELECTRIC) random_in_unit_sphere(st, P.scale_m11, qx, qy, qz, l2);
+    R qx = (R)0, qy = (R)0, qz = (R)0, l2 = (R)1;
+    if (kind != RT_MAT_DIELECTRIC) random_in_unit_sphere(st, (R)P.scale_m11, qx, qy, qz, l2);
 #ifdef RT_PROBE_FAST_SHADE  // timing probe: NOT the product
-    const double inv = __builtin_amdgcn_rsq(kind == RT_MAT_LAMBERTIAN ? l2 : r.a);
+    const R inv = __builtin_amdgcn_rsq(kind == RT_MAT_LAMBERTIAN ? l2 : r.a);
 #else
-    const double inv = 1.0 / __builtin_sqrt(kind == RT_MAT_LAMBERTIAN ? l2 : r.a);
+    const R inv = (R)1 / r_sqrt(kind == RT_MAT_LAMBERTIAN ? l2 : r.a);
 #endif
-    double sdx, sdy, sdz, ar = 1.0, ag = 1.0, ab = 1.0;
+    R sdx, sdy, sdz, ar = (R)1, ag = (R)1, ab = (R)1;
     bool scattered = true;
     if (kind == RT_MAT_LAMBERTIAN) {  // material.rs:36-48
         sdx = h.nx + qx * inv;
         sdy = h.ny + qy * inv;
         sdz = h.nz + qz * inv;
-        if (__builtin_fabs(sdx) < 1e-8 && __builtin_fabs(sdy) < 1e-8 && __builtin_fabs(sdz) < 1e-8) {
+        if (r_fabs(sdx) < (R)1e-8 && r_fabs(sdy) < (R)1e-8 && r_fabs(sdz) < (R)1e-8) {
             sdx = h.nx; sdy = h.ny; sdz = h.nz;
         }
     } else if (kind == RT_MAT_METAL || kind == RT_MAT_DIELECTRIC) {
-        const double ux = r.dx * inv, uy = r.dy * inv, uz = r.dz * inv;  // normalize(r_in.direction)
+        const R ux = r.dx * inv, uy = r.dy * inv, uz = r.dz * inv;  // normalize(r_in.direction)
         if (kind == RT_MAT_METAL) {  // material.rs:50-60
-            const double k2 = 2.0 * (ux * h.nx + uy * h.ny + uz * h.nz);
-            sdx = (ux - h.nx * k2) + qx * m.fuzz;
-            sdy = (uy - h.ny * k2) + qy * m.fuzz;
-            sdz = (uz - h.nz * k2) + qz * m.fuzz;
-            scattered = sdx * h.nx + sdy * h.ny + sdz * h.nz > 0.0;
-            ar = m.albedo[0]; ag = m.albedo[1]; ab = m.albedo[2];
+            const R fuzz = (R)m.fuzz;
+            const R k2 = (R)2 * (ux * h.nx + uy * h.ny + uz * h.nz);
+            sdx = (ux - h.nx * k2) + qx * fuzz;
+            sdy = (uy - h.ny * k2) + qy * fuzz;
+            sdz = (uz - h.nz * k2) + qz * fuzz;
+            scattered = sdx * h.nx + sdy * h.ny + sdz * h.nz > (R)0;
+            ar = (R)m.albedo[0]; ag = (R)m.albedo[1]; ab = (R)m.albedo[2];
         } else {  // material.rs:62-82, 89-94
-            const double ratio = h.front ? (1.0 / m.ir) : m.ir;
-            const double cos_theta = fmin((-ux) * h.nx + (-uy) * h.ny + (-uz) * h.nz, 1.0);
-            const double sin_theta = __builtin_sqrt(1.0 - cos_theta * cos_theta);
-            const bool cannot_refract = ratio * sin_theta > 1.0;
+            const R ir = (R)m.ir;
+            const R ratio = h.front ? ((R)1 / ir) : ir;
+            const R cos_theta = r_fmin((-ux) * h.nx + (-uy) * h.ny + (-uz) * h.nz, (R)1);
+            const R sin_theta = r_sqrt((R)1 - cos_theta * cos_theta);
+            const bool cannot_refract = ratio * sin_theta > (R)1;
             bool reflect = cannot_refract;
             if (!reflect) {  // the draw is skipped on TIR (the || short-circuit of material.rs:72)
-                double r0 = (1.0 - ratio) / (1.0 + ratio);
+                R r0 = ((R)1 - ratio) / ((R)1 + ratio);
                 r0 = r0 * r0;
-                const double refl = r0 + (1.0 - r0) * rt_pow5(1.0 - cos_theta);
-                reflect = refl > rt_unit53(ds_u64(st));
+                const R refl = r0 + ((R)1 - r0) * r_pow5((R)1 - cos_theta);
+                reflect = refl > draw_unit(st, (R)0);
             }
             if (reflect) {
-                const double k2 = 2.0 * (ux * h.nx + uy * h.ny + uz * h.nz);
+                const R k2 = (R)2 * (ux * h.nx + uy * h.ny + uz * h.nz);
                 sdx = ux - h.nx * k2;
                 sdy = uy - h.ny * k2;
                 sdz = uz - h.nz * k2;
             } else {  // math.rs:110-117 (cos_theta recomputed there from the same inputs)
-                const double px = (ux + h.nx * cos_theta) * ratio;
-                const double py = (uy + h.ny * cos_theta) * ratio;
-                const double pz = (uz + h.nz * cos_theta) * ratio;
-                const double pl = px * px + py * py + pz * pz;
-                const double kk = -__builtin_sqrt(__builtin_fabs(1.0 - pl));
+                const R px = (ux + h.nx * cos_theta) * ratio;
+                const R py = (uy + h.ny * cos_theta) * ratio;
+                const R pz = (uz + h.nz * cos_theta) * ratio;
+                const R pl = px * px + py * py + pz * pz;
+                const R kk = -r_sqrt(r_fabs((R)1 - pl));
                 sdx = px + h.nx * kk;
                 sdy = py + h.ny * kk;
                 sdz = pz + h.nz * kk;
@@ -1095,13 +1226,17 @@ __device__ __forceinline__ bool lane_work(const KParams& P, LaneWork& w)
 #ifndef RT_MIN_WAVES_MEDIA
 #define RT_MIN_WAVES_MEDIA 3
 #endif
+#ifndef RT_MIN_WAVES_FINAL
+#define RT_MIN_WAVES_FINAL 3
+#endif
 // minimum waves per SIMD requested from the register allocator, per feature set
 template <class C>
 constexpr int min_waves()
 {
     return C::F == FEAT_SET_SPHERES ? RT_MIN_WAVES_SPHERES
            : C::F == FEAT_SET_RECTINST ? RT_MIN_WAVES_RECTINST
-           : C::F == FEAT_SET_MEDIA    ? RT_MIN_WAVES_MEDIA : RT_MIN_WAVES_ALL;
+           : C::F == FEAT_SET_MEDIA    ? RT_MIN_WAVES_MEDIA
+           : C::F == FEAT_SET_FINAL    ? RT_MIN_WAVES_FINAL : RT_MIN_WAVES_ALL;
 }
 
 // KParams comes by pointer: read where used (scalar loads) instead of pinning ~70 SGPRs
@@ -1126,11 +1261,12 @@ __global__ void __launch_bounds__(256, min_waves<C>()) trace_chunks(SceneDev S, 
     Count cnt{};
     uint64_t t_cam = 0, t_trace = 0, t_shade = 0, t_prev = 0;
     if (C::COUNT) t_prev = __builtin_amdgcn_s_memtime();
+    using R = typename C::Real;
     double sum_r = 0.0, sum_g = 0.0, sum_b = 0.0;
     Keyed key{P.seed, w.pixel, 0, 0};
     rt_pstream st;
-    Ray r;
-    double Tr = 1, Tg = 1, Tb = 1;
+    RayT<R> r;
+    R Tr = 1, Tg = 1, Tb = 1;
     int depth = 0;
     int s = w.s_begin;
     bool new_sample = true;
@@ -1142,7 +1278,7 @@ __global__ void __launch_bounds__(256, min_waves<C>()) trace_chunks(SceneDev S, 
             key.sample = (uint32_t)s;
             camera_ray(P, w.x, w.y, st, r);
             finish_ray<C>(r, S.has_spheres != 0);
-            Tr = Tg = Tb = 1.0;
+            Tr = Tg = Tb = (R)1;
             depth = P.max_depth;
         }
         if (C::COUNT) { const uint64_t t = __builtin_amdgcn_s_memtime(); t_cam += t - t_prev; t_prev = t; }
@@ -1150,7 +1286,7 @@ __global__ void __launch_bounds__(256, min_waves<C>()) trace_chunks(SceneDev S, 
         if (depth > 0) {  // main.rs:21-23: depth 0 is black
             key.bounce = (uint32_t)(P.max_depth - depth);
             if (C::COUNT) cnt.casts++;
-            Hit h;
+            HitT<R> h;
             const bool hit = trace_world<C>(S, r, h, stack, key, cnt);
             if (C::COUNT) { const uint64_t t = __builtin_amdgcn_s_memtime(); t_trace += t - t_prev; t_prev = t; }
             if (!hit) {  // main.rs:37: background
@@ -1235,7 +1371,11 @@ __global__ void __launch_bounds__(256, min_waves<C>()) trace_pool(SceneDev S, co
     if (C::COUNT) t_prev = __builtin_amdgcn_s_memtime();
     const int lane = threadIdx.x & 63;
     const unsigned n_tiles = (unsigned)P.tiles_x * (unsigned)P.tiles_y;
-    const unsigned n_blocks = n_tiles * (unsigned)P.n_chunks;
+    // a work block = one tile x block_chunks consecutive chunks (items chunk-major; the
+    // per-sample pool's units sample-major): lanes stay on one tile longer, and its rays
+    // are coherent (C2 item pool, chunks of 4: 108.4 ms with blocks of one chunk, 101.8 with 8)
+    const unsigned group = (unsigned)P.block_chunks;
+    const unsigned n_blocks = n_tiles * (((unsigned)P.n_chunks + group - 1) / group);
     const size_t n_px = (size_t)P.n_rows * (size_t)P.width;
     // current work block (wave-uniform)
     unsigned blk_units = 0, blk_next = 0, nvalid = 1;
@@ -1246,10 +1386,12 @@ __global__ void __launch_bounds__(256, min_waves<C>()) trace_pool(SceneDev S, co
     int x = 0, k = 0, s = 0, depth = 0;
     int left = 0;      // ITEMS: samples of the lane's item still to trace after the current one
     bool own = false;  // ITEMS: the lane's item has a next sample (taken before any new unit)
-    double cr = 0, cg = 0, cb = 0, Tr = 1, Tg = 1, Tb = 1;
+    using R = typename C::Real;
+    double cr = 0, cg = 0, cb = 0;
+    R Tr = 1, Tg = 1, Tb = 1;
     Keyed key{P.seed, 0, 0, 0};
     rt_pstream st;
-    Ray r;
+    RayT<R> r;
     for (;;) {
         if (ITEMS && own) {
             own = false;
@@ -1268,13 +1410,14 @@ __global__ void __launch_bounds__(256, min_waves<C>()) trace_pool(SceneDev S, co
                     exhausted = true;
                     break;
                 }
-                const unsigned chunk = b / n_tiles, tile = b - chunk * n_tiles;
+                const unsigned chunk = b / n_tiles * group, tile = b - (chunk / group) * n_tiles;
                 tx0 = (int)(tile % (unsigned)P.tiles_x) * 8;
                 tk0 = (int)(tile / (unsigned)P.tiles_x) * 8;
                 vw = min(8, P.width - tx0);
                 nvalid = (unsigned)(vw * min(8, P.n_rows - tk0));
                 s0 = P.sample_begin + (int)chunk * P.spp_chunk;
-                blk_units = ITEMS ? nvalid : nvalid * (unsigned)(min(P.spp, s0 + P.spp_chunk) - s0);
+                blk_units = ITEMS ? nvalid * min(group, (unsigned)P.n_chunks - chunk)
+                                  : nvalid * (unsigned)(min(P.spp, s0 + (int)group * P.spp_chunk) - s0);
                 blk_next = 0;
             }
             const unsigned rank = lanes_below(need);
@@ -1292,10 +1435,12 @@ __global__ void __launch_bounds__(256, min_waves<C>()) trace_pool(SceneDev S, co
                     x = tx0 + (int)(p % (unsigned)vw);
                     k = tk0 + (int)(p / (unsigned)vw);
                 }
-                s = s0 + (int)si;  // ITEMS: si = 0, the item's first sample
-                if constexpr (ITEMS) {
-                    left = min(P.spp, s0 + P.spp_chunk) - s0 - 1;
+                if constexpr (ITEMS) {  // si: the item's chunk within the block; s its first sample
+                    s = s0 + (int)si * P.spp_chunk;
+                    left = min(P.spp, s + P.spp_chunk) - s - 1;
                     cr = cg = cb = 0.0;
+                } else {
+                    s = s0 + (int)si;
                 }
                 active = true;
                 new_sample = true;
@@ -1318,7 +1463,7 @@ __global__ void __launch_bounds__(256, min_waves<C>()) trace_pool(SceneDev S, co
             ds_start(st, P.seed, key.pixel, (uint32_t)s);
             camera_ray(P, x, y, st, r);
             finish_ray<C>(r, S.has_spheres != 0);
-            Tr = Tg = Tb = 1.0;
+            Tr = Tg = Tb = (R)1;
             if constexpr (!ITEMS) cr = cg = cb = 0.0;  // ITEMS: the chunk's running sum
             depth = P.max_depth;
         }
@@ -1327,7 +1472,7 @@ __global__ void __launch_bounds__(256, min_waves<C>()) trace_pool(SceneDev S, co
         if (depth > 0) {  // main.rs:21-23: depth 0 is black
             key.bounce = (uint32_t)(P.max_depth - depth);
             if (C::COUNT) cnt.casts++;
-            Hit h;
+            HitT<R> h;
             const bool hit = trace_world<C>(S, r, h, stack, key, cnt);
             if (C::COUNT) { const uint64_t t = __builtin_amdgcn_s_memtime(); t_trace += t - t_prev; t_prev = t; }
             if (!hit) {  // main.rs:37: background
@@ -1409,7 +1554,7 @@ static unsigned resident_blocks(K kernel, size_t lds)
     return (unsigned)(cus * per_cu);
 }
 
-template <uint32_t F, bool S32, bool LDS, bool COUNT>
+template <uint32_t F, bool S32, bool LDS, bool COUNT, bool F32>
 static void launch_one(const Launch& L, hipStream_t stream, bool nall)
 {
     const SceneDev& S = *L.S;
@@ -1420,20 +1565,20 @@ static void launch_one(const Launch& L, hipStream_t stream, bool nall)
             hipLaunchKernelGGL(kernel, dim3(nb), dim3(256), lds, stream, S, L.P, L.out, L.counters, L.work);
         };
         if (L.pool == 2) {
-            if (nall) go(trace_pool<Cfg<F, S32, LDS, true, COUNT>, true>);
-            else go(trace_pool<Cfg<F, S32, LDS, false, COUNT>, true>);
+            if (nall) go(trace_pool<Cfg<F, S32, LDS, true, COUNT, F32>, true>);
+            else go(trace_pool<Cfg<F, S32, LDS, false, COUNT, F32>, true>);
         } else {
-            if (nall) go(trace_pool<Cfg<F, S32, LDS, true, COUNT>, false>);
-            else go(trace_pool<Cfg<F, S32, LDS, false, COUNT>, false>);
+            if (nall) go(trace_pool<Cfg<F, S32, LDS, true, COUNT, F32>, false>);
+            else go(trace_pool<Cfg<F, S32, LDS, false, COUNT, F32>, false>);
         }
         return;
     }
     const unsigned nb = (unsigned)((L.n_blocks + 3) / 4);
     if (nall)
-        hipLaunchKernelGGL((trace_chunks<Cfg<F, S32, LDS, true, COUNT>>), dim3(nb), dim3(256), lds, stream, S,
+        hipLaunchKernelGGL((trace_chunks<Cfg<F, S32, LDS, true, COUNT, F32>>), dim3(nb), dim3(256), lds, stream, S,
                            L.P, L.out, L.counters);
     else
-        hipLaunchKernelGGL((trace_chunks<Cfg<F, S32, LDS, false, COUNT>>), dim3(nb), dim3(256), lds, stream, S,
+        hipLaunchKernelGGL((trace_chunks<Cfg<F, S32, LDS, false, COUNT, F32>>), dim3(nb), dim3(256), lds, stream, S,
                            L.P, L.out, L.counters);
 }
 
@@ -1445,11 +1590,11 @@ static void launch_f(const Launch& L, int slab32, int lds, hipStream_t stream)
     const SceneDev& S = *L.S;
     const bool nall = S.n_lds_nodes > 0 && S.n_lds_nodes == S.n_tlas_nodes;
     if (slab32) {
-        if (lds) launch_one<F, true, true, COUNT>(L, stream, nall);
-        else launch_one<F, true, false, COUNT>(L, stream, nall);
+        if (lds) launch_one<F, true, true, COUNT, false>(L, stream, nall);
+        else launch_one<F, true, false, COUNT, false>(L, stream, nall);
     } else {
-        if (lds) launch_one<F, false, true, COUNT>(L, stream, nall);
-        else launch_one<F, false, false, COUNT>(L, stream, nall);
+        if (lds) launch_one<F, false, true, COUNT, false>(L, stream, nall);
+        else launch_one<F, false, false, COUNT, false>(L, stream, nall);
     }
 }
 
@@ -1461,16 +1606,37 @@ hipError_t launch_variant(const Launch& L, const LaunchOpts& o, hipStream_t stre
     launch_f<F, COUNT>(L, o.slab32, o.lds_stack, stream);
     return hipGetLastError();
 }
+
+// The f32 fast mode's kernels of one feature set (trace_f32_*.hip): f32 slab tests always
+// (an f32 path gains nothing from f64 boxes), no count variant.
+template <uint32_t F>
+hipError_t launch_variant_f32(const Launch& L, const LaunchOpts& o, hipStream_t stream)
+{
+    const bool nall = L.S->n_lds_nodes > 0 && L.S->n_lds_nodes == L.S->n_tlas_nodes;
+    if (o.lds_stack) launch_one<F, true, true, false, true>(L, stream, nall);
+    else launch_one<F, true, false, false, true>(L, stream, nall);
+    return hipGetLastError();
+}
 #define RT_VARIANT_DECL(F, COUNT) \
     extern template hipError_t launch_variant<F, COUNT>(const Launch&, const LaunchOpts&, hipStream_t);
+#define RT_VARIANT_F32_DECL(F) \
+    extern template hipError_t launch_variant_f32<F>(const Launch&, const LaunchOpts&, hipStream_t);
 RT_VARIANT_DECL(FEAT_SET_SPHERES, false)
 RT_VARIANT_DECL(FEAT_SET_SPHERES, true)
 RT_VARIANT_DECL(FEAT_SET_RECTINST, false)
 RT_VARIANT_DECL(FEAT_SET_RECTINST, true)
 RT_VARIANT_DECL(FEAT_SET_MEDIA, false)
 RT_VARIANT_DECL(FEAT_SET_MEDIA, true)
+RT_VARIANT_DECL(FEAT_SET_FINAL, false)
+RT_VARIANT_DECL(FEAT_SET_FINAL, true)
 RT_VARIANT_DECL(FEAT_ALL, false)
 RT_VARIANT_DECL(FEAT_ALL, true)
+RT_VARIANT_F32_DECL(FEAT_SET_SPHERES)
+RT_VARIANT_F32_DECL(FEAT_SET_RECTINST)
+RT_VARIANT_F32_DECL(FEAT_SET_MEDIA)
+RT_VARIANT_F32_DECL(FEAT_SET_FINAL)
+RT_VARIANT_F32_DECL(FEAT_ALL)
 #undef RT_VARIANT_DECL
+#undef RT_VARIANT_F32_DECL
 
 }  // namespace rtk

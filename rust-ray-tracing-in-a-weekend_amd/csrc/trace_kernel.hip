@@ -126,7 +126,7 @@ __global__ void eval_numerics(int fn, const double* x, const double* y, const do
     case 3: r = rt_atan2(x[i], y[i]); break;
     case 4: r = rt_acos(x[i]); break;
     case 5: case 6: {
-        Hit h;
+        HitT<double> h;
         h.uvkind = 1;
         h.uv0 = x[i]; h.uv1 = y[i]; h.uv2 = z[i];
         double u, v;
@@ -154,6 +154,7 @@ uint32_t variant_features(uint32_t scene_features)
     if ((scene_features & ~FEAT_SET_SPHERES) == 0) return FEAT_SET_SPHERES;
     if ((scene_features & ~FEAT_SET_RECTINST) == 0) return FEAT_SET_RECTINST;
     if ((scene_features & ~FEAT_SET_MEDIA) == 0) return FEAT_SET_MEDIA;
+    if ((scene_features & ~FEAT_SET_FINAL) == 0) return FEAT_SET_FINAL;
     return FEAT_ALL;
 }
 
@@ -167,7 +168,9 @@ hipError_t launch_trace(const SceneDev& S, const KParams& Ph, const KParams* P, 
     L.counters = counters;
     L.work = work;
     L.pool = o.pool;
-    L.n_blocks = (unsigned long long)Ph.tiles_x * Ph.tiles_y * Ph.n_chunks;  // waves of the chunk schedule
+    // waves of the chunk schedule / work blocks of the pools
+    const int group = o.pool ? std::max(1, Ph.block_chunks) : 1;
+    L.n_blocks = (unsigned long long)Ph.tiles_x * Ph.tiles_y * ((Ph.n_chunks + group - 1) / group);
     if (L.n_blocks == 0) return hipSuccess;
     if (L.n_blocks > 0xfffffff0ULL) return hipErrorInvalidValue;
     if (o.pool) {
@@ -175,15 +178,24 @@ hipError_t launch_trace(const SceneDev& S, const KParams& Ph, const KParams* P, 
         if (e != hipSuccess) return e;
     }
     const uint32_t f = variant_features(o.features);
+    if (o.f32) {
+        if (f == FEAT_SET_SPHERES) return launch_variant_f32<FEAT_SET_SPHERES>(L, o, stream);
+        if (f == FEAT_SET_RECTINST) return launch_variant_f32<FEAT_SET_RECTINST>(L, o, stream);
+        if (f == FEAT_SET_MEDIA) return launch_variant_f32<FEAT_SET_MEDIA>(L, o, stream);
+        if (f == FEAT_SET_FINAL) return launch_variant_f32<FEAT_SET_FINAL>(L, o, stream);
+        return launch_variant_f32<FEAT_ALL>(L, o, stream);
+    }
     if (o.count) {
         if (f == FEAT_SET_SPHERES) return launch_variant<FEAT_SET_SPHERES, true>(L, o, stream);
         if (f == FEAT_SET_RECTINST) return launch_variant<FEAT_SET_RECTINST, true>(L, o, stream);
         if (f == FEAT_SET_MEDIA) return launch_variant<FEAT_SET_MEDIA, true>(L, o, stream);
+        if (f == FEAT_SET_FINAL) return launch_variant<FEAT_SET_FINAL, true>(L, o, stream);
         return launch_variant<FEAT_ALL, true>(L, o, stream);
     }
     if (f == FEAT_SET_SPHERES) return launch_variant<FEAT_SET_SPHERES, false>(L, o, stream);
     if (f == FEAT_SET_RECTINST) return launch_variant<FEAT_SET_RECTINST, false>(L, o, stream);
     if (f == FEAT_SET_MEDIA) return launch_variant<FEAT_SET_MEDIA, false>(L, o, stream);
+    if (f == FEAT_SET_FINAL) return launch_variant<FEAT_SET_FINAL, false>(L, o, stream);
     return launch_variant<FEAT_ALL, false>(L, o, stream);
 }
 

@@ -41,6 +41,7 @@ struct KParams {
     int32_t row_begin, row_stride, n_rows;
     int32_t tiles_x, tiles_y;   // 8x8 pixel tiles over (width, n_rows)
     int32_t sample_begin;       // chunk c covers samples [sample_begin + c*spp_chunk, ..) up to spp
+    int32_t block_chunks;       // pools: chunks per work block (a block = one tile x this many chunks)
 };
 
 // Scene features (which code a kernel variant must contain).
@@ -50,10 +51,14 @@ enum : uint32_t {
     FEAT_MEDIUM = 4,    // ConstantMedium
     FEAT_NOISE = 8,     // Perlin noise texture
     FEAT_IMAGE = 16,    // image texture
-    FEAT_ALL = 31,
-    FEAT_SET_SPHERES = 0,                      // compiled variant: spheres + solid/checker
-    FEAT_SET_RECTINST = FEAT_RECT | FEAT_INST,  // compiled variant: + rects, boxes, instances
-    FEAT_SET_MEDIA = FEAT_SET_RECTINST | FEAT_MEDIUM  // compiled variant: + constant media
+    FEAT_INST_RECT = 32,    // rects or boxes inside an instance (its child prim or BLAS)
+    FEAT_MEDIUM_INST = 64,  // a medium boundary that is not a sphere (box, rect, instance)
+    FEAT_ALL = 127,
+    FEAT_SET_SPHERES = 0,                                          // compiled variant: spheres + solid/checker
+    FEAT_SET_RECTINST = FEAT_RECT | FEAT_INST | FEAT_INST_RECT,    // + rects, boxes, instances (Cornell)
+    FEAT_SET_MEDIA = FEAT_SET_RECTINST | FEAT_MEDIUM | FEAT_MEDIUM_INST,  // + constant media (Cornell smoke)
+    // + Perlin and image textures, instances over spheres, media bounded by spheres (final scene)
+    FEAT_SET_FINAL = FEAT_RECT | FEAT_INST | FEAT_MEDIUM | FEAT_NOISE | FEAT_IMAGE
 };
 
 struct LaunchOpts {
@@ -62,6 +67,7 @@ struct LaunchOpts {
     int lds_stack;      // traversal stack in LDS (1) or scratch (0)
     int count;          // count_work variant
     int pool;           // RT_SCHED_*: 0 chunks, 1 per-sample pool (per-sample output), 2 item pool (partials)
+    int f32;            // the f32 fast mode (RT_PREC_F32)
 };
 
 uint32_t variant_features(uint32_t scene_features);

@@ -36,6 +36,8 @@ RT_SCHED_CHUNKS = 0
 RT_SCHED_POOL = 1
 RT_SCHED_ITEMS = 2
 RT_SCHED_AUTO = 3
+RT_PREC_F64 = 0
+RT_PREC_F32 = 1
 RT_ACCEL_SAH = 0
 RT_ACCEL_LINEAR = 1     # hit_hittables linear scan (hittable.rs:31-41)
 RT_ACCEL_MEDIAN = 2     # the reference BvhNode hierarchy (hittable.rs:77-130)
@@ -52,7 +54,7 @@ EXPORTED = [
     "rt_scene_preset_get", "rt_scene_camera", "rt_world_flatten", "rt_ctx_upload_soa",
     "rt_ctx_upload_world", "rt_render", "rt_rows_in_shard", "rt_last_stats", "rt_write_ppm",
     "rt_ctx_set_variant", "rt_device_eval", "rt_accum_create", "rt_accum_destroy", "rt_accum_add",
-    "rt_accum_get", "rt_accum_set", "rt_accum_resolve", "rt_render_progressive", "rt_ctx_set_schedule",
+    "rt_accum_get", "rt_accum_set", "rt_accum_resolve", "rt_render_progressive", "rt_ctx_set_schedule", "rt_ctx_set_precision",
     "rt_scene_validate",
 ]
 
@@ -122,7 +124,7 @@ class Stats(ctypes.Structure):
                 ("schedule", ctypes.c_int32), ("n_batches", ctypes.c_int32),
                 ("wave_leaf_steps", ctypes.c_uint64), ("camera_lanes", ctypes.c_uint64),
                 ("camera_steps", ctypes.c_uint64), ("shade_lanes", ctypes.c_uint64),
-                ("shade_steps", ctypes.c_uint64)]
+                ("shade_steps", ctypes.c_uint64), ("precision", ctypes.c_int32), ("pad_", ctypes.c_int32)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -171,6 +173,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "rt_device_eval": ([P, I, P, P, P, P, I], I), "rt_ctx_set_variant": ([P, I, I, I], I),
         "rt_accum_create": ([P, ctypes.POINTER(RenderParams), ctypes.POINTER(P)], I),
         "rt_ctx_set_schedule": ([P, I], I),
+        "rt_ctx_set_precision": ([P, I], I),
         "rt_accum_destroy": ([P], None),
         "rt_accum_add": ([P, P, ctypes.POINTER(Camera), ctypes.POINTER(RenderParams), I], I),
         "rt_accum_get": ([P, P, ctypes.POINTER(ctypes.c_int64)], I),
@@ -425,6 +428,10 @@ class Renderer:
 
     def set_schedule(self, schedule: int):
         _check(self.lib.rt_ctx_set_schedule(self.h, schedule), "rt_ctx_set_schedule")
+
+    def set_precision(self, precision: int):
+        """RT_PREC_F64 (default, bit-exact against the oracle) or RT_PREC_F32 (fast mode)."""
+        _check(self.lib.rt_ctx_set_precision(self.h, precision), "rt_ctx_set_precision")
 
     def set_variant(self, slab32: int = 1, lds_stack: int = 1, lds_nodes: int = 1):
         _check(self.lib.rt_ctx_set_variant(self.h, slab32, lds_stack, lds_nodes), "rt_ctx_set_variant")

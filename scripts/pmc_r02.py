@@ -137,7 +137,7 @@ def bench(d, tag, workload, note=""):
     import __graft_entry__ as ge
 
     def sel(name):
-        m = re.search(r"(trace_pool|trace_chunks)<rtk::Cfg<(\d+)u, (\w+), (\w+), (\w+), (\w+)>", name)
+        m = re.search(r"(trace_pool|trace_chunks)<rtk::Cfg<(\d+)u, (\w+), (\w+), (\w+), (\w+)(?:, (\w+))?>", name)
         if not m or m.group(6) == "true":      # skip the count_work variant
             return None
         return m.group(1)
@@ -152,7 +152,7 @@ def bench(d, tag, workload, note=""):
     if os.path.exists(stats):
         shutil.copy(stats, os.path.join(REPO, "profiles", f"{tag}_kernel_stats.csv"))
         for r in csv.DictReader(open(stats)):
-            if kern in r["Name"] and ", false>" in r["Name"].split("(")[0]:
+            if sel(r["Name"]) == kern:
                 avg_ns = float(r["AverageNs"])
     cycles = c["GRBM_GUI_ACTIVE"] / 8.0
     clk = cycles / (dur_ns * 1e-9) / 1e9
@@ -160,7 +160,13 @@ def bench(d, tag, workload, note=""):
     write = c.get("WRITE_SIZE", 0.0) * 1024
     dram = 2 * fetch + write
     doc = load()
-    entry = {"tag": tag, "src_hash": ge.source_hash(), "workload": workload, "kernel": knames[kern],
+    src_hash = ge.source_hash()
+    kt_log = os.path.join(d, "kt.log")   # the profiled bench's own line names the build it ran
+    if os.path.exists(kt_log):
+        for line in open(kt_log):
+            if line.startswith("{"):
+                src_hash = json.loads(line)["roofline"].get("src_hash", src_hash)
+    entry = {"tag": tag, "src_hash": src_hash, "workload": workload, "kernel": knames[kern],
              "kernel_ms": (avg_ns or dur_ns) / 1e6, "pmc_dispatch_ms": dur_ns / 1e6, "clock_ghz": clk,
              "dram_bytes": dram, "fetch_bytes_raw": fetch, "write_bytes": write, "counters": c, "note": note}
     doc["entries"] = [e for e in doc["entries"] if not (e["src_hash"] == entry["src_hash"] and

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Per-kernel register / scratch / occupancy of trace_kernel.hip (compiler remarks), compact.
 
-usage: python scripts/res_usage.py [-DRT_TRACE_LOOP=2 ...]   (extra hipcc flags)
+usage: [RT_VARIANT_SRC=trace_v_spheres.hip] python scripts/res_usage.py [-DRT_TRACE_LOOP=2 ...]   (extra hipcc flags)
 """
 import os
 import re
@@ -9,7 +9,8 @@ import subprocess
 import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-src = os.path.join(REPO, "rust-ray-tracing-in-a-weekend_amd", "csrc", "trace_kernel.hip")
+CSRC = os.path.join(REPO, "rust-ray-tracing-in-a-weekend_amd", "csrc")
+src = os.path.join(CSRC, os.environ.get("RT_VARIANT_SRC", "trace_v_all.hip"))
 cmd = ["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math",
        "--offload-arch=gfx950", "-I" + os.path.join(REPO, "include"), "--cuda-device-only", "-c", src,
        "-o", "/tmp/res_usage.o", "-Rpass-analysis=kernel-resource-usage", *sys.argv[1:]]

@@ -7,6 +7,8 @@ diverged sample would move a pixel by ~1e-2, so this checks path identity; what 
 left is only the summation order of the bounce loop (iterative on the GPU, recursive
 in the reference).
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -184,6 +186,33 @@ def test_kernel_variants_identical(rt, renderer, scene_id, W, H):
     assert_parity(imgs[0], ob.render(scene_id, W, H, 4), f"variants scene {scene_id}")
 
 
+@pytest.mark.parametrize("scene_id,W,H,feat", [(0, 40, 24, 0), (5, 24, 24, 1 | 2 | 32), (6, 24, 24, 1 | 2 | 4 | 32 | 64),
+                                              (7, 32, 18, 31)])
+def test_feature_set_variants_identical(rt, renderer, scene_id, W, H, feat):
+    """Each scene runs on the smallest feature-set variant covering it (final scene: instances
+    over spheres only, media bounded by spheres); the all-features variant, which no reference
+    scene selects, renders the same bits (RT_EXTRA_FEATURES forces it)."""
+    world = rt.World(1).build_scene(scene_id)
+    cam, bg = rt.scene_camera(scene_id, W, H)
+    p = rt.Renderer.params(W, H, 4, 50, bg, 1, out_format=rt.RT_OUT_F64)
+    renderer.upload(world)
+    img = renderer.render(cam, p)
+    assert renderer.stats().variant_features == feat
+    os.environ["RT_EXTRA_FEATURES"] = "127"
+    try:
+        big = rt.Renderer(0)
+    finally:
+        del os.environ["RT_EXTRA_FEATURES"]
+    try:
+        big.upload(world)
+        img_all = big.render(cam, p)
+        assert big.stats().variant_features == 127
+    finally:
+        big.close()
+    assert np.array_equal(img, img_all)
+    assert_parity(img, ob.render(scene_id, W, H, 4), f"feature variant scene {scene_id}")
+
+
 def _golden_cases():
     from tests.golden import make_golden as mg
     return mg.CASES, mg.key
@@ -319,15 +348,20 @@ def test_schedules_render_identically(rt, scene_id, W, H, spp):
         small = rt.Renderer(0)                       # reads the buffer bound at creation
     finally:
         os.environ.pop("RT_SAMPLE_BUF_MB")
+    os.environ["RT_BLOCK_CHUNKS"] = "3"
+    try:
+        grouped = rt.Renderer(0)                     # item-pool blocks of 3 chunks per tile
+    finally:
+        os.environ.pop("RT_BLOCK_CHUNKS")
     r = rt.Renderer(0)
     runs = [(r, rt.RT_SCHED_CHUNKS), (r, rt.RT_SCHED_POOL), (r, rt.RT_SCHED_ITEMS), (small, rt.RT_SCHED_POOL),
-            (small, rt.RT_SCHED_ITEMS)]
+            (small, rt.RT_SCHED_ITEMS), (grouped, rt.RT_SCHED_ITEMS), (r, rt.RT_SCHED_AUTO)]
     for rr, sched in runs:
         rr.set_schedule(sched)
         rr.upload(world)
         imgs.append(rr.render(cam, rt.Renderer.params(W, H, spp, 50, bg, 1, row_begin=1, row_stride=2,
                                                       out_format=rt.RT_OUT_F64)))
-        assert rr.stats().schedule == sched
+        assert rr.stats().schedule == (sched if sched != rt.RT_SCHED_AUTO else rt.RT_SCHED_POOL)
     for im in imgs[1:]:
         assert np.array_equal(imgs[0], im)
     q = rt.Renderer.params(64, 48, 40, 50, bg, 1, out_format=rt.RT_OUT_F64)   # 73.7 KB per sample
@@ -349,6 +383,11 @@ def test_schedules_render_identically(rt, scene_id, W, H, spp):
     b2 = small.render(cam, q2)
     assert small.stats().n_batches == 12
     assert np.array_equal(b2, r.render(cam, q2))
+    grouped.set_schedule(rt.RT_SCHED_ITEMS)
+    assert np.array_equal(grouped.render(cam, q2), b2)
+    grouped.upload(world)
+    assert np.array_equal(grouped.render(cam, q), one)   # 40 spp: chunks of 3, groups of 3 chunks
+    grouped.close()
     assert_parity(imgs[2], ob.render(scene_id, W, H, spp, row_begin=1, row_stride=2), f"items scene {scene_id}")
 
 
