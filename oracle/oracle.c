@@ -1166,6 +1166,9 @@ static double now_s(void)
     return ts.tv_sec + 1e-9 * ts.tv_nsec;
 }
 
+static int render_world(const orc_params* p, const World* w, const Camera* cam, V3 background, double* out_mean,
+                        orc_stats* stats);
+
 int orc_render(const orc_params* p, double* out_mean, orc_stats* stats)
 {
     if (!p || !out_mean || p->width < 2 || p->height < 2 || p->spp < 1 || p->row_stride < 1 || p->row_begin < 0)
@@ -1177,6 +1180,18 @@ int orc_render(const orc_params* p, double* out_mean, orc_stats* stats)
     if (build_world(&w, p->scene_id, p->scene_seed, p->image_rgb, p->image_w, p->image_h)) return -1;
     double aspect = (double)p->width / (double)p->height;
     Camera cam = camera_new(sp.look_from, sp.look_at, v3(0.0, 1.0, 0.0), sp.vfov, aspect, 0.1, 10.0, 0.0, 1.0);
+    int rc = render_world(p, &w, &cam, sp.background, out_mean, stats);
+    world_free(&w);
+    return rc;
+}
+
+/* main.rs:466-551 for a built world, camera and background */
+static int render_world(const orc_params* p, const World* wp, const Camera* camp, V3 background, double* out_mean,
+                        orc_stats* stats)
+{
+    const World w = *wp;
+    const Camera cam = *camp;
+    const ScenePreset sp = {v3(0, 0, 0), v3(0, 0, 0), background, 0.0};
     int n_rows = p->row_begin < p->height ? (p->height - p->row_begin + p->row_stride - 1) / p->row_stride : 0;
     int T = p->threads > 0 ? p->threads : 1;
     double t0 = now_s();
@@ -1219,7 +1234,6 @@ int orc_render(const orc_params* p, double* out_mean, orc_stats* stats)
         stats->seconds = t1 - t0;
     }
     free(jobs); free(th); free(bufs);
-    world_free(&w);
     return 0;
 }
 
@@ -1314,4 +1328,154 @@ int orc_camera(int scene_id, int width, int height, double* o)
     o[22] = c.time0;
     o[23] = c.time1;
     return 0;
+}
+
+/* ------------------------------------------------------------------------- */
+/* world builder: the reference's constructor surface (main.rs:40-50,         */
+/* hittable.rs:77-207, material.rs:6-12, texture.rs:4-22) for custom worlds   */
+/* ------------------------------------------------------------------------- */
+struct orc_world {
+    World w;
+    OrcRng rng;                /* construction draws: Perlin::new, the BVH's random axis */
+    Texture* tex; int n_tex, cap_tex;
+    const Hittable** ids; int n_ids, cap_ids;
+};
+
+static int ow_add(orc_world* o, const Hittable* h)
+{
+    if (o->n_ids == o->cap_ids) {
+        o->cap_ids = o->cap_ids ? 2 * o->cap_ids : 64;
+        o->ids = (const Hittable**)realloc(o->ids, (size_t)o->cap_ids * sizeof(void*));
+    }
+    o->ids[o->n_ids] = h;
+    return o->n_ids++;
+}
+static int ow_tex(orc_world* o, Texture t)
+{
+    if (o->n_tex == o->cap_tex) {
+        o->cap_tex = o->cap_tex ? 2 * o->cap_tex : 16;
+        o->tex = (Texture*)realloc(o->tex, (size_t)o->cap_tex * sizeof(Texture));
+    }
+    o->tex[o->n_tex] = t;
+    return o->n_tex++;
+}
+static const Hittable* ow_get(const orc_world* o, int id) { return (id >= 0 && id < o->n_ids) ? o->ids[id] : NULL; }
+
+int orc_world_create(uint64_t scene_seed, orc_world** out)
+{
+    orc_world* o = (orc_world*)calloc(1, sizeof(orc_world));
+    if (!o) return -1;
+    rt_stream_init(&o->rng.s, scene_seed, 0, 0, RT_STREAM_SCENE);   /* as build_world */
+    o->rng.seed = scene_seed;
+    *out = o;
+    return 0;
+}
+void orc_world_destroy(orc_world* o)
+{
+    if (!o) return;
+    world_free(&o->w);
+    free(o->tex);
+    free(o->ids);
+    free(o);
+}
+int orc_world_texture(orc_world* o, int kind, const double c0[3], const double c1[3], double scale)
+{
+    switch (kind) {
+    case TEX_SOLID: return ow_tex(o, tex_solid(v3(c0[0], c0[1], c0[2])));
+    case TEX_CHECKER: return ow_tex(o, tex_checker(v3(c0[0], c0[1], c0[2]), v3(c1[0], c1[1], c1[2])));
+    case TEX_NOISE: {
+        OrcRng* saved = tl_rng;
+        tl_rng = &o->rng;
+        Perlin* p = world_perlin(&o->w);
+        tl_rng = saved;
+        return ow_tex(o, tex_noise(p, scale));
+    }
+    default: return -1;
+    }
+}
+int orc_world_material(orc_world* o, int kind, int tex, const double albedo[3], double fuzz, double ir)
+{
+    Texture t;
+    memset(&t, 0, sizeof t);
+    if (kind == MAT_LAMBERTIAN || kind == MAT_DIFFUSE_LIGHT || kind == MAT_ISOTROPIC) {
+        if (tex < 0 || tex >= o->n_tex) return -1;
+        t = o->tex[tex];
+    }
+    switch (kind) {
+    case MAT_LAMBERTIAN: return register_material(&o->w, mat_lambertian(t));
+    case MAT_METAL: return register_material(&o->w, mat_metal(v3(albedo[0], albedo[1], albedo[2]), fuzz));
+    case MAT_DIELECTRIC: return register_material(&o->w, mat_dielectric(ir));
+    case MAT_DIFFUSE_LIGHT: return register_material(&o->w, mat_light(t));
+    case MAT_ISOTROPIC: return register_material(&o->w, mat_isotropic(t));
+    default: return -1;
+    }
+}
+int orc_world_sphere(orc_world* o, int mat, const double c[3], double r)
+{
+    return ow_add(o, h_sphere(&o->w, mat, v3(c[0], c[1], c[2]), r));
+}
+int orc_world_moving_sphere(orc_world* o, int mat, const double c0[3], const double c1[3], double t0, double t1,
+                            double r)
+{
+    return ow_add(o, h_moving_sphere(&o->w, mat, v3(c0[0], c0[1], c0[2]), v3(c1[0], c1[1], c1[2]), t0, t1, r));
+}
+int orc_world_rect(orc_world* o, int axis, int mat, double a0, double a1, double b0, double b1, double k)
+{
+    const int kind = axis == 0 ? H_XY : axis == 1 ? H_XZ : H_YZ;
+    return ow_add(o, h_rect(&o->w, kind, mat, a0, a1, b0, b1, k));
+}
+int orc_world_box(orc_world* o, const double mn[3], const double mx[3], int mat)
+{
+    return ow_add(o, h_box(&o->w, v3(mn[0], mn[1], mn[2]), v3(mx[0], mx[1], mx[2]), mat));
+}
+int orc_world_translate(orc_world* o, int id, const double off[3])
+{
+    const Hittable* p = ow_get(o, id);
+    return p ? ow_add(o, h_translate(&o->w, p, v3(off[0], off[1], off[2]))) : -1;
+}
+int orc_world_rotate_y(orc_world* o, int id, double angle)
+{
+    const Hittable* p = ow_get(o, id);
+    return p ? ow_add(o, h_rotate_y(&o->w, angle, p)) : -1;
+}
+int orc_world_constant_medium(orc_world* o, int boundary, double density, int phase)
+{
+    const Hittable* p = ow_get(o, boundary);
+    return p ? ow_add(o, h_constant_medium(&o->w, p, density, phase)) : -1;
+}
+int orc_world_bvh(orc_world* o, const int* ids, int n, double t0, double t1)
+{
+    if (n < 1) return -1;
+    const Hittable** list = (const Hittable**)malloc((size_t)n * sizeof(void*));
+    for (int i = 0; i < n; ++i) {
+        list[i] = ow_get(o, ids[i]);
+        if (!list[i]) { free(list); return -1; }
+    }
+    OrcRng* saved = tl_rng;
+    tl_rng = &o->rng;
+    const Hittable* h = new_bvh_node(&o->w, list, 0, n, t0, t1);
+    tl_rng = saved;
+    free(list);
+    return ow_add(o, h);
+}
+int orc_world_push(orc_world* o, int id)
+{
+    const Hittable* p = ow_get(o, id);
+    if (!p) return -1;
+    world_push(&o->w, p);
+    return 0;
+}
+int orc_world_render(const orc_world* o, const orc_params* p, const double* cam24, const double bg[3],
+                     double* out_mean, orc_stats* stats)
+{
+    if (!o || !p || !cam24 || !bg || !out_mean || p->width < 2 || p->height < 2 || p->spp < 1 ||
+        p->row_stride < 1 || p->row_begin < 0)
+        return -1;
+    Camera cam;
+    V3* vs[7] = {&cam.origin, &cam.lower_left_corner, &cam.horizontal, &cam.vertical, &cam.u, &cam.v, &cam.w};
+    for (int i = 0; i < 7; ++i) *vs[i] = v3(cam24[3 * i], cam24[3 * i + 1], cam24[3 * i + 2]);
+    cam.lens_radius = cam24[21];
+    cam.time0 = cam24[22];
+    cam.time1 = cam24[23];
+    return render_world(p, &o->w, &cam, v3(bg[0], bg[1], bg[2]), out_mean, stats);
 }

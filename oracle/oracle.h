@@ -86,6 +86,31 @@ void orc_pstream(uint64_t seed, uint32_t pixel, uint32_t sample, int n, uint64_t
  * 24 doubles: origin, lower_left_corner, horizontal, vertical, u, v, w, lens_radius, t0, t1. */
 int orc_camera(int scene_id, int width, int height, double* out24);
 
+/* Custom worlds through the reference's constructor surface (main.rs:40-50,
+ * hittable.rs:77-207, material.rs:6-12, texture.rs:4-22), built by the same calls as the
+ * product's rt_world_* so tests can render one world on both sides. Ids: textures
+ * 0-based, material handles 1-based (main.rs:46-49), hittables 0-based; negative = error.
+ * The scene seed drives the construction draws (Perlin::new, the BVH's random axis). */
+typedef struct orc_world orc_world;
+int orc_world_create(uint64_t scene_seed, orc_world** out);
+void orc_world_destroy(orc_world* w);
+int orc_world_texture(orc_world* w, int kind, const double c0[3], const double c1[3], double scale); /* 0 solid 1 checker 2 noise */
+int orc_world_material(orc_world* w, int kind, int tex, const double albedo[3], double fuzz, double ir);
+int orc_world_sphere(orc_world* w, int mat, const double c[3], double r);
+int orc_world_moving_sphere(orc_world* w, int mat, const double c0[3], const double c1[3], double t0, double t1,
+                            double r);
+int orc_world_rect(orc_world* w, int axis, int mat, double a0, double a1, double b0, double b1, double k);
+int orc_world_box(orc_world* w, const double mn[3], const double mx[3], int mat);
+int orc_world_translate(orc_world* w, int id, const double off[3]);
+int orc_world_rotate_y(orc_world* w, int id, double angle);
+int orc_world_constant_medium(orc_world* w, int boundary, double density, int phase);
+int orc_world_bvh(orc_world* w, const int* ids, int n, double t0, double t1);
+int orc_world_push(orc_world* w, int id);
+/* p: geometry, spp, depth, seeds, rows, threads (scene_id and image unused); cam24 as
+ * orc_camera's output; bg the background color. */
+int orc_world_render(const orc_world* w, const orc_params* p, const double* cam24, const double bg[3],
+                     double* out_mean, orc_stats* stats);
+
 #ifdef __cplusplus
 }
 #endif

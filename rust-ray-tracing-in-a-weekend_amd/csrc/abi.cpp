@@ -83,7 +83,7 @@ struct rt_ctx {
     bool pending_counts = false;
     rt_stats stats{};
     uint32_t features = rtk::FEAT_ALL;  // of the uploaded scene
-    int block_chunks = 1;               // RT_BLOCK_CHUNKS: chunks per work block of the pools
+    int block_chunks = 0;               // RT_BLOCK_CHUNKS: chunks per work block of the pools (0: auto)
     uint32_t extra_features = 0;        // RT_EXTRA_FEATURES: a larger kernel variant than the scene needs (tests)
     double pad_extent = 0.0;
     int opt_slab32 = 1;                 // rt_ctx_set_variant / RT_SLAB32
@@ -517,8 +517,19 @@ static int validate_soa(const rt_scene_soa* s, int& tlas_depth, int& blas_depth,
         if (in.child_kind != RT_CHILD_PRIM && in.child_kind != RT_CHILD_BVH) return fail(RT_ERR_INVALID, "bad instance child kind");
         if (in.child_kind == RT_CHILD_PRIM ? (in.child < 0 || in.child >= s->n_prims) : !check_ref(in.child))
             return fail(RT_ERR_INVALID, "bad instance child");
-        if (in.child_kind == RT_CHILD_PRIM && !simple_kind(s->prims[in.child].kind))
-            return fail(RT_ERR_UNSUPPORTED, "instance child must be a simple primitive or a BVH");
+        if (in.child_kind == RT_CHILD_PRIM && !simple_kind(s->prims[in.child].kind) &&
+            s->prims[in.child].kind != RT_PRIM_MEDIUM)
+            return fail(RT_ERR_UNSUPPORTED, "instance child must be a primitive, a medium or a BVH");
+    }
+    // what the kernel's nested calls assume (flatten.cpp lowers any nesting into this shape):
+    // a medium's boundary instance has no medium child (no recursion), and an instance BLAS
+    // holds simple primitives only
+    for (int i = 0; i < s->n_prims; ++i) {
+        const rt_prim& p = s->prims[i];
+        if (p.kind != RT_PRIM_MEDIUM || s->prims[p.a].kind != RT_PRIM_INSTANCE) continue;
+        const rt_instance& in = s->instances[s->prims[p.a].a];
+        if (in.child_kind == RT_CHILD_PRIM && s->prims[in.child].kind == RT_PRIM_MEDIUM)
+            return fail(RT_ERR_UNSUPPORTED, "a medium's boundary holds a medium");
     }
     // stack needs (the kernel: TLAS walk in entries [0, tlas), a nested BLAS walk above it)
     std::vector<int> need((size_t)s->n_nodes, 0);
@@ -534,6 +545,23 @@ static int validate_soa(const rt_scene_soa* s, int& tlas_depth, int& blas_depth,
         const int b = walk_need(s, in.child, need, colour);
         if (b < 0) return fail(RT_ERR_INVALID, "cycle in an instance BVH");
         blas_depth = std::max(blas_depth, b + 1);
+        std::vector<int> todo{in.child};   // acyclic (checked above): every leaf slot is a simple prim
+        std::fill(colour.begin(), colour.end(), 0);
+        while (!todo.empty()) {
+            const int ref = todo.back();
+            todo.pop_back();
+            if (ref >= 0) {
+                if (colour[ref]) continue;
+                colour[ref] = 1;
+                todo.push_back(s->nodes[ref].child[0]);
+                todo.push_back(s->nodes[ref].child[1]);
+                continue;
+            }
+            const int code = ~ref;
+            for (int j = code >> 5; j < (code >> 5) + (code & 31); ++j)
+                if (!simple_kind(s->prims[s->prim_refs[j]].kind))
+                    return fail(RT_ERR_UNSUPPORTED, "an instance BVH holds a non-primitive");
+        }
     }
     if (tlas_depth > 32 || blas_depth > 32) return fail(RT_ERR_UNSUPPORTED, "BVH too deep for the traversal stack");
     // the TLAS-in-LDS claim: every node reachable from the root lies in [0, n_tlas_nodes)
@@ -638,7 +666,13 @@ int rt_ctx_upload_soa(rt_ctx* c, const rt_scene_soa* s)
     for (int i = 0; i < s->n_instances; ++i) {
         const rt_instance& in = s->instances[i];
         if (in.child_kind == RT_CHILD_PRIM) {
-            if (is_rect(s->prims[in.child].kind)) feat |= rtk::FEAT_INST_RECT;
+            const int ck = s->prims[in.child].kind;
+            if (is_rect(ck)) feat |= rtk::FEAT_INST_RECT;
+            if (ck == RT_PRIM_MEDIUM) {
+                feat |= rtk::FEAT_INST_MEDIUM | rtk::FEAT_MEDIUM;
+                const int bk = s->prims[s->prims[in.child].a].kind;   // its boundary, tested in object space
+                if (bk != RT_PRIM_SPHERE && bk != RT_PRIM_MOVING_SPHERE) feat |= rtk::FEAT_MEDIUM_INST;
+            }
             continue;
         }
         std::vector<int> todo{in.child};   // validate_soa checked refs and acyclicity
@@ -754,7 +788,6 @@ static int run_range(rt_ctx* c, const rt_camera* cam, const rt_render_params* p,
     K.n_rows = n_rows;
     K.tiles_x = (p->width + 7) / 8;
     K.tiles_y = (n_rows + 7) / 8;
-    K.block_chunks = c->block_chunks;
 
     const bool count = p->count_work != 0;
     // conservative f32 slab tests need every ray origin within 2M of the origin (flatten.cpp):
@@ -787,6 +820,10 @@ static int run_range(rt_ctx* c, const rt_camera* cam, const rt_render_params* p,
     // pool: samples x pixels x 24 B; chunk and item schedules: chunks x pixels x 24 B, batches
     // on chunk boundaries (relative to s_begin), so the partials add in one-launch order.
     const bool per_sample = o.pool == RT_SCHED_POOL;
+    // work blocks of one tile: 16-sample chunks, per-sample pool one chunk per block, item pool
+    // two (C2 kernel ms, pool 1/2/4 chunks: 99.8/100.2/103.2; items 1/2/4: 106.8/104.1/105.0;
+    // profiles/r02f_*, r02g_*)
+    K.block_chunks = c->block_chunks > 0 ? c->block_chunks : (o.pool == RT_SCHED_ITEMS ? 2 : 1);
     const long long fit = (long long)std::max<size_t>(1, c->sample_buf_cap / px_bytes);
     const long long batch = std::min<long long>(total, per_sample ? fit : fit * chunk);
     const int n_batches = (int)((total + batch - 1) / batch);

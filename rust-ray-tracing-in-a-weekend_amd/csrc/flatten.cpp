@@ -10,8 +10,9 @@
 //                                                     is a single prim or its own BLAS
 //   ConstantMedium (:417-473)                       -> RT_PRIM_MEDIUM whose boundary is a
 //                                                     hidden prim (sphere / box / instance)
-// The top-level list becomes the TLAS. A medium or an instance below an instance is
-// not lowered (RT_ERR_UNSUPPORTED); none of the reference scenes builds one.
+// The top-level list becomes the TLAS. Nested instances, BVHs and media are lowered by
+// pushing Translate/RotateY chains down (lower_instance); a medium boundary that holds
+// instances or media, and chains longer than 4 ops, are not (RT_ERR_UNSUPPORTED).
 //
 // accel (rt_scene.h) picks the hierarchy: SAH (above), LINEAR (every list a chain of
 // unbounded nodes over <=31-prim leaves, in list order: hit_hittables' linear scan), or
@@ -98,21 +99,6 @@ struct Builder {
         return add_prim(p);
     }
 
-    // Collects the simple leaves under id (through BvhNodes). Returns false on an
-    // instance or medium inside.
-    bool collect_simple(int id, std::vector<int>& out)
-    {
-        const HNode& h = w.nodes[id];
-        if (h.kind == HKind::BvhNode) {
-            if (!collect_simple(h.left, out)) return false;
-            if (h.right != h.left && !collect_simple(h.right, out)) return false;  // span-1 duplicate
-            return true;
-        }
-        if (!is_simple(h.kind)) return false;
-        out.push_back(id);
-        return true;
-    }
-
     Item item_of(int prim, int hid)
     {
         Item it;
@@ -126,73 +112,228 @@ struct Builder {
         return it;
     }
 
-    int lower_instance(int id, int& prim_out)
+    // ---- Translate / RotateY (hittable.rs:232-244, 386-415) and general nesting --------
+    // A chain of ops (outermost first) is pushed down through everything under it: for the
+    // closest hit, Outer(BVH[a, b]) = BVH[Outer(a), Outer(b)] (the ray is transformed the
+    // same way for each child, the hit parameter t is the ray's, and the record is mapped
+    // back op by op — with each op's set_face_normal quirk — for the winning child only),
+    // and Outer(Inner(x)) is one chain of Outer's ops followed by Inner's. So any nesting of
+    // instances, BVHs and media lowers to instances whose child is one primitive, one medium
+    // or a BLAS of primitives, each with a chain of <= 4 ops.
+    struct Ops {
+        int n = 0;
+        int32_t kind[4] = {0, 0, 0, 0};
+        double op[4][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}};
+    };
+
+    // Appends the Translate / RotateY chain starting at id to ops; returns the node it ends on.
+    int chain(int id, Ops& ops, int& rc)
+    {
+        int cur = id;
+        while (w.nodes[cur].kind == HKind::Translate || w.nodes[cur].kind == HKind::RotateY) {
+            if (ops.n == 4) {
+                err = "instance chain longer than 4 Translate/RotateY ops";
+                rc = RT_ERR_UNSUPPORTED;
+                return -1;
+            }
+            const HNode& h = w.nodes[cur];
+            if (h.kind == HKind::Translate) {
+                ops.kind[ops.n] = RT_OP_TRANSLATE;
+                ops.op[ops.n][0] = h.offset.x; ops.op[ops.n][1] = h.offset.y; ops.op[ops.n][2] = h.offset.z;
+            } else {
+                ops.kind[ops.n] = RT_OP_ROTATE_Y;
+                ops.op[ops.n][0] = h.sin_theta; ops.op[ops.n][1] = h.cos_theta; ops.op[ops.n][2] = 0.0;
+            }
+            ops.n++;
+            cur = h.ptr;
+        }
+        return cur;
+    }
+
+    // The world box of an object-space box seen through ops (corners mapped back op by op,
+    // innermost first: rotate back x' = c x + s z, z' = -s x + c z; translate back + offset).
+    static AABB box_through(const Ops& ops, AABB b)
+    {
+        for (int i = ops.n - 1; i >= 0; --i) {
+            if (ops.kind[i] == RT_OP_TRANSLATE) {
+                const V3 off = v3(ops.op[i][0], ops.op[i][1], ops.op[i][2]);
+                b.minimum = b.minimum + off;
+                b.maximum = b.maximum + off;
+                continue;
+            }
+            const double sn = ops.op[i][0], cs = ops.op[i][1];
+            AABB r{v3(INFINITY, b.minimum.y, INFINITY), v3(-INFINITY, b.maximum.y, -INFINITY)};
+            for (int k = 0; k < 4; ++k) {
+                const double x = (k & 1) ? b.maximum.x : b.minimum.x, z = (k & 2) ? b.maximum.z : b.minimum.z;
+                const double nx = cs * x + sn * z, nz = -sn * x + cs * z;
+                r.minimum.x = std::min(r.minimum.x, nx); r.maximum.x = std::max(r.maximum.x, nx);
+                r.minimum.z = std::min(r.minimum.z, nz); r.maximum.z = std::max(r.maximum.z, nz);
+            }
+            b = r;
+        }
+        return b;
+    }
+
+    Item item_box(int prim, const AABB& b)
+    {
+        Item it;
+        it.prim = prim;
+        it.ref = 0;
+        it.lo[0] = b.minimum.x; it.lo[1] = b.minimum.y; it.lo[2] = b.minimum.z;
+        it.hi[0] = b.maximum.x; it.hi[1] = b.maximum.y; it.hi[2] = b.maximum.z;
+        for (int a = 0; a < 3; ++a) it.c[a] = 0.5 * (it.lo[a] + it.hi[a]);
+        return it;
+    }
+
+    AABB box_of(int hid) const
+    {
+        AABB b;
+        w.bounding_box(hid, 0.0, 1.0, b);
+        return b;
+    }
+
+    int make_instance(const Ops& ops, int child_kind, int child)
     {
         rt_instance in;
         std::memset(&in, 0, sizeof in);
-        int cur = id;
-        while (w.nodes[cur].kind == HKind::Translate || w.nodes[cur].kind == HKind::RotateY) {
-            if (in.n_ops == 4) { err = "instance chain longer than 4 Translate/RotateY ops"; return RT_ERR_UNSUPPORTED; }
-            const HNode& h = w.nodes[cur];
-            if (h.kind == HKind::Translate) {
-                in.op_kind[in.n_ops] = RT_OP_TRANSLATE;
-                in.op[in.n_ops][0] = h.offset.x; in.op[in.n_ops][1] = h.offset.y; in.op[in.n_ops][2] = h.offset.z;
-            } else {
-                in.op_kind[in.n_ops] = RT_OP_ROTATE_Y;
-                in.op[in.n_ops][0] = h.sin_theta; in.op[in.n_ops][1] = h.cos_theta;
-            }
-            in.n_ops++;
-            cur = h.ptr;
-        }
-        const HNode& child = w.nodes[cur];
-        if (is_simple(child.kind)) {
-            in.child_kind = RT_CHILD_PRIM;
-            in.child = lower_simple(cur);
-        } else if (child.kind == HKind::BvhNode) {
-            in.child_kind = RT_CHILD_BVH;
-            double off = 0.0;  // object-space origins: |o_obj| <= |o_world| + sum |offsets|
-            for (int i = 0; i < in.n_ops; ++i)
-                if (in.op_kind[i] == RT_OP_TRANSLATE)
-                    off += std::sqrt(in.op[i][0] * in.op[i][0] + in.op[i][1] * in.op[i][1] + in.op[i][2] * in.op[i][2]);
-            const double saved = pad_abs;
-            pad_abs = 0x1.0p-18 * (world_extent + off);
-            if (accel == RT_ACCEL_MEDIAN) {
-                int rc = RT_OK;
-                in.child = lower_ref_bvh(cur, /*in_instance=*/true, rc);
-                if (rc) return rc;
-            } else {
-                std::vector<int> leaves;
-                if (!collect_simple(cur, leaves)) {
-                    err = "instance over a BVH that contains an instance or a medium";
-                    return RT_ERR_UNSUPPORTED;
-                }
-                std::vector<Item> items;
-                for (int hid : leaves) items.push_back(item_of(lower_simple(hid), hid));
-                in.child = build_bvh(items);
-            }
-            pad_abs = saved;
-            blas_depth = std::max(blas_depth, stack_need(in.child) + 1);
-        } else {
-            err = "instance over an instance or a medium";
-            return RT_ERR_UNSUPPORTED;
+        in.n_ops = ops.n;
+        in.child_kind = child_kind;
+        in.child = child;
+        for (int i = 0; i < ops.n; ++i) {
+            in.op_kind[i] = ops.kind[i];
+            for (int a = 0; a < 3; ++a) in.op[i][a] = ops.op[i][a];
         }
         f.instances.push_back(in);
         rt_prim p = blank(RT_PRIM_INSTANCE, -1);
         p.a = (int)f.instances.size() - 1;
-        prim_out = add_prim(p);
+        return add_prim(p);
+    }
+
+    // A BLAS over simple leaves seen through ops (object-space origins: |o_obj| <= |o_world|
+    // + sum |offsets|, which the box padding must cover).
+    int make_blas(const Ops& ops, const std::vector<int>& leaves, int bvh_node, int& rc)
+    {
+        double off = 0.0;
+        for (int i = 0; i < ops.n; ++i)
+            if (ops.kind[i] == RT_OP_TRANSLATE)
+                off += std::sqrt(ops.op[i][0] * ops.op[i][0] + ops.op[i][1] * ops.op[i][1] + ops.op[i][2] * ops.op[i][2]);
+        const double saved = pad_abs;
+        pad_abs = 0x1.0p-18 * (world_extent + off);
+        int root;
+        if (accel == RT_ACCEL_MEDIAN && bvh_node >= 0) {
+            root = lower_ref_bvh(bvh_node, /*in_instance=*/true, rc);
+        } else {
+            std::vector<Item> items;
+            for (int hid : leaves) items.push_back(item_of(lower_simple(hid), hid));
+            root = build_bvh(items);
+        }
+        pad_abs = saved;
+        if (rc) return 0;
+        blas_depth = std::max(blas_depth, stack_need(root) + 1);
+        return root;
+    }
+
+    // The leaves under a BVH node (through nested BvhNodes): simple ones and the rest.
+    void collect_split(int id, std::vector<int>& simple, std::vector<int>& complex)
+    {
+        const HNode& h = w.nodes[id];
+        if (h.kind == HKind::BvhNode) {
+            collect_split(h.left, simple, complex);
+            if (h.right != h.left) collect_split(h.right, simple, complex);  // span-1 duplicate
+            return;
+        }
+        (is_simple(h.kind) ? simple : complex).push_back(id);
+    }
+
+    // Lowers the object `id` seen through the ops `prefix` into instance items.
+    int lower_instance(int id, const Ops& prefix, std::vector<Item>& items)
+    {
+        Ops ops = prefix;
+        int rc = RT_OK;
+        const int child = chain(id, ops, rc);
+        if (rc) return rc;
+        const HNode& c = w.nodes[child];
+        if (is_simple(c.kind)) {
+            items.push_back(item_box(make_instance(ops, RT_CHILD_PRIM, lower_simple(child)), box_through(ops, box_of(child))));
+            return RT_OK;
+        }
+        if (c.kind == HKind::ConstantMedium) return lower_medium(child, ops, items);
+        if (c.kind != HKind::BvhNode) {
+            err = "unsupported hittable under an instance";
+            return RT_ERR_UNSUPPORTED;
+        }
+        std::vector<int> simple, complex;
+        collect_split(child, simple, complex);
+        if (!simple.empty()) {
+            AABB b = box_of(simple[0]);
+            for (int hid : simple) {
+                const AABB bi = box_of(hid);
+                b.minimum = v3(std::min(b.minimum.x, bi.minimum.x), std::min(b.minimum.y, bi.minimum.y),
+                               std::min(b.minimum.z, bi.minimum.z));
+                b.maximum = v3(std::max(b.maximum.x, bi.maximum.x), std::max(b.maximum.y, bi.maximum.y),
+                               std::max(b.maximum.z, bi.maximum.z));
+            }
+            const int root = make_blas(ops, simple, complex.empty() ? child : -1, rc);
+            if (rc) return rc;
+            items.push_back(item_box(make_instance(ops, RT_CHILD_BVH, root), box_through(ops, b)));
+        }
+        for (int k : complex) {
+            const HKind kk = w.nodes[k].kind;
+            if (kk == HKind::Translate || kk == HKind::RotateY) rc = lower_instance(k, ops, items);
+            else if (kk == HKind::ConstantMedium) rc = lower_medium(k, ops, items);
+            else { err = "unsupported hittable under an instance"; rc = RT_ERR_UNSUPPORTED; }
+            if (rc) return rc;
+        }
         return RT_OK;
     }
 
-    int lower_boundary(int id, int& prim_out)
+    // ConstantMedium (hittable.rs:417-473) seen through ops: a medium primitive (boundary: a
+    // primitive, or an instance over a primitive or a BLAS), itself the child of an instance
+    // when ops is not empty.
+    int lower_medium(int id, const Ops& ops, std::vector<Item>& items)
     {
         const HNode& h = w.nodes[id];
-        if (h.kind == HKind::Sphere || h.kind == HKind::MovingSphere || h.kind == HKind::Box ||
-            h.kind == HKind::XYRect || h.kind == HKind::XZRect || h.kind == HKind::YZRect) {
+        int bprim;
+        int rc = lower_boundary(h.ptr, bprim);
+        if (rc) return rc;
+        rt_prim p = blank(RT_PRIM_MEDIUM, h.mat - 1);
+        p.a = bprim;
+        p.b = h.medium_id;
+        p.p[0] = h.neg_inv_density;
+        const int mprim = add_prim(p);
+        if (ops.n == 0) items.push_back(item_of(mprim, id));
+        else items.push_back(item_box(make_instance(ops, RT_CHILD_PRIM, mprim), box_through(ops, box_of(id))));
+        return RT_OK;
+    }
+
+    // One primitive standing for a medium's boundary: a simple primitive, or an instance (a
+    // Translate/RotateY chain, or none for a bare BvhNode) over a primitive or a BLAS. A
+    // boundary holding instances or media below its chain is not lowered.
+    int lower_boundary(int id, int& prim_out)
+    {
+        if (is_simple(w.nodes[id].kind)) {
             prim_out = lower_simple(id);
             return RT_OK;
         }
-        if (h.kind == HKind::Translate || h.kind == HKind::RotateY) return lower_instance(id, prim_out);
-        err = "constant medium boundary must be a primitive or a Translate/RotateY chain";
+        Ops ops;
+        int rc = RT_OK;
+        const int child = chain(id, ops, rc);
+        if (rc) return rc;
+        if (is_simple(w.nodes[child].kind)) {
+            prim_out = make_instance(ops, RT_CHILD_PRIM, lower_simple(child));
+            return RT_OK;
+        }
+        if (w.nodes[child].kind == HKind::BvhNode) {
+            std::vector<int> simple, complex;
+            collect_split(child, simple, complex);
+            if (complex.empty() && !simple.empty()) {
+                const int root = make_blas(ops, simple, child, rc);
+                if (rc) return rc;
+                prim_out = make_instance(ops, RT_CHILD_BVH, root);
+                return RT_OK;
+            }
+        }
+        err = "a medium boundary holding instances or media is not lowered";
         return RT_ERR_UNSUPPORTED;
     }
 
@@ -254,24 +395,8 @@ struct Builder {
             if (h.right != h.left) return lower_top(h.right, items);
             return RT_OK;
         }
-        case HKind::Translate: case HKind::RotateY: {
-            int prim;
-            int rc = lower_instance(id, prim);
-            if (rc) return rc;
-            items.push_back(item_of(prim, id));
-            return RT_OK;
-        }
-        case HKind::ConstantMedium: {
-            int bprim;
-            int rc = lower_boundary(h.ptr, bprim);
-            if (rc) return rc;
-            rt_prim p = blank(RT_PRIM_MEDIUM, h.mat - 1);
-            p.a = bprim;
-            p.b = h.medium_id;
-            p.p[0] = h.neg_inv_density;
-            items.push_back(item_of(add_prim(p), id));
-            return RT_OK;
-        }
+        case HKind::Translate: case HKind::RotateY: return lower_instance(id, Ops(), items);
+        case HKind::ConstantMedium: return lower_medium(id, Ops(), items);
         default:
             items.push_back(item_of(lower_simple(id), id));
             return RT_OK;

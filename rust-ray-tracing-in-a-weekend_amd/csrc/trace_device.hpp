@@ -122,7 +122,9 @@ struct CfgDrop : C {
 template <class C>
 using InstC = CfgDrop<C, (C::F & FEAT_INST_RECT) ? 0u : (uint32_t)FEAT_RECT>;
 template <class C>
-using BoundC = CfgDrop<C, (C::F & FEAT_MEDIUM_INST) ? 0u : (uint32_t)(FEAT_RECT | FEAT_INST)>;
+using BoundC = CfgDrop<C, FEAT_INST_MEDIUM | ((C::F & FEAT_MEDIUM_INST) ? 0u : (uint32_t)(FEAT_RECT | FEAT_INST))>;
+template <class C>
+using InstMedC = CfgDrop<C, FEAT_INST_MEDIUM>;   // a medium under an instance: no medium below it
 
 // Traversal stack. LDS: a lane-interleaved dynamic LDS array [entry][256 threads]
 // (consecutive lanes hit consecutive banks) sized per scene by the host (TLAS depth +
@@ -685,16 +687,31 @@ __device__ __forceinline__ void instance_ray(const rt_instance& in, RayT<R>& r)
     }
 }
 
+template <class C, class R = typename C::Real>
+__device__ bool medium_t(const SceneDev& S, const rt_prim& m, const RayT<R>& r, R t_min, R t_max, R& t,
+                         StackT<C>& stack, int sp0, const Keyed& key, Count& cnt);
+template <class R>
+__device__ __forceinline__ void medium_finish(const rt_prim& m, const RayT<R>& r, R t, HitT<R>& h);
+
 // t-only: the closest hit of the instance's child; sub = BLAS prim (or the child prim),
 // side = winning box side.
 template <class C, class R = typename C::Real>
 __device__ bool instance_t(const SceneDev& S, const rt_instance& in, const RayT<R>& ray, R t_min, R t_max,
-                           HitRefT<R>& ref, StackT<C>& stack, int sp0, Count& cnt)
+                           HitRefT<R>& ref, StackT<C>& stack, int sp0, const Keyed& key, Count& cnt)
 {
     RayT<R> r = ray;
     instance_ray(in, r);
     finish_ray<C>(r, S.has_spheres != 0);
     if (in.child_kind == RT_CHILD_PRIM) {
+        if constexpr ((C::F & FEAT_INST_MEDIUM) != 0) {
+            const rt_prim& cp = S.prims[in.child];
+            if (cp.kind == RT_PRIM_MEDIUM) {   // the medium in object space (its boundary walks at sp0)
+                if (!medium_t<InstMedC<C>>(S, cp, r, t_min, t_max, ref.t, stack, sp0, key, cnt)) return false;
+                ref.sub = in.child;
+                ref.side = 0;
+                return true;
+            }
+        }
         int side = 0;
         if (!simple_t<InstC<C>>(S.prims[in.child], r, t_min, t_max, ref.t, side, cnt)) return false;
         ref.sub = in.child;
@@ -739,7 +756,14 @@ __device__ void instance_finish(const SceneDev& S, const rt_instance& in, const 
     RayT<R> r = ray;
     instance_ray(in, r);
     // ref.sub: the child prim (RT_CHILD_PRIM) or the BLAS leaf slot
-    simple_finish<InstC<C>>(in.child_kind == RT_CHILD_PRIM ? S.prims[ref.sub] : S.leaf_prims[ref.sub], r, ref.t,
+    bool done = false;
+    if constexpr ((C::F & FEAT_INST_MEDIUM) != 0) {
+        if (in.child_kind == RT_CHILD_PRIM && S.prims[ref.sub].kind == RT_PRIM_MEDIUM) {
+            medium_finish(S.prims[ref.sub], r, ref.t, h);   // hittable.rs:452-463 in object space
+            done = true;
+        }
+    }
+    if (!done) simple_finish<InstC<C>>(in.child_kind == RT_CHILD_PRIM ? S.prims[ref.sub] : S.leaf_prims[ref.sub], r, ref.t,
                             ref.side, h);
     const int n = in.n_ops;
 #pragma unroll
@@ -766,13 +790,13 @@ __device__ void instance_finish(const SceneDev& S, const rt_instance& in, const 
 // t of a medium boundary (a simple prim or an instance).
 template <class C, class R = typename C::Real>
 __device__ __forceinline__ bool boundary_t(const SceneDev& S, int prim, const RayT<R>& r, R t_min, R t_max, R& t,
-                                           StackT<C>& stack, int sp0, Count& cnt)
+                                           StackT<C>& stack, int sp0, const Keyed& key, Count& cnt)
 {
     const rt_prim& p = S.prims[prim];
     if constexpr ((BoundC<C>::F & FEAT_INST) != 0) {
         if (p.kind == RT_PRIM_INSTANCE) {
             HitRefT<R> ref;
-            if (!instance_t<C>(S, S.instances[p.a], r, t_min, t_max, ref, stack, sp0, cnt)) return false;
+            if (!instance_t<BoundC<C>>(S, S.instances[p.a], r, t_min, t_max, ref, stack, sp0, key, cnt)) return false;
             t = ref.t;
             return true;
         }
@@ -782,13 +806,17 @@ __device__ __forceinline__ bool boundary_t(const SceneDev& S, int prim, const Ra
 }
 
 // ConstantMedium (hittable.rs:417-473), keyed draw instead of the in-hit thread_rng().
-template <class C, class R = typename C::Real>
+template <class C, class R>
 __device__ bool medium_t(const SceneDev& S, const rt_prim& m, const RayT<R>& r, R t_min, R t_max, R& t,
                          StackT<C>& stack, int sp0, const Keyed& key, Count& cnt)
 {
     R t1, t2;
-    if (!boundary_t<C>(S, m.a, r, (R)-RT_INF, (R)RT_INF, t1, stack, sp0, cnt)) return false;
-    if (!boundary_t<C>(S, m.a, r, t1 + (R)0.0001, (R)RT_INF, t2, stack, sp0, cnt)) return false;
+    if (!boundary_t<C>(S, m.a, r, (R)-RT_INF, (R)RT_INF, t1, stack, sp0, key, cnt)) return false;
+    // the second boundary hit after t1 + 0.0001 (hittable.rs:433); in f32 the step must
+    // also clear t1's own rounding (a fog sphere of r = 5000 has ulp(t1) = 4.9e-4 > 1e-4)
+    R t1_next = t1 + (R)0.0001;
+    if constexpr (C::F32) t1_next = t1 + fmaxf(0.0001f, __builtin_fabsf(t1) * 0x1.0p-19f);
+    if (!boundary_t<C>(S, m.a, r, t1_next, (R)RT_INF, t2, stack, sp0, key, cnt)) return false;
     if (t1 < t_min) t1 = t_min;
     if (t2 > t_max) t2 = t_max;
     if (t1 >= t2) return false;
@@ -833,7 +861,7 @@ __device__ bool trace_world(const SceneDev& S, const RayT<R>& r, HitT<R>& h, Sta
         const rt_prim& p = S.leaf_prims[slot];
         if constexpr ((C::F & FEAT_INST) != 0)
             if (p.kind == RT_PRIM_INSTANCE)
-                return instance_t<C>(S, S.instances[p.a], r, t_min, tmax, b, stack, S.blas_base, cnt);
+                return instance_t<C>(S, S.instances[p.a], r, t_min, tmax, b, stack, S.blas_base, key, cnt);
         if constexpr ((C::F & FEAT_MEDIUM) != 0)
             if (p.kind == RT_PRIM_MEDIUM) return medium_t<C>(S, p, r, t_min, tmax, b.t, stack, S.blas_base, key, cnt);
         return simple_t<C>(p, r, t_min, tmax, b.t, b.side, cnt);
@@ -1180,6 +1208,20 @@ __device__ __forceinline__ bool shade(const SceneDev& S, const KParams& P, const
     Tg = Tg * ag;
     Tb = Tb * ab;
     r.ox = h.px; r.oy = h.py; r.oz = h.pz;
+    if constexpr (C::F32) {
+        // f32 mode: the hit point carries ~|p| 2^-24 of rounding, which t_min = 0.001 does not
+        // cover at grazing angles on the final scene's |p| ~ 1000 boxes (the next ray would hit
+        // its own surface again); move the origin off the surface, to the side the new ray
+        // leaves on (Wachter & Binder, Ray Tracing Gems ch. 6). Media (uvkind 0) have no surface.
+        if (h.uvkind != 0) {
+            const float m = fmaxf(fmaxf(__builtin_fabsf(h.px), __builtin_fabsf(h.py)), __builtin_fabsf(h.pz));
+            float eps = m * 0x1.0p-19f + 1e-5f;
+            if (sdx * h.nx + sdy * h.ny + sdz * h.nz < 0.0f) eps = -eps;
+            r.ox = h.px + h.nx * eps;
+            r.oy = h.py + h.ny * eps;
+            r.oz = h.pz + h.nz * eps;
+        }
+    }
     r.dx = sdx; r.dy = sdy; r.dz = sdz;
     finish_ray<C>(r, S.has_spheres != 0);
     return true;

@@ -53,7 +53,8 @@ enum : uint32_t {
     FEAT_IMAGE = 16,    // image texture
     FEAT_INST_RECT = 32,    // rects or boxes inside an instance (its child prim or BLAS)
     FEAT_MEDIUM_INST = 64,  // a medium boundary that is not a sphere (box, rect, instance)
-    FEAT_ALL = 127,
+    FEAT_INST_MEDIUM = 128, // a medium inside an instance (nested Translate/RotateY over a ConstantMedium)
+    FEAT_ALL = 255,
     FEAT_SET_SPHERES = 0,                                          // compiled variant: spheres + solid/checker
     FEAT_SET_RECTINST = FEAT_RECT | FEAT_INST | FEAT_INST_RECT,    // + rects, boxes, instances (Cornell)
     FEAT_SET_MEDIA = FEAT_SET_RECTINST | FEAT_MEDIUM | FEAT_MEDIUM_INST,  // + constant media (Cornell smoke)

@@ -15,6 +15,10 @@ def pytest_configure(config):
 @pytest.fixture(scope="session")
 def rt():
     """The Python binding of the C ABI (builds the library first if it is missing)."""
+    try:   # torch first when present: its HIP runtime is the one the library then shares
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     import __graft_entry__ as ge
     lib = os.path.join(ge.PKG, "lib", "librtiow_amd.so")
     if not os.path.exists(lib):

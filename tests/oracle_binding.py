@@ -55,6 +55,17 @@ def lib() -> ctypes.CDLL:
     l.orc_pstream.restype = None
     l.orc_camera.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
     l.orc_camera.restype = ctypes.c_int
+    P, I, D = ctypes.c_void_p, ctypes.c_int, ctypes.c_double
+    for name, args in {"orc_world_create": [ctypes.c_uint64, P], "orc_world_texture": [P, I, P, P, D],
+                       "orc_world_material": [P, I, I, P, D, D], "orc_world_sphere": [P, I, P, D],
+                       "orc_world_moving_sphere": [P, I, P, P, D, D, D], "orc_world_rect": [P, I, I, D, D, D, D, D],
+                       "orc_world_box": [P, P, P, I], "orc_world_translate": [P, I, P], "orc_world_rotate_y": [P, I, D],
+                       "orc_world_constant_medium": [P, I, D, I], "orc_world_bvh": [P, P, I, D, D],
+                       "orc_world_push": [P, I], "orc_world_render": [P, ctypes.POINTER(Params), P, P, P, P]}.items():
+        getattr(l, name).argtypes = args
+        getattr(l, name).restype = I
+    l.orc_world_destroy.argtypes = [P]
+    l.orc_world_destroy.restype = None
     return l
 
 
@@ -124,3 +135,109 @@ def pstream(seed: int, pixel: int, sample: int, n: int) -> np.ndarray:
     out = np.zeros(n, np.uint64)
     lib().orc_pstream(seed, pixel, sample, n, out.ctypes.data)
     return out
+
+
+class OracleWorld:
+    """A custom world in the oracle (orc_world_*), built with the calls of the product's
+    rtiow_amd.World; TwinWorld below issues every call to both."""
+
+    def __init__(self, scene_seed: int = 1):
+        l = lib()
+        self.h = ctypes.c_void_p()
+        if l.orc_world_create(ctypes.c_uint64(scene_seed), ctypes.byref(self.h)) != 0:
+            raise RuntimeError("orc_world_create")
+
+    def close(self):
+        if self.h:
+            lib().orc_world_destroy(self.h)
+            self.h = ctypes.c_void_p()
+
+    def __del__(self):
+        self.close()
+
+    @staticmethod
+    def _d3(v):
+        return (ctypes.c_double * 3)(*[float(x) for x in v])
+
+    def _id(self, rc):
+        if rc < 0:
+            raise RuntimeError(f"oracle world call failed: {rc}")
+        return rc
+
+    def solid(self, r, g, b): return self._id(lib().orc_world_texture(self.h, 0, self._d3((r, g, b)), self._d3((0, 0, 0)), 0.0))
+    def checker(self, even, odd): return self._id(lib().orc_world_texture(self.h, 1, self._d3(even), self._d3(odd), 0.0))
+    def noise(self, scale): return self._id(lib().orc_world_texture(self.h, 2, self._d3((0, 0, 0)), self._d3((0, 0, 0)), scale))
+    def _mat(self, kind, tex=0, albedo=(0, 0, 0), fuzz=0.0, ir=0.0):
+        return self._id(lib().orc_world_material(self.h, kind, tex, self._d3(albedo), fuzz, ir))
+    def lambertian(self, tex): return self._mat(0, tex)
+    def metal(self, albedo, fuzz): return self._mat(1, albedo=albedo, fuzz=fuzz)
+    def dielectric(self, ir): return self._mat(2, ir=ir)
+    def diffuse_light(self, tex): return self._mat(3, tex)
+    def isotropic(self, tex): return self._mat(4, tex)
+    def sphere(self, mat, c, r): return self._id(lib().orc_world_sphere(self.h, mat, self._d3(c), r))
+    def moving_sphere(self, mat, c0, c1, t0, t1, r):
+        return self._id(lib().orc_world_moving_sphere(self.h, mat, self._d3(c0), self._d3(c1), t0, t1, r))
+    def xy_rect(self, mat, a0, a1, b0, b1, k): return self._id(lib().orc_world_rect(self.h, 0, mat, a0, a1, b0, b1, k))
+    def xz_rect(self, mat, a0, a1, b0, b1, k): return self._id(lib().orc_world_rect(self.h, 1, mat, a0, a1, b0, b1, k))
+    def yz_rect(self, mat, a0, a1, b0, b1, k): return self._id(lib().orc_world_rect(self.h, 2, mat, a0, a1, b0, b1, k))
+    def box(self, mn, mx, mat): return self._id(lib().orc_world_box(self.h, self._d3(mn), self._d3(mx), mat))
+    def translate(self, child, off): return self._id(lib().orc_world_translate(self.h, child, self._d3(off)))
+    def rotate_y(self, child, angle): return self._id(lib().orc_world_rotate_y(self.h, child, angle))
+    def constant_medium(self, b, density, phase): return self._id(lib().orc_world_constant_medium(self.h, b, density, phase))
+
+    def bvh(self, ids, t0=0.0, t1=1.0):
+        arr = (ctypes.c_int * len(ids))(*ids)
+        return self._id(lib().orc_world_bvh(self.h, arr, len(ids), t0, t1))
+
+    def push(self, hid):
+        self._id(lib().orc_world_push(self.h, hid))
+
+    def render(self, cam24, bg, width, height, spp, max_depth=50, render_seed=1, row_begin=0, row_stride=1,
+               spp_chunk=0, threads=0):
+        if threads <= 0:
+            threads = min(8, os.cpu_count() or 1)
+        if spp_chunk <= 0:
+            spp_chunk = min(16, max(1, (spp + 15) // 16))
+        n_rows = 0 if row_begin >= height else (height - row_begin + row_stride - 1) // row_stride
+        p = Params(-1, 0, render_seed, width, height, spp, max_depth, spp_chunk, row_begin, row_stride, threads,
+                   SPLIT_ROWS, None, 0, 0)
+        out = np.zeros((n_rows, width, 3), dtype=np.float64)
+        cam = np.ascontiguousarray(cam24, dtype=np.float64)
+        rc = lib().orc_world_render(self.h, ctypes.byref(p), cam.ctypes.data, self._d3(bg), out.ctypes.data, None)
+        if rc != 0:
+            raise RuntimeError(f"orc_world_render failed: {rc}")
+        return out
+
+
+class TwinWorld:
+    """One custom world built in the product (rtiow_amd.World) and in the oracle by the same
+    constructor calls. Texture ids and material handles agree on both sides (checked);
+    hittable ids are each side's own (the product's arena also holds a BVH's inner nodes),
+    so hittable arguments are translated through a product-id -> oracle-id table."""
+
+    HITTABLE_ARGS = {"translate": (0,), "rotate_y": (0,), "constant_medium": (0,), "push": (0,)}
+    SAME_IDS = {"solid", "checker", "noise", "lambertian", "metal", "dielectric", "diffuse_light", "isotropic"}
+
+    def __init__(self, rt, scene_seed: int = 1):
+        self.product = rt.World(scene_seed)
+        self.oracle = OracleWorld(scene_seed)
+        self.to_oracle = {}
+
+    def bvh(self, ids, t0=0.0, t1=1.0):
+        a = self.product.bvh(ids, t0, t1)
+        self.to_oracle[a] = self.oracle.bvh([self.to_oracle[i] for i in ids], t0, t1)
+        return a
+
+    def __getattr__(self, name):
+        def call(*args):
+            a = getattr(self.product, name)(*args)
+            oargs = list(args)
+            for i in self.HITTABLE_ARGS.get(name, ()):
+                oargs[i] = self.to_oracle[args[i]]
+            b = getattr(self.oracle, name)(*oargs)
+            if name in self.SAME_IDS:
+                assert a == b, (name, a, b)
+            elif isinstance(a, int) and name != "push":
+                self.to_oracle[a] = b
+            return a
+        return call

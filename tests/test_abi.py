@@ -187,14 +187,42 @@ def test_errors_do_not_abort(rt):
 
 
 def test_unsupported_nesting_reported(rt):
+    """What the lowering still refuses: chains of more than 4 Translate/RotateY ops, and a
+    medium boundary that holds a medium."""
     w = rt.World(1)
     m = w.lambertian(w.solid(1, 1, 1))
-    s = w.sphere(m, (0, 0, 0), 1.0)
-    med = w.constant_medium(s, 0.5, w.isotropic(w.solid(1, 1, 1)))
-    inst = w.translate(med, (1, 0, 0))       # a medium under an instance is not lowered
-    w.push(inst)
+    x = w.sphere(m, (0, 0, 0), 1.0)
+    for i in range(5):
+        x = w.translate(x, (1, 0, 0))
+    w.push(x)
     with pytest.raises(rt.RTError, match="UNSUPPORTED"):
         w.flatten()
+    w = rt.World(1)
+    m = w.lambertian(w.solid(1, 1, 1))
+    phase = w.isotropic(w.solid(1, 1, 1))
+    inner = w.constant_medium(w.sphere(m, (0, 0, 0), 1.0), 0.5, phase)
+    boundary = w.translate(w.bvh([inner, w.sphere(m, (3, 0, 0), 1.0)]), (0, 1, 0))
+    w.push(w.constant_medium(boundary, 0.1, phase))
+    with pytest.raises(rt.RTError, match="UNSUPPORTED"):
+        w.flatten()
+
+
+def test_nested_instances_and_media_flatten(rt):
+    """hittable.rs:30-41 composes freely: instances over instances, instances over BVHs of
+    instances and media, media under instances, a bare BVH as a medium boundary. The lowering
+    pushes Translate/RotateY chains down (flatten.cpp lower_instance): every instance ends on
+    one primitive, one medium or a BLAS of primitives, and validation accepts the tables."""
+    w = rt.World(2)
+    m = w.lambertian(w.solid(0.5, 0.5, 0.5))
+    phase = w.isotropic(w.solid(0.8, 0.8, 0.8))
+    inner = w.rotate_y(w.translate(w.box((0, 0, 0), (1, 2, 1), m), (0.5, 0, 0)), 20.0)
+    fog = w.constant_medium(w.sphere(m, (0, 1, 0), 0.8), 0.7, phase)
+    group = w.bvh([inner, fog, w.sphere(m, (2, 0.5, 0), 0.5), w.sphere(m, (-2, 0.5, 0), 0.5)])
+    w.push(w.translate(w.rotate_y(group, -30.0), (0, 0, 3)))
+    w.push(w.constant_medium(w.bvh([w.sphere(m, (5, 1, 0), 1.0), w.sphere(m, (6, 1, 0), 1.0)]), 0.3, phase))
+    soa = w.flatten()
+    assert soa.n_media == 2 and soa.n_instances == 4   # box chain, fog, the spheres' BLAS, the bare-BVH boundary
+    assert rt.validate_soa(rt.SceneSoA.from_buffer_copy(soa)) == (soa.tlas_depth, soa.blas_depth)
 
 
 def test_custom_world_flattens(rt):

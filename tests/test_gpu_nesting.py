@@ -1,0 +1,90 @@
+"""General Hittable nesting (hittable.rs:30-41: Translate / RotateY wrap any Hittable, a
+ConstantMedium's boundary is any Hittable) on the GPU against the oracle.
+
+Each world is built twice by the same constructor calls — in the product (rt_world_*) and
+in the oracle (orc_world_*, tests/oracle_binding.py TwinWorld) — and rendered by both. The
+product lowers the nesting by pushing Translate/RotateY chains down (flatten.cpp
+lower_instance); the oracle evaluates the reference's recursion as written. Bar as in
+tests/test_gpu_parity.py: L_inf <= 1e-3 and path identity (relative 1e-9).
+"""
+import numpy as np
+import pytest
+
+from tests import oracle_binding as ob
+from tests.test_gpu_parity import assert_parity
+
+pytestmark = pytest.mark.gpu
+
+
+def _cam24(cam):
+    v = []
+    for f in ("origin", "lower_left_corner", "horizontal", "vertical", "u", "v", "w"):
+        v += list(getattr(cam, f))
+    return np.array(v + [cam.lens_radius, cam.time0, cam.time1])
+
+
+def _render_both(rt, renderer, tw, W, H, spp, look_from, look_at, bg, vfov=40.0, accel=None):
+    cam = rt.camera_new(look_from, look_at, (0.0, 1.0, 0.0), vfov, W / H, 0.1, 10.0, 0.0, 1.0)
+    renderer.upload(tw.product, rt.RT_ACCEL_SAH if accel is None else accel)
+    got = renderer.render(cam, rt.Renderer.params(W, H, spp, 50, bg, 1, out_format=rt.RT_OUT_F64))
+    ref = tw.oracle.render(_cam24(cam), bg, W, H, spp)
+    return got, ref
+
+
+def _nested_world(rt):
+    """Instances over instances, an instance over a BVH holding instances, a medium and
+    spheres, a medium under two instances whose boundary is itself an instanced box, a bare
+    BVH as a medium boundary, and a light."""
+    tw = ob.TwinWorld(rt, 5)
+    white = tw.lambertian(tw.solid(0.73, 0.73, 0.73))
+    red = tw.lambertian(tw.checker((0.65, 0.05, 0.05), (0.9, 0.9, 0.9)))
+    metal = tw.metal((0.8, 0.8, 0.9), 0.1)
+    glass = tw.dielectric(1.5)
+    light = tw.diffuse_light(tw.solid(6.0, 6.0, 6.0))
+    phase = tw.isotropic(tw.solid(0.8, 0.8, 0.9))
+    tw.push(tw.sphere(white, (0.0, -1000.0, 0.0), 1000.0))
+    tw.push(tw.xz_rect(light, -2.0, 2.0, -2.0, 2.0, 6.0))
+    # Translate(RotateY(BVH[RotateY(Translate(box)), medium(sphere), spheres]))
+    inner = tw.rotate_y(tw.translate(tw.box((0.0, 0.0, 0.0), (0.8, 1.6, 0.8), red), (0.3, 0.0, 0.0)), 25.0)
+    fog = tw.constant_medium(tw.sphere(white, (-1.2, 0.7, 0.0), 0.7), 0.9, phase)
+    group = tw.bvh([inner, fog, tw.sphere(metal, (1.4, 0.5, 0.3), 0.5), tw.sphere(glass, (0.2, 0.4, 1.3), 0.4)])
+    tw.push(tw.translate(tw.rotate_y(group, -30.0), (0.0, 0.0, -1.0)))
+    # Translate(RotateY(medium(Translate(RotateY(box))))): a medium under instances with an
+    # instanced boundary, like cornell_smoke's boxes one level further down
+    smoke = tw.constant_medium(tw.translate(tw.rotate_y(tw.box((0.0, 0.0, 0.0), (1.0, 1.0, 1.0), white), 15.0),
+                                            (-0.5, 0.0, -0.5)), 1.5, phase)
+    tw.push(tw.translate(tw.rotate_y(smoke, 40.0), (-2.5, 0.0, 1.5)))
+    # a medium bounded by a bare BVH of two spheres
+    tw.push(tw.constant_medium(tw.bvh([tw.sphere(white, (2.6, 0.6, 1.8), 0.6), tw.sphere(white, (3.3, 0.6, 1.8), 0.6)]),
+                               1.2, phase))
+    # an instance over an instance over a BVH of spheres (a chain of 3 ops)
+    balls = tw.bvh([tw.sphere(white, (0.4 * i, 0.25, 0.0), 0.2) for i in range(6)])
+    tw.push(tw.translate(tw.rotate_y(tw.translate(balls, (-1.0, 0.0, 0.0)), 70.0), (1.5, 0.0, -3.0)))
+    return tw
+
+
+def test_nested_world_matches_oracle(rt, renderer):
+    tw = _nested_world(rt)
+    soa = tw.product.flatten()
+    assert soa.n_media == 3 and soa.n_instances >= 5
+    got, ref = _render_both(rt, renderer, tw, 48, 32, 6, (7.0, 4.0, 9.0), (0.0, 0.7, 0.0), (0.5, 0.6, 0.8))
+    assert renderer.stats().variant_features == 255          # media under instances: the all-features variant
+    assert float(ref.max()) > 0.0
+    assert_parity(got, ref, "nested world")
+
+
+def test_nested_world_accel_modes_and_f32(rt, renderer):
+    """The same world through the LINEAR and MEDIAN lowerings gives the same bits; the f32
+    mode renders it too (finite, mean within 10 % of the f64 image)."""
+    tw = _nested_world(rt)
+    imgs = [_render_both(rt, renderer, tw, 32, 24, 4, (7.0, 4.0, 9.0), (0.0, 0.7, 0.0), (0.5, 0.6, 0.8), accel=a)[0]
+            for a in (rt.RT_ACCEL_SAH, rt.RT_ACCEL_LINEAR, rt.RT_ACCEL_MEDIAN)]
+    for im in imgs[1:]:
+        assert np.array_equal(im, imgs[0])
+    renderer.set_precision(rt.RT_PREC_F32)
+    try:
+        f32 = _render_both(rt, renderer, tw, 32, 24, 32, (7.0, 4.0, 9.0), (0.0, 0.7, 0.0), (0.5, 0.6, 0.8))[0]
+    finally:
+        renderer.set_precision(rt.RT_PREC_F64)
+    f64 = _render_both(rt, renderer, tw, 32, 24, 32, (7.0, 4.0, 9.0), (0.0, 0.7, 0.0), (0.5, 0.6, 0.8))[0]
+    assert np.all(np.isfinite(f32)) and abs(float(f32.mean()) / float(f64.mean()) - 1.0) < 0.1
