@@ -33,7 +33,9 @@ enum {
     RT_PRIM_XY_RECT = 2,       /* p: x0 x1 y0 y1 k */
     RT_PRIM_XZ_RECT = 3,       /* p: x0 x1 z0 z1 k */
     RT_PRIM_YZ_RECT = 4,       /* p: y0 y1 z0 z1 k */
-    RT_PRIM_BOX = 5,           /* p: minxyz maxxyz (6 rects, hittable.rs:132-145) */
+    RT_PRIM_BOX = 5,           /* p: minxyz maxxyz (6 rects, hittable.rs:132-145); b = 1: p[6..8] hold
+                                  the box's f32 bounds (lo xyz, hi xyz), padded and rounded outward
+                                  like a node's, for a conservative pre-test (b = 0: none) */
     RT_PRIM_INSTANCE = 6,      /* a: instance index */
     RT_PRIM_MEDIUM = 7         /* a: boundary prim index (SPHERE/BOX/INSTANCE), b: medium id, p[0]: -1/density */
 };

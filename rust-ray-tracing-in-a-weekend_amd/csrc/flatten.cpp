@@ -89,11 +89,19 @@ struct Builder {
                                                                                          : RT_PRIM_YZ_RECT;
             p.p[0] = h.a0; p.p[1] = h.a1; p.p[2] = h.b0; p.p[3] = h.b1; p.p[4] = h.k;
             break;
-        case HKind::Box:
+        case HKind::Box: {
             p.kind = RT_PRIM_BOX;
             p.p[0] = h.bmin.x; p.p[1] = h.bmin.y; p.p[2] = h.bmin.z;
             p.p[3] = h.bmax.x; p.p[4] = h.bmax.y; p.p[5] = h.bmax.z;
+            // the box's own bounds in f32, padded and rounded outward like a BVH node's, for
+            // the kernel's conservative pre-test before the 6 rect tests (rt_scene.h)
+            const double lo[3] = {h.bmin.x, h.bmin.y, h.bmin.z}, hi[3] = {h.bmax.x, h.bmax.y, h.bmax.z};
+            float fb[6];
+            to_f32_box(lo, hi, fb, fb + 3);
+            std::memcpy(&p.p[6], fb, sizeof fb);
+            p.b = 1;
             break;
+        }
         default: break;
         }
         return add_prim(p);
@@ -209,16 +217,31 @@ struct Builder {
         return add_prim(p);
     }
 
-    // A BLAS over simple leaves seen through ops (object-space origins: |o_obj| <= |o_world|
-    // + sum |offsets|, which the box padding must cover).
-    int make_blas(const Ops& ops, const std::vector<int>& leaves, int bvh_node, int& rc)
+    // Box padding for object space seen through ops: object-space origins have |o_obj| <=
+    // |o_world| + sum |offsets|, which the padding must cover.
+    double pad_through(const Ops& ops) const
     {
         double off = 0.0;
         for (int i = 0; i < ops.n; ++i)
             if (ops.kind[i] == RT_OP_TRANSLATE)
                 off += std::sqrt(ops.op[i][0] * ops.op[i][0] + ops.op[i][1] * ops.op[i][1] + ops.op[i][2] * ops.op[i][2]);
+        return 0x1.0p-18 * (world_extent + off);
+    }
+
+    int lower_simple_in(const Ops& ops, int hid)
+    {
         const double saved = pad_abs;
-        pad_abs = 0x1.0p-18 * (world_extent + off);
+        pad_abs = pad_through(ops);
+        const int prim = lower_simple(hid);
+        pad_abs = saved;
+        return prim;
+    }
+
+    // A BLAS over simple leaves seen through ops.
+    int make_blas(const Ops& ops, const std::vector<int>& leaves, int bvh_node, int& rc)
+    {
+        const double saved = pad_abs;
+        pad_abs = pad_through(ops);
         int root;
         if (accel == RT_ACCEL_MEDIAN && bvh_node >= 0) {
             root = lower_ref_bvh(bvh_node, /*in_instance=*/true, rc);
@@ -254,7 +277,8 @@ struct Builder {
         if (rc) return rc;
         const HNode& c = w.nodes[child];
         if (is_simple(c.kind)) {
-            items.push_back(item_box(make_instance(ops, RT_CHILD_PRIM, lower_simple(child)), box_through(ops, box_of(child))));
+            items.push_back(item_box(make_instance(ops, RT_CHILD_PRIM, lower_simple_in(ops, child)),
+                                     box_through(ops, box_of(child))));
             return RT_OK;
         }
         if (c.kind == HKind::ConstantMedium) return lower_medium(child, ops, items);
@@ -320,7 +344,7 @@ struct Builder {
         const int child = chain(id, ops, rc);
         if (rc) return rc;
         if (is_simple(w.nodes[child].kind)) {
-            prim_out = make_instance(ops, RT_CHILD_PRIM, lower_simple(child));
+            prim_out = make_instance(ops, RT_CHILD_PRIM, lower_simple_in(ops, child));
             return RT_OK;
         }
         if (w.nodes[child].kind == HKind::BvhNode) {

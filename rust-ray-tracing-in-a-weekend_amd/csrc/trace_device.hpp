@@ -44,6 +44,7 @@ struct RayT {
     R a;                      // length_squared(direction)
     R ya;                     // f64: 1 / a correctly rounded (NaN outside [2^-900, 2^900]: see div_rcp)
     R ix, iy, iz;             // 1 / direction (f64 slab tests only)
+    R yx, yy, yz;             // f64, scenes with rects: RN(1 / direction) for div_rcp (NaN outside its range)
     float fix, fiy, fiz;      // f32 1 / direction (f32 slab tests only)
     float fox, foy, foz;      // -origin * (1 / direction) in f32
     uint32_t onx, ony, onz;   // byte offsets in a node of child 0's near planes (by direction sign)
@@ -96,6 +97,15 @@ __device__ __forceinline__ bool first_active_lane()
 // Traversal is while-while (Aila & Laine 2009); the if-if form and a per-lane state
 // machine with ballot-gated shading both measured slower.
 //   NALL   every TLAS node is in LDS (no per-node LDS/global choice)
+#ifndef RT_RECT_RCP
+#define RT_RECT_RCP 0   // rect / box tests divide through precomputed reciprocals (measured: Cornell 58.1 vs 56.5 ms without; rejected)
+#endif
+#ifndef RT_BOX_PRETEST
+#define RT_BOX_PRETEST 0   // slab pre-test of a Box before its 6 rect tests (measured slower: Cornell 58.5 vs 56.6 ms, final 83.3 vs 82.6, smoke 41.9 vs 39.9 — a culled lane saves no wave instructions unless the whole wave is culled)
+#endif
+#ifndef RT_PK_SLAB
+#define RT_PK_SLAB 0   // packed-f32 (v_pk_fma_f32) slab test of the two children (C2 101.6 vs 99.9 ms: rejected)
+#endif
 #ifndef RT_TRACE_LOOP
 #define RT_TRACE_LOOP 1   // 0 if-if, 1 while-while, 2 while-while with speculative node visits
 #endif
@@ -201,12 +211,26 @@ __device__ __forceinline__ int32_t r_sat_i32(R x) { return rt_sat_i32((double)x)
 template <class R>
 __device__ __forceinline__ uint64_t r_sat_u64(R x) { return rt_sat_u64((double)x); }
 
+// Rect / box tests divide through the ray's correctly rounded reciprocals (div_rcp, same
+// bits, 3 FMAs instead of an f64 division per face): in the rects + instances variant only —
+// the media and final-scene variants would spill the 6 VGPRs the reciprocals hold.
+template <class C>
+constexpr bool RectRcp()
+{
+    return RT_RECT_RCP && !C::F32 && (C::F & FEAT_RECT) != 0 && (C::F & (FEAT_MEDIUM | FEAT_NOISE | FEAT_IMAGE)) == 0;
+}
+
 // spheres: the scene has spheres (wave-uniform); otherwise no root division needs 1/a
 template <class C>
 __device__ __forceinline__ void finish_ray(RayT<typename C::Real>& r, bool spheres)
 {
     r.a = r.dx * r.dx + r.dy * r.dy + r.dz * r.dz;
     if constexpr (!C::F32) r.ya = (C::F == FEAT_SET_SPHERES || spheres) ? rcp_for_div(r.a) : __builtin_nan("");
+    if constexpr (RectRcp<C>()) {
+        r.yx = rcp_for_div(r.dx);
+        r.yy = rcp_for_div(r.dy);
+        r.yz = rcp_for_div(r.dz);
+    }
     if constexpr (C::S32) {
         r.fix = f32_inv_dir(r.dx);
         r.fiy = f32_inv_dir(r.dy);
@@ -319,13 +343,21 @@ __device__ __forceinline__ void rect_axes(int axis, const RayT<R>& r, R& ok, R& 
     else { ok = r.ox; dk = r.dx; oa = r.oy; da = r.dy; ob = r.oz; db = r.dz; }
 }
 
-template <class R>
+template <bool RCP = false, class R>
 __device__ __forceinline__ bool rect_t(int axis, R a0, R a1, R b0, R b1, R k, const RayT<R>& r, R t_min, R t_max,
                                        R& t_out)
 {
     R ok, dk, oa, da, ob, db;
     rect_axes(axis, r, ok, dk, oa, da, ob, db);
-    const R t = (k - ok) / dk;
+    R t;
+    if constexpr (RCP) {
+        // (k - o) / d through the ray's correctly rounded 1/d: the same bits (div_rcp), 3 FMAs
+        // instead of a division per rect (a Box tests 6)
+        const R yk = axis == 0 ? r.yz : axis == 1 ? r.yy : r.yx;
+        t = div_rcp(k - ok, dk, yk);
+    } else {
+        t = (k - ok) / dk;
+    }
     if (t < t_min || t > t_max) return false;
     const R x = oa + t * da;
     const R y = ob + t * db;
@@ -358,99 +390,7 @@ __device__ __forceinline__ void rect_finish(int axis, R a0, R a1, R b0, R b1, co
     h.pz = r.oz + r.dz * t;
 }
 
-// the six sides of new_box (hittable.rs:135-142): side -> axis, (a0 a1 b0 b1 k) from min/max
-template <class R>
-__device__ __forceinline__ void box_side(const rt_prim& p, int side, int& axis, R& a0, R& a1, R& b0, R& b1, R& k)
-{
-    const R mnx = (R)p.p[0], mny = (R)p.p[1], mnz = (R)p.p[2], mxx = (R)p.p[3], mxy = (R)p.p[4], mxz = (R)p.p[5];
-    if (side < 2) { axis = 0; a0 = mnx; a1 = mxx; b0 = mny; b1 = mxy; k = side == 0 ? mxz : mnz; }
-    else if (side < 4) { axis = 1; a0 = mnx; a1 = mxx; b0 = mnz; b1 = mxz; k = side == 2 ? mxy : mny; }
-    else { axis = 2; a0 = mny; a1 = mxy; b0 = mnz; b1 = mxz; k = side == 4 ? mxx : mnx; }
-}
-
-// Box::hit = hit_hittables over its sides (hittable.rs:229-231): closest, ties to the later side.
-template <class R>
-__device__ __forceinline__ bool box_t(const rt_prim& p, const RayT<R>& r, R t_min, R t_max, R& t, int& side)
-{
-    bool any = false;
-#pragma unroll
-    for (int s = 0; s < 6; ++s) {
-        int axis;
-        R a0, a1, b0, b1, k, ts;
-        box_side(p, s, axis, a0, a1, b0, b1, k);
-        if (rect_t(axis, a0, a1, b0, b1, k, r, t_min, t_max, ts)) {
-            t_max = ts;
-            t = ts;
-            side = s;
-            any = true;
-        }
-    }
-    return any;
-}
-
-// The centre of a Sphere, or of a MovingSphere at the ray's time: center_0 +
-// ((time - time_0) / (time_1 - time_0)) * (center_1 - center_0) (hittable.rs:556-558).
-// Both kinds go through one code path (the moving centre is a select), so a wave whose
-// lanes hold both kinds runs the sphere test once, not once per kind.
-template <class R>
-__device__ __forceinline__ void sphere_center(const rt_prim& p, const RayT<R>& r, double& cx, double& cy, double& cz)
-{
-    const double c0x = p.p[0], c0y = p.p[1], c0z = p.p[2];
-    const double vx = p.p[5], vy = p.p[6], vz = p.p[7];
-    const bool moving = p.kind == RT_PRIM_MOVING_SPHERE;
-    double s = (double)r.time;
-    if (moving && !p.a) s = ((double)r.time - p.p[8]) / (p.p[9] - p.p[8]);
-    cx = moving ? c0x + vx * s : c0x;
-    cy = moving ? c0y + vy * s : c0y;
-    cz = moving ? c0z + vz * s : c0z;
-}
-
-// Sphere, MovingSphere, rects, Box: t-only (hittable.rs:211-231).
-template <class C, class R = typename C::Real>
-__device__ __forceinline__ bool simple_t(const rt_prim& p, const RayT<R>& r, R t_min, R t_max, R& t, int& side,
-                                         Count& cnt)
-{
-    if (C::COUNT) cnt.prims++;
-    if (!(C::F & FEAT_RECT) || p.kind <= RT_PRIM_MOVING_SPHERE) {
-        double cx, cy, cz;
-        sphere_center(p, r, cx, cy, cz);
-        return sphere_t(cx, cy, cz, p.p[3], r, t_min, t_max, t);
-    } else {
-        const R q0 = (R)p.p[0], q1 = (R)p.p[1], q2 = (R)p.p[2], q3 = (R)p.p[3], q4 = (R)p.p[4];
-        switch (p.kind) {
-        case RT_PRIM_XY_RECT: return rect_t(0, q0, q1, q2, q3, q4, r, t_min, t_max, t);
-        case RT_PRIM_XZ_RECT: return rect_t(1, q0, q1, q2, q3, q4, r, t_min, t_max, t);
-        case RT_PRIM_YZ_RECT: return rect_t(2, q0, q1, q2, q3, q4, r, t_min, t_max, t);
-        case RT_PRIM_BOX: return box_t(p, r, t_min, t_max, t, side);
-        default: return false;
-        }
-    }
-}
-
-template <class C, class R = typename C::Real>
-__device__ __forceinline__ void simple_finish(const rt_prim& p, const RayT<R>& r, R t, int side, HitT<R>& h)
-{
-    if constexpr ((C::F & FEAT_RECT) != 0) {
-        if (p.kind >= RT_PRIM_XY_RECT && p.kind <= RT_PRIM_YZ_RECT) {
-            rect_finish<C>(p.kind - RT_PRIM_XY_RECT, (R)p.p[0], (R)p.p[1], (R)p.p[2], (R)p.p[3], r, t, p.mat, h);
-            return;
-        }
-        if (p.kind == RT_PRIM_BOX) {
-            int axis;
-            R a0, a1, b0, b1, k;
-            box_side(p, side, axis, a0, a1, b0, b1, k);
-            rect_finish<C>(axis, a0, a1, b0, b1, r, t, p.mat, h);
-            return;
-        }
-    }
-    double cx, cy, cz;
-    sphere_center(p, r, cx, cy, cz);
-    sphere_finish<C>((R)cx, (R)cy, (R)cz, (R)p.p[4], r, t, p.mat, h);
-}
-
-// ---------------------------------------------------------------------------
-// BVH traversal
-// ---------------------------------------------------------------------------
+// slab tests of an f32 box (BVH nodes, Box pre-tests)
 template <class RayType>
 __device__ __forceinline__ bool slab32(const float* lo, const float* hi, const RayType& r, float t_min, float t_max,
                                        float& t_near)
@@ -492,6 +432,113 @@ __device__ __forceinline__ bool slab(const float* lo, const float* hi, const Ray
     return tn <= tf;
 }
 
+// the six sides of new_box (hittable.rs:135-142): side -> axis, (a0 a1 b0 b1 k) from min/max
+template <class R>
+__device__ __forceinline__ void box_side(const rt_prim& p, int side, int& axis, R& a0, R& a1, R& b0, R& b1, R& k)
+{
+    const R mnx = (R)p.p[0], mny = (R)p.p[1], mnz = (R)p.p[2], mxx = (R)p.p[3], mxy = (R)p.p[4], mxz = (R)p.p[5];
+    if (side < 2) { axis = 0; a0 = mnx; a1 = mxx; b0 = mny; b1 = mxy; k = side == 0 ? mxz : mnz; }
+    else if (side < 4) { axis = 1; a0 = mnx; a1 = mxx; b0 = mnz; b1 = mxz; k = side == 2 ? mxy : mny; }
+    else { axis = 2; a0 = mny; a1 = mxy; b0 = mnz; b1 = mxz; k = side == 4 ? mxx : mnx; }
+}
+
+// Box::hit = hit_hittables over its sides (hittable.rs:229-231): closest, ties to the later side.
+// The reference has no bounding-box pre-test (Q8); a conservative one on the box's padded
+// f32 bounds (flatten.cpp) only skips rect tests that cannot hit, like a BVH node box does.
+template <bool RCP = false, bool S32 = true, class R>
+__device__ __forceinline__ bool box_t(const rt_prim& p, const RayT<R>& r, R t_min, R t_max, R& t, int& side)
+{
+    if (RT_BOX_PRETEST && p.b) {
+        const float* fb = reinterpret_cast<const float*>(&p.p[6]);
+        bool hit;
+        if constexpr (S32) {
+            float tn;
+            hit = slab32(fb, fb + 3, r, f32_down(t_min), f32_up(t_max), tn);
+        } else {
+            R tn;
+            hit = slab(fb, fb + 3, r, t_min, t_max, tn);
+        }
+        if (!hit) return false;
+    }
+    bool any = false;
+#pragma unroll
+    for (int s = 0; s < 6; ++s) {
+        int axis;
+        R a0, a1, b0, b1, k, ts;
+        box_side(p, s, axis, a0, a1, b0, b1, k);
+        if (rect_t<RCP>(axis, a0, a1, b0, b1, k, r, t_min, t_max, ts)) {
+            t_max = ts;
+            t = ts;
+            side = s;
+            any = true;
+        }
+    }
+    return any;
+}
+
+// The centre of a Sphere, or of a MovingSphere at the ray's time: center_0 +
+// ((time - time_0) / (time_1 - time_0)) * (center_1 - center_0) (hittable.rs:556-558).
+// Both kinds go through one code path (the moving centre is a select), so a wave whose
+// lanes hold both kinds runs the sphere test once, not once per kind.
+template <class R>
+__device__ __forceinline__ void sphere_center(const rt_prim& p, const RayT<R>& r, double& cx, double& cy, double& cz)
+{
+    const double c0x = p.p[0], c0y = p.p[1], c0z = p.p[2];
+    const double vx = p.p[5], vy = p.p[6], vz = p.p[7];
+    const bool moving = p.kind == RT_PRIM_MOVING_SPHERE;
+    double s = (double)r.time;
+    if (moving && !p.a) s = ((double)r.time - p.p[8]) / (p.p[9] - p.p[8]);
+    cx = moving ? c0x + vx * s : c0x;
+    cy = moving ? c0y + vy * s : c0y;
+    cz = moving ? c0z + vz * s : c0z;
+}
+
+// Sphere, MovingSphere, rects, Box: t-only (hittable.rs:211-231).
+template <class C, class R = typename C::Real>
+__device__ __forceinline__ bool simple_t(const rt_prim& p, const RayT<R>& r, R t_min, R t_max, R& t, int& side,
+                                         Count& cnt)
+{
+    if (C::COUNT) cnt.prims++;
+    if (!(C::F & FEAT_RECT) || p.kind <= RT_PRIM_MOVING_SPHERE) {
+        double cx, cy, cz;
+        sphere_center(p, r, cx, cy, cz);
+        return sphere_t(cx, cy, cz, p.p[3], r, t_min, t_max, t);
+    } else {
+        const R q0 = (R)p.p[0], q1 = (R)p.p[1], q2 = (R)p.p[2], q3 = (R)p.p[3], q4 = (R)p.p[4];
+        switch (p.kind) {
+        case RT_PRIM_XY_RECT: return rect_t<RectRcp<C>()>(0, q0, q1, q2, q3, q4, r, t_min, t_max, t);
+        case RT_PRIM_XZ_RECT: return rect_t<RectRcp<C>()>(1, q0, q1, q2, q3, q4, r, t_min, t_max, t);
+        case RT_PRIM_YZ_RECT: return rect_t<RectRcp<C>()>(2, q0, q1, q2, q3, q4, r, t_min, t_max, t);
+        case RT_PRIM_BOX: return box_t<RectRcp<C>(), C::S32>(p, r, t_min, t_max, t, side);
+        default: return false;
+        }
+    }
+}
+
+template <class C, class R = typename C::Real>
+__device__ __forceinline__ void simple_finish(const rt_prim& p, const RayT<R>& r, R t, int side, HitT<R>& h)
+{
+    if constexpr ((C::F & FEAT_RECT) != 0) {
+        if (p.kind >= RT_PRIM_XY_RECT && p.kind <= RT_PRIM_YZ_RECT) {
+            rect_finish<C>(p.kind - RT_PRIM_XY_RECT, (R)p.p[0], (R)p.p[1], (R)p.p[2], (R)p.p[3], r, t, p.mat, h);
+            return;
+        }
+        if (p.kind == RT_PRIM_BOX) {
+            int axis;
+            R a0, a1, b0, b1, k;
+            box_side(p, side, axis, a0, a1, b0, b1, k);
+            rect_finish<C>(axis, a0, a1, b0, b1, r, t, p.mat, h);
+            return;
+        }
+    }
+    double cx, cy, cz;
+    sphere_center(p, r, cx, cy, cz);
+    sphere_finish<C>((R)cx, (R)cy, (R)cz, (R)p.p[4], r, t, p.mat, h);
+}
+
+// ---------------------------------------------------------------------------
+// BVH traversal
+// ---------------------------------------------------------------------------
 constexpr int RT_DONE = (int)0x80000000;
 
 // A node as four 16-B loads (ds_read_b128 from LDS, global_load_dwordx4 from L1/L2).
@@ -551,6 +598,26 @@ __device__ __forceinline__ bool traverse(const SceneDev& S, int root, const RayT
             auto plane = [&](const char* p, int child) { return *reinterpret_cast<const float*>(p + o + 24 * child); };
             const int2 ch = *reinterpret_cast<const int2*>(lb + o + 48);
             float tn[2], tf[2];
+#if RT_PK_SLAB
+          if constexpr (C::F == FEAT_SET_SPHERES) {
+            // both children's plane of one axis as a pair: one v_pk_fma_f32 per plane (the
+            // spheres variant only: the broadcast pairs cost 6 VGPRs, which the 3-wave
+            // variants pay in spills)
+            typedef float f2 __attribute__((ext_vector_type(2)));
+            auto pair = [&](const char* p) { return f2{plane(p, 0), plane(p, 1)}; };
+            const f2 ix = {r.fix, r.fix}, iy = {r.fiy, r.fiy}, iz = {r.fiz, r.fiz};
+            const f2 ox = {r.fox, r.fox}, oy = {r.foy, r.foy}, oz = {r.foz, r.foz};
+            const f2 nx = __builtin_elementwise_fma(pair(pnx), ix, ox), fx = __builtin_elementwise_fma(pair(pfx), ix, ox);
+            const f2 ny = __builtin_elementwise_fma(pair(pny), iy, oy), fy = __builtin_elementwise_fma(pair(pfy), iy, oy);
+            const f2 nz = __builtin_elementwise_fma(pair(pnz), iz, oz), fz = __builtin_elementwise_fma(pair(pfz), iz, oz);
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+                tn[c] = fmaxf(fmaxf(nx[c], ny[c]), fmaxf(nz[c], tmin_f));
+                tf[c] = fminf(fminf(fx[c], fy[c]), fminf(fz[c], tmax_f));
+            }
+          } else
+#endif
+          {
 #pragma unroll
             for (int c = 0; c < 2; ++c) {
                 const float nx = __builtin_fmaf(plane(pnx, c), r.fix, r.fox);
@@ -562,6 +629,7 @@ __device__ __forceinline__ bool traverse(const SceneDev& S, int root, const RayT
                 tn[c] = fmaxf(fmaxf(nx, ny), fmaxf(nz, tmin_f));
                 tf[c] = fminf(fminf(fx, fy), fminf(fz, tmax_f));
             }
+          }
             const bool h0 = tn[0] <= tf[0], h1 = tn[1] <= tf[1], near0 = tn[0] <= tn[1];
             if (h0 && h1) {
                 stack[sp++] = near0 ? ch.y : ch.x;

@@ -198,7 +198,7 @@ def test_feature_set_variants_identical(rt, renderer, scene_id, W, H, feat):
     renderer.upload(world)
     img = renderer.render(cam, p)
     assert renderer.stats().variant_features == feat
-    os.environ["RT_EXTRA_FEATURES"] = "127"
+    os.environ["RT_EXTRA_FEATURES"] = "255"
     try:
         big = rt.Renderer(0)
     finally:
@@ -206,7 +206,7 @@ def test_feature_set_variants_identical(rt, renderer, scene_id, W, H, feat):
     try:
         big.upload(world)
         img_all = big.render(cam, p)
-        assert big.stats().variant_features == 127
+        assert big.stats().variant_features == 255
     finally:
         big.close()
     assert np.array_equal(img, img_all)
