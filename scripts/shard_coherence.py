@@ -1,0 +1,49 @@
+#!/usr/bin/env python3
+"""Per-sample cost of one rank's row shard vs the whole frame (C2 geometry).
+
+A rank of N renders rows y = r + k*N; its 8x8 work tiles then span 8 columns x 8N image
+rows, i.e. camera rays over a taller solid angle. This times rank 0's shard for N = 1, 2, 4,
+8 on one GPU (kernel ms per shard, Msamples/s of the shard), so the multi-GPU scaling loss
+from tile coherence can be read apart from the gather.
+
+usage: python scripts/shard_coherence.py [--spp 500] [--reps 3]
+"""
+import argparse
+import json
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--spp", type=int, default=500)
+    ap.add_argument("--reps", type=int, default=3)
+    a = ap.parse_args()
+    import numpy as np
+    import torch  # noqa: F401  (one HIP runtime: torch's)
+    import __graft_entry__ as ge
+    rt = ge.import_binding()
+    W, H = 1200, 800
+    world = rt.World(1).build_scene(0)
+    cam, bg = rt.scene_camera(0, W, H)
+    r = rt.Renderer(0)
+    r.upload(world)
+    for n in (1, 2, 4, 8):
+        rows = rt.rows_in_shard(H, 0, n)
+        p = rt.Renderer.params(W, H, a.spp, 50, bg, 1, row_begin=0, row_stride=n, out_format=rt.RT_OUT_F32)
+        out = np.empty((rows, W, 3), np.float32)
+        r.render(cam, p, out)
+        ms = []
+        for _ in range(a.reps):
+            r.render(cam, p, out)
+            ms.append(r.stats().kernel_ms)
+        k = float(np.median(ms))
+        print(json.dumps({"n": n, "rows": rows, "kernel_ms": round(k, 3),
+                          "msamples_per_s": round(rows * W * a.spp / k / 1e3, 1)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
