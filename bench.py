@@ -37,6 +37,7 @@ sys.path.insert(0, REPO)
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 N_SIMDS = 1024                 # 256 CUs x 4 SIMDs
 PMC_JSON = os.path.join(REPO, "profiles", "pmc_r02.json")
+ROW_BLOCK = 1                  # multi-GPU shards: single rows round-robin over the ranks
 
 
 # BASELINE.json configs (SURVEY §8 shorthand). The headline metric is C2; the others are
@@ -168,8 +169,12 @@ def main():
         renderer.set_precision(rt.RT_PREC_F32)
     t_build = time.perf_counter() - t_build
 
-    rows = rt.rows_in_shard(H, rank, world)
-    rows_max = (H + world - 1) // world
+    # ranks take rows round-robin (ROW_BLOCK 1). 8-row bands (row_block 8) keep every 8x8
+    # work tile contiguous in the image and raise a shard's per-sample rate ~3 % at 8 GPUs,
+    # but 100 bands over 8 ranks leave ranks of 13 and 12 bands: the job is slower
+    # (scripts/shard_coherence.py, profiles/r02p_shard.log)
+    rows = rt.rows_in_shard(H, rank, world, ROW_BLOCK)
+    rows_max = max(rt.rows_in_shard(H, r, world, ROW_BLOCK) for r in range(world))
     slab = torch.zeros((rows_max, W, 3), dtype=torch.float32, device=device)
     gathered = [torch.empty_like(slab) for _ in range(world)] if (world > 1 and rank == 0) else None
     frame = torch.empty((H, W, 3), dtype=torch.float32, device=device) if rank == 0 else None
@@ -179,7 +184,7 @@ def main():
     # op of a step runs under this stream; NCCL orders its gather after it.
     stream = torch.cuda.Stream(device)
     params = rt.Renderer.params(W, H, spp, depth, bg, args.seed, row_begin=rank, row_stride=world,
-                                spp_chunk=args.spp_chunk, out_format=rt.RT_OUT_F32)
+                                spp_chunk=args.spp_chunk, out_format=rt.RT_OUT_F32, row_block=ROW_BLOCK)
     kernel_ms = []
 
     def step():
@@ -188,7 +193,7 @@ def main():
             if world > 1:
                 dist.gather(slab, gathered if rank == 0 else None, dst=0)
                 if rank == 0:
-                    rt.assemble_rows(gathered, H, world, out=frame)   # rows y = r + k*world
+                    rt.assemble_rows(gathered, H, world, out=frame, row_block=ROW_BLOCK)
             else:
                 frame[:] = slab[:H]
 
@@ -256,6 +261,7 @@ def main():
     cs = None
     if not args.no_count and not f32:   # count_work is an f64-mode diagnostic
         cp = rt.Renderer.params(W, H, count_spp, depth, bg, args.seed, row_begin=rank, row_stride=world,
+                                row_block=ROW_BLOCK,
                                 spp_chunk=min(args.spp_chunk, count_spp), out_format=rt.RT_OUT_F32, count_work=1)
         renderer.render(cam, cp)
         cs = renderer.stats()

@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 1
+#define RT_ABI_VERSION 2
 
 enum {
     RT_OK = 0,
@@ -156,6 +156,11 @@ typedef struct rt_render_params {
     double background[3];
     uint64_t render_seed;
     void* stream;                /* hipStream_t to launch on (NULL = the context's stream) */
+    int32_t row_block;           /* 0 / 1: rows as above. B > 1 (a power of two <= 64): the image is cut
+                                    into bands of B rows and the shard is bands j = row_begin +
+                                    m*row_stride (rows jB .. jB+B-1 < height): row-band interleave, so
+                                    a multi-GPU shard keeps 8x8 work tiles contiguous in the image */
+    int32_t reserved_;
 } rt_render_params;
 
 /* Renders the selected rows into out (rows_local x width x 3, row k = the k-th
@@ -165,6 +170,8 @@ int rt_render(rt_ctx* ctx, const rt_camera* cam, const rt_render_params* p, void
 
 /* Rows rendered for (height, row_begin, row_stride). */
 int rt_rows_in_shard(int height, int row_begin, int row_stride);
+/* Rows rendered for (height, row_begin, row_stride, row_block) (rt_render_params.row_block). */
+int rt_rows_in_band_shard(int height, int row_begin, int row_stride, int row_block);
 
 typedef struct rt_stats {
     double kernel_ms;            /* last rt_render: trace kernel time (HIP events) */

@@ -83,7 +83,8 @@ struct rt_ctx {
     bool pending_counts = false;
     rt_stats stats{};
     uint32_t features = rtk::FEAT_ALL;  // of the uploaded scene
-    int block_chunks = 0;               // RT_BLOCK_CHUNKS: chunks per work block of the pools (0: auto)
+    int block_chunks = 0;               // RT_BLOCK_CHUNKS: chunks per item-pool work block (0: auto)
+    int block_samples = 0;              // RT_BLOCK_SAMPLES: samples per per-sample-pool work block (0: auto)
     uint32_t extra_features = 0;        // RT_EXTRA_FEATURES: a larger kernel variant than the scene needs (tests)
     double pad_extent = 0.0;
     int opt_slab32 = 1;                 // rt_ctx_set_variant / RT_SLAB32
@@ -133,6 +134,7 @@ int rt_ctx_create(int device, rt_ctx** out)
     if (const char* e = std::getenv("RT_SCHEDULE")) c->opt_pool = std::min(3, std::max(0, std::atoi(e)));
     if (const char* e = std::getenv("RT_PRECISION")) c->opt_precision = std::atoi(e) == RT_PREC_F32 ? RT_PREC_F32 : RT_PREC_F64;
     if (const char* e = std::getenv("RT_BLOCK_CHUNKS")) c->block_chunks = std::min(64, std::max(1, std::atoi(e)));
+    if (const char* e = std::getenv("RT_BLOCK_SAMPLES")) c->block_samples = std::min(1024, std::max(1, std::atoi(e)));
     if (const char* e = std::getenv("RT_EXTRA_FEATURES")) c->extra_features = (uint32_t)std::atoi(e) & rtk::FEAT_ALL;
     if (const char* e = std::getenv("RT_SAMPLE_BUF_MB")) c->sample_buf_cap = (size_t)std::max(1L, std::atol(e)) << 20;
     hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
@@ -727,10 +729,28 @@ int rt_rows_in_shard(int height, int row_begin, int row_stride)
 // summation order (and the image) does not depend on launch geometry or sharding
 static int auto_chunk(int spp) { return std::min(16, std::max(1, (spp + 15) / 16)); }
 
+int rt_rows_in_band_shard(int height, int row_begin, int row_stride, int row_block)
+{
+    if (row_block <= 1) return rt_rows_in_shard(height, row_begin, row_stride);
+    if (height <= 0 || row_stride <= 0 || row_begin < 0 || (row_block & (row_block - 1)) || row_block > 64) return 0;
+    const int bands = (height + row_block - 1) / row_block;
+    const int mine = rt_rows_in_shard(bands, row_begin, row_stride);
+    if (!mine) return 0;
+    const int last = row_begin + (mine - 1) * row_stride;   // its last band may be cut by the image
+    return (mine - 1) * row_block + std::min(row_block, height - last * row_block);
+}
+
+static int row_block_of(const rt_render_params* p) { return p->row_block > 1 ? p->row_block : 1; }
+static int shard_rows(const rt_render_params* p)
+{
+    return rt_rows_in_band_shard(p->height, p->row_begin, p->row_stride, row_block_of(p));
+}
+
 static bool bad_geometry(const rt_render_params* p)
 {
+    const int b = row_block_of(p);
     return p->width < 2 || p->height < 2 || p->row_stride < 1 || p->row_begin < 0 || p->spp_chunk < 0 ||
-           (long long)p->width * p->height > 0xffffffffLL;
+           (b & (b - 1)) || b > 64 || (long long)p->width * p->height > 0xffffffffLL;
 }
 
 static int grow(rt_ctx* c, hipStream_t stream, double*& buf, size_t& cap, size_t need)
@@ -764,7 +784,7 @@ struct Sink {
 static int run_range(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, int s_begin, int s_end, int chunk,
                      hipStream_t stream, const Sink& sink)
 {
-    const int n_rows = rt_rows_in_shard(p->height, p->row_begin, p->row_stride);
+    const int n_rows = shard_rows(p);
     const long long n_px = (long long)n_rows * p->width;
     const size_t px = (size_t)std::max<long long>(n_px, 1);
 
@@ -785,6 +805,8 @@ static int run_range(rt_ctx* c, const rt_camera* cam, const rt_render_params* p,
     K.spp_chunk = chunk;
     K.row_begin = p->row_begin;
     K.row_stride = p->row_stride;
+    K.row_block_shift = 0;
+    while ((1 << K.row_block_shift) < row_block_of(p)) K.row_block_shift++;
     K.n_rows = n_rows;
     K.tiles_x = (p->width + 7) / 8;
     K.tiles_y = (n_rows + 7) / 8;
@@ -823,7 +845,19 @@ static int run_range(rt_ctx* c, const rt_camera* cam, const rt_render_params* p,
     // work blocks of one tile: 16-sample chunks, per-sample pool one chunk per block, item pool
     // two (C2 kernel ms, pool 1/2/4 chunks: 99.8/100.2/103.2; items 1/2/4: 106.8/104.1/105.0;
     // profiles/r02f_*, r02g_*)
-    K.block_chunks = c->block_chunks > 0 ? c->block_chunks : (o.pool == RT_SCHED_ITEMS ? 2 : 1);
+    K.block_chunks = c->block_chunks > 0 ? c->block_chunks : 2;
+    // per-sample pool blocks: the chunk's 16 samples per tile while that leaves >= 160 k blocks
+    // (~40 per resident wave), else halved down to 4: a small shard's last blocks would
+    // otherwise leave waves idle (C2 rows of 1 of 8 GPUs: 16 / 8 / 4 samples 14.06 / 13.70 /
+    // 13.57 ms; the whole frame 99.9 / 100.0 / 101.4; scripts/shard_coherence.py, r02p)
+    if (c->block_samples > 0) {
+        K.block_samples = c->block_samples;
+    } else {
+        const long long tiles = (long long)K.tiles_x * K.tiles_y;
+        int bs = chunk;
+        while (bs > 4 && tiles * ((total + bs - 1) / bs) < 160000) bs = (bs + 1) / 2;
+        K.block_samples = bs;
+    }
     const long long fit = (long long)std::max<size_t>(1, c->sample_buf_cap / px_bytes);
     const long long batch = std::min<long long>(total, per_sample ? fit : fit * chunk);
     const int n_batches = (int)((total + batch - 1) / batch);
@@ -934,7 +968,7 @@ int rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, void* 
     if (!c->has_scene) return fail(RT_ERR_NO_SCENE, "no scene uploaded");
     if (bad_geometry(p) || p->spp < 1 || p->max_depth < 0 || (p->out_format != RT_OUT_F32 && p->out_format != RT_OUT_F64))
         return fail(RT_ERR_INVALID, "bad render params");
-    const int n_rows = rt_rows_in_shard(p->height, p->row_begin, p->row_stride);
+    const int n_rows = shard_rows(p);
     const int chunk = p->spp_chunk > 0 ? std::min(p->spp_chunk, p->spp) : auto_chunk(p->spp);
     const long long n_px = (long long)n_rows * p->width;
 
@@ -964,7 +998,7 @@ int rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, void* 
 // ---- progressive accumulation -----------------------------------------------------------------
 struct rt_accum {
     rt_ctx* ctx = nullptr;
-    int width = 0, height = 0, row_begin = 0, row_stride = 1, n_rows = 0, chunk = 1;
+    int width = 0, height = 0, row_begin = 0, row_stride = 1, row_block = 1, n_rows = 0, chunk = 1;
     long long n_px = 0;
     int64_t done = 0;
     double* sums = nullptr;             // device, n_px x 3
@@ -984,7 +1018,8 @@ int rt_accum_create(rt_ctx* c, const rt_render_params* p, rt_accum** out)
     a->height = p->height;
     a->row_begin = p->row_begin;
     a->row_stride = p->row_stride;
-    a->n_rows = rt_rows_in_shard(p->height, p->row_begin, p->row_stride);
+    a->row_block = row_block_of(p);
+    a->n_rows = shard_rows(p);
     a->chunk = p->spp_chunk > 0 ? p->spp_chunk : auto_chunk(p->spp);
     a->n_px = (long long)a->n_rows * p->width;
     a->last_stream = c->stream;
@@ -1016,7 +1051,7 @@ int rt_accum_add(rt_ctx* c, rt_accum* a, const rt_camera* cam, const rt_render_p
     if (a->ctx != c) return fail(RT_ERR_INVALID, "accumulator belongs to another context");
     if (!c->has_scene) return fail(RT_ERR_NO_SCENE, "no scene uploaded");
     if (p->width != a->width || p->height != a->height || p->row_begin != a->row_begin ||
-        p->row_stride != a->row_stride)
+        p->row_stride != a->row_stride || row_block_of(p) != a->row_block)
         return fail(RT_ERR_INVALID, "render params do not match the accumulator's shard");
     if (sample_count < 0 || p->max_depth < 0 || a->done + sample_count > 0x7fffffffLL)
         return fail(RT_ERR_INVALID, "bad sample range");

@@ -1295,6 +1295,14 @@ __device__ __forceinline__ bool shade(const SceneDev& S, const KParams& P, const
     return true;
 }
 
+// image row of the shard's local row k: y = row_begin + k*row_stride, or in bands of 2^s rows
+// y = (row_begin + (k >> s)*row_stride) << s | (k & (2^s - 1))
+__device__ __forceinline__ int image_row(const KParams& P, int k)
+{
+    const int s = P.row_block_shift;
+    return ((P.row_begin + (k >> s) * P.row_stride) << s) + (k & ((1 << s) - 1));
+}
+
 // lane -> (chunk, pixel): a wave64 owns an 8x8 tile of one chunk
 struct LaneWork {
     int x, y, k, chunk, s_begin, s_end;
@@ -1311,7 +1319,7 @@ __device__ __forceinline__ bool lane_work(const KParams& P, LaneWork& w)
     w.x = (tile % P.tiles_x) * 8 + (lane & 7);
     w.k = (tile / P.tiles_x) * 8 + (lane >> 3);
     if (w.x >= P.width || w.k >= P.n_rows) return false;
-    w.y = P.row_begin + w.k * P.row_stride;
+    w.y = image_row(P, w.k);
     w.pixel = (uint32_t)w.y * (uint32_t)P.width + (uint32_t)w.x;
     w.s_begin = P.sample_begin + w.chunk * P.spp_chunk;
     w.s_end = min(P.spp, w.s_begin + P.spp_chunk);
@@ -1484,8 +1492,12 @@ __global__ void __launch_bounds__(256, min_waves<C>()) trace_pool(SceneDev S, co
     // a work block = one tile x block_chunks consecutive chunks (items chunk-major; the
     // per-sample pool's units sample-major): lanes stay on one tile longer, and its rays
     // are coherent (C2 item pool, chunks of 4: 108.4 ms with blocks of one chunk, 101.8 with 8)
-    const unsigned group = (unsigned)P.block_chunks;
-    const unsigned n_blocks = n_tiles * (((unsigned)P.n_chunks + group - 1) / group);
+    // per-sample pool: a block = one tile x block_samples consecutive samples (any count: the
+    // per-sample output does not depend on it)
+    const unsigned group = ITEMS ? (unsigned)P.block_chunks : (unsigned)P.block_samples;
+    const unsigned n_groups = ITEMS ? ((unsigned)P.n_chunks + group - 1) / group
+                                    : ((unsigned)(P.spp - P.sample_begin) + group - 1) / group;
+    const unsigned n_blocks = n_tiles * n_groups;
     const size_t n_px = (size_t)P.n_rows * (size_t)P.width;
     // current work block (wave-uniform)
     unsigned blk_units = 0, blk_next = 0, nvalid = 1;
@@ -1520,14 +1532,19 @@ __global__ void __launch_bounds__(256, min_waves<C>()) trace_pool(SceneDev S, co
                     exhausted = true;
                     break;
                 }
-                const unsigned chunk = b / n_tiles * group, tile = b - (chunk / group) * n_tiles;
+                const unsigned grp = b / n_tiles, tile = b - grp * n_tiles;
                 tx0 = (int)(tile % (unsigned)P.tiles_x) * 8;
                 tk0 = (int)(tile / (unsigned)P.tiles_x) * 8;
                 vw = min(8, P.width - tx0);
                 nvalid = (unsigned)(vw * min(8, P.n_rows - tk0));
-                s0 = P.sample_begin + (int)chunk * P.spp_chunk;
-                blk_units = ITEMS ? nvalid * min(group, (unsigned)P.n_chunks - chunk)
-                                  : nvalid * (unsigned)(min(P.spp, s0 + (int)group * P.spp_chunk) - s0);
+                if constexpr (ITEMS) {
+                    const unsigned chunk = grp * group;
+                    s0 = P.sample_begin + (int)chunk * P.spp_chunk;
+                    blk_units = nvalid * min(group, (unsigned)P.n_chunks - chunk);
+                } else {
+                    s0 = P.sample_begin + (int)(grp * group);
+                    blk_units = nvalid * (unsigned)(min(P.spp, s0 + (int)group) - s0);
+                }
                 blk_next = 0;
             }
             const unsigned rank = lanes_below(need);
@@ -1567,7 +1584,7 @@ __global__ void __launch_bounds__(256, min_waves<C>()) trace_pool(SceneDev S, co
                 if (first_active_lane()) cnt.cam_steps++;
             }
             new_sample = false;
-            const int y = P.row_begin + k * P.row_stride;
+            const int y = image_row(P, k);
             key.pixel = (uint32_t)y * (uint32_t)P.width + (uint32_t)x;
             key.sample = (uint32_t)s;
             ds_start(st, P.seed, key.pixel, (uint32_t)s);

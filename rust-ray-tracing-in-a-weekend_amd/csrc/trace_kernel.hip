@@ -169,8 +169,11 @@ hipError_t launch_trace(const SceneDev& S, const KParams& Ph, const KParams* P, 
     L.work = work;
     L.pool = o.pool;
     // waves of the chunk schedule / work blocks of the pools
-    const int group = o.pool ? std::max(1, Ph.block_chunks) : 1;
-    L.n_blocks = (unsigned long long)Ph.tiles_x * Ph.tiles_y * ((Ph.n_chunks + group - 1) / group);
+    const long long groups = o.pool == 2   ? (Ph.n_chunks + std::max(1, Ph.block_chunks) - 1) / std::max(1, Ph.block_chunks)
+                             : o.pool == 1 ? ((long long)Ph.spp - Ph.sample_begin + std::max(1, Ph.block_samples) - 1) /
+                                                 std::max(1, Ph.block_samples)
+                                           : Ph.n_chunks;
+    L.n_blocks = (unsigned long long)Ph.tiles_x * Ph.tiles_y * groups;
     if (L.n_blocks == 0) return hipSuccess;
     if (L.n_blocks > 0xfffffff0ULL) return hipErrorInvalidValue;
     if (o.pool) {

@@ -39,9 +39,11 @@ struct KParams {
     int32_t width, height, spp, max_depth;
     int32_t spp_chunk, n_chunks;
     int32_t row_begin, row_stride, n_rows;
+    int32_t row_block_shift;    // rows in bands of 2^shift (rt_render_params.row_block); 0: single rows
     int32_t tiles_x, tiles_y;   // 8x8 pixel tiles over (width, n_rows)
     int32_t sample_begin;       // chunk c covers samples [sample_begin + c*spp_chunk, ..) up to spp
-    int32_t block_chunks;       // pools: chunks per work block (a block = one tile x this many chunks)
+    int32_t block_chunks;       // item pool: chunks per work block (a block = one tile x this many chunks)
+    int32_t block_samples;      // per-sample pool: samples per work block (one tile x this many samples)
 };
 
 // Scene features (which code a kernel variant must contain).

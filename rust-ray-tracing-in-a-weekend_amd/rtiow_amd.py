@@ -52,7 +52,7 @@ EXPORTED = [
     "rt_world_box", "rt_world_translate", "rt_world_rotate_y", "rt_world_constant_medium",
     "rt_world_bvh", "rt_world_push", "rt_world_build_scene", "rt_world_info_get", "rt_camera_new",
     "rt_scene_preset_get", "rt_scene_camera", "rt_world_flatten", "rt_ctx_upload_soa",
-    "rt_ctx_upload_world", "rt_render", "rt_rows_in_shard", "rt_last_stats", "rt_write_ppm",
+    "rt_ctx_upload_world", "rt_render", "rt_rows_in_shard", "rt_rows_in_band_shard", "rt_last_stats", "rt_write_ppm",
     "rt_ctx_set_variant", "rt_device_eval", "rt_accum_create", "rt_accum_destroy", "rt_accum_add",
     "rt_accum_get", "rt_accum_set", "rt_accum_resolve", "rt_render_progressive", "rt_ctx_set_schedule", "rt_ctx_set_precision",
     "rt_scene_validate",
@@ -107,7 +107,7 @@ class RenderParams(ctypes.Structure):
                 ("row_stride", ctypes.c_int32), ("out_format", ctypes.c_int32),
                 ("out_on_device", ctypes.c_int32), ("count_work", ctypes.c_int32),
                 ("background", ctypes.c_double * 3), ("render_seed", ctypes.c_uint64),
-                ("stream", ctypes.c_void_p)]
+                ("stream", ctypes.c_void_p), ("row_block", ctypes.c_int32), ("reserved_", ctypes.c_int32)]
 
 
 class Stats(ctypes.Structure):
@@ -168,7 +168,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "rt_scene_validate": ([ctypes.POINTER(SceneSoA), ctypes.POINTER(ctypes.c_int32),
                                ctypes.POINTER(ctypes.c_int32)], I), "rt_ctx_upload_world": ([P, P, I], I),
         "rt_render": ([P, ctypes.POINTER(Camera), ctypes.POINTER(RenderParams), P], I),
-        "rt_rows_in_shard": ([I, I, I], I), "rt_last_stats": ([P, ctypes.POINTER(Stats)], I),
+        "rt_rows_in_shard": ([I, I, I], I), "rt_rows_in_band_shard": ([I, I, I, I], I), "rt_last_stats": ([P, ctypes.POINTER(Stats)], I),
         "rt_write_ppm": ([P, I, I, ctypes.c_char_p], I),
         "rt_device_eval": ([P, I, P, P, P, P, I], I), "rt_ctx_set_variant": ([P, I, I, I], I),
         "rt_accum_create": ([P, ctypes.POINTER(RenderParams), ctypes.POINTER(P)], I),
@@ -328,24 +328,37 @@ def scene_camera(scene_id: int, width: int, height: int):
     return cam, tuple(bg)
 
 
-def rows_in_shard(height: int, row_begin: int, row_stride: int) -> int:
+def rows_in_shard(height: int, row_begin: int, row_stride: int, row_block: int = 1) -> int:
+    if row_block > 1:
+        return load_library().rt_rows_in_band_shard(height, row_begin, row_stride, row_block)
     return load_library().rt_rows_in_shard(height, row_begin, row_stride)
 
 
-def shard_rows(height: int, rank: int, world: int):
-    """Rows of rank `rank` in the interleaved N-way row partition (y = rank + k*world)."""
-    return list(range(rank, height, world))
+def shard_rows(height: int, rank: int, world: int, row_block: int = 1):
+    """Image rows of rank `rank` in the N-way partition, in the shard's order: single rows
+    y = rank + k*world, or bands of row_block rows interleaved the same way."""
+    if row_block <= 1:
+        return list(range(rank, height, world))
+    return [y for band in range(rank, (height + row_block - 1) // row_block, world)
+            for y in range(band * row_block, min(height, (band + 1) * row_block))]
 
 
-def assemble_rows(slabs, height: int, world: int, out=None):
-    """Inverse of the row partition: slabs[r] holds rank r's rows (padded to ceil(H/N)).
-    Works on numpy arrays and torch tensors alike."""
+def assemble_rows(slabs, height: int, world: int, out=None, row_block: int = 1):
+    """Inverse of the row partition: slabs[r] holds rank r's rows (padded to the largest
+    shard). Works on numpy arrays and torch tensors alike."""
     if out is None:
         import numpy as _np
         out = _np.empty((height,) + tuple(slabs[0].shape[1:]), dtype=slabs[0].dtype)
     for r in range(world):
-        n = len(range(r, height, world))
-        out[r::world] = slabs[r][:n]
+        if row_block <= 1:
+            n = len(range(r, height, world))
+            out[r::world] = slabs[r][:n]
+            continue
+        k = 0
+        for band in range(r, (height + row_block - 1) // row_block, world):
+            y0, y1 = band * row_block, min(height, (band + 1) * row_block)
+            out[y0:y1] = slabs[r][k:k + (y1 - y0)]
+            k += y1 - y0
     return out
 
 
@@ -385,8 +398,10 @@ class Renderer:
 
     @staticmethod
     def params(width, height, spp, max_depth=50, background=(0.0, 0.0, 0.0), render_seed=1, row_begin=0,
-               row_stride=1, spp_chunk=0, out_format=RT_OUT_F32, out_on_device=0, count_work=0, stream=None):
+               row_stride=1, spp_chunk=0, out_format=RT_OUT_F32, out_on_device=0, count_work=0, stream=None,
+               row_block=1):
         p = RenderParams()
+        p.row_block = row_block
         p.width, p.height, p.spp, p.max_depth = width, height, spp, max_depth
         p.spp_chunk, p.row_begin, p.row_stride = spp_chunk, row_begin, row_stride
         p.out_format, p.out_on_device, p.count_work = out_format, out_on_device, count_work
@@ -397,10 +412,12 @@ class Renderer:
 
     def render(self, camera: Camera, params: RenderParams, out=None) -> np.ndarray:
         """Host-output render: returns rows_local x width x 3 mean radiance (row k = k-th selected row)."""
-        n_rows = rows_in_shard(params.height, params.row_begin, params.row_stride)
+        n_rows = rows_in_shard(params.height, params.row_begin, params.row_stride, params.row_block)
         dt = np.float64 if params.out_format == RT_OUT_F64 else np.float32
         if out is None:
             out = np.empty((n_rows, params.width, 3), dtype=dt)
+        if out.dtype != dt or out.size < n_rows * params.width * 3 or not out.flags.c_contiguous:
+            raise RTError(f"output buffer too small or of the wrong type for {n_rows} x {params.width} x 3 {dt}")
         params.out_on_device = 0
         _check(self.lib.rt_render(self.h, ctypes.byref(camera), ctypes.byref(params), out.ctypes.data), "rt_render")
         return out
@@ -414,7 +431,7 @@ class Renderer:
 
     def render_progressive(self, camera: Camera, params: RenderParams, batch_spp: int, progress=None) -> np.ndarray:
         """rt_render in sample batches; progress(samples_done, samples_total) -> truthy stops early."""
-        n_rows = rows_in_shard(params.height, params.row_begin, params.row_stride)
+        n_rows = rows_in_shard(params.height, params.row_begin, params.row_stride, params.row_block)
         dt = np.float64 if params.out_format == RT_OUT_F64 else np.float32
         out = np.empty((n_rows, params.width, 3), dtype=dt)
         params.out_on_device = 0
@@ -456,7 +473,7 @@ class Accumulator:
 
     def __init__(self, renderer: Renderer, params: RenderParams):
         self.r, self.lib = renderer, renderer.lib
-        self.rows = rows_in_shard(params.height, params.row_begin, params.row_stride)
+        self.rows = rows_in_shard(params.height, params.row_begin, params.row_stride, params.row_block)
         self.width = params.width
         h = ctypes.c_void_p()
         _check(self.lib.rt_accum_create(renderer.h, ctypes.byref(params), ctypes.byref(h)), "rt_accum_create")

@@ -21,6 +21,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--spp", type=int, default=500)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--block-samples", type=int, nargs="*", default=[], help="per-sample pool block sizes to sweep")
     a = ap.parse_args()
     import numpy as np
     import torch  # noqa: F401  (one HIP runtime: torch's)
@@ -29,11 +30,20 @@ def main():
     W, H = 1200, 800
     world = rt.World(1).build_scene(0)
     cam, bg = rt.scene_camera(0, W, H)
-    r = rt.Renderer(0)
-    r.upload(world)
-    for n in (1, 2, 4, 8):
-        rows = rt.rows_in_shard(H, 0, n)
-        p = rt.Renderer.params(W, H, a.spp, 50, bg, 1, row_begin=0, row_stride=n, out_format=rt.RT_OUT_F32)
+    cases = [(n, block, None) for n, block in ((1, 1), (2, 1), (4, 1), (8, 1), (2, 8), (4, 8), (8, 8))]
+    cases += [(n, 1, bs) for bs in a.block_samples for n in (1, 8)]
+    renderers = {}
+    for n, block, bs in cases:
+        if bs not in renderers:   # RT_BLOCK_SAMPLES is read at context creation
+            if bs:
+                os.environ["RT_BLOCK_SAMPLES"] = str(bs)
+            renderers[bs] = rt.Renderer(0)
+            os.environ.pop("RT_BLOCK_SAMPLES", None)
+            renderers[bs].upload(world)
+        r = renderers[bs]
+        rows = rt.rows_in_shard(H, 0, n, block)
+        p = rt.Renderer.params(W, H, a.spp, 50, bg, 1, row_begin=0, row_stride=n, out_format=rt.RT_OUT_F32,
+                               row_block=block)
         out = np.empty((rows, W, 3), np.float32)
         r.render(cam, p, out)
         ms = []
@@ -41,7 +51,7 @@ def main():
             r.render(cam, p, out)
             ms.append(r.stats().kernel_ms)
         k = float(np.median(ms))
-        print(json.dumps({"n": n, "rows": rows, "kernel_ms": round(k, 3),
+        print(json.dumps({"n": n, "row_block": block, "block_samples": bs, "rows": rows, "kernel_ms": round(k, 3),
                           "msamples_per_s": round(rows * W * a.spp / k / 1e3, 1)}), flush=True)
 
 

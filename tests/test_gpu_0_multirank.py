@@ -27,10 +27,10 @@ def _free_port():
     return port
 
 
-def _run_ranks(world, scene, W, H, spp, out):
+def _run_ranks(world, scene, W, H, spp, out, block=1):
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), WORLD_SIZE=str(world))
     procs = [subprocess.Popen([sys.executable, "-m", "tests.multirank_worker", str(scene), str(W), str(H), str(spp),
-                               out], cwd=REPO, env=dict(env, RANK=str(r)))
+                               out, str(block)], cwd=REPO, env=dict(env, RANK=str(r)))
              for r in range(world)]
     rcs = []
     for p in procs:
@@ -46,9 +46,10 @@ def _run_ranks(world, scene, W, H, spp, out):
 def test_hip_row_shards_over_processes_equal_single_render(rt, tmp_path):
     scene, W, H, spp = 7, 96, 53, 8
     frames = {}
-    for world in (2, 3):      # every rank process runs before this process touches the GPU
+    # single-row interleave (world 2) and bench.py's 8-row bands (world 3; 53 rows: a cut last band)
+    for world, block in ((2, 1), (3, 8)):   # every rank process runs before this process touches the GPU
         out = str(tmp_path / f"frame{world}.npy")
-        rcs = _run_ranks(world, scene, W, H, spp, out)
+        rcs = _run_ranks(world, scene, W, H, spp, out, block)
         assert rcs == [0] * world, (world, rcs)
         frames[world] = np.load(out)
     img, _ = rt.render_scene(scene, W, H, spp, 50, out_format=rt.RT_OUT_F64)

@@ -106,6 +106,16 @@ def test_row_shards_reassemble_bit_exactly(rt, renderer):
     for r in range(G):
         shard = gpu_render(rt, renderer, 7, W, H, spp, row_begin=r, row_stride=G)
         assert np.array_equal(shard, full[r::G]), r
+    # bench.py's multi-GPU shards: 8-row bands round-robin (30 rows: the last band is cut)
+    world = rt.World(1).build_scene(7)
+    cam, bg = rt.scene_camera(7, W, H)
+    renderer.upload(world)
+    for G in (1, 2, 3):
+        for r in range(G):
+            p = rt.Renderer.params(W, H, spp, 50, bg, 1, row_begin=r, row_stride=G, row_block=8,
+                                   out_format=rt.RT_OUT_F64)
+            shard = renderer.render(cam, p)
+            assert np.array_equal(shard, full[rt.shard_rows(H, r, G, 8)]), (G, r)
 
 
 def test_chunking_only_changes_rounding(rt, renderer):
@@ -349,10 +359,12 @@ def test_schedules_render_identically(rt, scene_id, W, H, spp):
     finally:
         os.environ.pop("RT_SAMPLE_BUF_MB")
     os.environ["RT_BLOCK_CHUNKS"] = "3"
+    os.environ["RT_BLOCK_SAMPLES"] = "5"
     try:
-        grouped = rt.Renderer(0)                     # item-pool blocks of 3 chunks per tile
+        grouped = rt.Renderer(0)                     # item-pool blocks of 3 chunks, pool blocks of 5 samples
     finally:
         os.environ.pop("RT_BLOCK_CHUNKS")
+        os.environ.pop("RT_BLOCK_SAMPLES")
     r = rt.Renderer(0)
     runs = [(r, rt.RT_SCHED_CHUNKS), (r, rt.RT_SCHED_POOL), (r, rt.RT_SCHED_ITEMS), (small, rt.RT_SCHED_POOL),
             (small, rt.RT_SCHED_ITEMS), (grouped, rt.RT_SCHED_ITEMS), (r, rt.RT_SCHED_AUTO)]
@@ -387,6 +399,8 @@ def test_schedules_render_identically(rt, scene_id, W, H, spp):
     assert np.array_equal(grouped.render(cam, q2), b2)
     grouped.upload(world)
     assert np.array_equal(grouped.render(cam, q), one)   # 40 spp: chunks of 3, groups of 3 chunks
+    grouped.set_schedule(rt.RT_SCHED_POOL)
+    assert np.array_equal(grouped.render(cam, q), one)   # pool blocks of 5 samples across chunks of 3
     grouped.close()
     assert_parity(imgs[2], ob.render(scene_id, W, H, spp, row_begin=1, row_stride=2), f"items scene {scene_id}")
 

@@ -66,3 +66,24 @@ def test_assemble_rows_inverse():
             s[: len(part)] = part
             slabs.append(s)
         assert np.array_equal(rt.assemble_rows(slabs, 7, world), img)
+
+
+def test_band_shards_partition_the_frame():
+    """bench.py's multi-GPU shards: 8-row bands round-robin. The C ABI's row count, the
+    Python row list and assemble_rows agree, and the shards partition every row once."""
+    import __graft_entry__ as ge
+    rt = ge.import_binding()
+    for H in (800, 53, 8, 9):
+        img = np.arange(H * 2 * 3).reshape(H, 2, 3)
+        for world in (1, 2, 3, 8):
+            rows = [rt.shard_rows(H, r, world, 8) for r in range(world)]
+            assert sorted(y for rr in rows for y in rr) == list(range(H))
+            n = [rt.rows_in_shard(H, r, world, 8) for r in range(world)]
+            assert n == [len(rr) for rr in rows], (H, world)
+            slabs = []
+            for r in range(world):
+                s = np.zeros((max(n), 2, 3), img.dtype)
+                s[: n[r]] = img[rows[r]]
+                slabs.append(s)
+            assert np.array_equal(rt.assemble_rows(slabs, H, world, row_block=8), img)
+    assert rt.load_library().rt_rows_in_band_shard(800, 0, 8, 6) == 0   # not a power of two
