@@ -604,16 +604,27 @@ int rt_ctx_upload_soa(rt_ctx* c, const rt_scene_soa* s)
     int vrc = validate_soa(s, tlas_depth, blas_depth, n_tlas_nodes);
     if (vrc) return vrc;
 
-    // the primitive records in leaf-slot order (prims[prim_refs[j]]): the kernel's leaf
-    // loops read a record without first loading its index
+    // The device's primitive records. A Sphere is stored as a MovingSphere that does not
+    // move (velocity 0, a = 1: the centre c0 + 0 * time is c0 bit for bit), so the kernel's
+    // sphere test reads no kind and selects nothing (sphere_center). Then the records in
+    // leaf-slot order (prims[prim_refs[j]]): the leaf loops read a record without first
+    // loading its index.
+    std::vector<rt_prim> prims(s->prims, s->prims + s->n_prims);
+    for (rt_prim& p : prims)
+        if (p.kind == RT_PRIM_SPHERE) {
+            p.a = 1;
+            p.p[5] = p.p[6] = p.p[7] = 0.0;
+            p.p[8] = 0.0;
+            p.p[9] = 1.0;
+        }
     std::vector<rt_prim> leaf_prims((size_t)s->n_prim_refs);
-    for (int j = 0; j < s->n_prim_refs; ++j) leaf_prims[(size_t)j] = s->prims[s->prim_refs[j]];
+    for (int j = 0; j < s->n_prim_refs; ++j) leaf_prims[(size_t)j] = prims[(size_t)s->prim_refs[j]];
     size_t off[10], bytes[10] = {
         (size_t)s->n_nodes * sizeof(rt_bvh_node), (size_t)s->n_prim_refs * 4, (size_t)s->n_prims * sizeof(rt_prim),
         (size_t)s->n_instances * sizeof(rt_instance), (size_t)s->n_materials * sizeof(rt_material),
         (size_t)s->n_textures * sizeof(rt_texture), (size_t)s->n_perlin * 768 * 8, (size_t)s->n_perlin * 768 * 4,
         (size_t)s->image_bytes, (size_t)s->n_prim_refs * sizeof(rt_prim)};
-    const void* src[10] = {s->nodes, s->prim_refs, s->prims, s->instances, s->materials, s->textures,
+    const void* src[10] = {s->nodes, s->prim_refs, prims.data(), s->instances, s->materials, s->textures,
                            s->perlin_ranvec, s->perlin_perm, s->image_data, leaf_prims.data()};
     size_t total = 0;
     for (int i = 0; i < 10; ++i) {

@@ -478,19 +478,17 @@ __device__ __forceinline__ bool box_t(const rt_prim& p, const RayT<R>& r, R t_mi
 
 // The centre of a Sphere, or of a MovingSphere at the ray's time: center_0 +
 // ((time - time_0) / (time_1 - time_0)) * (center_1 - center_0) (hittable.rs:556-558).
-// Both kinds go through one code path (the moving centre is a select), so a wave whose
-// lanes hold both kinds runs the sphere test once, not once per kind.
+// Both kinds go through one code path with no select: the upload stores a Sphere as a
+// MovingSphere of velocity 0 (abi.cpp), whose c0 + 0 * s is c0 bit for bit (s finite), so
+// a wave whose lanes hold both kinds runs one test and loads no kind.
 template <class R>
 __device__ __forceinline__ void sphere_center(const rt_prim& p, const RayT<R>& r, double& cx, double& cy, double& cz)
 {
-    const double c0x = p.p[0], c0y = p.p[1], c0z = p.p[2];
-    const double vx = p.p[5], vy = p.p[6], vz = p.p[7];
-    const bool moving = p.kind == RT_PRIM_MOVING_SPHERE;
     double s = (double)r.time;
-    if (moving && !p.a) s = ((double)r.time - p.p[8]) / (p.p[9] - p.p[8]);
-    cx = moving ? c0x + vx * s : c0x;
-    cy = moving ? c0y + vy * s : c0y;
-    cz = moving ? c0z + vz * s : c0z;
+    if (!p.a) s = ((double)r.time - p.p[8]) / (p.p[9] - p.p[8]);   // a MovingSphere with a general shutter
+    cx = p.p[0] + p.p[5] * s;
+    cy = p.p[1] + p.p[6] * s;
+    cz = p.p[2] + p.p[7] * s;
 }
 
 // Sphere, MovingSphere, rects, Box: t-only (hittable.rs:211-231).
