@@ -47,6 +47,8 @@ constexpr int kMaxLdsStack = 48;
 // TLAS nodes kept in LDS (32 KB per block): the first kMaxLdsNodes in BFS order, i.e.
 // the top levels; deeper ones are read from L1/L2
 constexpr int kMaxLdsNodes = 512;
+// material (64 B) and texture (96 B) tables staged in LDS when both are this small (10 KB)
+constexpr int kMaxLdsMaterials = 64;
 
 }  // namespace
 
@@ -83,6 +85,7 @@ struct rt_ctx {
     bool pending_counts = false;
     rt_stats stats{};
     uint32_t features = rtk::FEAT_ALL;  // of the uploaded scene
+    int n_materials = 0, n_textures = 0;
     int block_chunks = 0;               // RT_BLOCK_CHUNKS: chunks per item-pool work block (0: auto)
     int block_samples = 0;              // RT_BLOCK_SAMPLES: samples per per-sample-pool work block (0: auto)
     uint32_t extra_features = 0;        // RT_EXTRA_FEATURES: a larger kernel variant than the scene needs (tests)
@@ -662,6 +665,8 @@ int rt_ctx_upload_soa(rt_ctx* c, const rt_scene_soa* s)
     c->S.blas_base = tlas_depth;
     c->S.stack_entries = std::max(1, tlas_depth + blas_depth);
     c->n_tlas_nodes = n_tlas_nodes;
+    c->n_materials = s->n_materials;
+    c->n_textures = s->n_textures;
     c->S.n_tlas_nodes = c->n_tlas_nodes;
     c->has_scene = true;
     uint32_t feat = 0;
@@ -848,6 +853,11 @@ static int run_range(rt_ctx* c, const rt_camera* cam, const rt_render_params* p,
     // the TLAS in LDS (read-only, shared by the block) when it fits the per-block budget
     rtk::SceneDev S = c->S;
     S.n_lds_nodes = c->opt_lds_nodes ? std::min(c->n_tlas_nodes, kMaxLdsNodes) : 0;
+    // small material and texture tables in LDS too (the variants with rects or media)
+    const bool stage = c->opt_lds_nodes && c->n_materials <= kMaxLdsMaterials && c->n_textures <= kMaxLdsMaterials &&
+                       c->n_materials > 0;
+    S.n_lds_materials = stage ? c->n_materials : 0;
+    S.n_lds_textures = stage ? c->n_textures : 0;
 
     // Buffer batches: the trace output of one launch is bounded by sample_buf_cap. Per-sample
     // pool: samples x pixels x 24 B; chunk and item schedules: chunks x pixels x 24 B, batches

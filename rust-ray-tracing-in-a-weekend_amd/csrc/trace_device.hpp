@@ -1045,7 +1045,7 @@ __device__ __forceinline__ bool checker_odd(const HitT<double>& h)
 template <class C, class R = typename C::Real>
 __device__ void tex_value(const SceneDev& S, int ti, const HitT<R>& h, R& cr, R& cg, R& cb)
 {
-    const rt_texture& t = S.textures[ti];
+    const rt_texture& t = texture_of<C>(S, ti);
     if constexpr (!(C::F & (FEAT_NOISE | FEAT_IMAGE))) {
         if (t.kind == RT_TEX_CHECKER) {
             const double* c = checker_odd(h) ? t.c1 : t.c0;
@@ -1187,6 +1187,61 @@ __device__ __forceinline__ void camera_ray(const KParams& P, int x, int y, rt_ps
     r.time = rt_uniform_sample(ds_u64(st), P.cam.time0, P.scale_time);
 }
 
+// The material / texture table a shading step reads: staged in LDS by the block prologue
+// (north_star: "stages the top BVH levels and material table in LDS") when the variant
+// has rects or media and the tables are small (Cornell 4-6 materials, final scene 10), else
+// global memory (the random scene's 485 materials would cost the spheres variant blocks per
+// CU). The flag is per launch, so the choice is wave-uniform.
+template <class C>
+constexpr bool StageShade() { return C::F != FEAT_SET_SPHERES; }
+__device__ __forceinline__ int lds_shade_offset(const SceneDev& S, bool lds_stack)
+{
+    return (lds_stack ? S.stack_entries * 256 : 0) + S.n_lds_nodes * 16;   // in ints
+}
+template <class C>
+__device__ __forceinline__ const rt_material& material_of(const SceneDev& S, int i)
+{
+    if constexpr (StageShade<C>()) {
+        if (S.n_lds_materials > 0)
+            return reinterpret_cast<const rt_material*>(rt_lds + lds_shade_offset(S, C::LDS))[i];
+    }
+    return S.materials[i];
+}
+template <class C>
+__device__ __forceinline__ const rt_texture& texture_of(const SceneDev& S, int i)
+{
+    if constexpr (StageShade<C>()) {
+        if (S.n_lds_materials > 0)
+            return reinterpret_cast<const rt_texture*>(rt_lds + lds_shade_offset(S, C::LDS) + S.n_lds_materials * 16)[i];
+    }
+    return S.textures[i];
+}
+// block prologue: TLAS nodes, then the material and texture tables (every thread takes part)
+template <class C>
+__device__ __forceinline__ void stage_lds(const SceneDev& S)
+{
+    bool any = false;
+    const int off = C::LDS ? S.stack_entries * 256 : 0;
+    if (S.n_lds_nodes > 0) {
+        uint4* dst = reinterpret_cast<uint4*>(rt_lds + off);
+        const uint4* src = reinterpret_cast<const uint4*>(S.nodes);
+        for (int i = threadIdx.x; i < S.n_lds_nodes * 4; i += 256) dst[i] = src[i];
+        any = true;
+    }
+    if constexpr (StageShade<C>()) {
+        if (S.n_lds_materials > 0) {
+            uint4* dm = reinterpret_cast<uint4*>(rt_lds + lds_shade_offset(S, C::LDS));
+            const uint4* sm = reinterpret_cast<const uint4*>(S.materials);
+            for (int i = threadIdx.x; i < S.n_lds_materials * 4; i += 256) dm[i] = sm[i];
+            uint4* dt = dm + S.n_lds_materials * 4;
+            const uint4* stx = reinterpret_cast<const uint4*>(S.textures);
+            for (int i = threadIdx.x; i < S.n_lds_textures * 6; i += 256) dt[i] = stx[i];
+            any = true;
+        }
+    }
+    if (any) __syncthreads();
+}
+
 // One hit of ray_color (main.rs:25-34): emitted + attenuation * (next), with the
 // recursion unrolled into the throughput T. A path carries at most one emission (a
 // DiffuseLight ends it), so adding T*e straight into the chunk sum gives the same bits
@@ -1196,7 +1251,7 @@ __device__ __forceinline__ bool shade(const SceneDev& S, const KParams& P, const
                                       rt_pstream& st, R& Tr, R& Tg, R& Tb, double& sum_r, double& sum_g,
                                       double& sum_b)
 {
-    const rt_material& m = S.materials[h.mat];
+    const rt_material& m = material_of<C>(S, h.mat);
     const int kind = m.kind;
     if (kind == RT_MAT_DIFFUSE_LIGHT) {  // material.rs:25-34 (emits on both faces, never scatters)
         R er, eg, eb;
@@ -1363,13 +1418,7 @@ __global__ void __launch_bounds__(256, min_waves<C>()) trace_chunks(SceneDev S, 
                                                                     unsigned long long* __restrict__ counters)
 {
     const KParams& P = *Pp;
-    if (S.n_lds_nodes > 0) {  // every thread of the block takes part, before any early return
-        const int off = C::LDS ? S.stack_entries * 256 : 0;
-        uint4* dst = reinterpret_cast<uint4*>(rt_lds + off);
-        const uint4* src = reinterpret_cast<const uint4*>(S.nodes);
-        for (int i = threadIdx.x; i < S.n_lds_nodes * 4; i += 256) dst[i] = src[i];
-        __syncthreads();
-    }
+    stage_lds<C>(S);   // every thread of the block takes part, before any early return
     LaneWork w;
     if (!lane_work(P, w)) return;
     StackT<C> stack;
@@ -1473,13 +1522,7 @@ __global__ void __launch_bounds__(256, min_waves<C>()) trace_pool(SceneDev S, co
                                                                   unsigned* __restrict__ work)
 {
     const KParams& P = *Pp;
-    if (S.n_lds_nodes > 0) {
-        const int off = C::LDS ? S.stack_entries * 256 : 0;
-        uint4* dst = reinterpret_cast<uint4*>(rt_lds + off);
-        const uint4* src = reinterpret_cast<const uint4*>(S.nodes);
-        for (int i = threadIdx.x; i < S.n_lds_nodes * 4; i += 256) dst[i] = src[i];
-        __syncthreads();
-    }
+    stage_lds<C>(S);
     StackT<C> stack;
     if constexpr (C::LDS) stack.base = rt_lds + threadIdx.x;
     Count cnt{};
@@ -1683,7 +1726,8 @@ template <uint32_t F, bool S32, bool LDS, bool COUNT, bool F32>
 static void launch_one(const Launch& L, hipStream_t stream, bool nall)
 {
     const SceneDev& S = *L.S;
-    const size_t lds = (LDS ? (size_t)S.stack_entries * 256 * sizeof(int) : 0) + (size_t)S.n_lds_nodes * 64;
+    const size_t lds = (LDS ? (size_t)S.stack_entries * 256 * sizeof(int) : 0) + (size_t)S.n_lds_nodes * 64 +
+                       (F != FEAT_SET_SPHERES ? (size_t)S.n_lds_materials * 64 + (size_t)S.n_lds_textures * 96 : 0);
     if (L.pool) {
         auto go = [&](auto kernel) {
             const unsigned nb = std::min<unsigned long long>(resident_blocks(kernel, lds), (L.n_blocks + 3) / 4);

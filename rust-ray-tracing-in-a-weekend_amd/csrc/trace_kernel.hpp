@@ -26,6 +26,8 @@ struct SceneDev {
     int32_t n_lds_nodes;    // the first n TLAS nodes (BFS order, nodes[0, n)) are copied into LDS
     int32_t n_tlas_nodes;   // TLAS size (its nodes are nodes[0, n_tlas_nodes))
     int32_t has_spheres;    // any Sphere / MovingSphere: rays need 1/|d|^2 for the root divisions
+    int32_t n_lds_materials;  // > 0: the material and texture tables are staged in LDS after the
+    int32_t n_lds_textures;   // TLAS nodes (the kernel variants with rects or media; small tables)
 };
 
 struct KParams {
