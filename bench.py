@@ -363,7 +363,7 @@ def main():
             "cpu_baseline": cpu,
             "parity": parity,
             "detail": {"kernel_ms_mean": round(k_ms, 3), "reduce_ms": round(last.reduce_ms, 3),
-                       "schedule": last.schedule, "n_batches": last.n_batches, "spp_chunk": last.spp_chunk,
+                       "schedule": last.schedule, "n_batches": last.n_batches, "waves_per_simd": last.waves_per_simd, "spp_chunk": last.spp_chunk,
                        "scene_bytes": int(last.scene_bytes), "scene_build_upload_s": round(t_build, 3),
                        "algorithmic_bytes_survey_8d": alg},
         }

@@ -206,7 +206,7 @@ typedef struct rt_stats {
     uint64_t shade_lanes;        /* count_work only: lanes shading a hit, summed over the */
     uint64_t shade_steps;        /*   wave iterations in which any lane did (shade_steps) */
     int32_t precision;           /* RT_PREC_* the last render ran with */
-    int32_t pad_;
+    int32_t waves_per_simd;      /* resident waves per SIMD of the last trace kernel (occupancy) */
 } rt_stats;
 int rt_last_stats(rt_ctx* ctx, rt_stats* out);
 

@@ -100,6 +100,7 @@ struct rt_ctx {
     double* acc_tmp = nullptr;          // running sums when a render takes several buffer batches
     size_t acc_tmp_cap = 0;
     int n_tlas_nodes = 0;
+    int n_nodes = 0;                    // BVH nodes of the uploaded scene (TLAS + BLASes)
 };
 
 extern "C" {
@@ -665,6 +666,7 @@ int rt_ctx_upload_soa(rt_ctx* c, const rt_scene_soa* s)
     c->S.blas_base = tlas_depth;
     c->S.stack_entries = std::max(1, tlas_depth + blas_depth);
     c->n_tlas_nodes = n_tlas_nodes;
+    c->n_nodes = s->n_nodes;
     c->n_materials = s->n_materials;
     c->n_textures = s->n_textures;
     c->S.n_tlas_nodes = c->n_tlas_nodes;
@@ -693,6 +695,7 @@ int rt_ctx_upload_soa(rt_ctx* c, const rt_scene_soa* s)
             }
             continue;
         }
+        feat |= rtk::FEAT_INST_BLAS;
         std::vector<int> todo{in.child};   // validate_soa checked refs and acyclicity
         while (!todo.empty() && !(feat & rtk::FEAT_INST_RECT)) {
             const int ref = todo.back();
@@ -842,6 +845,10 @@ static int run_range(rt_ctx* c, const rt_camera* cam, const rt_render_params* p,
     o.f32 = c->opt_precision == RT_PREC_F32;
     if (o.f32 && count) return fail(RT_ERR_UNSUPPORTED, "count_work is an f64-mode diagnostic");
     if (o.f32) o.slab32 = 1;   // statistical mode: f32 boxes whatever the camera
+    // a scene with no BVH node (the Cornell scenes: one top-level leaf, instances over one
+    // box) tests no slab: the f64-slab instantiation then, which holds no f32 ray terms
+    // (rects + instances variant 125 vs 130 VGPRs: 4 vs 3 waves per SIMD)
+    if (c->n_nodes == 0 && !o.f32) o.slab32 = 0;
     const long long total = s_end - s_begin;
     const size_t px_bytes = px * 3 * sizeof(double);
     // AUTO: the per-sample pool when its [sample][pixel] buffer takes at most 4 batches (C2:
@@ -906,6 +913,8 @@ static int run_range(rt_ctx* c, const rt_camera* cam, const rt_render_params* p,
     int rc = grow(c, stream, c->partial, c->partial_cap, need);
     if (rc) return rc;
     if (count) HIP_TRY(hipMemsetAsync(c->counters, 0, kCounters * sizeof(unsigned long long), stream));
+    int waves_per_simd = 0;
+    o.waves_per_simd = &waves_per_simd;
     HIP_TRY(hipEventRecord(c->ev[0], stream));
     for (int bi = 0; bi < n_batches; ++bi) {
         const int b0 = s_begin + (int)(bi * batch);
@@ -939,6 +948,7 @@ static int run_range(rt_ctx* c, const rt_camera* cam, const rt_render_params* p,
     c->stats.lds_stack = o.lds_stack;
     c->stats.schedule = o.pool;
     c->stats.precision = o.f32 ? RT_PREC_F32 : RT_PREC_F64;
+    c->stats.waves_per_simd = waves_per_simd;
     c->stats.n_batches = n_batches;
     c->stats.samples = (uint64_t)n_px * (uint64_t)total;
     c->stats.n_chunks = (int32_t)((total + chunk - 1) / chunk);

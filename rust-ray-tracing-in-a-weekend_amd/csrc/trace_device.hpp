@@ -784,6 +784,9 @@ __device__ bool instance_t(const SceneDev& S, const rt_instance& in, const RayT<
         ref.side = side;
         return true;
     }
+    // an instance over a BVH: a nested walk (its state on top of the TLAS walk's is what
+    // set the Cornell variants' register count, 157 vs 125 VGPRs: 3 vs 4 waves per SIMD)
+    if constexpr ((C::F & FEAT_INST_BLAS) == 0) return false;
     HitRefT<R> inner;
     if (!traverse<C>(S, in.child, r, t_min, t_max, inner, stack, sp0, cnt,
                      [&](int slot, R tmax, HitRefT<R>& b) {
@@ -829,8 +832,10 @@ __device__ void instance_finish(const SceneDev& S, const rt_instance& in, const 
             done = true;
         }
     }
-    if (!done) simple_finish<InstC<C>>(in.child_kind == RT_CHILD_PRIM ? S.prims[ref.sub] : S.leaf_prims[ref.sub], r, ref.t,
-                            ref.side, h);
+    if (!done)
+        simple_finish<InstC<C>>((C::F & FEAT_INST_BLAS) == 0 || in.child_kind == RT_CHILD_PRIM ? S.prims[ref.sub]
+                                                                                               : S.leaf_prims[ref.sub],
+                                r, ref.t, ref.side, h);
     const int n = in.n_ops;
 #pragma unroll
     for (int i = 3; i >= 0; --i) {
@@ -1705,11 +1710,22 @@ struct Launch {
     unsigned* work;                // pool / items: work-block counter
     int pool;                      // 0 chunks, 1 per-sample pool, 2 item pool
     unsigned long long n_blocks;   // 8x8 tiles x chunks
+    int* waves_per_simd;           // out (optional): resident blocks per CU = waves per SIMD (4-wave blocks)
 };
+
+// Resident 256-thread blocks per CU of a kernel (registers, LDS), reported to the caller.
+template <class K>
+static int blocks_per_cu(const Launch& L, K kernel, size_t lds)
+{
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, 256, lds) != hipSuccess || per_cu <= 0) per_cu = 1;
+    if (L.waves_per_simd) *L.waves_per_simd = per_cu;
+    return per_cu;
+}
 
 // Persistent grid for the pool schedule: as many blocks as fit on the device at once.
 template <class K>
-static unsigned resident_blocks(K kernel, size_t lds)
+static unsigned resident_blocks(const Launch& L, K kernel, size_t lds)
 {
     static int cus = 0;
     if (!cus) {
@@ -1717,9 +1733,7 @@ static unsigned resident_blocks(K kernel, size_t lds)
         (void)hipGetDevice(&dev);
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
     }
-    int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, 256, lds) != hipSuccess || per_cu <= 0) per_cu = 1;
-    return (unsigned)(cus * per_cu);
+    return (unsigned)(cus * blocks_per_cu(L, kernel, lds));
 }
 
 template <uint32_t F, bool S32, bool LDS, bool COUNT, bool F32>
@@ -1730,7 +1744,7 @@ static void launch_one(const Launch& L, hipStream_t stream, bool nall)
                        (F != FEAT_SET_SPHERES ? (size_t)S.n_lds_materials * 64 + (size_t)S.n_lds_textures * 96 : 0);
     if (L.pool) {
         auto go = [&](auto kernel) {
-            const unsigned nb = std::min<unsigned long long>(resident_blocks(kernel, lds), (L.n_blocks + 3) / 4);
+            const unsigned nb = std::min<unsigned long long>(resident_blocks(L, kernel, lds), (L.n_blocks + 3) / 4);
             hipLaunchKernelGGL(kernel, dim3(nb), dim3(256), lds, stream, S, L.P, L.out, L.counters, L.work);
         };
         if (L.pool == 2) {
@@ -1743,12 +1757,12 @@ static void launch_one(const Launch& L, hipStream_t stream, bool nall)
         return;
     }
     const unsigned nb = (unsigned)((L.n_blocks + 3) / 4);
-    if (nall)
-        hipLaunchKernelGGL((trace_chunks<Cfg<F, S32, LDS, true, COUNT, F32>>), dim3(nb), dim3(256), lds, stream, S,
-                           L.P, L.out, L.counters);
-    else
-        hipLaunchKernelGGL((trace_chunks<Cfg<F, S32, LDS, false, COUNT, F32>>), dim3(nb), dim3(256), lds, stream, S,
-                           L.P, L.out, L.counters);
+    auto go = [&](auto kernel) {
+        if (L.waves_per_simd) (void)blocks_per_cu(L, kernel, lds);
+        hipLaunchKernelGGL(kernel, dim3(nb), dim3(256), lds, stream, S, L.P, L.out, L.counters);
+    };
+    if (nall) go(trace_chunks<Cfg<F, S32, LDS, true, COUNT, F32>>);
+    else go(trace_chunks<Cfg<F, S32, LDS, false, COUNT, F32>>);
 }
 
 // Variant table: feature set x slab precision x loop form. The launcher takes the

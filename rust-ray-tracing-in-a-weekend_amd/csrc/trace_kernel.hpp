@@ -58,12 +58,13 @@ enum : uint32_t {
     FEAT_INST_RECT = 32,    // rects or boxes inside an instance (its child prim or BLAS)
     FEAT_MEDIUM_INST = 64,  // a medium boundary that is not a sphere (box, rect, instance)
     FEAT_INST_MEDIUM = 128, // a medium inside an instance (nested Translate/RotateY over a ConstantMedium)
-    FEAT_ALL = 255,
+    FEAT_INST_BLAS = 256,   // an instance over a BVH (a nested walk; instances over one primitive need none)
+    FEAT_ALL = 511,
     FEAT_SET_SPHERES = 0,                                          // compiled variant: spheres + solid/checker
-    FEAT_SET_RECTINST = FEAT_RECT | FEAT_INST | FEAT_INST_RECT,    // + rects, boxes, instances (Cornell)
+    FEAT_SET_RECTINST = FEAT_RECT | FEAT_INST | FEAT_INST_RECT,    // + rects, boxes, instances of one prim (Cornell)
     FEAT_SET_MEDIA = FEAT_SET_RECTINST | FEAT_MEDIUM | FEAT_MEDIUM_INST,  // + constant media (Cornell smoke)
     // + Perlin and image textures, instances over spheres, media bounded by spheres (final scene)
-    FEAT_SET_FINAL = FEAT_RECT | FEAT_INST | FEAT_MEDIUM | FEAT_NOISE | FEAT_IMAGE
+    FEAT_SET_FINAL = FEAT_RECT | FEAT_INST | FEAT_MEDIUM | FEAT_NOISE | FEAT_IMAGE | FEAT_INST_BLAS
 };
 
 struct LaunchOpts {
@@ -73,6 +74,7 @@ struct LaunchOpts {
     int count;          // count_work variant
     int pool;           // RT_SCHED_*: 0 chunks, 1 per-sample pool (per-sample output), 2 item pool (partials)
     int f32;            // the f32 fast mode (RT_PREC_F32)
+    int* waves_per_simd = nullptr;  // out (optional): resident waves per SIMD of the launched trace kernel
 };
 
 uint32_t variant_features(uint32_t scene_features);

@@ -98,7 +98,8 @@ def test_variants_bit_identical_at_full_size(rt, renderer, scene_id, W, H, spp):
             renderer.set_variant(*v)
             img = renderer.render(cam, p)
             st = renderer.stats()
-            assert st.slab32 == v[0]
+            # a scene without BVH nodes (Cornell) tests no slab: it runs the f64-slab kernel
+            assert st.slab32 == (v[0] if scene_id != 5 else 0)
             if ref is None:
                 ref = img
             else:

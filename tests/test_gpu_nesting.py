@@ -68,7 +68,7 @@ def test_nested_world_matches_oracle(rt, renderer):
     soa = tw.product.flatten()
     assert soa.n_media == 3 and soa.n_instances >= 5
     got, ref = _render_both(rt, renderer, tw, 48, 32, 6, (7.0, 4.0, 9.0), (0.0, 0.7, 0.0), (0.5, 0.6, 0.8))
-    assert renderer.stats().variant_features == 255          # media under instances: the all-features variant
+    assert renderer.stats().variant_features == 511          # media under instances: the all-features variant
     assert float(ref.max()) > 0.0
     assert_parity(got, ref, "nested world")
 

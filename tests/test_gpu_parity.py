@@ -197,7 +197,7 @@ def test_kernel_variants_identical(rt, renderer, scene_id, W, H):
 
 
 @pytest.mark.parametrize("scene_id,W,H,feat", [(0, 40, 24, 0), (5, 24, 24, 1 | 2 | 32), (6, 24, 24, 1 | 2 | 4 | 32 | 64),
-                                              (7, 32, 18, 31)])
+                                              (7, 32, 18, 31 | 256)])
 def test_feature_set_variants_identical(rt, renderer, scene_id, W, H, feat):
     """Each scene runs on the smallest feature-set variant covering it (final scene: instances
     over spheres only, media bounded by spheres); the all-features variant, which no reference
@@ -208,7 +208,7 @@ def test_feature_set_variants_identical(rt, renderer, scene_id, W, H, feat):
     renderer.upload(world)
     img = renderer.render(cam, p)
     assert renderer.stats().variant_features == feat
-    os.environ["RT_EXTRA_FEATURES"] = "255"
+    os.environ["RT_EXTRA_FEATURES"] = "511"
     try:
         big = rt.Renderer(0)
     finally:
@@ -216,11 +216,25 @@ def test_feature_set_variants_identical(rt, renderer, scene_id, W, H, feat):
     try:
         big.upload(world)
         img_all = big.render(cam, p)
-        assert big.stats().variant_features == 255
+        assert big.stats().variant_features == 511
     finally:
         big.close()
     assert np.array_equal(img, img_all)
     assert_parity(img, ob.render(scene_id, W, H, 4), f"feature variant scene {scene_id}")
+
+
+def test_cornell_variant_occupancy(rt, renderer):
+    """The Cornell scenes have no BVH node (one top-level leaf; instances over one box): they
+    run the f64-slab instantiation of the rects + instances variant without the nested BLAS
+    walk, whose registers fit 4 waves per SIMD (the spheres variant's occupancy)."""
+    for scene_id, waves in ((5, 4), (0, 4)):
+        world = rt.World(1).build_scene(scene_id)
+        cam, bg = rt.scene_camera(scene_id, 16, 16)
+        renderer.upload(world)
+        renderer.render(cam, rt.Renderer.params(16, 16, 2, 50, bg, 1, out_format=rt.RT_OUT_F64))
+        st = renderer.stats()
+        assert st.waves_per_simd == waves, (scene_id, st.waves_per_simd)
+        assert st.slab32 == (0 if scene_id == 5 else 1)
 
 
 def _golden_cases():
