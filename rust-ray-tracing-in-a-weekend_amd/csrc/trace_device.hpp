@@ -103,6 +103,9 @@ __device__ __forceinline__ bool first_active_lane()
 #ifndef RT_BOX_PRETEST
 #define RT_BOX_PRETEST 0   // slab pre-test of a Box before its 6 rect tests (measured slower: Cornell 58.5 vs 56.6 ms, final 83.3 vs 82.6, smoke 41.9 vs 39.9 — a culled lane saves no wave instructions unless the whole wave is culled)
 #endif
+#ifndef RT_BOX_RCP
+#define RT_BOX_RCP 1   // a Box's six sides divide through three per-box reciprocals (BoxRcp)
+#endif
 #ifndef RT_PK_SLAB
 #define RT_PK_SLAB 0   // packed-f32 (v_pk_fma_f32) slab test of the two children (C2 101.6 vs 99.9 ms: rejected)
 #endif
@@ -218,6 +221,16 @@ template <class C>
 constexpr bool RectRcp()
 {
     return RT_RECT_RCP && !C::F32 && (C::F & FEAT_RECT) != 0 && (C::F & (FEAT_MEDIUM | FEAT_NOISE | FEAT_IMAGE)) == 0;
+}
+
+// A Box's six sides through three per-box reciprocals (box_t): in the variants with Perlin or
+// image textures (final scene: 80.0 -> 78.6 ms), whose 3 waves per SIMD the extra live values do
+// not change; the 4-wave Cornell variant spills them (49.6 -> 51.6 ms) and Cornell smoke's
+// media variant loses too (39.1 -> 39.5; profiles/r02_ab_boxrcp_*.log)
+template <class C>
+constexpr bool BoxRcp()
+{
+    return RT_BOX_RCP && !C::F32 && (C::F & (FEAT_NOISE | FEAT_IMAGE)) != 0;
 }
 
 // spheres: the scene has spheres (wave-uniform); otherwise no root division needs 1/a
@@ -366,6 +379,24 @@ __device__ __forceinline__ bool rect_t(int axis, R a0, R a1, R b0, R b1, R k, co
     return true;
 }
 
+// rect_t with the caller's RN(1 / d_axis), |d_axis| in [2^-900, 2^900] (div_rcp: the division's bits)
+__device__ __forceinline__ bool rect_t_y(int axis, double a0, double a1, double b0, double b1, double k,
+                                         const RayT<double>& r, double yk, double t_min, double t_max, double& t_out)
+{
+    double ok, dk, oa, da, ob, db;
+    rect_axes(axis, r, ok, dk, oa, da, ob, db);
+    const double q = k - ok, q0 = q * yk;   // div_rcp without its guard (the caller checked the range)
+    const double t = __builtin_fma(__builtin_fma(-dk, q0, q), yk, q0);
+    if (t < t_min || t > t_max) return false;
+    const double x = oa + t * da;
+    const double y = ob + t * db;
+    if (x < a0 || x > a1 || y < b0 || y > b1) return false;
+    t_out = t;
+    return true;
+}
+template <class R>
+__device__ __forceinline__ bool rect_t_y(int, R, R, R, R, R, const RayT<R>&, R, R, R, R&) { return false; }
+
 // hittable.rs:322-331
 template <class C, class R = typename C::Real>
 __device__ __forceinline__ void rect_finish(int axis, R a0, R a1, R b0, R b1, const RayT<R>& r, R t, int mat,
@@ -445,7 +476,7 @@ __device__ __forceinline__ void box_side(const rt_prim& p, int side, int& axis, 
 // Box::hit = hit_hittables over its sides (hittable.rs:229-231): closest, ties to the later side.
 // The reference has no bounding-box pre-test (Q8); a conservative one on the box's padded
 // f32 bounds (flatten.cpp) only skips rect tests that cannot hit, like a BVH node box does.
-template <bool RCP = false, bool S32 = true, class R>
+template <bool RCP = false, bool S32 = true, bool LRCP = false, class R>
 __device__ __forceinline__ bool box_t(const rt_prim& p, const RayT<R>& r, R t_min, R t_max, R& t, int& side)
 {
     if (RT_BOX_PRETEST && p.b) {
@@ -461,6 +492,29 @@ __device__ __forceinline__ bool box_t(const rt_prim& p, const RayT<R>& r, R t_mi
         if (!hit) return false;
     }
     bool any = false;
+    // f64: the six sides divide by three directions; one correctly rounded reciprocal y per
+    // direction and a Markstein step per side (RN(q / d) bit for bit when y = RN(1 / d): see
+    // div_rcp) instead of six divisions. The range guard is taken once per box (a ray with a
+    // direction component outside [2^-900, 2^900], e.g. an exact 0, divides as the reference).
+    constexpr bool LOCAL_RCP = LRCP && !RCP && std::is_same<R, double>::value;
+    auto in_range = [](R d) { const R m = r_fabs(d); return m >= (R)0x1.0p-900 && m <= (R)0x1.0p+900; };
+    if (LOCAL_RCP && in_range(r.dx) && in_range(r.dy) && in_range(r.dz)) {
+        R y = (R)0;   // of the side pair's direction (sides 2a, 2a+1 share axis a)
+#pragma unroll
+        for (int s = 0; s < 6; ++s) {
+            int axis;
+            R a0, a1, b0, b1, k, ts;
+            box_side(p, s, axis, a0, a1, b0, b1, k);
+            if ((s & 1) == 0) y = (R)1 / (s == 0 ? r.dz : s == 2 ? r.dy : r.dx);
+            if (rect_t_y(axis, a0, a1, b0, b1, k, r, y, t_min, t_max, ts)) {
+                t_max = ts;
+                t = ts;
+                side = s;
+                any = true;
+            }
+        }
+        return any;
+    }
 #pragma unroll
     for (int s = 0; s < 6; ++s) {
         int axis;
@@ -507,7 +561,7 @@ __device__ __forceinline__ bool simple_t(const rt_prim& p, const RayT<R>& r, R t
         case RT_PRIM_XY_RECT: return rect_t<RectRcp<C>()>(0, q0, q1, q2, q3, q4, r, t_min, t_max, t);
         case RT_PRIM_XZ_RECT: return rect_t<RectRcp<C>()>(1, q0, q1, q2, q3, q4, r, t_min, t_max, t);
         case RT_PRIM_YZ_RECT: return rect_t<RectRcp<C>()>(2, q0, q1, q2, q3, q4, r, t_min, t_max, t);
-        case RT_PRIM_BOX: return box_t<RectRcp<C>(), C::S32>(p, r, t_min, t_max, t, side);
+        case RT_PRIM_BOX: return box_t<RectRcp<C>(), C::S32, BoxRcp<C>()>(p, r, t_min, t_max, t, side);
         default: return false;
         }
     }
@@ -1391,7 +1445,8 @@ __device__ __forceinline__ bool lane_work(const KParams& P, LaneWork& w)
 #ifndef RT_MIN_WAVES_RECTINST
 // measured (Cornell 800x800x200): chunk schedule 4 waves 190 vs 202 ms; pool schedule 4: 80.7,
 // 3: 81.0; after the reciprocal divisions (more live state, 4 waves spilled to scratch):
-// 4: 66.6, 3: 58.6
+// 4: 66.6, 3: 58.6; round 2: without the nested BLAS walk (FEAT_INST_BLAS), the f64-slab
+// instantiation the node-free Cornell scenes run needs 125 VGPRs: 4 waves at this bound
 #define RT_MIN_WAVES_RECTINST 3
 #endif
 #ifndef RT_MIN_WAVES_ALL
