@@ -613,14 +613,23 @@ int rt_ctx_upload_soa(rt_ctx* c, const rt_scene_soa* s)
     // sphere test reads no kind and selects nothing (sphere_center). Then the records in
     // leaf-slot order (prims[prim_refs[j]]): the leaf loops read a record without first
     // loading its index.
+    // A MovingSphere's a says whether its shutter is [0, 1] ((time - 0) / (1 - 0) is time
+    // exactly); it is recomputed here rather than trusted from a foreign SoA. Only a scene
+    // with another shutter needs FEAT_SHUTTER (the per-primitive flag and the division);
+    // without it a sphere test issues all its loads at once.
     std::vector<rt_prim> prims(s->prims, s->prims + s->n_prims);
-    for (rt_prim& p : prims)
+    bool general_shutter = false;
+    for (rt_prim& p : prims) {
         if (p.kind == RT_PRIM_SPHERE) {
             p.a = 1;
             p.p[5] = p.p[6] = p.p[7] = 0.0;
             p.p[8] = 0.0;
             p.p[9] = 1.0;
+        } else if (p.kind == RT_PRIM_MOVING_SPHERE) {
+            p.a = (p.p[8] == 0.0 && p.p[9] == 1.0) ? 1 : 0;
+            if (!p.a) general_shutter = true;
         }
+    }
     std::vector<rt_prim> leaf_prims((size_t)s->n_prim_refs);
     for (int j = 0; j < s->n_prim_refs; ++j) leaf_prims[(size_t)j] = prims[(size_t)s->prim_refs[j]];
     size_t off[10], bytes[10] = {
@@ -719,6 +728,7 @@ int rt_ctx_upload_soa(rt_ctx* c, const rt_scene_soa* s)
         if (s->textures[i].kind == RT_TEX_NOISE) feat |= rtk::FEAT_NOISE;
         if (s->textures[i].kind == RT_TEX_IMAGE) feat |= rtk::FEAT_IMAGE;
     }
+    if (general_shutter) feat |= rtk::FEAT_SHUTTER;
     c->features = feat;
     c->S.has_spheres = 0;
     for (int i = 0; i < s->n_prims; ++i)

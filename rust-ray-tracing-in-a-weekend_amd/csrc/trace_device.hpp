@@ -106,9 +106,6 @@ __device__ __forceinline__ bool first_active_lane()
 #ifndef RT_BOX_RCP
 #define RT_BOX_RCP 1   // a Box's six sides divide through three per-box reciprocals (BoxRcp)
 #endif
-#ifndef RT_PK_SLAB
-#define RT_PK_SLAB 0   // packed-f32 (v_pk_fma_f32) slab test of the two children (C2 101.6 vs 99.9 ms: rejected)
-#endif
 #ifndef RT_TRACE_LOOP
 #define RT_TRACE_LOOP 1   // 0 if-if, 1 while-while, 2 while-while with speculative node visits
 #endif
@@ -156,7 +153,7 @@ struct Stack<false> {
 };
 template <class C>
 using StackT = Stack<C::LDS>;
-extern __shared__ int rt_lds[];  // [stack entries x 256 lanes] [cached TLAS nodes]
+extern __shared__ int rt_lds[];  // [cached TLAS nodes] [stack entries x 256 lanes] [materials, textures]
 
 // Division by a value b used many times, through its correctly rounded reciprocal
 // y = RN(1/b): q0 = RN(q*y), then one correction q1 = RN(q0 + RN-exact(q - b*q0) * y).
@@ -251,10 +248,11 @@ __device__ __forceinline__ void finish_ray(RayT<typename C::Real>& r, bool spher
         r.fox = -(float)r.ox * r.fix;
         r.foy = -(float)r.oy * r.fiy;
         r.foz = -(float)r.oz * r.fiz;
-        // rt_bvh_node: lo0 at bytes 0/4/8, hi0 at 12/16/20 (x/y/z); child 1's box 24 bytes on
-        r.onx = r.fix >= 0.0f ? 0u : 12u;
-        r.ony = r.fiy >= 0.0f ? 4u : 16u;
-        r.onz = r.fiz >= 0.0f ? 8u : 20u;
+        // the LDS node (LdsNode): per axis [lo0 lo1 hi0 hi1 lo0 lo1] at bytes 0/24/48; the
+        // near planes of both children at +0 (direction >= 0) or +8, the far ones 8 bytes on
+        r.onx = r.fix >= 0.0f ? 0u : 8u;
+        r.ony = r.fiy >= 0.0f ? 24u : 32u;
+        r.onz = r.fiz >= 0.0f ? 48u : 56u;
     } else {
         r.ix = (typename C::Real)1 / r.dx;
         r.iy = (typename C::Real)1 / r.dy;
@@ -536,10 +534,13 @@ __device__ __forceinline__ bool box_t(const rt_prim& p, const RayT<R>& r, R t_mi
 // MovingSphere of velocity 0 (abi.cpp), whose c0 + 0 * s is c0 bit for bit (s finite), so
 // a wave whose lanes hold both kinds runs one test and loads no kind.
 template <class R>
-__device__ __forceinline__ void sphere_center(const rt_prim& p, const RayT<R>& r, double& cx, double& cy, double& cz)
+__device__ __forceinline__ void sphere_center(const rt_prim& p, const RayT<R>& r, bool general, double& cx, double& cy,
+                                              double& cz)
 {
     double s = (double)r.time;
-    if (!p.a) s = ((double)r.time - p.p[8]) / (p.p[9] - p.p[8]);   // a MovingSphere with a general shutter
+    // general: the variant has FEAT_SHUTTER (no reference scene does: their moving spheres
+    // all have the [0, 1] shutter); without it the flag is not loaded at all
+    if (general && !p.a) s = ((double)r.time - p.p[8]) / (p.p[9] - p.p[8]);   // a MovingSphere with a general shutter
     cx = p.p[0] + p.p[5] * s;
     cy = p.p[1] + p.p[6] * s;
     cz = p.p[2] + p.p[7] * s;
@@ -548,12 +549,12 @@ __device__ __forceinline__ void sphere_center(const rt_prim& p, const RayT<R>& r
 // Sphere, MovingSphere, rects, Box: t-only (hittable.rs:211-231).
 template <class C, class R = typename C::Real>
 __device__ __forceinline__ bool simple_t(const rt_prim& p, const RayT<R>& r, R t_min, R t_max, R& t, int& side,
-                                         Count& cnt)
+                                         Count& cnt, bool gs)
 {
     if (C::COUNT) cnt.prims++;
     if (!(C::F & FEAT_RECT) || p.kind <= RT_PRIM_MOVING_SPHERE) {
         double cx, cy, cz;
-        sphere_center(p, r, cx, cy, cz);
+        sphere_center(p, r, gs, cx, cy, cz);
         return sphere_t(cx, cy, cz, p.p[3], r, t_min, t_max, t);
     } else {
         const R q0 = (R)p.p[0], q1 = (R)p.p[1], q2 = (R)p.p[2], q3 = (R)p.p[3], q4 = (R)p.p[4];
@@ -568,7 +569,7 @@ __device__ __forceinline__ bool simple_t(const rt_prim& p, const RayT<R>& r, R t
 }
 
 template <class C, class R = typename C::Real>
-__device__ __forceinline__ void simple_finish(const rt_prim& p, const RayT<R>& r, R t, int side, HitT<R>& h)
+__device__ __forceinline__ void simple_finish(const rt_prim& p, const RayT<R>& r, R t, int side, HitT<R>& h, bool gs)
 {
     if constexpr ((C::F & FEAT_RECT) != 0) {
         if (p.kind >= RT_PRIM_XY_RECT && p.kind <= RT_PRIM_YZ_RECT) {
@@ -584,7 +585,7 @@ __device__ __forceinline__ void simple_finish(const rt_prim& p, const RayT<R>& r
         }
     }
     double cx, cy, cz;
-    sphere_center(p, r, cx, cy, cz);
+    sphere_center(p, r, gs, cx, cy, cz);
     sphere_finish<C>((R)cx, (R)cy, (R)cz, (R)p.p[4], r, t, p.mat, h);
 }
 
@@ -612,6 +613,29 @@ __device__ __forceinline__ Node load_node(const rt_bvh_node* base, int i)
     return n;
 }
 
+// The TLAS node as staged in LDS by the variants whose whole TLAS is there and whose slab
+// tests are f32 (OctNodes): per axis both children's lower planes, upper planes and the lower
+// ones again, so a ray reads its near and far planes with one 16-B (2 x 8-B) read at an
+// offset its direction sign selects (RayT::onx..onz); children as byte offsets of LdsNode
+// (leaf codes unchanged). 80 B instead of rt_bvh_node's 64.
+struct LdsNode {
+    float ax[3][6];   // [axis][lo0 lo1 hi0 hi1 lo0 lo1]
+    int32_t child[2];
+};
+static_assert(sizeof(LdsNode) == 80, "LdsNode layout");
+template <class C>
+constexpr bool OctNodes() { return C::NALL && C::S32; }
+// LDS byte address of a __shared__ object (the low 32 bits of its flat address), and an LDS
+// pointer from one: OctNodes node references are such addresses, so a node read needs no add
+__device__ __forceinline__ uint32_t lds_addr(const void* p) { return (uint32_t)(uintptr_t)p; }
+template <class T>
+__device__ __forceinline__ const __attribute__((address_space(3))) T* lds_ptr(uint32_t a)
+{
+    return (const __attribute__((address_space(3))) T*)(uintptr_t)a;
+}
+template <class C>
+constexpr int lds_node_bytes() { return OctNodes<C>() ? (int)sizeof(LdsNode) : (int)sizeof(rt_bvh_node); }
+
 // Closest hit in a BVH (nodes + leaf ranges of slots j, whose records are leaf_prims[j]).
 // `leaf(slot, t_max, best)` tests one primitive; on a closer hit it fills best (t and sub
 // ids) and returns true; best.prim is then the slot.
@@ -622,7 +646,7 @@ __device__ __forceinline__ bool traverse(const SceneDev& S, int root, const RayT
     // NL: this is the TLAS, whose first S.n_lds_nodes nodes (BFS order) were copied into
     // LDS at block start; deeper nodes are read from L1/L2
     const rt_bvh_node* lds_nodes =
-        reinterpret_cast<const rt_bvh_node*>(rt_lds + (C::LDS ? S.stack_entries * 256 : 0));
+        reinterpret_cast<const rt_bvh_node*>(rt_lds);   // at LDS address 0: node offsets are addresses
     bool any = false;
     int sp = sp0;
     int cur = root;
@@ -631,57 +655,43 @@ __device__ __forceinline__ bool traverse(const SceneDev& S, int root, const RayT
         tmin_f = f32_down(t_min);
         tmax_f = f32_up(t_max);
     }
-    // TLAS entirely in LDS, f32 slabs: each plane is read at the offset the ray's
-    // direction signs select (near plane first), so the slab test needs no min/max pair
-    // per axis: t_near = max(near planes), t_far = min(far planes)
-    constexpr bool OCT = NL && C::NALL && C::S32;
+    // TLAS entirely in LDS, f32 slabs (OctNodes): the node is the 80-B LdsNode layout and
+    // node references are byte offsets; per axis one 16-B read at the offset the ray's
+    // direction sign selects gives both children's near planes, then their far planes, so
+    // the slab test needs no min/max pair per axis: t_near = max(near planes), t_far =
+    // min(far planes). One address add per axis, the child pair at a fixed offset.
+    constexpr bool OCT = NL && OctNodes<C>();
     const char* const lb = reinterpret_cast<const char*>(lds_nodes);
-    const char *pnx = lb, *pny = lb, *pnz = lb, *pfx = lb, *pfy = lb, *pfz = lb;
-    if constexpr (OCT) {
-        pnx = lb + r.onx; pfx = lb + (r.onx ^ 12u);
-        pny = lb + r.ony; pfy = lb + (r.ony ^ 20u);
-        pnz = lb + r.onz; pfz = lb + (r.onz ^ 28u);
-    }
+    if constexpr (OCT) cur = cur >= 0 ? (int)(lds_addr(lb) + (uint32_t)cur * (uint32_t)sizeof(LdsNode)) : cur;
     // one node visit: test both children, continue with the nearer, push the farther
     auto visit = [&](int node) -> int {
         if (C::COUNT) cnt.nodes++;
         if constexpr (OCT) {
-            const int o = node * 64;
-            auto plane = [&](const char* p, int child) { return *reinterpret_cast<const float*>(p + o + 24 * child); };
-            const int2 ch = *reinterpret_cast<const int2*>(lb + o + 48);
+            const uint32_t nb = (uint32_t)node;   // LDS address of the node
+            typedef float f2v __attribute__((ext_vector_type(2)));
+            typedef int i2v __attribute__((ext_vector_type(2)));
+            auto pairs = [&](uint32_t off, f2v& n, f2v& f) {
+                const auto q = lds_ptr<f2v>(nb + off);   // one ds_read2_b64
+                n = q[0];
+                f = q[1];
+            };
+            f2v npx, fpx, npy, fpy, npz, fpz;
+            pairs(r.onx, npx, fpx);
+            pairs(r.ony, npy, fpy);
+            pairs(r.onz, npz, fpz);
+            const i2v ch = *lds_ptr<i2v>(nb + (uint32_t)offsetof(LdsNode, child));
             float tn[2], tf[2];
-#if RT_PK_SLAB
-          if constexpr (C::F == FEAT_SET_SPHERES) {
-            // both children's plane of one axis as a pair: one v_pk_fma_f32 per plane (the
-            // spheres variant only: the broadcast pairs cost 6 VGPRs, which the 3-wave
-            // variants pay in spills)
-            typedef float f2 __attribute__((ext_vector_type(2)));
-            auto pair = [&](const char* p) { return f2{plane(p, 0), plane(p, 1)}; };
-            const f2 ix = {r.fix, r.fix}, iy = {r.fiy, r.fiy}, iz = {r.fiz, r.fiz};
-            const f2 ox = {r.fox, r.fox}, oy = {r.foy, r.foy}, oz = {r.foz, r.foz};
-            const f2 nx = __builtin_elementwise_fma(pair(pnx), ix, ox), fx = __builtin_elementwise_fma(pair(pfx), ix, ox);
-            const f2 ny = __builtin_elementwise_fma(pair(pny), iy, oy), fy = __builtin_elementwise_fma(pair(pfy), iy, oy);
-            const f2 nz = __builtin_elementwise_fma(pair(pnz), iz, oz), fz = __builtin_elementwise_fma(pair(pfz), iz, oz);
 #pragma unroll
             for (int c = 0; c < 2; ++c) {
-                tn[c] = fmaxf(fmaxf(nx[c], ny[c]), fmaxf(nz[c], tmin_f));
-                tf[c] = fminf(fminf(fx[c], fy[c]), fminf(fz[c], tmax_f));
-            }
-          } else
-#endif
-          {
-#pragma unroll
-            for (int c = 0; c < 2; ++c) {
-                const float nx = __builtin_fmaf(plane(pnx, c), r.fix, r.fox);
-                const float ny = __builtin_fmaf(plane(pny, c), r.fiy, r.foy);
-                const float nz = __builtin_fmaf(plane(pnz, c), r.fiz, r.foz);
-                const float fx = __builtin_fmaf(plane(pfx, c), r.fix, r.fox);
-                const float fy = __builtin_fmaf(plane(pfy, c), r.fiy, r.foy);
-                const float fz = __builtin_fmaf(plane(pfz, c), r.fiz, r.foz);
+                const float nx = __builtin_fmaf(c ? npx.y : npx.x, r.fix, r.fox);
+                const float ny = __builtin_fmaf(c ? npy.y : npy.x, r.fiy, r.foy);
+                const float nz = __builtin_fmaf(c ? npz.y : npz.x, r.fiz, r.foz);
+                const float fx = __builtin_fmaf(c ? fpx.y : fpx.x, r.fix, r.fox);
+                const float fy = __builtin_fmaf(c ? fpy.y : fpy.x, r.fiy, r.foy);
+                const float fz = __builtin_fmaf(c ? fpz.y : fpz.x, r.fiz, r.foz);
                 tn[c] = fmaxf(fmaxf(nx, ny), fmaxf(nz, tmin_f));
                 tf[c] = fminf(fminf(fx, fy), fminf(fz, tmax_f));
             }
-          }
             const bool h0 = tn[0] <= tf[0], h1 = tn[1] <= tf[1], near0 = tn[0] <= tn[1];
             if (h0 && h1) {
                 stack[sp++] = near0 ? ch.y : ch.x;
@@ -833,7 +843,7 @@ __device__ bool instance_t(const SceneDev& S, const rt_instance& in, const RayT<
             }
         }
         int side = 0;
-        if (!simple_t<InstC<C>>(S.prims[in.child], r, t_min, t_max, ref.t, side, cnt)) return false;
+        if (!simple_t<InstC<C>>(S.prims[in.child], r, t_min, t_max, ref.t, side, cnt, (C::F & FEAT_SHUTTER) != 0)) return false;
         ref.sub = in.child;
         ref.side = side;
         return true;
@@ -844,7 +854,7 @@ __device__ bool instance_t(const SceneDev& S, const rt_instance& in, const RayT<
     HitRefT<R> inner;
     if (!traverse<C>(S, in.child, r, t_min, t_max, inner, stack, sp0, cnt,
                      [&](int slot, R tmax, HitRefT<R>& b) {
-                         return simple_t<InstC<C>>(S.leaf_prims[slot], r, t_min, tmax, b.t, b.side, cnt);
+                         return simple_t<InstC<C>>(S.leaf_prims[slot], r, t_min, tmax, b.t, b.side, cnt, (C::F & FEAT_SHUTTER) != 0);
                      }))
         return false;
     ref.t = inner.t;
@@ -889,7 +899,7 @@ __device__ void instance_finish(const SceneDev& S, const rt_instance& in, const 
     if (!done)
         simple_finish<InstC<C>>((C::F & FEAT_INST_BLAS) == 0 || in.child_kind == RT_CHILD_PRIM ? S.prims[ref.sub]
                                                                                                : S.leaf_prims[ref.sub],
-                                r, ref.t, ref.side, h);
+                                r, ref.t, ref.side, h, (C::F & FEAT_SHUTTER) != 0);
     const int n = in.n_ops;
 #pragma unroll
     for (int i = 3; i >= 0; --i) {
@@ -927,7 +937,7 @@ __device__ __forceinline__ bool boundary_t(const SceneDev& S, int prim, const Ra
         }
     }
     int side = 0;
-    return simple_t<BoundC<C>>(p, r, t_min, t_max, t, side, cnt);
+    return simple_t<BoundC<C>>(p, r, t_min, t_max, t, side, cnt, (C::F & FEAT_SHUTTER) != 0);
 }
 
 // ConstantMedium (hittable.rs:417-473), keyed draw instead of the in-hit thread_rng().
@@ -989,7 +999,7 @@ __device__ bool trace_world(const SceneDev& S, const RayT<R>& r, HitT<R>& h, Sta
                 return instance_t<C>(S, S.instances[p.a], r, t_min, tmax, b, stack, S.blas_base, key, cnt);
         if constexpr ((C::F & FEAT_MEDIUM) != 0)
             if (p.kind == RT_PRIM_MEDIUM) return medium_t<C>(S, p, r, t_min, tmax, b.t, stack, S.blas_base, key, cnt);
-        return simple_t<C>(p, r, t_min, tmax, b.t, b.side, cnt);
+        return simple_t<C>(p, r, t_min, tmax, b.t, b.side, cnt, (C::F & FEAT_SHUTTER) != 0);
     };
     const bool hit = traverse<C, true>(S, S.tlas_root, r, t_min, (R)RT_INF, best, stack, 0, cnt, leaf);
     if (!hit) return false;
@@ -1006,7 +1016,7 @@ __device__ bool trace_world(const SceneDev& S, const RayT<R>& r, HitT<R>& h, Sta
             return true;
         }
     }
-    simple_finish<C>(p, r, best.t, best.side, h);
+    simple_finish<C>(p, r, best.t, best.side, h, (C::F & FEAT_SHUTTER) != 0);
     return true;
 }
 
@@ -1253,16 +1263,22 @@ __device__ __forceinline__ void camera_ray(const KParams& P, int x, int y, rt_ps
 // CU). The flag is per launch, so the choice is wave-uniform.
 template <class C>
 constexpr bool StageShade() { return C::F != FEAT_SET_SPHERES; }
-__device__ __forceinline__ int lds_shade_offset(const SceneDev& S, bool lds_stack)
+template <class C>
+__device__ __forceinline__ int lds_stack_offset(const SceneDev& S)   // in ints, after the TLAS nodes
 {
-    return (lds_stack ? S.stack_entries * 256 : 0) + S.n_lds_nodes * 16;   // in ints
+    return S.n_lds_nodes * (lds_node_bytes<C>() / 4);
+}
+template <class C>
+__device__ __forceinline__ int lds_shade_offset(const SceneDev& S)
+{
+    return (C::LDS ? S.stack_entries * 256 : 0) + S.n_lds_nodes * (lds_node_bytes<C>() / 4);   // in ints
 }
 template <class C>
 __device__ __forceinline__ const rt_material& material_of(const SceneDev& S, int i)
 {
     if constexpr (StageShade<C>()) {
         if (S.n_lds_materials > 0)
-            return reinterpret_cast<const rt_material*>(rt_lds + lds_shade_offset(S, C::LDS))[i];
+            return reinterpret_cast<const rt_material*>(rt_lds + lds_shade_offset<C>(S))[i];
     }
     return S.materials[i];
 }
@@ -1271,7 +1287,7 @@ __device__ __forceinline__ const rt_texture& texture_of(const SceneDev& S, int i
 {
     if constexpr (StageShade<C>()) {
         if (S.n_lds_materials > 0)
-            return reinterpret_cast<const rt_texture*>(rt_lds + lds_shade_offset(S, C::LDS) + S.n_lds_materials * 16)[i];
+            return reinterpret_cast<const rt_texture*>(rt_lds + lds_shade_offset<C>(S) + S.n_lds_materials * 16)[i];
     }
     return S.textures[i];
 }
@@ -1280,16 +1296,35 @@ template <class C>
 __device__ __forceinline__ void stage_lds(const SceneDev& S)
 {
     bool any = false;
-    const int off = C::LDS ? S.stack_entries * 256 : 0;
+    const int off = 0;   // the TLAS nodes first (traverse)
     if (S.n_lds_nodes > 0) {
-        uint4* dst = reinterpret_cast<uint4*>(rt_lds + off);
-        const uint4* src = reinterpret_cast<const uint4*>(S.nodes);
-        for (int i = threadIdx.x; i < S.n_lds_nodes * 4; i += 256) dst[i] = src[i];
+        if constexpr (OctNodes<C>()) {   // one node per thread, rt_bvh_node -> LdsNode
+            LdsNode* dst = reinterpret_cast<LdsNode*>(rt_lds + off);
+            for (int i = threadIdx.x; i < S.n_lds_nodes; i += 256) {
+                const rt_bvh_node n = S.nodes[i];
+                LdsNode o;
+#pragma unroll
+                for (int a = 0; a < 3; ++a) {
+                    o.ax[a][0] = n.lo0[a]; o.ax[a][1] = n.lo1[a];
+                    o.ax[a][2] = n.hi0[a]; o.ax[a][3] = n.hi1[a];
+                    o.ax[a][4] = n.lo0[a]; o.ax[a][5] = n.lo1[a];
+                }
+#pragma unroll
+                for (int c = 0; c < 2; ++c)   // node references: LDS addresses (leaf codes stay < 0)
+                    o.child[c] = n.child[c] >= 0 ? (int)(lds_addr(dst) + (uint32_t)n.child[c] * (uint32_t)sizeof(LdsNode))
+                                                 : n.child[c];
+                dst[i] = o;
+            }
+        } else {
+            uint4* dst = reinterpret_cast<uint4*>(rt_lds + off);
+            const uint4* src = reinterpret_cast<const uint4*>(S.nodes);
+            for (int i = threadIdx.x; i < S.n_lds_nodes * 4; i += 256) dst[i] = src[i];
+        }
         any = true;
     }
     if constexpr (StageShade<C>()) {
         if (S.n_lds_materials > 0) {
-            uint4* dm = reinterpret_cast<uint4*>(rt_lds + lds_shade_offset(S, C::LDS));
+            uint4* dm = reinterpret_cast<uint4*>(rt_lds + lds_shade_offset<C>(S));
             const uint4* sm = reinterpret_cast<const uint4*>(S.materials);
             for (int i = threadIdx.x; i < S.n_lds_materials * 4; i += 256) dm[i] = sm[i];
             uint4* dt = dm + S.n_lds_materials * 4;
@@ -1482,7 +1517,7 @@ __global__ void __launch_bounds__(256, min_waves<C>()) trace_chunks(SceneDev S, 
     LaneWork w;
     if (!lane_work(P, w)) return;
     StackT<C> stack;
-    if constexpr (C::LDS) stack.base = rt_lds + threadIdx.x;
+    if constexpr (C::LDS) stack.base = rt_lds + lds_stack_offset<C>(S) + threadIdx.x;
     Count cnt{};
     uint64_t t_cam = 0, t_trace = 0, t_shade = 0, t_prev = 0;
     if (C::COUNT) t_prev = __builtin_amdgcn_s_memtime();
@@ -1584,7 +1619,7 @@ __global__ void __launch_bounds__(256, min_waves<C>()) trace_pool(SceneDev S, co
     const KParams& P = *Pp;
     stage_lds<C>(S);
     StackT<C> stack;
-    if constexpr (C::LDS) stack.base = rt_lds + threadIdx.x;
+    if constexpr (C::LDS) stack.base = rt_lds + lds_stack_offset<C>(S) + threadIdx.x;
     Count cnt{};
     uint64_t t_cam = 0, t_trace = 0, t_shade = 0, t_prev = 0;
     if (C::COUNT) t_prev = __builtin_amdgcn_s_memtime();
@@ -1795,7 +1830,8 @@ template <uint32_t F, bool S32, bool LDS, bool COUNT, bool F32>
 static void launch_one(const Launch& L, hipStream_t stream, bool nall)
 {
     const SceneDev& S = *L.S;
-    const size_t lds = (LDS ? (size_t)S.stack_entries * 256 * sizeof(int) : 0) + (size_t)S.n_lds_nodes * 64 +
+    const size_t node_bytes = nall && S32 ? sizeof(LdsNode) : sizeof(rt_bvh_node);   // lds_node_bytes
+    const size_t lds = (LDS ? (size_t)S.stack_entries * 256 * sizeof(int) : 0) + (size_t)S.n_lds_nodes * node_bytes +
                        (F != FEAT_SET_SPHERES ? (size_t)S.n_lds_materials * 64 + (size_t)S.n_lds_textures * 96 : 0);
     if (L.pool) {
         auto go = [&](auto kernel) {

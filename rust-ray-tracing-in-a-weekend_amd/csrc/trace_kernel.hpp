@@ -59,7 +59,8 @@ enum : uint32_t {
     FEAT_MEDIUM_INST = 64,  // a medium boundary that is not a sphere (box, rect, instance)
     FEAT_INST_MEDIUM = 128, // a medium inside an instance (nested Translate/RotateY over a ConstantMedium)
     FEAT_INST_BLAS = 256,   // an instance over a BVH (a nested walk; instances over one primitive need none)
-    FEAT_ALL = 511,
+    FEAT_SHUTTER = 512,     // a MovingSphere whose shutter is not [0, 1] (its centre needs a division)
+    FEAT_ALL = 1023,
     FEAT_SET_SPHERES = 0,                                          // compiled variant: spheres + solid/checker
     FEAT_SET_RECTINST = FEAT_RECT | FEAT_INST | FEAT_INST_RECT,    // + rects, boxes, instances of one prim (Cornell)
     FEAT_SET_MEDIA = FEAT_SET_RECTINST | FEAT_MEDIUM | FEAT_MEDIUM_INST,  // + constant media (Cornell smoke)

@@ -68,7 +68,7 @@ def test_nested_world_matches_oracle(rt, renderer):
     soa = tw.product.flatten()
     assert soa.n_media == 3 and soa.n_instances >= 5
     got, ref = _render_both(rt, renderer, tw, 48, 32, 6, (7.0, 4.0, 9.0), (0.0, 0.7, 0.0), (0.5, 0.6, 0.8))
-    assert renderer.stats().variant_features == 511          # media under instances: the all-features variant
+    assert renderer.stats().variant_features == 1023          # media under instances: the all-features variant
     assert float(ref.max()) > 0.0
     assert_parity(got, ref, "nested world")
 
@@ -88,3 +88,27 @@ def test_nested_world_accel_modes_and_f32(rt, renderer):
         renderer.set_precision(rt.RT_PREC_F64)
     f64 = _render_both(rt, renderer, tw, 32, 24, 32, (7.0, 4.0, 9.0), (0.0, 0.7, 0.0), (0.5, 0.6, 0.8))[0]
     assert np.all(np.isfinite(f32)) and abs(float(f32.mean()) / float(f64.mean()) - 1.0) < 0.1
+
+
+def _moving_world(rt, t0, t1):
+    tw = ob.TwinWorld(rt, 3)
+    white = tw.lambertian(tw.checker((0.2, 0.3, 0.1), (0.9, 0.9, 0.9)))
+    red = tw.lambertian(tw.solid(0.7, 0.1, 0.1))
+    metal = tw.metal((0.8, 0.8, 0.9), 0.2)
+    tw.push(tw.sphere(white, (0.0, -1000.0, 0.0), 1000.0))
+    for i in range(5):
+        c0 = (-2.0 + i, 0.3, 0.2 * i)
+        tw.push(tw.moving_sphere(red if i % 2 else metal, c0, (c0[0], c0[1] + 0.4, c0[2]), t0, t1, 0.3))
+    tw.push(tw.moving_sphere(red, (0.5, 1.2, -1.0), (0.9, 1.2, -1.0), 0.0, 1.0, 0.4))
+    return tw
+
+
+@pytest.mark.parametrize("t0,t1,feat", [(0.0, 1.0, 0), (0.25, 0.75, 1023), (-1.0, 2.0, 1023)])
+def test_moving_sphere_shutters_match_oracle(rt, renderer, t0, t1, feat):
+    """MovingSphere::center (hittable.rs:556-558) for any shutter: [0, 1] shutters (every
+    reference scene) take the spheres variant, which loads no per-primitive shutter flag;
+    another shutter selects FEAT_SHUTTER (the all-features variant) and its division."""
+    tw = _moving_world(rt, t0, t1)
+    got, ref = _render_both(rt, renderer, tw, 40, 24, 6, (6.0, 2.0, 5.0), (0.0, 0.5, 0.0), (0.7, 0.8, 1.0))
+    assert renderer.stats().variant_features == feat
+    assert_parity(got, ref, f"moving spheres, shutter [{t0}, {t1}]")

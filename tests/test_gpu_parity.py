@@ -208,7 +208,7 @@ def test_feature_set_variants_identical(rt, renderer, scene_id, W, H, feat):
     renderer.upload(world)
     img = renderer.render(cam, p)
     assert renderer.stats().variant_features == feat
-    os.environ["RT_EXTRA_FEATURES"] = "511"
+    os.environ["RT_EXTRA_FEATURES"] = "1023"
     try:
         big = rt.Renderer(0)
     finally:
@@ -216,7 +216,7 @@ def test_feature_set_variants_identical(rt, renderer, scene_id, W, H, feat):
     try:
         big.upload(world)
         img_all = big.render(cam, p)
-        assert big.stats().variant_features == 511
+        assert big.stats().variant_features == 1023
     finally:
         big.close()
     assert np.array_equal(img, img_all)
