@@ -671,9 +671,10 @@ int rt_ctx_upload_soa(rt_ctx* c, const rt_scene_soa* s)
     c->S.tlas_root = s->tlas_root;
     c->S.n_lds_nodes = 0;
     // traversal stack: TLAS walk, then a nested BLAS walk (instances) above it, sized from the
-    // depths validate_soa measured (<= 32 each, so the 64-entry scratch stack always fits)
-    c->S.blas_base = tlas_depth;
-    c->S.stack_entries = std::max(1, tlas_depth + blas_depth);
+    // depths validate_soa measured (<= 32 each), each walk's bottom entry holding its RT_DONE
+    // sentinel (traverse): the 66-entry scratch stack always fits
+    c->S.blas_base = tlas_depth + 1;
+    c->S.stack_entries = tlas_depth + 1 + (blas_depth > 0 ? blas_depth + 1 : 0);
     c->n_tlas_nodes = n_tlas_nodes;
     c->n_nodes = s->n_nodes;
     c->n_materials = s->n_materials;

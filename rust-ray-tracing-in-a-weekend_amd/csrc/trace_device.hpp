@@ -148,7 +148,7 @@ struct Stack<true> {
 };
 template <>
 struct Stack<false> {
-    int v[64];
+    int v[66];   // 32 + 32 entries + the two walks' RT_DONE sentinels
     __device__ __forceinline__ int& operator[](int i) { return v[i]; }
 };
 template <class C>
@@ -648,7 +648,10 @@ __device__ __forceinline__ bool traverse(const SceneDev& S, int root, const RayT
     const rt_bvh_node* lds_nodes =
         reinterpret_cast<const rt_bvh_node*>(rt_lds);   // at LDS address 0: node offsets are addresses
     bool any = false;
-    int sp = sp0;
+    // the walk's bottom entry is RT_DONE (the host reserves it: SceneDev.stack_entries,
+    // blas_base), so a pop needs no empty-stack test: popping it ends the walk
+    stack[sp0] = RT_DONE;
+    int sp = sp0 + 1;
     int cur = root;
     float tmin_f = 0.0f, tmax_f = 0.0f;
     if constexpr (C::S32) {
@@ -699,7 +702,7 @@ __device__ __forceinline__ bool traverse(const SceneDev& S, int root, const RayT
             }
             if (h0) return ch.x;
             if (h1) return ch.y;
-            return sp == sp0 ? RT_DONE : stack[--sp];
+            return stack[--sp];
         }
         const Node nd = (NL && (C::NALL || node < S.n_lds_nodes)) ? load_node(lds_nodes, node)
                                                                   : load_node(S.nodes, node);
@@ -721,7 +724,7 @@ __device__ __forceinline__ bool traverse(const SceneDev& S, int root, const RayT
         }
         if (h0) return nd.child[0];
         if (h1) return nd.child[1];
-        return sp == sp0 ? RT_DONE : stack[--sp];
+        return stack[--sp];
     };
     auto do_leaf = [&](int code) {
         code = ~code;
@@ -741,7 +744,7 @@ __device__ __forceinline__ bool traverse(const SceneDev& S, int root, const RayT
         while (cur != RT_DONE) {
             if (cur < 0) {
                 do_leaf(cur);
-                cur = sp == sp0 ? RT_DONE : stack[--sp];
+                cur = stack[--sp];
             } else {
                 cur = visit(cur);
             }
@@ -758,7 +761,7 @@ __device__ __forceinline__ bool traverse(const SceneDev& S, int root, const RayT
             if (cur == RT_DONE) break;
             do_leaf(cur);
             if (C::COUNT) cnt.t_leaves += __builtin_amdgcn_s_memtime() - t0;
-            cur = sp == sp0 ? RT_DONE : stack[--sp];
+            cur = stack[--sp];
         }
     } else {
         // Speculative while-while (Aila & Laine 2009, §4): a lane that reaches a leaf parks
@@ -771,7 +774,7 @@ __device__ __forceinline__ bool traverse(const SceneDev& S, int root, const RayT
                 cur = visit(cur);
                 if (cur < 0 && cur != RT_DONE && parked == 0) {
                     parked = cur;
-                    cur = sp == sp0 ? RT_DONE : stack[--sp];
+                    cur = stack[--sp];
                 }
                 if (__all(parked != 0)) break;
             }
@@ -781,7 +784,7 @@ __device__ __forceinline__ bool traverse(const SceneDev& S, int root, const RayT
                 parked = 0;
             } else if (cur != RT_DONE && cur < 0) {
                 lf = cur;
-                cur = sp == sp0 ? RT_DONE : stack[--sp];
+                cur = stack[--sp];
             } else if (cur == RT_DONE) {
                 break;
             } else {

@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--spp", type=int, default=500)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--block-samples", type=int, nargs="*", default=[], help="per-sample pool block sizes to sweep")
+    ap.add_argument("--row-blocks", type=int, nargs="*", default=[1, 8], help="rt_render_params.row_block values to sweep")
     a = ap.parse_args()
     import numpy as np
     import torch  # noqa: F401  (one HIP runtime: torch's)
@@ -30,7 +31,7 @@ def main():
     W, H = 1200, 800
     world = rt.World(1).build_scene(0)
     cam, bg = rt.scene_camera(0, W, H)
-    cases = [(n, block, None) for n, block in ((1, 1), (2, 1), (4, 1), (8, 1), (2, 8), (4, 8), (8, 8))]
+    cases = [(n, block, None) for block in a.row_blocks for n in ((1, 2, 4, 8) if block == 1 else (2, 4, 8))]
     cases += [(n, 1, bs) for bs in a.block_samples for n in (1, 8)]
     renderers = {}
     for n, block, bs in cases:
