@@ -106,6 +106,9 @@ __device__ __forceinline__ bool first_active_lane()
 #ifndef RT_BOX_RCP
 #define RT_BOX_RCP 1   // a Box's six sides divide through three per-box reciprocals (BoxRcp)
 #endif
+#ifndef RT_PK_SLAB
+#define RT_PK_SLAB 0   // packed-f32 (v_pk_fma_f32) plane products of the two children (LDS node pairs)
+#endif
 #ifndef RT_TRACE_LOOP
 #define RT_TRACE_LOOP 1   // 0 if-if, 1 while-while, 2 while-while with speculative node visits
 #endif
@@ -613,6 +616,11 @@ __device__ __forceinline__ Node load_node(const rt_bvh_node* base, int i)
     return n;
 }
 
+// The variants whose LDS node visits use packed-f32 plane products (v_pk_fma_f32: 6 instead of
+// 12 FMAs; the ray's broadcast pairs cost ~4 VGPRs, which the texture variants would spill)
+template <class C>
+constexpr bool PkSlab() { return RT_PK_SLAB && (C::F & (FEAT_NOISE | FEAT_IMAGE)) == 0; }
+
 // The TLAS node as staged in LDS by the variants whose whole TLAS is there and whose slab
 // tests are f32 (OctNodes): per axis both children's lower planes, upper planes and the lower
 // ones again, so a ray reads its near and far planes with one 16-B (2 x 8-B) read at an
@@ -684,6 +692,19 @@ __device__ __forceinline__ bool traverse(const SceneDev& S, int root, const RayT
             pairs(r.onz, npz, fpz);
             const i2v ch = *lds_ptr<i2v>(nb + (uint32_t)offsetof(LdsNode, child));
             float tn[2], tf[2];
+            if constexpr (PkSlab<C>()) {
+            // both children's plane of one axis as one v_pk_fma_f32 (the pair comes from one read)
+            const f2v ix = {r.fix, r.fix}, iy = {r.fiy, r.fiy}, iz = {r.fiz, r.fiz};
+            const f2v ox = {r.fox, r.fox}, oy = {r.foy, r.foy}, oz = {r.foz, r.foz};
+            const f2v nx = __builtin_elementwise_fma(npx, ix, ox), fx = __builtin_elementwise_fma(fpx, ix, ox);
+            const f2v ny = __builtin_elementwise_fma(npy, iy, oy), fy = __builtin_elementwise_fma(fpy, iy, oy);
+            const f2v nz = __builtin_elementwise_fma(npz, iz, oz), fz = __builtin_elementwise_fma(fpz, iz, oz);
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+                tn[c] = fmaxf(fmaxf(nx[c], ny[c]), fmaxf(nz[c], tmin_f));
+                tf[c] = fminf(fminf(fx[c], fy[c]), fminf(fz[c], tmax_f));
+            }
+            } else {
 #pragma unroll
             for (int c = 0; c < 2; ++c) {
                 const float nx = __builtin_fmaf(c ? npx.y : npx.x, r.fix, r.fox);
@@ -694,6 +715,7 @@ __device__ __forceinline__ bool traverse(const SceneDev& S, int root, const RayT
                 const float fz = __builtin_fmaf(c ? fpz.y : fpz.x, r.fiz, r.foz);
                 tn[c] = fmaxf(fmaxf(nx, ny), fmaxf(nz, tmin_f));
                 tf[c] = fminf(fminf(fx, fy), fminf(fz, tmax_f));
+            }
             }
             const bool h0 = tn[0] <= tf[0], h1 = tn[1] <= tf[1], near0 = tn[0] <= tn[1];
             if (h0 && h1) {
