@@ -43,6 +43,9 @@ size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 constexpr int kParamSlots = 16;
 
 // LDS stack entries per lane above which the scratch stack is used (48 KB per block)
+#ifndef RT_HOIST_DEFAULT
+#define RT_HOIST_DEFAULT 1
+#endif
 constexpr int kMaxLdsStack = 48;
 // TLAS nodes kept in LDS (32 KB per block): the first kMaxLdsNodes in BFS order, i.e.
 // the top levels; deeper ones are read from L1/L2
@@ -93,6 +96,7 @@ struct rt_ctx {
     int opt_slab32 = 1;                 // rt_ctx_set_variant / RT_SLAB32
     int opt_lds = 1;                    // rt_ctx_set_variant / RT_LDS_STACK
     int opt_lds_nodes = 1;              // RT_LDS_NODES: keep the TLAS in LDS when it fits
+    int opt_hoist = RT_HOIST_DEFAULT;   // RT_HOIST: test a huge root-child leaf before the walk (pre_leaf)
     int opt_pool = RT_SCHED_AUTO;       // rt_ctx_set_schedule / RT_SCHEDULE: RT_SCHED_*
     int opt_precision = RT_PREC_F64;    // rt_ctx_set_precision / RT_PRECISION: RT_PREC_*
     size_t sample_buf_cap = (size_t)32 << 30;  // RT_SAMPLE_BUF_MB: bound of one launch's trace output
@@ -135,6 +139,7 @@ int rt_ctx_create(int device, rt_ctx** out)
     if (const char* e = std::getenv("RT_SLAB32")) c->opt_slab32 = std::atoi(e) != 0;
     if (const char* e = std::getenv("RT_LDS_STACK")) c->opt_lds = std::atoi(e) != 0;
     if (const char* e = std::getenv("RT_LDS_NODES")) c->opt_lds_nodes = std::atoi(e) != 0;
+    if (const char* e = std::getenv("RT_HOIST")) c->opt_hoist = std::atoi(e) != 0;
     if (const char* e = std::getenv("RT_SCHEDULE")) c->opt_pool = std::min(3, std::max(0, std::atoi(e)));
     if (const char* e = std::getenv("RT_PRECISION")) c->opt_precision = std::atoi(e) == RT_PREC_F32 ? RT_PREC_F32 : RT_PREC_F64;
     if (const char* e = std::getenv("RT_BLOCK_CHUNKS")) c->block_chunks = std::min(64, std::max(1, std::atoi(e)));
@@ -466,6 +471,37 @@ static int walk_need(const rt_scene_soa* s, int ref, std::vector<int>& need, std
     return need[ref];
 }
 
+// SceneDev.pre_leaf: a root child that is a leaf of <= 2 primitives whose box holds at least
+// 8x the volume of its sibling's (a ground or fog sphere around the whole scene) is tested
+// before the walk, which then starts at the sibling (in the kernel variants that do this). The closest hit does not depend on the
+// order of the tests, so the image does not change (tests/test_gpu_parity.py); only SAH
+// tables (the LINEAR / MEDIAN modes keep the reference's structures as they are).
+static void hoist_root_leaf(const rt_scene_soa* s, rtk::SceneDev& S)
+{
+    if (s->accel != RT_ACCEL_SAH || s->tlas_root < 0 || s->tlas_root >= s->n_nodes) return;
+    const rt_bvh_node& root = s->nodes[s->tlas_root];
+    auto volume = [](const float* lo, const float* hi) {
+        double v = 1.0;
+        for (int a = 0; a < 3; ++a) v *= std::max(0.0, (double)hi[a] - (double)lo[a]);
+        return v;
+    };
+    for (int c = 0; c < 2; ++c) {
+        const int leaf = root.child[c], other = root.child[1 - c];
+        if (leaf >= 0 || (~leaf & 31) > 2) continue;
+        const float* lo = c ? root.lo1 : root.lo0;
+        const float* hi = c ? root.hi1 : root.hi0;
+        const double v = volume(lo, hi), vo = volume(c ? root.lo0 : root.lo1, c ? root.hi0 : root.hi1);
+        if (!(v >= 8.0 * vo) || !std::isfinite(v)) continue;
+        S.pre_leaf = leaf;
+        for (int a = 0; a < 3; ++a) {
+            S.pre_lo[a] = lo[a];
+            S.pre_hi[a] = hi[a];
+        }
+        S.pre_root = other;
+        return;
+    }
+}
+
 // Validates a (possibly foreign) SoA so the kernel never indexes out of bounds, never
 // overruns its traversal stack and never walks a cycle; computes the stack needs itself
 // (the tlas_depth / blas_depth fields are not trusted) and whether the TLAS really lies in
@@ -669,6 +705,8 @@ int rt_ctx_upload_soa(rt_ctx* c, const rt_scene_soa* s)
     c->S.image = (const uint8_t*)(base + off[8]);
     c->S.leaf_prims = (const rt_prim*)(base + off[9]);
     c->S.tlas_root = s->tlas_root;
+    c->S.pre_leaf = 0;
+    if (c->opt_hoist) hoist_root_leaf(s, c->S);
     c->S.n_lds_nodes = 0;
     // traversal stack: TLAS walk, then a nested BLAS walk (instances) above it, sized from the
     // depths validate_soa measured (<= 32 each), each walk's bottom entry holding its RT_DONE

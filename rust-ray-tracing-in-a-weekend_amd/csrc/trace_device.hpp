@@ -1008,6 +1008,12 @@ __device__ __forceinline__ void medium_finish(const rt_prim& m, const RayT<R>& r
 }
 
 // hit_hittables(world, ray, 0.001, inf) (hittable.rs:43-55) over the TLAS, then the
+// The variants that test SceneDev.pre_leaf before the walk: the spheres ones (random scene:
+// C2 19.17 -> 17.70 ms); the final scene gains nothing (its fog medium's test inlined twice
+// spills) and the Cornell variant would drop to 3 waves per SIMD.
+template <class C>
+constexpr bool PreLeaf() { return C::F == FEAT_SET_SPHERES; }
+
 // HitRecord of the closest primitive.
 template <class C, class R = typename C::Real>
 __device__ bool trace_world(const SceneDev& S, const RayT<R>& r, HitT<R>& h, StackT<C>& stack, const Keyed& key,
@@ -1026,7 +1032,36 @@ __device__ bool trace_world(const SceneDev& S, const RayT<R>& r, HitT<R>& h, Sta
             if (p.kind == RT_PRIM_MEDIUM) return medium_t<C>(S, p, r, t_min, tmax, b.t, stack, S.blas_base, key, cnt);
         return simple_t<C>(p, r, t_min, tmax, b.t, b.side, cnt, (C::F & FEAT_SHUTTER) != 0);
     };
-    const bool hit = traverse<C, true>(S, S.tlas_root, r, t_min, (R)RT_INF, best, stack, 0, cnt, leaf);
+    bool hit;
+    if constexpr (PreLeaf<C>()) {
+        R t_max = (R)RT_INF;
+        hit = false;
+        int root = S.tlas_root;
+        if (S.pre_leaf != 0) {   // wave-uniform: the huge root-child leaf first (SceneDev.pre_leaf)
+            root = S.pre_root;
+            bool in_box;
+            if constexpr (C::S32) {
+                float tn;
+                in_box = slab32(S.pre_lo, S.pre_hi, r, f32_down(t_min), f32_up(t_max), tn);
+            } else {
+                R tn;
+                in_box = slab(S.pre_lo, S.pre_hi, r, t_min, t_max, tn);
+            }
+            if (in_box) {
+                const int code = ~S.pre_leaf;
+                for (int slot = code >> 5, end = (code >> 5) + (code & 31); slot < end; ++slot) {
+                    if (leaf(slot, t_max, best)) {
+                        best.prim = slot;
+                        t_max = best.t;
+                        hit = true;
+                    }
+                }
+            }
+        }
+        hit |= traverse<C, true>(S, root, r, t_min, t_max, best, stack, 0, cnt, leaf);
+    } else {
+        hit = traverse<C, true>(S, S.tlas_root, r, t_min, (R)RT_INF, best, stack, 0, cnt, leaf);
+    }
     if (!hit) return false;
     const rt_prim& p = S.leaf_prims[best.prim];
     if constexpr ((C::F & FEAT_INST) != 0) {

@@ -28,6 +28,15 @@ struct SceneDev {
     int32_t has_spheres;    // any Sphere / MovingSphere: rays need 1/|d|^2 for the root divisions
     int32_t n_lds_materials;  // > 0: the material and texture tables are staged in LDS after the
     int32_t n_lds_textures;   // TLAS nodes (the kernel variants with rects or media; small tables)
+    // A leaf the cast tests before the TLAS walk (0: none): a root child holding a primitive
+    // far larger than the rest of the scene (the random scene's r = 1000 ground, the final
+    // scene's r = 5000 fog), whose test then runs once per cast with the whole wave instead
+    // of whenever each lane's walk reaches it; the walk starts below the root with t_max from
+    // it. Its (padded) box gates the test; the walk then starts at pre_root, the other root
+    // child. Only the spheres variants use it (PreLeaf: elsewhere the extra inlined leaf code
+    // costs the variant its occupancy); the others walk from tlas_root as before.
+    int32_t pre_leaf, pre_root;
+    float pre_lo[3], pre_hi[3];
 };
 
 struct KParams {
