@@ -145,7 +145,19 @@ int rt_ctx_create(int device, rt_ctx** out)
     if (const char* e = std::getenv("RT_BLOCK_CHUNKS")) c->block_chunks = std::min(64, std::max(1, std::atoi(e)));
     if (const char* e = std::getenv("RT_BLOCK_SAMPLES")) c->block_samples = std::min(1024, std::max(1, std::atoi(e)));
     if (const char* e = std::getenv("RT_EXTRA_FEATURES")) c->extra_features = (uint32_t)std::atoi(e) & rtk::FEAT_ALL;
-    if (const char* e = std::getenv("RT_SAMPLE_BUF_MB")) c->sample_buf_cap = (size_t)std::max(1L, std::atol(e)) << 20;
+    if (const char* e = std::getenv("RT_SAMPLE_BUF_MB")) {
+        c->sample_buf_cap = (size_t)std::max(1L, std::atol(e)) << 20;
+    } else {
+        // sized for the device: 3/8 of its free HBM, at most 128 GiB (an MI355X: ~107 GB, so
+        // C4's 49.8 GB of per-sample radiance is one launch), at least 32 GiB where half the
+        // free memory allows it (allocated lazily, only as large as a render needs)
+        size_t fr = 0, tot = 0;
+        if (hipMemGetInfo(&fr, &tot) == hipSuccess && fr > 0) {
+            size_t cap = std::min(fr / 8 * 3, (size_t)128 << 30);
+            cap = std::max(cap, std::min((size_t)32 << 30, fr / 2));
+            c->sample_buf_cap = std::max(cap >> 20, (size_t)1) << 20;
+        }
+    }
     hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     for (int i = 0; i < 3 && e == hipSuccess; ++i) e = hipEventCreate(&c->ev[i]);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_done, hipEventDisableTiming);

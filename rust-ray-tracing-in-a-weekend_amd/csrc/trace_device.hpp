@@ -106,6 +106,12 @@ __device__ __forceinline__ bool first_active_lane()
 #ifndef RT_BOX_RCP
 #define RT_BOX_RCP 1   // a Box's six sides divide through three per-box reciprocals (BoxRcp)
 #endif
+#ifndef RT_FINISH_AT_TRACE
+// pool schedules: a ray's traversal set-up (finish_ray) runs once per bounce iteration, for
+// every lane about to trace, instead of once in the camera step and once in shading (the wave
+// issued both exec-masked copies every iteration)
+#define RT_FINISH_AT_TRACE 1
+#endif
 #ifndef RT_PK_SLAB
 #define RT_PK_SLAB 0   // packed-f32 (v_pk_fma_f32) plane products of the two children (LDS node pairs)
 #endif
@@ -1400,7 +1406,7 @@ __device__ __forceinline__ void stage_lds(const SceneDev& S)
 // recursion unrolled into the throughput T. A path carries at most one emission (a
 // DiffuseLight ends it), so adding T*e straight into the chunk sum gives the same bits
 // as the reference's per-sample sum. Returns true if the path continues with r.
-template <class C, class R = typename C::Real>
+template <class C, bool FIN = true, class R = typename C::Real>
 __device__ __forceinline__ bool shade(const SceneDev& S, const KParams& P, const HitT<R>& h, RayT<R>& r,
                                       rt_pstream& st, R& Tr, R& Tg, R& Tb, double& sum_r, double& sum_g,
                                       double& sum_b)
@@ -1498,7 +1504,7 @@ __device__ __forceinline__ bool shade(const SceneDev& S, const KParams& P, const
         }
     }
     r.dx = sdx; r.dy = sdy; r.dz = sdz;
-    finish_ray<C>(r, S.has_spheres != 0);
+    if constexpr (FIN) finish_ray<C>(r, S.has_spheres != 0);   // else the caller's trace step does it
     return true;
 }
 
@@ -1785,7 +1791,7 @@ __global__ void __launch_bounds__(256, min_waves<C>()) trace_pool(SceneDev S, co
             key.sample = (uint32_t)s;
             ds_start(st, P.seed, key.pixel, (uint32_t)s);
             camera_ray(P, x, y, st, r);
-            finish_ray<C>(r, S.has_spheres != 0);
+            if constexpr (!RT_FINISH_AT_TRACE) finish_ray<C>(r, S.has_spheres != 0);
             Tr = Tg = Tb = (R)1;
             if constexpr (!ITEMS) cr = cg = cb = 0.0;  // ITEMS: the chunk's running sum
             depth = P.max_depth;
@@ -1795,6 +1801,7 @@ __global__ void __launch_bounds__(256, min_waves<C>()) trace_pool(SceneDev S, co
         if (depth > 0) {  // main.rs:21-23: depth 0 is black
             key.bounce = (uint32_t)(P.max_depth - depth);
             if (C::COUNT) cnt.casts++;
+            if constexpr (RT_FINISH_AT_TRACE) finish_ray<C>(r, S.has_spheres != 0);
             HitT<R> h;
             const bool hit = trace_world<C>(S, r, h, stack, key, cnt);
             if (C::COUNT) { const uint64_t t = __builtin_amdgcn_s_memtime(); t_trace += t - t_prev; t_prev = t; }
@@ -1807,7 +1814,7 @@ __global__ void __launch_bounds__(256, min_waves<C>()) trace_pool(SceneDev S, co
                     cnt.shade_lanes++;
                     if (first_active_lane()) cnt.shade_steps++;
                 }
-                cont = shade<C>(S, P, h, r, st, Tr, Tg, Tb, cr, cg, cb);
+                cont = shade<C, !RT_FINISH_AT_TRACE>(S, P, h, r, st, Tr, Tg, Tb, cr, cg, cb);
             }
         }
         if (C::COUNT) { const uint64_t t = __builtin_amdgcn_s_memtime(); t_shade += t - t_prev; t_prev = t; }
