@@ -112,6 +112,11 @@ __device__ __forceinline__ bool first_active_lane()
 // issued both exec-masked copies every iteration)
 #define RT_FINISH_AT_TRACE 1
 #endif
+#ifndef RT_MERGED_DRAWS
+// pool schedules: camera rays of new samples and scattered rays of the last iteration's hits
+// are generated in one step, their rejection-loop tries in one loop
+#define RT_MERGED_DRAWS 1
+#endif
 #ifndef RT_PK_SLAB
 #define RT_PK_SLAB 0   // packed-f32 (v_pk_fma_f32) plane products of the two children (LDS node pairs)
 #endif
@@ -1267,17 +1272,40 @@ __device__ __forceinline__ void random_in_unit_sphere(rt_pstream& st, R scale_m1
 // the integrator
 // ---------------------------------------------------------------------------
 
-// main.rs:517-520 + Camera::get_ray (camera.rs:58-66), f32 mode
-__device__ __forceinline__ void camera_ray(const KParams& P, int x, int y, rt_pstream& st, RayT<float>& r)
+// main.rs:517-520 + Camera::get_ray (camera.rs:58-66) in three steps: camera_begin (the
+// pixel jitter draws), the lens draws (random_in_unit_disk: 2 draws per try, the same
+// mapping as random_in_unit_sphere's, whose loop the pool schedules share with it) and
+// camera_end (the ray and its time draw). camera_ray runs them in a row.
+__device__ __forceinline__ void camera_begin(const KParams& P, int x, int y, rt_pstream& st, float& u, float& v)
+{   // f32 mode
+    u = ((float)x + draw_unit(st, 0.0f)) / (float)P.wm1;
+    v = ((float)y + draw_unit(st, 0.0f)) / (float)P.hm1;
+}
+__device__ __forceinline__ void camera_begin(const KParams& P, int x, int y, rt_pstream& st, double& u, double& v)
 {
-    const float u = ((float)x + draw_unit(st, 0.0f)) / (float)P.wm1;
-    const float v = ((float)y + draw_unit(st, 0.0f)) / (float)P.hm1;
-    float dxl, dyl;
-    for (;;) {
-        dxl = draw_m11(st, 0.0f);
-        dyl = draw_m11(st, 0.0f);
-        if (dxl * dxl + dyl * dyl < 1.0f) break;
-    }
+#ifdef RT_PROBE_FAST_CAMERA  // timing probe: NOT the product
+    u = ((double)x + rt_unit53(ds_u64(st))) * __builtin_amdgcn_rcp((double)P.width - 1.0);
+    v = ((double)y + rt_unit53(ds_u64(st))) * __builtin_amdgcn_rcp((double)P.height - 1.0);
+#else
+    u = div_rcp((double)x + rt_unit53(ds_u64(st)), P.wm1, P.inv_wm1);
+    v = div_rcp((double)y + rt_unit53(ds_u64(st)), P.hm1, P.inv_hm1);
+#endif
+}
+// one try of random_in_unit_disk (3 = false) or random_in_unit_sphere (3 = true): the
+// length test of a disk candidate is x*x + y*y + 0*0, the same value as x*x + y*y
+template <class R>
+__device__ __forceinline__ bool unit_try(rt_pstream& st, R scale_m11, bool three, R& x, R& y, R& z, R& len2)
+{
+    x = draw_m11(st, scale_m11);
+    y = draw_m11(st, scale_m11);
+    z = (R)0;
+    if (three) z = draw_m11(st, scale_m11);
+    len2 = x * x + y * y + z * z;
+    return len2 < (R)1;
+}
+__device__ __forceinline__ void camera_end(const KParams& P, rt_pstream& st, float u, float v, float dxl, float dyl,
+                                           RayT<float>& r)
+{   // f32 mode
     const rt_camera& c = P.cam;
     const float rdx = dxl * (float)c.lens_radius, rdy = dyl * (float)c.lens_radius;
     const float offx = (float)c.u[0] * rdx + (float)c.v[0] * rdy;
@@ -1292,23 +1320,9 @@ __device__ __forceinline__ void camera_ray(const KParams& P, int x, int y, rt_ps
     r.dz = (float)(c.lower_left_corner[2] - c.origin[2]) + (float)c.horizontal[2] * u + (float)c.vertical[2] * v - offz;
     r.time = (float)c.time0 + draw_unit(st, 0.0f) * (float)(c.time1 - c.time0);
 }
-
-// main.rs:517-520 + Camera::get_ray (camera.rs:58-66)
-__device__ __forceinline__ void camera_ray(const KParams& P, int x, int y, rt_pstream& st, RayT<double>& r)
+__device__ __forceinline__ void camera_end(const KParams& P, rt_pstream& st, double u, double v, double dxl,
+                                           double dyl, RayT<double>& r)
 {
-#ifdef RT_PROBE_FAST_CAMERA  // timing probe: NOT the product
-    const double u = ((double)x + rt_unit53(ds_u64(st))) * __builtin_amdgcn_rcp((double)P.width - 1.0);
-    const double v = ((double)y + rt_unit53(ds_u64(st))) * __builtin_amdgcn_rcp((double)P.height - 1.0);
-#else
-    const double u = div_rcp((double)x + rt_unit53(ds_u64(st)), P.wm1, P.inv_wm1);
-    const double v = div_rcp((double)y + rt_unit53(ds_u64(st)), P.hm1, P.inv_hm1);
-#endif
-    double dxl, dyl;
-    for (;;) {
-        dxl = rt_uniform_sample(ds_u64(st), -1.0, P.scale_m11);
-        dyl = rt_uniform_sample(ds_u64(st), -1.0, P.scale_m11);
-        if (dxl * dxl + dyl * dyl + 0.0 * 0.0 < 1.0) break;
-    }
     const double rdx = dxl * P.cam.lens_radius, rdy = dyl * P.cam.lens_radius;
     const double offx = P.cam.u[0] * rdx + P.cam.v[0] * rdy;
     const double offy = P.cam.u[1] * rdx + P.cam.v[1] * rdy;
@@ -1320,6 +1334,15 @@ __device__ __forceinline__ void camera_ray(const KParams& P, int x, int y, rt_ps
     r.dy = P.cam.lower_left_corner[1] + P.cam.horizontal[1] * u + P.cam.vertical[1] * v - P.cam.origin[1] - offy;
     r.dz = P.cam.lower_left_corner[2] + P.cam.horizontal[2] * u + P.cam.vertical[2] * v - P.cam.origin[2] - offz;
     r.time = rt_uniform_sample(ds_u64(st), P.cam.time0, P.scale_time);
+}
+template <class R>
+__device__ __forceinline__ void camera_ray(const KParams& P, int x, int y, rt_pstream& st, RayT<R>& r)
+{
+    R u, v, dxl, dyl, dzl, l2;
+    camera_begin(P, x, y, st, u, v);
+    while (!unit_try(st, (R)P.scale_m11, false, dxl, dyl, dzl, l2)) {
+    }
+    camera_end(P, st, u, v, dxl, dyl, r);
 }
 
 // The material / texture table a shading step reads: staged in LDS by the block prologue
@@ -1405,15 +1428,16 @@ __device__ __forceinline__ void stage_lds(const SceneDev& S)
 // One hit of ray_color (main.rs:25-34): emitted + attenuation * (next), with the
 // recursion unrolled into the throughput T. A path carries at most one emission (a
 // DiffuseLight ends it), so adding T*e straight into the chunk sum gives the same bits
-// as the reference's per-sample sum. Returns true if the path continues with r.
-template <class C, bool FIN = true, class R = typename C::Real>
-__device__ __forceinline__ bool shade(const SceneDev& S, const KParams& P, const HitT<R>& h, RayT<R>& r,
-                                      rt_pstream& st, R& Tr, R& Tg, R& Tb, double& sum_r, double& sum_g,
-                                      double& sum_b)
+// as the reference's per-sample sum. In three steps: shade_begin (emission; false if the
+// path ends there), the material's draws (random_in_unit_sphere unless Dielectric), and
+// shade_end (the scattered ray; false if Metal absorbs it). shade() runs them in a row; the
+// pool schedules run the draws in one rejection loop with the camera's (RT_MERGED_DRAWS).
+template <class C, class R = typename C::Real>
+__device__ __forceinline__ bool shade_begin(const SceneDev& S, const HitT<R>& h, R Tr, R Tg, R Tb, double& sum_r,
+                                            double& sum_g, double& sum_b)
 {
     const rt_material& m = material_of<C>(S, h.mat);
-    const int kind = m.kind;
-    if (kind == RT_MAT_DIFFUSE_LIGHT) {  // material.rs:25-34 (emits on both faces, never scatters)
+    if (m.kind == RT_MAT_DIFFUSE_LIGHT) {  // material.rs:25-34 (emits on both faces, never scatters)
         R er, eg, eb;
         tex_value<C>(S, m.tex, h, er, eg, eb);
         sum_r = sum_r + (double)(Tr * er);   // the chunk sums stay f64 in the f32 mode too
@@ -1421,12 +1445,25 @@ __device__ __forceinline__ bool shade(const SceneDev& S, const KParams& P, const
         sum_b = sum_b + (double)(Tb * eb);
         return false;
     }
+    return true;
+}
+// whether the material draws a random_in_unit_sphere candidate (Lambertian, Metal, Isotropic)
+template <class C>
+__device__ __forceinline__ bool shade_draws(const SceneDev& S, int mat)
+{
+    return material_of<C>(S, mat).kind != RT_MAT_DIELECTRIC;
+}
+// (qx, qy, qz, l2): the material's random_in_unit_sphere draw (0, 0, 0, 1 for Dielectric)
+template <class C, bool FIN = true, class R = typename C::Real>
+__device__ __forceinline__ bool shade_end(const SceneDev& S, const HitT<R>& h, RayT<R>& r, rt_pstream& st, R& Tr,
+                                          R& Tg, R& Tb, R qx, R qy, R qz, R l2)
+{
+    const rt_material& m = material_of<C>(S, h.mat);
+    const int kind = m.kind;
     // The materials share their expensive steps, so a wave holding several materials runs
     // each once: one unit-sphere loop (Lambertian, Metal, Isotropic), one 1/sqrt (of the
     // candidate for Lambertian, of the ray direction for Metal and Dielectric), one texture
     // lookup (Lambertian, Isotropic).
-    R qx = (R)0, qy = (R)0, qz = (R)0, l2 = (R)1;
-    if (kind != RT_MAT_DIELECTRIC) random_in_unit_sphere(st, (R)P.scale_m11, qx, qy, qz, l2);
 #ifdef RT_PROBE_FAST_SHADE  // timing probe: NOT the product
     const R inv = __builtin_amdgcn_rsq(kind == RT_MAT_LAMBERTIAN ? l2 : r.a);
 #else
@@ -1506,6 +1543,16 @@ __device__ __forceinline__ bool shade(const SceneDev& S, const KParams& P, const
     r.dx = sdx; r.dy = sdy; r.dz = sdz;
     if constexpr (FIN) finish_ray<C>(r, S.has_spheres != 0);   // else the caller's trace step does it
     return true;
+}
+template <class C, bool FIN = true, class R = typename C::Real>
+__device__ __forceinline__ bool shade(const SceneDev& S, const KParams& P, const HitT<R>& h, RayT<R>& r,
+                                      rt_pstream& st, R& Tr, R& Tg, R& Tb, double& sum_r, double& sum_g,
+                                      double& sum_b)
+{
+    if (!shade_begin<C>(S, h, Tr, Tg, Tb, sum_r, sum_g, sum_b)) return false;
+    R qx = (R)0, qy = (R)0, qz = (R)0, l2 = (R)1;
+    if (shade_draws<C>(S, h.mat)) random_in_unit_sphere(st, (R)P.scale_m11, qx, qy, qz, l2);
+    return shade_end<C, FIN>(S, h, r, st, Tr, Tg, Tb, qx, qy, qz, l2);
 }
 
 // image row of the shard's local row k: y = row_begin + k*row_stride, or in bands of 2^s rows
@@ -1716,6 +1763,9 @@ __global__ void __launch_bounds__(256, min_waves<C>()) trace_pool(SceneDev S, co
     Keyed key{P.seed, 0, 0, 0};
     rt_pstream st;
     RayT<R> r;
+    HitT<R> h;             // RT_MERGED_DRAWS: a hit whose scattered ray the next iteration draws
+    bool pending = false;
+    (void)pending;
     for (;;) {
         if (ITEMS && own) {
             own = false;
@@ -1780,6 +1830,79 @@ __global__ void __launch_bounds__(256, min_waves<C>()) trace_pool(SceneDev S, co
         if (!__any(active)) break;
         if (C::COUNT && first_active_lane()) cnt.wave_steps++;
         if (!active) continue;
+#if RT_MERGED_DRAWS
+        // Ray generation: the camera rays of new samples and the scattered rays of last
+        // iteration's hits (pending), whose random_in_unit_disk / random_in_unit_sphere tries
+        // run in one rejection loop (the wave used to run the two loops one after the other).
+        // Each lane's draws keep their order (its stream is its own), so the bits do not change.
+        bool go = true;   // the lane traces this iteration
+        {
+            R u = 0, v = 0;
+            bool tries = false;
+            if (new_sample) {
+                if (C::COUNT) {
+                    cnt.cam_lanes++;
+                    if (first_active_lane()) cnt.cam_steps++;
+                }
+                const int y = image_row(P, k);
+                key.pixel = (uint32_t)y * (uint32_t)P.width + (uint32_t)x;
+                key.sample = (uint32_t)s;
+                ds_start(st, P.seed, key.pixel, (uint32_t)s);
+                camera_begin(P, x, y, st, u, v);
+                Tr = Tg = Tb = (R)1;
+                if constexpr (!ITEMS) cr = cg = cb = 0.0;  // ITEMS: the chunk's running sum
+                depth = P.max_depth;
+                tries = true;
+            } else if (pending) {
+                tries = shade_draws<C>(S, h.mat);
+            }
+            R qx = (R)0, qy = (R)0, qz = (R)0, l2 = (R)1;
+            const bool three = !new_sample;
+            while (tries && !unit_try(st, (R)P.scale_m11, three, qx, qy, qz, l2)) {
+            }
+            if (new_sample) {
+                new_sample = false;
+                camera_end(P, st, u, v, qx, qy, r);
+            } else if (pending) {
+                pending = false;
+                go = shade_end<C, false>(S, h, r, st, Tr, Tg, Tb, qx, qy, qz, l2);
+                if (go) depth -= 1;
+            }
+        }
+        if (C::COUNT) { const uint64_t t = __builtin_amdgcn_s_memtime(); t_cam += t - t_prev; t_prev = t; }
+        if (go && depth > 0) {  // main.rs:21-23: depth 0 is black
+            key.bounce = (uint32_t)(P.max_depth - depth);
+            if (C::COUNT) cnt.casts++;
+            finish_ray<C>(r, S.has_spheres != 0);
+            const bool hit = trace_world<C>(S, r, h, stack, key, cnt);
+            if (C::COUNT) { const uint64_t t = __builtin_amdgcn_s_memtime(); t_trace += t - t_prev; t_prev = t; }
+            if (!hit) {  // main.rs:37: background
+                cr = cr + Tr * P.bg[0];
+                cg = cg + Tg * P.bg[1];
+                cb = cb + Tb * P.bg[2];
+            } else {
+                if (C::COUNT) {
+                    cnt.shade_lanes++;
+                    if (first_active_lane()) cnt.shade_steps++;
+                }
+                pending = shade_begin<C>(S, h, Tr, Tg, Tb, cr, cg, cb);
+            }
+        }
+        if (C::COUNT) { const uint64_t t = __builtin_amdgcn_s_memtime(); t_shade += t - t_prev; t_prev = t; }
+        if (pending) {
+        } else if (ITEMS && left > 0) {  // the item's next sample: the lane takes it at the loop top
+            active = false;
+            own = true;
+        } else {
+            const size_t slot = ITEMS ? (size_t)((unsigned)(s - P.sample_begin) / (unsigned)P.spp_chunk)
+                                      : (size_t)(s - P.sample_begin);
+            double* o = samples + (slot * n_px + (size_t)k * P.width + x) * 3;
+            o[0] = cr;
+            o[1] = cg;
+            o[2] = cb;
+            active = false;
+        }
+#else
         if (new_sample) {
             if (C::COUNT) {
                 cnt.cam_lanes++;
@@ -1834,6 +1957,7 @@ __global__ void __launch_bounds__(256, min_waves<C>()) trace_pool(SceneDev S, co
             o[2] = cb;
             active = false;
         }
+#endif
     }
     if (C::COUNT) {
         atomicAdd(&counters[0], (unsigned long long)cnt.casts);
