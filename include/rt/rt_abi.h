@@ -270,8 +270,10 @@ int rt_ctx_set_variant(rt_ctx* ctx, int slab32, int lds_stack, int lds_nodes);
  *           buffer bytes); a lane whose item ended takes the next item at once.
  *   AUTO:   POOL when the render's [sample][pixel] buffer takes at most 4 batches (it is
  *           the faster of the two), otherwise ITEMS; rt_stats.schedule reports which ran.
- * One launch's trace output is bounded by RT_SAMPLE_BUF_MB (default 32 GiB); a larger
- * render runs in buffer batches (on chunk boundaries) whose sums are carried across. */
+ * One launch's trace output is bounded by RT_SAMPLE_BUF_MB (default: sized at context
+ * creation to 3/8 of the device's free memory, at most 128 GiB, at least 32 GiB where half
+ * the free memory allows; allocated lazily, as large as a render needs); a larger render
+ * runs in buffer batches (on chunk boundaries) whose sums are carried across. */
 enum { RT_SCHED_CHUNKS = 0, RT_SCHED_POOL = 1, RT_SCHED_ITEMS = 2, RT_SCHED_AUTO = 3 };
 int rt_ctx_set_schedule(rt_ctx* ctx, int schedule);
 

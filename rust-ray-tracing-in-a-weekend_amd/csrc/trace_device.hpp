@@ -117,6 +117,12 @@ __device__ __forceinline__ bool first_active_lane()
 // are generated in one step, their rejection-loop tries in one loop
 #define RT_MERGED_DRAWS 1
 #endif
+#ifndef RT_SPTR
+#define RT_SPTR 1
+#endif
+#ifndef RT_MED3
+#define RT_MED3 1
+#endif
 #ifndef RT_PK_SLAB
 #define RT_PK_SLAB 0   // packed-f32 (v_pk_fma_f32) plane products of the two children (LDS node pairs)
 #endif
@@ -669,8 +675,21 @@ __device__ __forceinline__ bool traverse(const SceneDev& S, int root, const RayT
     bool any = false;
     // the walk's bottom entry is RT_DONE (the host reserves it: SceneDev.stack_entries,
     // blas_base), so a pop needs no empty-stack test: popping it ends the walk
+#if RT_SPTR
+    // the stack pointer as an address, pre-scaled by the entry stride: a push or pop is one
+    // add (not an add plus a shift-add of the index)
+    constexpr int SSTR = C::LDS ? 256 : 1;
+    int* sptr = &stack[sp0];
+    *sptr = RT_DONE;
+    sptr += SSTR;
+    auto push = [&](int v) { *sptr = v; sptr += SSTR; };
+    auto pop = [&]() -> int { sptr -= SSTR; return *sptr; };
+#else
     stack[sp0] = RT_DONE;
     int sp = sp0 + 1;
+    auto push = [&](int v) { stack[sp++] = v; };
+    auto pop = [&]() -> int { return stack[--sp]; };
+#endif
     int cur = root;
     float tmin_f = 0.0f, tmax_f = 0.0f;
     if constexpr (C::S32) {
@@ -683,6 +702,8 @@ __device__ __forceinline__ bool traverse(const SceneDev& S, int root, const RayT
     // the slab test needs no min/max pair per axis: t_near = max(near planes), t_far =
     // min(far planes). One address add per axis, the child pair at a fixed offset.
     constexpr bool OCT = NL && OctNodes<C>();
+    float ninf = -__builtin_inff();
+    if constexpr (OCT && RT_MED3) asm("s_mov_b32 %0, 0xff800000" : "=s"(ninf));
     const char* const lb = reinterpret_cast<const char*>(lds_nodes);
     if constexpr (OCT) cur = cur >= 0 ? (int)(lds_addr(lb) + (uint32_t)cur * (uint32_t)sizeof(LdsNode)) : cur;
     // one node visit: test both children, continue with the nearer, push the farther
@@ -725,17 +746,21 @@ __device__ __forceinline__ bool traverse(const SceneDev& S, int root, const RayT
                 const float fy = __builtin_fmaf(c ? fpy.y : fpy.x, r.fiy, r.foy);
                 const float fz = __builtin_fmaf(c ? fpz.y : fpz.x, r.fiz, r.foz);
                 tn[c] = fmaxf(fmaxf(nx, ny), fmaxf(nz, tmin_f));
-                tf[c] = fminf(fminf(fx, fy), fminf(fz, tmax_f));
+                // min(fz, t_max) as v_med3(fz, t_max, -inf): fminf would re-quiet the loop-carried
+                // t_max (a v_max_f32 t, t) at every visit; the plane products are never NaN.
+                // (-inf from an SGPR: with the constant the compiler folds med3 back to fminf.)
+                tf[c] = RT_MED3 ? fminf(fminf(fx, fy), __builtin_amdgcn_fmed3f(fz, tmax_f, ninf))
+                                : fminf(fminf(fx, fy), fminf(fz, tmax_f));
             }
             }
             const bool h0 = tn[0] <= tf[0], h1 = tn[1] <= tf[1], near0 = tn[0] <= tn[1];
             if (h0 && h1) {
-                stack[sp++] = near0 ? ch.y : ch.x;
+                push(near0 ? ch.y : ch.x);
                 return near0 ? ch.x : ch.y;
             }
             if (h0) return ch.x;
             if (h1) return ch.y;
-            return stack[--sp];
+            return pop();
         }
         const Node nd = (NL && (C::NALL || node < S.n_lds_nodes)) ? load_node(lds_nodes, node)
                                                                   : load_node(S.nodes, node);
@@ -752,12 +777,12 @@ __device__ __forceinline__ bool traverse(const SceneDev& S, int root, const RayT
             near0 = tn0 <= tn1;
         }
         if (h0 && h1) {
-            stack[sp++] = near0 ? nd.child[1] : nd.child[0];
+            push(near0 ? nd.child[1] : nd.child[0]);
             return near0 ? nd.child[0] : nd.child[1];
         }
         if (h0) return nd.child[0];
         if (h1) return nd.child[1];
-        return stack[--sp];
+        return pop();
     };
     auto do_leaf = [&](int code) {
         code = ~code;
@@ -777,7 +802,7 @@ __device__ __forceinline__ bool traverse(const SceneDev& S, int root, const RayT
         while (cur != RT_DONE) {
             if (cur < 0) {
                 do_leaf(cur);
-                cur = stack[--sp];
+                cur = pop();
             } else {
                 cur = visit(cur);
             }
@@ -794,7 +819,7 @@ __device__ __forceinline__ bool traverse(const SceneDev& S, int root, const RayT
             if (cur == RT_DONE) break;
             do_leaf(cur);
             if (C::COUNT) cnt.t_leaves += __builtin_amdgcn_s_memtime() - t0;
-            cur = stack[--sp];
+            cur = pop();
         }
     } else {
         // Speculative while-while (Aila & Laine 2009, §4): a lane that reaches a leaf parks
@@ -807,7 +832,7 @@ __device__ __forceinline__ bool traverse(const SceneDev& S, int root, const RayT
                 cur = visit(cur);
                 if (cur < 0 && cur != RT_DONE && parked == 0) {
                     parked = cur;
-                    cur = stack[--sp];
+                    cur = pop();
                 }
                 if (__all(parked != 0)) break;
             }
@@ -817,7 +842,7 @@ __device__ __forceinline__ bool traverse(const SceneDev& S, int root, const RayT
                 parked = 0;
             } else if (cur != RT_DONE && cur < 0) {
                 lf = cur;
-                cur = stack[--sp];
+                cur = pop();
             } else if (cur == RT_DONE) {
                 break;
             } else {
