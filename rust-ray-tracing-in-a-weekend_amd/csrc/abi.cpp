@@ -719,6 +719,9 @@ int rt_ctx_upload_soa(rt_ctx* c, const rt_scene_soa* s)
     c->S.tlas_root = s->tlas_root;
     c->S.pre_leaf = 0;
     if (c->opt_hoist) hoist_root_leaf(s, c->S);
+    // Stack16 (trace_device.hpp): node records at LDS addresses < 32 KB (80 B each) and leaf
+    // codes ((first slot << 5) | count, stored complemented) above the -32768 sentinel
+    c->S.stack16_ok = (n_tlas_nodes * (int64_t)80 <= 32767 - 80 && s->n_prim_refs <= 1023) ? 1 : 0;
     c->S.n_lds_nodes = 0;
     // traversal stack: TLAS walk, then a nested BLAS walk (instances) above it, sized from the
     // depths validate_soa measured (<= 32 each), each walk's bottom entry holding its RT_DONE

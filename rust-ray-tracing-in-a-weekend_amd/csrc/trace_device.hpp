@@ -171,8 +171,21 @@ struct Stack<false> {
     int v[66];   // 32 + 32 entries + the two walks' RT_DONE sentinels
     __device__ __forceinline__ int& operator[](int i) { return v[i]; }
 };
+#ifndef RT_STACK16
+// 16-bit LDS stack entries in the spheres variant with the whole TLAS in LDS: its 35 KB of LDS
+// per block (22.7 KB of node records + a 12-entry 32-bit stack) let only 4 blocks share a CU's
+// 160 KB; with 6.1 KB of stack 5 blocks fit, and the variant runs at 5 waves per SIMD (96
+// VGPRs, min_waves) — C2 1200x800x100 16.48 -> 15.40 ms, same bits (profiles/r02ao_*)
+#define RT_STACK16 1
+#endif
+struct Stack16 {   // node records at LDS addresses < 32 KB, leaf codes > -32768 (SceneDev.stack16_ok)
+    short* base;
+    __device__ __forceinline__ short& operator[](int i) const { return base[i * 256]; }
+};
 template <class C>
-using StackT = Stack<C::LDS>;
+constexpr bool Stack16Cfg() { return RT_STACK16 && C::LDS && C::NALL && C::S32 && C::F == FEAT_SET_SPHERES && !C::F32; }
+template <class C>
+using StackT = typename std::conditional<Stack16Cfg<C>(), Stack16, Stack<C::LDS>>::type;
 extern __shared__ int rt_lds[];  // [cached TLAS nodes] [stack entries x 256 lanes] [materials, textures]
 
 // Division by a value b used many times, through its correctly rounded reciprocal
@@ -675,17 +688,19 @@ __device__ __forceinline__ bool traverse(const SceneDev& S, int root, const RayT
     bool any = false;
     // the walk's bottom entry is RT_DONE (the host reserves it: SceneDev.stack_entries,
     // blas_base), so a pop needs no empty-stack test: popping it ends the walk
+    constexpr int DONE = Stack16Cfg<C>() ? -32768 : RT_DONE;   // the walk's bottom entry
 #if RT_SPTR
     // the stack pointer as an address, pre-scaled by the entry stride: a push or pop is one
     // add (not an add plus a shift-add of the index)
     constexpr int SSTR = C::LDS ? 256 : 1;
-    int* sptr = &stack[sp0];
-    *sptr = RT_DONE;
+    auto* sptr = &stack[sp0];
+    using SE = typename std::remove_reference<decltype(*sptr)>::type;
+    *sptr = (SE)DONE;
     sptr += SSTR;
-    auto push = [&](int v) { *sptr = v; sptr += SSTR; };
-    auto pop = [&]() -> int { sptr -= SSTR; return *sptr; };
+    auto push = [&](int v) { *sptr = (SE)v; sptr += SSTR; };
+    auto pop = [&]() -> int { sptr -= SSTR; return (int)*sptr; };
 #else
-    stack[sp0] = RT_DONE;
+    stack[sp0] = DONE;
     int sp = sp0 + 1;
     auto push = [&](int v) { stack[sp++] = v; };
     auto pop = [&]() -> int { return stack[--sp]; };
@@ -799,7 +814,7 @@ __device__ __forceinline__ bool traverse(const SceneDev& S, int root, const RayT
         }
     };
     if constexpr (C::LOOP == 0) {
-        while (cur != RT_DONE) {
+        while (cur != DONE) {
             if (cur < 0) {
                 do_leaf(cur);
                 cur = pop();
@@ -809,14 +824,14 @@ __device__ __forceinline__ bool traverse(const SceneDev& S, int root, const RayT
         }
     } else if constexpr (C::LOOP == 1) {
         uint64_t t0 = 0;
-        while (cur != RT_DONE) {
+        while (cur != DONE) {
             if (C::COUNT) t0 = __builtin_amdgcn_s_memtime();
             while (cur >= 0) {
                 if (C::COUNT && first_active_lane()) cnt.wave_nodes++;
                 cur = visit(cur);
             }
             if (C::COUNT) { const uint64_t t = __builtin_amdgcn_s_memtime(); cnt.t_nodes += t - t0; t0 = t; }
-            if (cur == RT_DONE) break;
+            if (cur == DONE) break;
             do_leaf(cur);
             if (C::COUNT) cnt.t_leaves += __builtin_amdgcn_s_memtime() - t0;
             cur = pop();
@@ -830,7 +845,7 @@ __device__ __forceinline__ bool traverse(const SceneDev& S, int root, const RayT
             while (cur >= 0) {
                 if (C::COUNT && first_active_lane()) cnt.wave_nodes++;
                 cur = visit(cur);
-                if (cur < 0 && cur != RT_DONE && parked == 0) {
+                if (cur < 0 && cur != DONE && parked == 0) {
                     parked = cur;
                     cur = pop();
                 }
@@ -840,10 +855,10 @@ __device__ __forceinline__ bool traverse(const SceneDev& S, int root, const RayT
             if (parked != 0) {
                 lf = parked;
                 parked = 0;
-            } else if (cur != RT_DONE && cur < 0) {
+            } else if (cur != DONE && cur < 0) {
                 lf = cur;
                 cur = pop();
-            } else if (cur == RT_DONE) {
+            } else if (cur == DONE) {
                 break;
             } else {
                 continue;
@@ -1637,7 +1652,8 @@ __device__ __forceinline__ bool lane_work(const KParams& P, LaneWork& w)
 template <class C>
 constexpr int min_waves()
 {
-    return C::F == FEAT_SET_SPHERES ? RT_MIN_WAVES_SPHERES
+    return Stack16Cfg<C>() ? 5
+           : C::F == FEAT_SET_SPHERES ? RT_MIN_WAVES_SPHERES
            : C::F == FEAT_SET_RECTINST ? RT_MIN_WAVES_RECTINST
            : C::F == FEAT_SET_MEDIA    ? RT_MIN_WAVES_MEDIA
            : C::F == FEAT_SET_FINAL    ? RT_MIN_WAVES_FINAL : RT_MIN_WAVES_ALL;
@@ -1655,7 +1671,8 @@ __global__ void __launch_bounds__(256, min_waves<C>()) trace_chunks(SceneDev S, 
     LaneWork w;
     if (!lane_work(P, w)) return;
     StackT<C> stack;
-    if constexpr (C::LDS) stack.base = rt_lds + lds_stack_offset<C>(S) + threadIdx.x;
+    if constexpr (Stack16Cfg<C>()) stack.base = reinterpret_cast<short*>(rt_lds + lds_stack_offset<C>(S)) + threadIdx.x;
+    else if constexpr (C::LDS) stack.base = rt_lds + lds_stack_offset<C>(S) + threadIdx.x;
     Count cnt{};
     uint64_t t_cam = 0, t_trace = 0, t_shade = 0, t_prev = 0;
     if (C::COUNT) t_prev = __builtin_amdgcn_s_memtime();
@@ -1757,7 +1774,8 @@ __global__ void __launch_bounds__(256, min_waves<C>()) trace_pool(SceneDev S, co
     const KParams& P = *Pp;
     stage_lds<C>(S);
     StackT<C> stack;
-    if constexpr (C::LDS) stack.base = rt_lds + lds_stack_offset<C>(S) + threadIdx.x;
+    if constexpr (Stack16Cfg<C>()) stack.base = reinterpret_cast<short*>(rt_lds + lds_stack_offset<C>(S)) + threadIdx.x;
+    else if constexpr (C::LDS) stack.base = rt_lds + lds_stack_offset<C>(S) + threadIdx.x;
     Count cnt{};
     uint64_t t_cam = 0, t_trace = 0, t_shade = 0, t_prev = 0;
     if (C::COUNT) t_prev = __builtin_amdgcn_s_memtime();
@@ -2047,7 +2065,8 @@ static void launch_one(const Launch& L, hipStream_t stream, bool nall)
 {
     const SceneDev& S = *L.S;
     const size_t node_bytes = nall && S32 ? sizeof(LdsNode) : sizeof(rt_bvh_node);   // lds_node_bytes
-    const size_t lds = (LDS ? (size_t)S.stack_entries * 256 * sizeof(int) : 0) + (size_t)S.n_lds_nodes * node_bytes +
+    const bool s16 = RT_STACK16 && LDS && nall && S32 && F == FEAT_SET_SPHERES && !F32;   // Stack16Cfg
+    const size_t lds = (LDS ? (size_t)S.stack_entries * 256 * (s16 ? 2 : 4) : 0) + (size_t)S.n_lds_nodes * node_bytes +
                        (F != FEAT_SET_SPHERES ? (size_t)S.n_lds_materials * 64 + (size_t)S.n_lds_textures * 96 : 0);
     if (L.pool) {
         auto go = [&](auto kernel) {
@@ -2078,7 +2097,10 @@ template <uint32_t F, bool COUNT>
 static void launch_f(const Launch& L, int slab32, int lds, hipStream_t stream)
 {
     const SceneDev& S = *L.S;
-    const bool nall = S.n_lds_nodes > 0 && S.n_lds_nodes == S.n_tlas_nodes;
+    bool nall = S.n_lds_nodes > 0 && S.n_lds_nodes == S.n_tlas_nodes;
+    // the whole-TLAS spheres instantiation keeps 16-bit stack entries (Stack16Cfg): a scene
+    // whose node addresses or leaf codes do not fit takes the partial-TLAS instantiation
+    if (RT_STACK16 && F == FEAT_SET_SPHERES && slab32 && lds && !S.stack16_ok) nall = false;
     if (slab32) {
         if (lds) launch_one<F, true, true, COUNT, false>(L, stream, nall);
         else launch_one<F, true, false, COUNT, false>(L, stream, nall);

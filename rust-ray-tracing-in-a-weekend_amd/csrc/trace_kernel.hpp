@@ -37,6 +37,9 @@ struct SceneDev {
     // costs the variant its occupancy); the others walk from tlas_root as before.
     int32_t pre_leaf, pre_root;
     float pre_lo[3], pre_hi[3];
+    // the TLAS walk's stack entries fit 16 bits (Stack16: node records at LDS byte addresses
+    // < 32 KB, i.e. <= 409 TLAS nodes, and leaf codes of <= 1023 leaf slots); set at upload
+    int32_t stack16_ok;
 };
 
 struct KParams {

@@ -112,3 +112,28 @@ def test_moving_sphere_shutters_match_oracle(rt, renderer, t0, t1, feat):
     got, ref = _render_both(rt, renderer, tw, 40, 24, 6, (6.0, 2.0, 5.0), (0.0, 0.5, 0.0), (0.7, 0.8, 1.0))
     assert renderer.stats().variant_features == feat
     assert_parity(got, ref, f"moving spheres, shutter [{t0}, {t1}]")
+
+
+def _sphere_field(rt, n):
+    """A spheres-only world of n small spheres on a grid plus the ground (the spheres variant)."""
+    tw = ob.TwinWorld(rt, 4)
+    ground = tw.lambertian(tw.checker((0.2, 0.3, 0.1), (0.9, 0.9, 0.9)))
+    mats = [tw.lambertian(tw.solid(0.7, 0.2, 0.1)), tw.metal((0.8, 0.8, 0.9), 0.1), tw.dielectric(1.5)]
+    tw.push(tw.sphere(ground, (0.0, -1000.0, 0.0), 1000.0))
+    side = int(np.ceil(np.sqrt(n)))
+    for i in range(n):
+        x, z = i % side, i // side
+        tw.push(tw.sphere(mats[i % 3], (-6.0 + 12.0 * x / side, 0.12, -6.0 + 12.0 * z / side), 0.1))
+    return tw
+
+
+@pytest.mark.parametrize("n", [300, 1100])
+def test_sphere_fields_both_stack_widths_match_oracle(rt, renderer, n):
+    """The spheres variant keeps 16-bit LDS stack entries when its TLAS node records lie
+    below 32 KB of LDS and its leaf codes fit (SceneDev.stack16_ok: <= 408 TLAS nodes, <= 1023
+    leaf slots); 1100 spheres exceed that and take the partial-TLAS instantiation with
+    32-bit entries. Both against the oracle."""
+    tw = _sphere_field(rt, n)
+    got, ref = _render_both(rt, renderer, tw, 32, 20, 3, (7.0, 2.0, 6.0), (0.0, 0.0, 0.0), (0.7, 0.8, 1.0))
+    assert renderer.stats().variant_features == 0
+    assert_parity(got, ref, f"sphere field of {n}")
