@@ -72,6 +72,12 @@ def parse():
     ap.add_argument("--spp-chunk", type=int, default=0, help="samples per chunk (0: the library's automatic choice)")
     ap.add_argument("--no-count", action="store_true", help="skip the count_work pass (profiling runs)")
     ap.add_argument("--ppm", default="", help="write the rendered frame (rank 0) as a P3 PPM")
+    ap.add_argument("--frame-npy", default="", help="save the rendered f32 frame (rank 0) as .npy")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="N > 1: nccl (RCCL over xGMI, the product) or gloo (host-staged slabs; lets several "
+                         "ranks share one GPU, for tests of this N > 1 path on a 1-GPU box)")
+    ap.add_argument("--device", type=int, default=None,
+                    help="GPU index for every rank (default: LOCAL_RANK); with --dist-backend gloo, ranks may share one")
     ap.add_argument("--precision", default="f64", choices=["f64", "f32"],
                     help="f64: the reference's arithmetic (the headline); f32: the fast mode (SURVEY §8 f3)")
     args = ap.parse_args()
@@ -148,11 +154,17 @@ def main():
     if world != args.gpus:
         if world == 1 and args.gpus > 1:
             raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run (one rank per GPU)")
+    gloo = world > 1 and args.dist_backend == "gloo"
+    if args.device is not None:
+        if world > 1 and not gloo:
+            raise SystemExit("--device with N > 1 needs --dist-backend gloo (RCCL needs one GPU per rank)")
+        local = args.device
+    torch.cuda.set_device(local)
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(local)
+        if gloo:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     device = torch.device("cuda", local)
 
     import __graft_entry__ as ge
@@ -176,7 +188,10 @@ def main():
     rows = rt.rows_in_shard(H, rank, world, ROW_BLOCK)
     rows_max = max(rt.rows_in_shard(H, r, world, ROW_BLOCK) for r in range(world))
     slab = torch.zeros((rows_max, W, 3), dtype=torch.float32, device=device)
-    gathered = [torch.empty_like(slab) for _ in range(world)] if (world > 1 and rank == 0) else None
+    # gloo gathers host copies of the slabs (staged through pinned memory), RCCL device slabs
+    stage = torch.empty(slab.shape, dtype=slab.dtype, pin_memory=True) if gloo else None
+    gathered = ([torch.empty_like(stage if gloo else slab) for _ in range(world)]
+                if (world > 1 and rank == 0) else None)
     frame = torch.empty((H, W, 3), dtype=torch.float32, device=device) if rank == 0 else None
     # A stream of our own: torch's default stream has the null handle, which the C ABI reads
     # as "the context's stream" (a non-blocking stream the default stream does not wait
@@ -190,7 +205,14 @@ def main():
     def step():
         with torch.cuda.stream(stream):
             renderer.render_device(cam, params, slab.data_ptr(), stream.cuda_stream)
-            if world > 1:
+            if gloo:
+                stage.copy_(slab, non_blocking=True)
+                stream.synchronize()
+                dist.gather(stage, gathered if rank == 0 else None, dst=0)
+                if rank == 0:
+                    dev = [g.to(device, non_blocking=True) for g in gathered]
+                    rt.assemble_rows(dev, H, world, out=frame, row_block=ROW_BLOCK)
+            elif world > 1:
                 dist.gather(slab, gathered if rank == 0 else None, dst=0)
                 if rank == 0:
                     rt.assemble_rows(gathered, H, world, out=frame, row_block=ROW_BLOCK)
@@ -220,7 +242,7 @@ def main():
     torch.cuda.synchronize(device)
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if gloo else device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     last = renderer.stats()
@@ -281,6 +303,8 @@ def main():
     frame_np = frame.cpu().numpy() if rank == 0 else None
     if args.ppm and rank == 0:
         rt.write_ppm(frame_np, args.ppm)
+    if args.frame_npy and rank == 0:
+        np.save(args.frame_npy, frame_np)
 
     progress("timed steps done; count pass, CPU baseline and parity")
     # ---- CPU baseline + parity (rank 0, N = 1 only)
@@ -358,7 +382,8 @@ def main():
                                    % (args.config, SCENE_NAMES.get(args.scene, "scene %d" % args.scene), W, H, spp,
                                       depth, world),
                        "scene": args.scene, "width": W, "height": H, "spp": spp, "max_depth": depth,
-                       "parallelism": "rows interleaved over %d rank(s), RCCL gather" % world},
+                       "parallelism": "rows interleaved over %d rank(s), %s gather"
+                                      % (world, "gloo (host-staged)" if gloo else "RCCL")},
             "roofline": roofline,
             "cpu_baseline": cpu,
             "parity": parity,

@@ -279,7 +279,12 @@ int rt_ctx_set_schedule(rt_ctx* ctx, int schedule);
 
 /* Arithmetic of a context's renders (default RT_PREC_F64, or the RT_PRECISION
  * environment variable 0/1).
- *   F64: the reference's f64 everywhere (math.rs:13-17), bit-exact against the oracle.
+ *   F64: the reference's f64 everywhere (math.rs:13-17), path-identical to the oracle: the
+ *        same rays, hits and draws; the per-pixel means differ only in the last ulps (the
+ *        throughput product T = a0*a1*...*e associates left here, right in the recursive
+ *        ray_color, main.rs:31; L_inf ~3e-16 at full C2 spp). Exact-t ties between two
+ *        primitives resolve by test order, which a BVH (and the hoisted root leaf) changes
+ *        against the reference's list order — a measure-zero event for spheres.
  *   F32: a fast mode: f32 rays, hit records, materials and textures (sphere tests keep
  *        |oc|^2 - r^2 in f64), one 32-bit draw per uniform; per-pixel sums
  *        stay f64. Statistically equal to F64 (independent-seed tests), not bitwise; never

@@ -24,6 +24,18 @@
  *     coefficients, restated), so host and device agree bit-for-bit where a
  *     libm / ocml pair would differ in the last ulp.
  *
+ * The sin / log / atan / acos restatements follow fdlibm (via musl's src/math), whose
+ * permission notice is preserved here as it asks:
+ *
+ *   ====================================================
+ *   Copyright (C) 1993 by Sun Microsystems, Inc. All rights reserved.
+ *
+ *   Developed at SunPro, a Sun Microsystems, Inc. business.
+ *   Permission to use, copy, modify, and distribute this
+ *   software is freely granted, provided that this notice
+ *   is preserved.
+ *   ====================================================
+ *
  * Everything here must be compiled WITHOUT fast-math and WITHOUT FP contraction
  * (-ffp-contract=off): the reference relies on IEEE NaN/inf comparison
  * semantics and parity relies on exact rounding.

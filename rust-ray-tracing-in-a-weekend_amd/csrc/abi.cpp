@@ -592,21 +592,25 @@ static int validate_soa(const rt_scene_soa* s, int& tlas_depth, int& blas_depth,
     if (t < 0) return fail(RT_ERR_INVALID, "cycle in the TLAS node graph");
     tlas_depth = t + 1;  // + 1 as flatten.cpp records it
     blas_depth = 0;
+    // Each node's need depends only on its subtree, and a completed walk leaves every node it
+    // reached done (colour 2) with its need recorded, so the walks of instance BLASes share
+    // one colour array: a BLAS shared by many instances, or a subtree of one already walked,
+    // costs nothing the second time (O(nodes) in total, not O(instances x nodes)). Likewise
+    // `checked` marks subtrees whose leaves were already found to hold simple primitives.
+    std::vector<uint8_t> checked((size_t)s->n_nodes, 0);
     for (int i = 0; i < s->n_instances; ++i) {
         const rt_instance& in = s->instances[i];
         if (in.child_kind != RT_CHILD_BVH) continue;
-        std::fill(colour.begin(), colour.end(), 0);
         const int b = walk_need(s, in.child, need, colour);
         if (b < 0) return fail(RT_ERR_INVALID, "cycle in an instance BVH");
         blas_depth = std::max(blas_depth, b + 1);
         std::vector<int> todo{in.child};   // acyclic (checked above): every leaf slot is a simple prim
-        std::fill(colour.begin(), colour.end(), 0);
         while (!todo.empty()) {
             const int ref = todo.back();
             todo.pop_back();
             if (ref >= 0) {
-                if (colour[ref]) continue;
-                colour[ref] = 1;
+                if (checked[ref]) continue;
+                checked[ref] = 1;
                 todo.push_back(s->nodes[ref].child[0]);
                 todo.push_back(s->nodes[ref].child[1]);
                 continue;
@@ -836,14 +840,21 @@ static bool bad_geometry(const rt_render_params* p)
            (b & (b - 1)) || b > 64 || (long long)p->width * p->height > 0xffffffffLL;
 }
 
-static int grow(rt_ctx* c, hipStream_t stream, double*& buf, size_t& cap, size_t need)
+static int grow(rt_ctx* c, hipStream_t stream, double*& buf, size_t& cap, size_t need, bool* oom = nullptr)
 {
     if (need <= cap) return RT_OK;
     HIP_TRY(hipStreamSynchronize(stream));
     (void)hipFree(buf);
     buf = nullptr;
     cap = 0;
-    HIP_TRY(hipMalloc((void**)&buf, need));
+    const hipError_t e = hipMalloc((void**)&buf, need);
+    if (e == hipErrorOutOfMemory && oom) {   // the caller retries with a smaller batch
+        (void)hipGetLastError();
+        buf = nullptr;
+        *oom = true;
+        return RT_ERR_HIP;
+    }
+    HIP_TRY(e);
     cap = need;
     return RT_OK;
 }
@@ -915,12 +926,6 @@ static int run_range(rt_ctx* c, const rt_camera* cam, const rt_render_params* p,
     if (c->n_nodes == 0 && !o.f32) o.slab32 = 0;
     const long long total = s_end - s_begin;
     const size_t px_bytes = px * 3 * sizeof(double);
-    // AUTO: the per-sample pool when its [sample][pixel] buffer takes at most 4 batches (C2:
-    // 11.5 GB in one, 101.6 vs 106.7 ms per frame for the item pool; C4: 49.8 GB in two,
-    // 1492 vs 1571 ms; profiles/r02d_*, r02e_*), else the item pool, whose partials take
-    // 1/chunk of those bytes and need no carried batches (C5: 1.6 TB of per-sample radiance)
-    o.pool = c->opt_pool != RT_SCHED_AUTO ? c->opt_pool
-             : ((size_t)total * px_bytes <= 4 * c->sample_buf_cap ? RT_SCHED_POOL : RT_SCHED_ITEMS);
     // the TLAS in LDS (read-only, shared by the block) when it fits the per-block budget
     rtk::SceneDev S = c->S;
     S.n_lds_nodes = c->opt_lds_nodes ? std::min(c->n_tlas_nodes, kMaxLdsNodes) : 0;
@@ -929,15 +934,62 @@ static int run_range(rt_ctx* c, const rt_camera* cam, const rt_render_params* p,
                        c->n_materials > 0;
     S.n_lds_materials = stage ? c->n_materials : 0;
     S.n_lds_textures = stage ? c->n_textures : 0;
-
-    // Buffer batches: the trace output of one launch is bounded by sample_buf_cap. Per-sample
-    // pool: samples x pixels x 24 B; chunk and item schedules: chunks x pixels x 24 B, batches
-    // on chunk boundaries (relative to s_begin), so the partials add in one-launch order.
-    const bool per_sample = o.pool == RT_SCHED_POOL;
     // work blocks of one tile: 16-sample chunks, per-sample pool one chunk per block, item pool
     // two (C2 kernel ms, pool 1/2/4 chunks: 99.8/100.2/103.2; items 1/2/4: 106.8/104.1/105.0;
     // profiles/r02f_*, r02g_*)
     K.block_chunks = c->block_chunks > 0 ? c->block_chunks : 2;
+
+    // Schedule and buffer batches, from the context's trace-output bound (sample_buf_cap). The
+    // bound is sized from the free HBM when the context is created; if the device has less by
+    // now (another context, torch or RCCL allocated since), the allocation below fails and the
+    // bound is halved until it fits: more batches (or the item pool), the same image.
+    bool per_sample = false;
+    long long batch = 0;
+    int n_batches = 0;
+    double* acc = sink.acc;
+    double* open = nullptr;
+    bool own_acc = false;
+    for (;;) {
+        // AUTO: the per-sample pool when its [sample][pixel] buffer takes at most 4 batches (C2:
+        // 11.5 GB in one, 101.6 vs 106.7 ms per frame for the item pool; C4: 49.8 GB in two,
+        // 1492 vs 1571 ms; profiles/r02d_*, r02e_*), else the item pool, whose partials take
+        // 1/chunk of those bytes and need no carried batches (C5: 1.6 TB of per-sample radiance)
+        o.pool = c->opt_pool != RT_SCHED_AUTO ? c->opt_pool
+                 : ((size_t)total * px_bytes <= 4 * c->sample_buf_cap ? RT_SCHED_POOL : RT_SCHED_ITEMS);
+        // Buffer batches: the trace output of one launch is bounded by sample_buf_cap. Per-sample
+        // pool: samples x pixels x 24 B; chunk and item schedules: chunks x pixels x 24 B, batches
+        // on chunk boundaries (relative to s_begin), so the partials add in one-launch order.
+        per_sample = o.pool == RT_SCHED_POOL;
+        const long long fit = (long long)std::max<size_t>(1, c->sample_buf_cap / px_bytes);
+        batch = std::min<long long>(total, per_sample ? fit : fit * chunk);
+        n_batches = (int)((total + batch - 1) / batch);
+        acc = sink.acc;
+        open = nullptr;
+        own_acc = false;
+        bool oom = false;
+        int rc = RT_OK;
+        if (per_sample && (n_batches > 1 || acc)) {  // acc_tmp = [open chunk sums | running total (no acc sink)]
+            rc = grow(c, stream, c->acc_tmp, c->acc_tmp_cap, 2 * px_bytes);
+            if (rc) return rc;
+            open = c->acc_tmp;
+            if (!acc) {
+                acc = c->acc_tmp + px * 3;
+                own_acc = true;
+            }
+        } else if (!per_sample && n_batches > 1 && !acc) {  // running total of the chunk partials
+            rc = grow(c, stream, c->acc_tmp, c->acc_tmp_cap, px_bytes);
+            if (rc) return rc;
+            acc = c->acc_tmp;
+            own_acc = true;
+        }
+        const int max_chunks = (int)((batch + chunk - 1) / chunk);
+        const size_t need = per_sample ? (size_t)batch * px_bytes : (size_t)max_chunks * px_bytes;
+        rc = grow(c, stream, c->partial, c->partial_cap, need, &oom);
+        if (rc == RT_OK) break;
+        if (!oom || c->sample_buf_cap <= ((size_t)1 << 20) || need <= px_bytes) return rc;
+        c->sample_buf_cap = std::max<size_t>(c->sample_buf_cap / 2, (size_t)1 << 20);
+    }
+    if (own_acc) HIP_TRY(hipMemsetAsync(acc, 0, px_bytes, stream));
     // per-sample pool blocks: the chunk's 16 samples per tile while that leaves >= 160 k blocks
     // (~40 per resident wave), else halved down to 4: a small shard's last blocks would
     // otherwise leave waves idle (C2 rows of 1 of 8 GPUs: 16 / 8 / 4 samples 14.06 / 13.70 /
@@ -950,32 +1002,6 @@ static int run_range(rt_ctx* c, const rt_camera* cam, const rt_render_params* p,
         while (bs > 4 && tiles * ((total + bs - 1) / bs) < 160000) bs = (bs + 1) / 2;
         K.block_samples = bs;
     }
-    const long long fit = (long long)std::max<size_t>(1, c->sample_buf_cap / px_bytes);
-    const long long batch = std::min<long long>(total, per_sample ? fit : fit * chunk);
-    const int n_batches = (int)((total + batch - 1) / batch);
-    double* acc = sink.acc;
-    double* open = nullptr;
-    bool own_acc = false;
-    if (per_sample && (n_batches > 1 || acc)) {  // acc_tmp = [open chunk sums | running total (no acc sink)]
-        int rc = grow(c, stream, c->acc_tmp, c->acc_tmp_cap, 2 * px_bytes);
-        if (rc) return rc;
-        open = c->acc_tmp;
-        if (!acc) {
-            acc = c->acc_tmp + px * 3;
-            own_acc = true;
-            HIP_TRY(hipMemsetAsync(acc, 0, px_bytes, stream));
-        }
-    } else if (!per_sample && n_batches > 1 && !acc) {  // running total of the chunk partials
-        int rc = grow(c, stream, c->acc_tmp, c->acc_tmp_cap, px_bytes);
-        if (rc) return rc;
-        acc = c->acc_tmp;
-        own_acc = true;
-        HIP_TRY(hipMemsetAsync(acc, 0, px_bytes, stream));
-    }
-    const int max_chunks = (int)((batch + chunk - 1) / chunk);
-    const size_t need = per_sample ? (size_t)batch * px_bytes : (size_t)max_chunks * px_bytes;
-    int rc = grow(c, stream, c->partial, c->partial_cap, need);
-    if (rc) return rc;
     if (count) HIP_TRY(hipMemsetAsync(c->counters, 0, kCounters * sizeof(unsigned long long), stream));
     int waves_per_simd = 0;
     o.waves_per_simd = &waves_per_simd;
@@ -1041,6 +1067,31 @@ static int end_on(rt_ctx* c, hipStream_t stream)
     c->any_enqueued = true;
     return RT_OK;
 }
+// begin_on ... end_on around every call that enqueues: once begin_on has run, end_on runs on
+// every way out, an early error return included — work already queued on `stream` before the
+// error still reads the context's buffers, and the next call on another stream must wait
+// for it (ev_done, last_stream), not for the call before
+struct StreamScope {
+    rt_ctx* c;
+    hipStream_t stream;
+    bool open = false;
+    StreamScope(rt_ctx* c_, hipStream_t s_) : c(c_), stream(s_) {}
+    int begin()
+    {
+        const int rc = begin_on(c, stream);
+        open = rc == RT_OK;
+        return rc;
+    }
+    int end()
+    {
+        open = false;
+        return end_on(c, stream);
+    }
+    ~StreamScope()
+    {
+        if (open) (void)end_on(c, stream);
+    }
+};
 
 // Device buffer for a host-bound result (grown on demand).
 static int out_staging(rt_ctx* c, hipStream_t stream, size_t out_bytes, void*& dev_out)
@@ -1069,7 +1120,8 @@ int rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, void* 
 
     HIP_TRY(hipSetDevice(c->device));
     hipStream_t stream = p->stream ? (hipStream_t)p->stream : c->stream;
-    int rc = begin_on(c, stream);
+    StreamScope scope(c, stream);
+    int rc = scope.begin();
     if (rc) return rc;
     const size_t out_bytes = (size_t)n_px * 3 * (p->out_format == RT_OUT_F64 ? 8 : 4);
     void* dev_out = out;
@@ -1084,7 +1136,7 @@ int rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, void* 
     rc = run_range(c, cam, p, 0, p->spp, chunk, stream, sink);
     if (rc) return rc;
     if (!p->out_on_device) HIP_TRY(hipMemcpyAsync(out, dev_out, out_bytes, hipMemcpyDeviceToHost, stream));
-    rc = end_on(c, stream);
+    rc = scope.end();
     if (rc) return rc;
     if (!p->out_on_device) HIP_TRY(hipStreamSynchronize(stream));
     return RT_OK;
@@ -1154,16 +1206,17 @@ int rt_accum_add(rt_ctx* c, rt_accum* a, const rt_camera* cam, const rt_render_p
     HIP_TRY(hipSetDevice(c->device));
     hipStream_t stream = p->stream ? (hipStream_t)p->stream : c->stream;
     if (stream != a->last_stream) HIP_TRY(hipStreamSynchronize(a->last_stream));
-    int rc = begin_on(c, stream);
+    StreamScope scope(c, stream);
+    int rc = scope.begin();
     if (rc) return rc;
+    a->last_stream = stream;   // the sums' stream from here on, even if a launch below fails
     Sink sink;
     sink.acc = a->sums;
     rc = run_range(c, cam, p, (int)a->done, (int)(a->done + sample_count), a->chunk, stream, sink);
     if (rc) return rc;
-    rc = end_on(c, stream);
+    rc = scope.end();
     if (rc) return rc;
     a->done += sample_count;
-    a->last_stream = stream;
     return RT_OK;
 }
 
@@ -1198,7 +1251,8 @@ int rt_accum_resolve(rt_ctx* c, rt_accum* a, double divisor, int out_format, int
     if (!(divisor > 0.0) || !std::isfinite(divisor)) return fail(RT_ERR_INVALID, "nothing accumulated / bad divisor");
     HIP_TRY(hipSetDevice(c->device));
     hipStream_t stream = a->last_stream;
-    int rc = begin_on(c, stream);
+    StreamScope scope(c, stream);
+    int rc = scope.begin();
     if (rc) return rc;
     const size_t out_bytes = (size_t)a->n_px * 3 * (out_format == RT_OUT_F64 ? 8 : 4);
     void* dev_out = out;
@@ -1209,7 +1263,7 @@ int rt_accum_resolve(rt_ctx* c, rt_accum* a, double divisor, int out_format, int
     // one "chunk" holding the running sums: 0.0 + sum = sum, then * (1/divisor) as rt_render
     HIP_TRY(rtk::launch_reduce(a->sums, dev_out, out_format == RT_OUT_F64, a->n_px, 1, 1.0 / divisor, stream));
     if (!out_on_device) HIP_TRY(hipMemcpyAsync(out, dev_out, out_bytes, hipMemcpyDeviceToHost, stream));
-    rc = end_on(c, stream);
+    rc = scope.end();
     if (rc) return rc;
     if (!out_on_device) HIP_TRY(hipStreamSynchronize(stream));
     return RT_OK;

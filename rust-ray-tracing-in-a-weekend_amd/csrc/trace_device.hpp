@@ -2101,6 +2101,23 @@ static void launch_f(const Launch& L, int slab32, int lds, hipStream_t stream)
     // the whole-TLAS spheres instantiation keeps 16-bit stack entries (Stack16Cfg): a scene
     // whose node addresses or leaf codes do not fit takes the partial-TLAS instantiation
     if (RT_STACK16 && F == FEAT_SET_SPHERES && slab32 && lds && !S.stack16_ok) nall = false;
+    // stack16_ok (abi.cpp) assumes the node records start at LDS address 0, i.e. that rt_lds is
+    // the kernels' only __shared__ object: a static __shared__ variable would move the dynamic
+    // base up, and 16-bit stack entries would truncate node addresses past 32 KB. Checked on the
+    // compiled kernels: any static LDS in them sends the scene to the 32-bit-stack instantiation.
+    if (RT_STACK16 && F == FEAT_SET_SPHERES && slab32 && lds && nall) {
+        static int static_lds = -1;
+        if (static_lds < 0) {
+            static_lds = 0;
+            hipFuncAttributes a;
+            const void* ks[3] = {(const void*)trace_pool<Cfg<F, true, true, true, COUNT, false>, false>,
+                                 (const void*)trace_pool<Cfg<F, true, true, true, COUNT, false>, true>,
+                                 (const void*)trace_chunks<Cfg<F, true, true, true, COUNT, false>>};
+            for (const void* k : ks)
+                if (hipFuncGetAttributes(&a, k) != hipSuccess || a.sharedSizeBytes != 0) static_lds = 1;
+        }
+        if (static_lds) nall = false;
+    }
     if (slab32) {
         if (lds) launch_one<F, true, true, COUNT, false>(L, stream, nall);
         else launch_one<F, true, false, COUNT, false>(L, stream, nall);

@@ -3,6 +3,11 @@ device 0, each render their interleaved row shard through librtiow_amd.so and ra
 gathers the shards over gloo and re-interleaves them. The frame must equal the
 one-process render bit for bit (every draw is keyed by pixel and sample).
 
+bench.py's own N > 1 branch runs here too: `torch.distributed.run
+--nproc-per-node 2 bench.py --gpus 2 --dist-backend gloo --device 0` (both ranks on the one
+GPU of the box; gloo, since RCCL refuses two ranks on one device) — its shard, gather,
+re-interleave, barrier and max-over-ranks timing — against bench.py at N = 1.
+
 This file sorts first among the GPU tests so the rank processes start before this test
 process has touched the GPU (they are children started with subprocess, never an exec
 of this process)."""
@@ -40,6 +45,43 @@ def _run_ranks(world, scene, W, H, spp, out, block=1):
             p.kill()
             rcs.append(-9)
     return rcs
+
+
+def _bench(tmp_path, world, tag, extra=()):
+    """bench.py as child processes (N > 1: torch.distributed.run, one child per rank), a
+    small random-scene workload; returns (JSON line of rank 0, frame, PPM bytes)."""
+    frame, ppm = str(tmp_path / f"{tag}.npy"), str(tmp_path / f"{tag}.ppm")
+    args = ["bench.py", "--gpus", str(world), "--device", "0", "--scene", "0", "--width", "160", "--height", "90",
+            "--spp", "8", "--depth", "50", "--steps", "2", "--warmup", "1", "--no-cpu-baseline", "--no-count",
+            "--frame-npy", frame, "--ppm", ppm, *extra]
+    if world > 1:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+               "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), *args, "--dist-backend", "gloo"]
+    else:
+        cmd = [sys.executable, *args]
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR",
+                                                               "MASTER_PORT")}
+    p = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=600)
+    assert p.returncode == 0, (world, p.returncode, p.stderr[-3000:])
+    import json
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:]   # rank 0 alone prints the JSON line
+    return json.loads(lines[0]), np.load(frame), open(ppm, "rb").read()
+
+
+@pytest.mark.timeout(1300)
+def test_bench_py_n2_branch_equals_n1(tmp_path):
+    """bench.py --gpus 2 (two ranks on device 0, gloo gather of the interleaved shards) writes
+    the N = 1 frame bit for bit, and its JSON line reports n_gpus 2 (runs before this test
+    process touches the GPU: every GPU user here is a child process)."""
+    j2, f2, p2 = _bench(tmp_path, 2, "n2")
+    j1, f1, p1 = _bench(tmp_path, 1, "n1")
+    assert j2["n_gpus"] == 2 and j1["n_gpus"] == 1
+    assert j2["steps"] == 2 and j2["value"] > 0 and j2["ms_per_step"] > 0
+    assert "gloo" in j2["config"]["parallelism"]
+    assert f2.shape == f1.shape == (90, 160, 3)
+    assert np.array_equal(f2, f1)
+    assert p2 == p1
 
 
 @pytest.mark.timeout(900)

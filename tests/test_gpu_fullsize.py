@@ -1,6 +1,10 @@
 """GPU checks at BASELINE.json's full frame sizes, through properties that do not need
 the oracle to render the whole frame:
 
+- every BASELINE config against the oracle at its FULL sample count and depth (VERDICT r02
+  item 2): C1's whole 1200x800x10 frame, C2 500 spp and C3 1000 spp on two rows, C4 1000 spp
+  on one row, C5 4096 spp on one 4096-pixel row of the 4096x4096 frame in many buffer
+  batches (both schedules), so the highest sample indices and the depth-50 tails are checked;
 - every BASELINE config against the oracle on a bounded row subset at its own geometry
   and depth: C1 (1200x800, 10 spp, depth 8), C2 (1200x800, depth 50, 64 spp), C3 (Cornell
   800x800, 64 spp), C4 (final scene 1920x1080, 48 spp) and C5 (4096x4096: pixel keys up to
@@ -53,6 +57,62 @@ def test_baseline_configs_against_oracle(rt, renderer, cfg, scene_id, W, H, spp,
     ref = ob.render(scene_id, W, H, spp, depth, row_begin=row_begin, row_stride=stride, threads=16)
     assert img.shape == (len(range(row_begin, H, stride)), W, 3)
     _parity(img, ref, cfg)
+
+
+# BASELINE.json configs at their FULL spp and depth: rows chosen so the
+# oracle (16 threads, reference-faithful linear scans) finishes in seconds
+FULL = {   # cfg: scene, W, H, spp, depth, row_begin, row_stride
+    "C1": (0, 1200, 800, 10, 8, 0, 1),          # the whole frame, 9.6 M samples
+    "C2": (0, 1200, 800, 500, 50, 330, 235),    # rows 330, 565: 1.2 M samples
+    "C3": (5, 800, 800, 1000, 50, 200, 320),    # rows 200, 520: 1.6 M samples
+    "C4": (7, 1920, 1080, 1000, 50, 540, 1080),  # row 540: 1.9 M samples
+}
+
+
+@pytest.mark.parametrize("cfg", sorted(FULL))
+@pytest.mark.timeout(300)
+def test_baseline_configs_full_spp_against_oracle(rt, renderer, cfg):
+    scene_id, W, H, spp, depth, row_begin, stride = FULL[cfg]
+    img, st = rt.render_scene(scene_id, W, H, spp, depth, row_begin=row_begin, row_stride=stride,
+                              out_format=rt.RT_OUT_F64, renderer=renderer)
+    assert st.samples == img.shape[0] * W * spp
+    ref = ob.render(scene_id, W, H, spp, depth, row_begin=row_begin, row_stride=stride, threads=16)
+    assert img.shape == ref.shape == (len(range(row_begin, H, stride)), W, 3)
+    _parity(img, ref, cfg + " full spp")
+
+
+_C5_REF = {}
+
+
+@pytest.mark.parametrize("sched", ["POOL", "ITEMS"])
+@pytest.mark.timeout(300)
+def test_c5_full_spp_row_against_oracle(rt, sched):
+    """C5 at its full 4096 spp and depth 50 on row 2100 of the 4096x4096 frame (16.8 M
+    samples; pixel keys ~8.6 M), under a 16 MB trace-output bound: the per-sample pool runs
+    in ~26 batches whose chunk sums are carried across batches (samples up to 4095), the item
+    pool in 2."""
+    import os
+    W = H = 4096
+    spp, rows = 4096, dict(row_begin=2100, row_stride=4096)
+    os.environ["RT_SAMPLE_BUF_MB"] = "16"
+    try:
+        r = rt.Renderer(0)
+    finally:
+        os.environ.pop("RT_SAMPLE_BUF_MB")
+    try:
+        r.set_schedule(getattr(rt, "RT_SCHED_" + sched))
+        world = rt.World(1).build_scene(0)
+        cam, bg = rt.scene_camera(0, W, H)
+        r.upload(world)
+        img = r.render(cam, rt.Renderer.params(W, H, spp, 50, bg, 1, out_format=rt.RT_OUT_F64, **rows))
+        st = r.stats()
+        assert st.n_batches >= (20 if sched == "POOL" else 2), st.n_batches
+    finally:
+        r.close()
+    if "ref" not in _C5_REF:
+        _C5_REF["ref"] = ob.render(0, W, H, spp, 50, threads=16, **rows)
+    assert img.shape == (1, W, 3)
+    _parity(img, _C5_REF["ref"], f"C5 full spp ({sched})")
 
 
 @pytest.mark.parametrize("sched", ["POOL", "ITEMS"])
