@@ -209,6 +209,12 @@ typedef struct rt_stats {
     int32_t waves_per_simd;      /* resident waves per SIMD of the last trace kernel (occupancy) */
 } rt_stats;
 int rt_last_stats(rt_ctx* ctx, rt_stats* out);
+/* Diagnostic: the raw count_work counters of the last render (n entries; returns how many
+ * exist). 0-14 as in rt_stats; wave-cycles (s_memtime) per phase of the pool kernels: 3 ray
+ * generation, 4 trace, 5 shading, 8 node loops, 9 leaf tests (both of the top-level walk),
+ * 15 ray set-up, 16 walk prologue (pre-leaf test), 17 hit record, 18 media and 19 instances
+ * (inside the leaf tests), 20 refill, 21 kernel total (summed over waves). */
+int rt_last_counters(rt_ctx* ctx, uint64_t* out, int n);
 
 /* ---- progressive / resumable accumulation ------------------------------------ */
 /* A device f64 running sum per pixel of one row shard. Batches render consecutive sample

@@ -55,7 +55,7 @@ typedef struct rt_instance {
     int32_t n_ops;
     int32_t child_kind;      /* RT_CHILD_* */
     int32_t child;           /* prim index, or BVH root reference */
-    int32_t pad;
+    int32_t pad;             /* reserved (0); the device copy keeps a BLAS's first leaf slot here */
     int32_t op_kind[4];
     double op[4][3];         /* translate: offset xyz; rotate_y: sin cos 0 */
 } rt_instance; /* 128 B */

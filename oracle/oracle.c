@@ -21,7 +21,7 @@
  *     Camera::new, sin/cos in new_rotate_y) uses the platform libm, as Rust does.
  *   - Image size: width and height are explicit and the camera aspect is
  *     width/height (main.rs:467 computes height = width*aspect).
- *   - Work split: threads take interleaved rows (or the reference's sample split)
+ *   - Work split: threads take pixels round-robin (or the reference's sample split)
  *     and every pixel always receives exactly spp samples (main.rs:516 truncates).
  */
 #define _GNU_SOURCE
@@ -1145,9 +1145,11 @@ static void* worker(void* arg)
     tl_rng = &rng;
     RenderCtx ctx = {job->world, job->background, p->max_depth, 0};
     for (int k = 0; k < job->n_rows; ++k) {
-        if (p->split == ORC_SPLIT_ROWS && k % job->nthreads != job->tid) continue;
         int y = p->row_begin + k * p->row_stride;
         for (int x = 0; x < p->width; ++x) {
+            /* the row split deals pixels round-robin (a pixel's sum does not depend on the
+               thread that computes it), so a render of a few rows still uses every thread */
+            if (p->split == ORC_SPLIT_ROWS && ((size_t)k * p->width + x) % job->nthreads != (size_t)job->tid) continue;
             V3 acc = v3(0, 0, 0);
             render_pixel(job, &ctx, &rng, x, y, job->s_begin, job->s_end, &acc);
             double* o = job->out + ((size_t)k * p->width + x) * 3;

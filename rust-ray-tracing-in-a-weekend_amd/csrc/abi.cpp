@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <functional>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -60,7 +61,7 @@ struct rt_world {
     rtw::World w;
 };
 
-constexpr int kCounters = 16;  // count_work counters (trace_kernel.hip: trace_chunks epilogue)
+constexpr int kCounters = 24;  // count_work counters (trace_device.hpp: the trace kernels' epilogues; rt_last_counters)
 
 struct rt_ctx {
     int device = 0;
@@ -91,6 +92,7 @@ struct rt_ctx {
     int n_materials = 0, n_textures = 0;
     int block_chunks = 0;               // RT_BLOCK_CHUNKS: chunks per item-pool work block (0: auto)
     int block_samples = 0;              // RT_BLOCK_SAMPLES: samples per per-sample-pool work block (0: auto)
+    unsigned long long raw_counters[kCounters] = {};   // the last count_work render's counters (rt_last_counters)
     uint32_t extra_features = 0;        // RT_EXTRA_FEATURES: a larger kernel variant than the scene needs (tests)
     double pad_extent = 0.0;
     int opt_slab32 = 1;                 // rt_ctx_set_variant / RT_SLAB32
@@ -684,12 +686,83 @@ int rt_ctx_upload_soa(rt_ctx* c, const rt_scene_soa* s)
     }
     std::vector<rt_prim> leaf_prims((size_t)s->n_prim_refs);
     for (int j = 0; j < s->n_prim_refs; ++j) leaf_prims[(size_t)j] = prims[(size_t)s->prim_refs[j]];
+    // Device copies of the nodes and instances in which every instance BLAS's leaf codes count
+    // slots from that BLAS's first leaf slot (kept in the device rt_instance.pad): the codes of
+    // both walks then stay small enough for 16-bit stack entries (Stack16: the final scene's
+    // 1000-sphere BLAS has slots 410..1409, relative 0..999). Only when every BLAS is disjoint
+    // from the TLAS and from the other BLASes (or shares a BLAS with its base); otherwise the
+    // codes stay absolute and the scene takes the 32-bit stack (stack16_ok 0).
+    std::vector<rt_bvh_node> nodes_dev(s->nodes, s->nodes + s->n_nodes);
+    std::vector<rt_instance> inst_dev(s->instances, s->instances + s->n_instances);
+    for (rt_instance& in : inst_dev) in.pad = 0;
+    int max_first = 0;            // the largest leaf-code first slot either walk pushes
+    bool rel_ok = true;
+    {
+        auto leaf_first = [](int ref) { return (~ref) >> 5; };
+        std::vector<int> owner((size_t)s->n_nodes, -1);   // -2: TLAS; else the BLAS base
+        std::vector<int> todo;
+        if (s->tlas_root >= 0) todo.push_back(s->tlas_root);
+        else max_first = std::max(max_first, leaf_first(s->tlas_root));
+        while (!todo.empty()) {   // validate_soa checked refs and acyclicity
+            const int i = todo.back();
+            todo.pop_back();
+            if (owner[(size_t)i] == -2) continue;
+            owner[(size_t)i] = -2;
+            for (int ch : s->nodes[i].child) {
+                if (ch >= 0) todo.push_back(ch);
+                else max_first = std::max(max_first, leaf_first(ch));
+            }
+        }
+        for (size_t ii = 0; ii < inst_dev.size() && rel_ok; ++ii) {
+            rt_instance& in = inst_dev[ii];
+            if (in.child_kind != RT_CHILD_BVH) continue;
+            std::vector<int> blas;   // the BLAS's nodes, and its smallest leaf slot
+            int base = 1 << 30;
+            if (in.child < 0) base = leaf_first(in.child);
+            else todo.push_back(in.child);
+            std::vector<uint8_t> seen((size_t)s->n_nodes, 0);
+            while (!todo.empty()) {
+                const int i = todo.back();
+                todo.pop_back();
+                if (seen[(size_t)i]) continue;
+                seen[(size_t)i] = 1;
+                blas.push_back(i);
+                for (int ch : s->nodes[i].child) {
+                    if (ch >= 0) todo.push_back(ch);
+                    else base = std::min(base, leaf_first(ch));
+                }
+            }
+            for (int i : blas)
+                if (owner[(size_t)i] == -2 || (owner[(size_t)i] >= 0 && owner[(size_t)i] != base)) rel_ok = false;
+            if (!rel_ok) break;
+            auto rel = [&](int ref) {
+                const int code = ~ref;
+                const int first = (code >> 5) - base;
+                max_first = std::max(max_first, first);
+                return ~((first << 5) | (code & 31));
+            };
+            for (int i : blas) {
+                if (owner[(size_t)i] == base) continue;   // shared with an instance already rewritten
+                owner[(size_t)i] = base;
+                for (int& ch : nodes_dev[(size_t)i].child)
+                    if (ch < 0) ch = rel(ch);
+            }
+            if (in.child < 0) in.child = rel(in.child);
+            in.pad = base;
+        }
+        if (!rel_ok) {   // absolute codes everywhere
+            nodes_dev.assign(s->nodes, s->nodes + s->n_nodes);
+            inst_dev.assign(s->instances, s->instances + s->n_instances);
+            for (rt_instance& in : inst_dev) in.pad = 0;
+            max_first = s->n_prim_refs;
+        }
+    }
     size_t off[10], bytes[10] = {
         (size_t)s->n_nodes * sizeof(rt_bvh_node), (size_t)s->n_prim_refs * 4, (size_t)s->n_prims * sizeof(rt_prim),
         (size_t)s->n_instances * sizeof(rt_instance), (size_t)s->n_materials * sizeof(rt_material),
         (size_t)s->n_textures * sizeof(rt_texture), (size_t)s->n_perlin * 768 * 8, (size_t)s->n_perlin * 768 * 4,
         (size_t)s->image_bytes, (size_t)s->n_prim_refs * sizeof(rt_prim)};
-    const void* src[10] = {s->nodes, s->prim_refs, prims.data(), s->instances, s->materials, s->textures,
+    const void* src[10] = {nodes_dev.data(), s->prim_refs, prims.data(), inst_dev.data(), s->materials, s->textures,
                            s->perlin_ranvec, s->perlin_perm, s->image_data, leaf_prims.data()};
     size_t total = 0;
     for (int i = 0; i < 10; ++i) {
@@ -723,9 +796,10 @@ int rt_ctx_upload_soa(rt_ctx* c, const rt_scene_soa* s)
     c->S.tlas_root = s->tlas_root;
     c->S.pre_leaf = 0;
     if (c->opt_hoist) hoist_root_leaf(s, c->S);
-    // Stack16 (trace_device.hpp): node records at LDS addresses < 32 KB (80 B each) and leaf
-    // codes ((first slot << 5) | count, stored complemented) above the -32768 sentinel
-    c->S.stack16_ok = (n_tlas_nodes * (int64_t)80 <= 32767 - 80 && s->n_prim_refs <= 1023) ? 1 : 0;
+    // Stack16 (trace_device.hpp): node records at LDS addresses < 32 KB (80 B each), BLAS node
+    // indices < 32768, and leaf codes ((first slot << 5) | count, stored complemented; BLAS slots
+    // relative, above) above the -32768 sentinel
+    c->S.stack16_ok = (n_tlas_nodes * (int64_t)80 <= 32767 - 80 && max_first <= 1023 && s->n_nodes <= 32767) ? 1 : 0;
     c->S.n_lds_nodes = 0;
     // traversal stack: TLAS walk, then a nested BLAS walk (instances) above it, sized from the
     // depths validate_soa measured (<= 32 each), each walk's bottom entry holding its RT_DONE
@@ -787,6 +861,53 @@ int rt_ctx_upload_soa(rt_ctx* c, const rt_scene_soa* s)
         if (s->textures[i].kind == RT_TEX_IMAGE) feat |= rtk::FEAT_IMAGE;
     }
     if (general_shutter) feat |= rtk::FEAT_SHUTTER;
+    // FEAT_NEST_MOVING: a sphere that really moves (nonzero velocity, or a shutter other than
+    // [0, 1], whose centre may not be c0) under an instance or inside a medium boundary; without
+    // it the kernel tests spheres there as static (FEAT_STATIC: c0, no velocity loads)
+    {
+        auto moving = [&](int i) {
+            const rt_prim& q = prims[(size_t)i];
+            return q.kind == RT_PRIM_MOVING_SPHERE && (!q.a || q.p[5] != 0.0 || q.p[6] != 0.0 || q.p[7] != 0.0);
+        };
+        std::vector<uint8_t> seen((size_t)s->n_nodes, 0);
+        auto bvh_moving = [&](int root) {   // validate_soa checked refs and acyclicity
+            std::vector<int> todo{root};
+            while (!todo.empty()) {
+                const int ref = todo.back();
+                todo.pop_back();
+                if (ref >= 0) {
+                    if (seen[(size_t)ref]) continue;
+                    seen[(size_t)ref] = 1;
+                    todo.push_back(s->nodes[ref].child[0]);
+                    todo.push_back(s->nodes[ref].child[1]);
+                    continue;
+                }
+                const int code = ~ref;
+                for (int j = code >> 5; j < (code >> 5) + (code & 31); ++j)
+                    if (moving(s->prim_refs[j])) return true;
+            }
+            return false;
+        };
+        // an instance's child prim (a medium: its boundary, which holds no medium) or BLAS
+        std::function<bool(int)> inst_moving = [&](int ii) {
+            const rt_instance& in = s->instances[ii];
+            if (in.child_kind == RT_CHILD_BVH) return bvh_moving(in.child);
+            const rt_prim& cp = s->prims[in.child];
+            if (cp.kind == RT_PRIM_MEDIUM) {
+                const rt_prim& b = s->prims[cp.a];
+                return b.kind == RT_PRIM_INSTANCE ? inst_moving(b.a) : moving(cp.a);
+            }
+            return moving(in.child);
+        };
+        bool nest = false;
+        for (int i = 0; i < s->n_instances && !nest; ++i) nest = inst_moving(i);
+        for (int i = 0; i < s->n_prims && !nest; ++i) {
+            if (s->prims[i].kind != RT_PRIM_MEDIUM) continue;
+            const int b = s->prims[i].a;
+            nest = s->prims[b].kind == RT_PRIM_INSTANCE ? inst_moving(s->prims[b].a) : moving(b);
+        }
+        if (nest) feat |= rtk::FEAT_NEST_MOVING;
+    }
     c->features = feat;
     c->S.has_spheres = 0;
     for (int i = 0; i < s->n_prims; ++i)
@@ -1330,6 +1451,7 @@ int rt_last_stats(rt_ctx* c, rt_stats* out)
             c->stats.camera_steps = h[12];
             c->stats.shade_lanes = h[13];
             c->stats.shade_steps = h[14];
+            for (int i = 0; i < kCounters; ++i) c->raw_counters[i] = h[i];
         } else {
             c->stats.casts = c->stats.node_visits = c->stats.prim_tests = 0;
             c->stats.cycles_camera = c->stats.cycles_trace = c->stats.cycles_shade = 0;
@@ -1337,11 +1459,22 @@ int rt_last_stats(rt_ctx* c, rt_stats* out)
             c->stats.cycles_nodes = c->stats.cycles_leaves = 0;
             c->stats.wave_leaf_steps = c->stats.camera_lanes = c->stats.camera_steps = 0;
             c->stats.shade_lanes = c->stats.shade_steps = 0;
+            for (int i = 0; i < kCounters; ++i) c->raw_counters[i] = 0;
         }
         c->pending_stats = false;
     }
     *out = c->stats;
     return RT_OK;
+}
+
+int rt_last_counters(rt_ctx* c, uint64_t* out, int n)
+{
+    if (!c || !out || n < 0) return fail(RT_ERR_INVALID, "null argument");
+    rt_stats st;
+    const int rc = rt_last_stats(c, &st);   // resolves a pending render's counters
+    if (rc) return rc;
+    for (int i = 0; i < n; ++i) out[i] = i < kCounters ? (uint64_t)c->raw_counters[i] : 0;
+    return std::min(n, kCounters);
 }
 
 // ---- output ---------------------------------------------------------------------------------

@@ -36,6 +36,7 @@ namespace rtk {
 
 // R: the path's arithmetic type — double (the reference's f64, math.rs:13-17; bit-exact
 // against the oracle) or float (the f32 fast mode; statistically equal).
+typedef float f2v __attribute__((ext_vector_type(2)));
 template <class R>
 struct RayT {
     R ox, oy, oz;
@@ -45,8 +46,10 @@ struct RayT {
     R ya;                     // f64: 1 / a correctly rounded (NaN outside [2^-900, 2^900]: see div_rcp)
     R ix, iy, iz;             // 1 / direction (f64 slab tests only)
     R yx, yy, yz;             // f64, scenes with rects: RN(1 / direction) for div_rcp (NaN outside its range)
-    float fix, fiy, fiz;      // f32 1 / direction (f32 slab tests only)
-    float fox, foy, foz;      // -origin * (1 / direction) in f32
+    // f32 slab terms per axis (f32 slab tests only): (1 / direction, -origin * (1 / direction)),
+    // a register pair each, so one v_pk_fma_f32 takes both for the two children of a node
+    // (op_sel: the pair's low half as the factor, its high half as the addend, in both lanes)
+    f2v sx, sy, sz;
     uint32_t onx, ony, onz;   // byte offsets in a node of child 0's near planes (by direction sign)
 };
 
@@ -81,7 +84,20 @@ struct Count {
     uint32_t cam_lanes, cam_steps;    // lanes starting a sample / iterations in which any did
     uint32_t shade_lanes, shade_steps;
     uint64_t t_nodes, t_leaves;       // wave-cycles in node-visit loops / leaf tests (same in every lane)
+    // pool kernels, finer phases (wave-cycles; each added by the first active lane of the region
+    // it times, so summed over lanes they are wave totals): ray set-up, the walk's prologue
+    // (pre-leaf test, bounds), the hit record, and inside the leaf tests the media and instances
+    uint64_t t_setup, t_pre, t_rec, t_med, t_inst, t_refill;
 };
+// COUNT phase stamps: tp is the lane's last stamp; the first active lane adds the interval
+#define RT_STAMP(acc, tp)                                                   \
+    do {                                                                    \
+        if (C::COUNT) {                                                     \
+            const uint64_t t_ = __builtin_amdgcn_s_memtime();               \
+            if (first_active_lane()) (acc) += t_ - (tp);                    \
+            (tp) = t_;                                                      \
+        }                                                                   \
+    } while (0)
 // COUNT only: true in exactly one active lane of the wave
 __device__ __forceinline__ bool first_active_lane()
 {
@@ -98,7 +114,7 @@ __device__ __forceinline__ bool first_active_lane()
 // machine with ballot-gated shading both measured slower.
 //   NALL   every TLAS node is in LDS (no per-node LDS/global choice)
 #ifndef RT_RECT_RCP
-#define RT_RECT_RCP 0   // rect / box tests divide through precomputed reciprocals (measured: Cornell 58.1 vs 56.5 ms without; rejected)
+#define RT_RECT_RCP 1   // rect / box tests divide through the ray's reciprocals (rects + instances variant only): round 3, without machine LICM, Cornell 800x800x200 45.76 vs 47.04 ms (r03d_ab_c3.log); round 2 measured it slower (58.1 vs 56.5) when its registers spilled
 #endif
 #ifndef RT_BOX_PRETEST
 #define RT_BOX_PRETEST 0   // slab pre-test of a Box before its 6 rect tests (measured slower: Cornell 58.5 vs 56.6 ms, final 83.3 vs 82.6, smoke 41.9 vs 39.9 — a culled lane saves no wave instructions unless the whole wave is culled)
@@ -124,10 +140,19 @@ __device__ __forceinline__ bool first_active_lane()
 #define RT_MED3 1
 #endif
 #ifndef RT_PK_SLAB
-#define RT_PK_SLAB 0   // packed-f32 (v_pk_fma_f32) plane products of the two children (LDS node pairs)
+#define RT_PK_SLAB 0   // packed-f32 (v_pk_fma_f32, op_sel) plane products of the two children: v_pk_fma_f32 issues in 4.1 cycles, two v_fma_f32 in 2 x 2.3 (profiles/r03b_calib.log); C2 76.34 vs 73.93 ms (r03b_ab_c2.log): rejected
 #endif
 #ifndef RT_TRACE_LOOP
 #define RT_TRACE_LOOP 1   // 0 if-if, 1 while-while, 2 while-while with speculative node visits
+#endif
+#ifndef RT_PERLIN_ROLLED
+#define RT_PERLIN_ROLLED 0   // rolled: C4 143.3 vs 136.9 ms unrolled (r03b_ab_c4.log); no spills either way without machine LICM
+#endif
+#ifndef RT_KILL_H
+// pool schedules: the hit record carried across the loop edge (RT_MERGED_DRAWS) is marked dead
+// before the next trace (trace_world writes only the fields its primitive kind has, so the
+// compiler otherwise keeps the whole old record live through the walk)
+#define RT_KILL_H 1
 #endif
 //   F32    the f32 fast mode (Real = float): statistically, not bitwise, equal
 template <uint32_t F_, bool S32_, bool LDS_, bool NALL_, bool COUNT_, bool F32_ = false>
@@ -149,12 +174,20 @@ template <class C, uint32_t DROP>
 struct CfgDrop : C {
     static constexpr uint32_t F = C::F & ~DROP;
 };
+// Spheres reached only through an instance or a medium boundary are static unless the scene
+// says otherwise (FEAT_NEST_MOVING): their test then loads no velocity (FEAT_STATIC; the final
+// scene's instanced cluster and its fog / glass-medium boundaries), which shortens the nested
+// walk's live ranges; c0 + 0 * s is c0 bit for bit, so the result is the same.
+template <class C, uint32_t DROP>
+struct CfgDropStatic : C {
+    static constexpr uint32_t F = (C::F & ~DROP) | ((C::F & FEAT_NEST_MOVING) ? 0u : (uint32_t)FEAT_STATIC);
+};
 template <class C>
-using InstC = CfgDrop<C, (C::F & FEAT_INST_RECT) ? 0u : (uint32_t)FEAT_RECT>;
+using InstC = CfgDropStatic<C, (C::F & FEAT_INST_RECT) ? 0u : (uint32_t)FEAT_RECT>;
 template <class C>
-using BoundC = CfgDrop<C, FEAT_INST_MEDIUM | ((C::F & FEAT_MEDIUM_INST) ? 0u : (uint32_t)(FEAT_RECT | FEAT_INST))>;
+using BoundC = CfgDropStatic<C, FEAT_INST_MEDIUM | ((C::F & FEAT_MEDIUM_INST) ? 0u : (uint32_t)(FEAT_RECT | FEAT_INST))>;
 template <class C>
-using InstMedC = CfgDrop<C, FEAT_INST_MEDIUM>;   // a medium under an instance: no medium below it
+using InstMedC = CfgDropStatic<C, FEAT_INST_MEDIUM>;   // a medium under an instance: no medium below it
 
 // Traversal stack. LDS: a lane-interleaved dynamic LDS array [entry][256 threads]
 // (consecutive lanes hit consecutive banks) sized per scene by the host (TLAS depth +
@@ -178,12 +211,22 @@ struct Stack<false> {
 // VGPRs, min_waves) — C2 1200x800x100 16.48 -> 15.40 ms, same bits (profiles/r02ao_*)
 #define RT_STACK16 1
 #endif
+#ifndef RT_STACK16_FINAL
+#define RT_STACK16_FINAL 1
+#endif
 struct Stack16 {   // node records at LDS addresses < 32 KB, leaf codes > -32768 (SceneDev.stack16_ok)
     short* base;
     __device__ __forceinline__ short& operator[](int i) const { return base[i * 256]; }
 };
 template <class C>
-constexpr bool Stack16Cfg() { return RT_STACK16 && C::LDS && C::NALL && C::S32 && C::F == FEAT_SET_SPHERES && !C::F32; }
+constexpr bool Stack16Cfg()
+{
+    return RT_STACK16 && C::LDS && C::NALL && C::S32 && (C::F == FEAT_SET_SPHERES || (RT_STACK16_FINAL && C::F == FEAT_SET_FINAL)) &&
+           !C::F32;
+}
+// (final-scene variant: 25 entries x 256 lanes x 2 B instead of 4 take its LDS per block from
+// 45.8 to 33.3 KB, so 4 blocks (4 waves per SIMD) share a CU instead of 3; the BLAS walk's leaf
+// codes are relative to the BLAS's first slot, rt_instance.pad on the device, abi.cpp)
 template <class C>
 using StackT = typename std::conditional<Stack16Cfg<C>(), Stack16, Stack<C::LDS>>::type;
 extern __shared__ int rt_lds[];  // [cached TLAS nodes] [stack entries x 256 lanes] [materials, textures]
@@ -257,10 +300,13 @@ constexpr bool RectRcp()
 // image textures (final scene: 80.0 -> 78.6 ms), whose 3 waves per SIMD the extra live values do
 // not change; the 4-wave Cornell variant spills them (49.6 -> 51.6 ms) and Cornell smoke's
 // media variant loses too (39.1 -> 39.5; profiles/r02_ab_boxrcp_*.log)
+#ifndef RT_BOX_RCP_ALL
+#define RT_BOX_RCP_ALL 0
+#endif
 template <class C>
 constexpr bool BoxRcp()
 {
-    return RT_BOX_RCP && !C::F32 && (C::F & (FEAT_NOISE | FEAT_IMAGE)) != 0;
+    return RT_BOX_RCP && !C::F32 && (RT_BOX_RCP_ALL || (C::F & (FEAT_NOISE | FEAT_IMAGE)) != 0);
 }
 
 // spheres: the scene has spheres (wave-uniform); otherwise no root division needs 1/a
@@ -275,17 +321,17 @@ __device__ __forceinline__ void finish_ray(RayT<typename C::Real>& r, bool spher
         r.yz = rcp_for_div(r.dz);
     }
     if constexpr (C::S32) {
-        r.fix = f32_inv_dir(r.dx);
-        r.fiy = f32_inv_dir(r.dy);
-        r.fiz = f32_inv_dir(r.dz);
-        r.fox = -(float)r.ox * r.fix;
-        r.foy = -(float)r.oy * r.fiy;
-        r.foz = -(float)r.oz * r.fiz;
+        r.sx.x = f32_inv_dir(r.dx);
+        r.sy.x = f32_inv_dir(r.dy);
+        r.sz.x = f32_inv_dir(r.dz);
+        r.sx.y = -(float)r.ox * r.sx.x;
+        r.sy.y = -(float)r.oy * r.sy.x;
+        r.sz.y = -(float)r.oz * r.sz.x;
         // the LDS node (LdsNode): per axis [lo0 lo1 hi0 hi1 lo0 lo1] at bytes 0/24/48; the
         // near planes of both children at +0 (direction >= 0) or +8, the far ones 8 bytes on
-        r.onx = r.fix >= 0.0f ? 0u : 8u;
-        r.ony = r.fiy >= 0.0f ? 24u : 32u;
-        r.onz = r.fiz >= 0.0f ? 48u : 56u;
+        r.onx = r.sx.x >= 0.0f ? 0u : 8u;
+        r.ony = r.sy.x >= 0.0f ? 24u : 32u;
+        r.onz = r.sz.x >= 0.0f ? 48u : 56u;
     } else {
         r.ix = (typename C::Real)1 / r.dx;
         r.iy = (typename C::Real)1 / r.dy;
@@ -457,9 +503,9 @@ template <class RayType>
 __device__ __forceinline__ bool slab32(const float* lo, const float* hi, const RayType& r, float t_min, float t_max,
                                        float& t_near)
 {
-    const float x0 = __builtin_fmaf(lo[0], r.fix, r.fox), x1 = __builtin_fmaf(hi[0], r.fix, r.fox);
-    const float y0 = __builtin_fmaf(lo[1], r.fiy, r.foy), y1 = __builtin_fmaf(hi[1], r.fiy, r.foy);
-    const float z0 = __builtin_fmaf(lo[2], r.fiz, r.foz), z1 = __builtin_fmaf(hi[2], r.fiz, r.foz);
+    const float x0 = __builtin_fmaf(lo[0], r.sx.x, r.sx.y), x1 = __builtin_fmaf(hi[0], r.sx.x, r.sx.y);
+    const float y0 = __builtin_fmaf(lo[1], r.sy.x, r.sy.y), y1 = __builtin_fmaf(hi[1], r.sy.x, r.sy.y);
+    const float z0 = __builtin_fmaf(lo[2], r.sz.x, r.sz.y), z1 = __builtin_fmaf(hi[2], r.sz.x, r.sz.y);
     const float tn = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fmaxf(fminf(z0, z1), t_min));
     const float tf = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fminf(fmaxf(z0, z1), t_max));
     t_near = tn;
@@ -568,8 +614,14 @@ __device__ __forceinline__ bool box_t(const rt_prim& p, const RayT<R>& r, R t_mi
 // a wave whose lanes hold both kinds runs one test and loads no kind.
 template <class R>
 __device__ __forceinline__ void sphere_center(const rt_prim& p, const RayT<R>& r, bool general, double& cx, double& cy,
-                                              double& cz)
+                                              double& cz, bool is_static = false)
 {
+    if (is_static) {   // FEAT_STATIC: a Sphere, whose c0 + 0 * s is c0 bit for bit
+        cx = p.p[0];
+        cy = p.p[1];
+        cz = p.p[2];
+        return;
+    }
     double s = (double)r.time;
     // general: the variant has FEAT_SHUTTER (no reference scene does: their moving spheres
     // all have the [0, 1] shutter); without it the flag is not loaded at all
@@ -587,7 +639,7 @@ __device__ __forceinline__ bool simple_t(const rt_prim& p, const RayT<R>& r, R t
     if (C::COUNT) cnt.prims++;
     if (!(C::F & FEAT_RECT) || p.kind <= RT_PRIM_MOVING_SPHERE) {
         double cx, cy, cz;
-        sphere_center(p, r, gs, cx, cy, cz);
+        sphere_center(p, r, gs, cx, cy, cz, (C::F & FEAT_STATIC) != 0);
         return sphere_t(cx, cy, cz, p.p[3], r, t_min, t_max, t);
     } else {
         const R q0 = (R)p.p[0], q1 = (R)p.p[1], q2 = (R)p.p[2], q3 = (R)p.p[3], q4 = (R)p.p[4];
@@ -618,7 +670,7 @@ __device__ __forceinline__ void simple_finish(const rt_prim& p, const RayT<R>& r
         }
     }
     double cx, cy, cz;
-    sphere_center(p, r, gs, cx, cy, cz);
+    sphere_center(p, r, gs, cx, cy, cz, (C::F & FEAT_STATIC) != 0);
     sphere_finish<C>((R)cx, (R)cy, (R)cz, (R)p.p[4], r, t, p.mat, h);
 }
 
@@ -646,10 +698,11 @@ __device__ __forceinline__ Node load_node(const rt_bvh_node* base, int i)
     return n;
 }
 
-// The variants whose LDS node visits use packed-f32 plane products (v_pk_fma_f32: 6 instead of
-// 12 FMAs; the ray's broadcast pairs cost ~4 VGPRs, which the texture variants would spill)
+// The variants whose LDS node visits use packed-f32 plane products (v_pk_fma_f32 with op_sel:
+// 6 instead of 12 FMAs per visit, no extra registers; round 2's broadcast-pair form cost ~4
+// VGPRs and was rejected)
 template <class C>
-constexpr bool PkSlab() { return RT_PK_SLAB && (C::F & (FEAT_NOISE | FEAT_IMAGE)) == 0; }
+constexpr bool PkSlab() { return RT_PK_SLAB != 0; }
 
 // The TLAS node as staged in LDS by the variants whose whole TLAS is there and whose slab
 // tests are f32 (OctNodes): per axis both children's lower planes, upper planes and the lower
@@ -720,6 +773,10 @@ __device__ __forceinline__ bool traverse(const SceneDev& S, int root, const RayT
     float ninf = -__builtin_inff();
     if constexpr (OCT && RT_MED3) asm("s_mov_b32 %0, 0xff800000" : "=s"(ninf));
     const char* const lb = reinterpret_cast<const char*>(lds_nodes);
+    // t_min's f32 bound in a register set once per walk (an asm result: not rematerialized as a
+    // v_mov inside the node loop, which machine LICM no longer hoists)
+    float tmin_v = tmin_f;
+    if constexpr (OCT && PkSlab<C>()) asm("v_mov_b32 %0, %1" : "=v"(tmin_v) : "v"(tmin_f));
     if constexpr (OCT) cur = cur >= 0 ? (int)(lds_addr(lb) + (uint32_t)cur * (uint32_t)sizeof(LdsNode)) : cur;
     // one node visit: test both children, continue with the nearer, push the farther
     auto visit = [&](int node) -> int {
@@ -740,26 +797,38 @@ __device__ __forceinline__ bool traverse(const SceneDev& S, int root, const RayT
             const i2v ch = *lds_ptr<i2v>(nb + (uint32_t)offsetof(LdsNode, child));
             float tn[2], tf[2];
             if constexpr (PkSlab<C>()) {
-            // both children's plane of one axis as one v_pk_fma_f32 (the pair comes from one read)
-            const f2v ix = {r.fix, r.fix}, iy = {r.fiy, r.fiy}, iz = {r.fiz, r.fiz};
-            const f2v ox = {r.fox, r.fox}, oy = {r.foy, r.foy}, oz = {r.foz, r.foz};
-            const f2v nx = __builtin_elementwise_fma(npx, ix, ox), fx = __builtin_elementwise_fma(fpx, ix, ox);
-            const f2v ny = __builtin_elementwise_fma(npy, iy, oy), fy = __builtin_elementwise_fma(fpy, iy, oy);
-            const f2v nz = __builtin_elementwise_fma(npz, iz, oz), fz = __builtin_elementwise_fma(fpz, iz, oz);
+            // Both children's plane of one axis in one v_pk_fma_f32, the ray's (1/d, -o/d) pair of
+            // the axis read as factor / addend for both halves (op_sel): 6 instead of 12 FMAs per
+            // visit, no broadcast copies, the same single rounding as v_fma_f32. The reductions
+            // are raw v_max3 / v_max / v_med3 / v_min3 as well: through fmaxf the compiler would
+            // first quiet each asm result (v_max x, x), which FMA results never need (the
+            // products are finite: f32_inv_dir bounds 1/d).
+            f2v nx, ny, nz, fx, fy, fz;
+#define RT_PKFMA(d, a, b) asm("v_pk_fma_f32 %0, %1, %2, %2 op_sel:[0,0,1] op_sel_hi:[1,0,1]" : "=v"(d) : "v"(a), "v"(b))
+            RT_PKFMA(nx, npx, r.sx);
+            RT_PKFMA(ny, npy, r.sy);
+            RT_PKFMA(nz, npz, r.sz);
+            RT_PKFMA(fx, fpx, r.sx);
+            RT_PKFMA(fy, fpy, r.sy);
+            RT_PKFMA(fz, fpz, r.sz);
+#undef RT_PKFMA
 #pragma unroll
             for (int c = 0; c < 2; ++c) {
-                tn[c] = fmaxf(fmaxf(nx[c], ny[c]), fmaxf(nz[c], tmin_f));
-                tf[c] = fminf(fminf(fx[c], fy[c]), fminf(fz[c], tmax_f));
+                float a, b;
+                asm("v_max3_f32 %0, %1, %2, %3" : "=v"(a) : "v"(nx[c]), "v"(ny[c]), "v"(nz[c]));
+                asm("v_max_f32 %0, %1, %2" : "=v"(tn[c]) : "v"(a), "v"(tmin_v));
+                asm("v_med3_f32 %0, %1, %2, %3" : "=v"(b) : "v"(fz[c]), "v"(tmax_f), "s"(ninf));
+                asm("v_min3_f32 %0, %1, %2, %3" : "=v"(tf[c]) : "v"(fx[c]), "v"(fy[c]), "v"(b));
             }
             } else {
 #pragma unroll
             for (int c = 0; c < 2; ++c) {
-                const float nx = __builtin_fmaf(c ? npx.y : npx.x, r.fix, r.fox);
-                const float ny = __builtin_fmaf(c ? npy.y : npy.x, r.fiy, r.foy);
-                const float nz = __builtin_fmaf(c ? npz.y : npz.x, r.fiz, r.foz);
-                const float fx = __builtin_fmaf(c ? fpx.y : fpx.x, r.fix, r.fox);
-                const float fy = __builtin_fmaf(c ? fpy.y : fpy.x, r.fiy, r.foy);
-                const float fz = __builtin_fmaf(c ? fpz.y : fpz.x, r.fiz, r.foz);
+                const float nx = __builtin_fmaf(c ? npx.y : npx.x, r.sx.x, r.sx.y);
+                const float ny = __builtin_fmaf(c ? npy.y : npy.x, r.sy.x, r.sy.y);
+                const float nz = __builtin_fmaf(c ? npz.y : npz.x, r.sz.x, r.sz.y);
+                const float fx = __builtin_fmaf(c ? fpx.y : fpx.x, r.sx.x, r.sx.y);
+                const float fy = __builtin_fmaf(c ? fpy.y : fpy.x, r.sy.x, r.sy.y);
+                const float fz = __builtin_fmaf(c ? fpz.y : fpz.x, r.sz.x, r.sz.y);
                 tn[c] = fmaxf(fmaxf(nx, ny), fmaxf(nz, tmin_f));
                 // min(fz, t_max) as v_med3(fz, t_max, -inf): fminf would re-quiet the loop-carried
                 // t_max (a v_max_f32 t, t) at every visit; the plane products are never NaN.
@@ -825,16 +894,16 @@ __device__ __forceinline__ bool traverse(const SceneDev& S, int root, const RayT
     } else if constexpr (C::LOOP == 1) {
         uint64_t t0 = 0;
         while (cur != DONE) {
-            if (C::COUNT) t0 = __builtin_amdgcn_s_memtime();
+            if (C::COUNT && NL) t0 = __builtin_amdgcn_s_memtime();
             while (cur >= 0) {
                 if (C::COUNT && first_active_lane()) cnt.wave_nodes++;
                 cur = visit(cur);
             }
-            if (C::COUNT) { const uint64_t t = __builtin_amdgcn_s_memtime(); cnt.t_nodes += t - t0; t0 = t; }
+            if (NL) RT_STAMP(cnt.t_nodes, t0);   // the TLAS walk only: a nested walk is part of its leaf
             if (cur == DONE) break;
             do_leaf(cur);
-            if (C::COUNT) cnt.t_leaves += __builtin_amdgcn_s_memtime() - t0;
             cur = pop();
+            if (NL) RT_STAMP(cnt.t_leaves, t0);
         }
     } else {
         // Speculative while-while (Aila & Laine 2009, §4): a lane that reaches a leaf parks
@@ -928,13 +997,14 @@ __device__ bool instance_t(const SceneDev& S, const rt_instance& in, const RayT<
     // set the Cornell variants' register count, 157 vs 125 VGPRs: 3 vs 4 waves per SIMD)
     if constexpr ((C::F & FEAT_INST_BLAS) == 0) return false;
     HitRefT<R> inner;
+    const rt_prim* const blas_prims = S.leaf_prims + in.pad;   // the BLAS's leaf codes count from its first slot
     if (!traverse<C>(S, in.child, r, t_min, t_max, inner, stack, sp0, cnt,
                      [&](int slot, R tmax, HitRefT<R>& b) {
-                         return simple_t<InstC<C>>(S.leaf_prims[slot], r, t_min, tmax, b.t, b.side, cnt, (C::F & FEAT_SHUTTER) != 0);
+                         return simple_t<InstC<C>>(blas_prims[slot], r, t_min, tmax, b.t, b.side, cnt, (C::F & FEAT_SHUTTER) != 0);
                      }))
         return false;
     ref.t = inner.t;
-    ref.sub = inner.prim;
+    ref.sub = in.pad + inner.prim;   // absolute leaf slot (instance_finish)
     ref.side = inner.side;
     return true;
 }
@@ -1077,12 +1147,25 @@ __device__ bool trace_world(const SceneDev& S, const RayT<R>& r, HitT<R>& h, Sta
     auto leaf = [&](int slot, R tmax, HitRefT<R>& b) {
         const rt_prim& p = S.leaf_prims[slot];
         if constexpr ((C::F & FEAT_INST) != 0)
-            if (p.kind == RT_PRIM_INSTANCE)
-                return instance_t<C>(S, S.instances[p.a], r, t_min, tmax, b, stack, S.blas_base, key, cnt);
+            if (p.kind == RT_PRIM_INSTANCE) {
+                uint64_t ti = 0;
+                if (C::COUNT) ti = __builtin_amdgcn_s_memtime();
+                const bool hit = instance_t<C>(S, S.instances[p.a], r, t_min, tmax, b, stack, S.blas_base, key, cnt);
+                RT_STAMP(cnt.t_inst, ti);
+                return hit;
+            }
         if constexpr ((C::F & FEAT_MEDIUM) != 0)
-            if (p.kind == RT_PRIM_MEDIUM) return medium_t<C>(S, p, r, t_min, tmax, b.t, stack, S.blas_base, key, cnt);
+            if (p.kind == RT_PRIM_MEDIUM) {
+                uint64_t tm = 0;
+                if (C::COUNT) tm = __builtin_amdgcn_s_memtime();
+                const bool hit = medium_t<C>(S, p, r, t_min, tmax, b.t, stack, S.blas_base, key, cnt);
+                RT_STAMP(cnt.t_med, tm);
+                return hit;
+            }
         return simple_t<C>(p, r, t_min, tmax, b.t, b.side, cnt, (C::F & FEAT_SHUTTER) != 0);
     };
+    uint64_t tp = 0;
+    if (C::COUNT) tp = __builtin_amdgcn_s_memtime();
     bool hit;
     if constexpr (PreLeaf<C>()) {
         R t_max = (R)RT_INF;
@@ -1109,25 +1192,30 @@ __device__ bool trace_world(const SceneDev& S, const RayT<R>& r, HitT<R>& h, Sta
                 }
             }
         }
+        RT_STAMP(cnt.t_pre, tp);
         hit |= traverse<C, true>(S, root, r, t_min, t_max, best, stack, 0, cnt, leaf);
     } else {
+        RT_STAMP(cnt.t_pre, tp);
         hit = traverse<C, true>(S, S.tlas_root, r, t_min, (R)RT_INF, best, stack, 0, cnt, leaf);
     }
+    if (C::COUNT) tp = __builtin_amdgcn_s_memtime();   // the walk stamped its own phases
     if (!hit) return false;
     const rt_prim& p = S.leaf_prims[best.prim];
+    bool done = false;
     if constexpr ((C::F & FEAT_INST) != 0) {
         if (p.kind == RT_PRIM_INSTANCE) {
             instance_finish<C>(S, S.instances[p.a], r, best, h);
-            return true;
+            done = true;
         }
     }
     if constexpr ((C::F & FEAT_MEDIUM) != 0) {
-        if (p.kind == RT_PRIM_MEDIUM) {
+        if (!done && p.kind == RT_PRIM_MEDIUM) {
             medium_finish(p, r, best.t, h);
-            return true;
+            done = true;
         }
     }
-    simple_finish<C>(p, r, best.t, best.side, h, (C::F & FEAT_SHUTTER) != 0);
+    if (!done) simple_finish<C>(p, r, best.t, best.side, h, (C::F & FEAT_SHUTTER) != 0);
+    RT_STAMP(cnt.t_rec, tp);
     return true;
 }
 
@@ -1147,11 +1235,26 @@ __device__ R perlin_noise(const double* ranvec, const int32_t* perm, R px, R py,
     const R vv = v * v * ((R)3 - (R)2 * v);
     const R ww = w * w * ((R)3 - (R)2 * w);
     R accum = (R)0;
+    // RT_PERLIN_ROLLED: the corner and octave loops stay rolled, so the 8 corners' table loads are
+    // not all in flight (and live) at once: the Perlin texture (one sphere of the final scene)
+    // set the final-scene variant's register peak (158 VGPRs before RA with the loops unrolled)
+#if RT_PERLIN_ROLLED
+#pragma unroll 1
+#else
 #pragma unroll
+#endif
     for (int di = 0; di < 2; ++di)
+#if RT_PERLIN_ROLLED
+#pragma unroll 1
+#else
 #pragma unroll
+#endif
         for (int dj = 0; dj < 2; ++dj)
+#if RT_PERLIN_ROLLED
+#pragma unroll 1
+#else
 #pragma unroll
+#endif
             for (int dk = 0; dk < 2; ++dk) {
                 const uint32_t xi = ((uint32_t)i + (uint32_t)di) & 255u;
                 const uint32_t yi = ((uint32_t)j + (uint32_t)dj) & 255u;
@@ -1170,6 +1273,9 @@ template <class R>
 __device__ R perlin_turb(const double* ranvec, const int32_t* perm, R px, R py, R pz)
 {
     R accum = (R)0, weight = (R)1;
+#if RT_PERLIN_ROLLED
+#pragma unroll 1
+#endif
     for (int i = 0; i < 7; ++i) {
         accum += weight * perlin_noise(ranvec, perm, px, py, pz);
         weight *= (R)0.5;
@@ -1221,6 +1327,9 @@ __device__ __forceinline__ bool checker_odd(const HitT<double>& h)
     if (sx == 2 || sy == 2 || sz == 2) return rt_sin(ax) * rt_sin(ay) * rt_sin(az) < 0.0;
     return sx * sy * sz < 0;
 }
+
+template <class C>
+__device__ __forceinline__ const rt_texture& texture_of(const SceneDev& S, int i);
 
 template <class C, class R = typename C::Real>
 __device__ void tex_value(const SceneDev& S, int ti, const HitT<R>& h, R& cr, R& cg, R& cb)
@@ -1392,15 +1501,33 @@ __device__ __forceinline__ void camera_ray(const KParams& P, int x, int y, rt_ps
 // CU). The flag is per launch, so the choice is wave-uniform.
 template <class C>
 constexpr bool StageShade() { return C::F != FEAT_SET_SPHERES; }
+// The block's dynamic LDS: [TLAS nodes][stack: entries x 256 lanes][materials][textures], one
+// layout for the kernel's offsets and the launcher's allocation (launch_one)
+struct LdsLayout {
+    size_t stack, shade, total;   // byte offsets of the stack and of the material table; bytes
+};
+__host__ __device__ constexpr LdsLayout lds_layout(int n_nodes, int node_bytes, int stack_entries, int entry_bytes,
+                                                   int n_materials, int n_textures)
+{
+    const size_t stack = (size_t)n_nodes * (size_t)node_bytes;
+    const size_t shade = stack + (size_t)stack_entries * 256 * (size_t)entry_bytes;
+    return LdsLayout{stack, shade, shade + (size_t)n_materials * 64 + (size_t)n_textures * 96};
+}
+template <class C>
+__device__ __forceinline__ LdsLayout lds_layout_of(const SceneDev& S)
+{
+    return lds_layout(S.n_lds_nodes, lds_node_bytes<C>(), C::LDS ? S.stack_entries : 0, Stack16Cfg<C>() ? 2 : 4,
+                      StageShade<C>() ? S.n_lds_materials : 0, StageShade<C>() ? S.n_lds_textures : 0);
+}
 template <class C>
 __device__ __forceinline__ int lds_stack_offset(const SceneDev& S)   // in ints, after the TLAS nodes
 {
-    return S.n_lds_nodes * (lds_node_bytes<C>() / 4);
+    return (int)(lds_layout_of<C>(S).stack / 4);
 }
 template <class C>
-__device__ __forceinline__ int lds_shade_offset(const SceneDev& S)
+__device__ __forceinline__ int lds_shade_offset(const SceneDev& S)   // in ints
 {
-    return (C::LDS ? S.stack_entries * 256 : 0) + S.n_lds_nodes * (lds_node_bytes<C>() / 4);   // in ints
+    return (int)(lds_layout_of<C>(S).shade / 4);
 }
 template <class C>
 __device__ __forceinline__ const rt_material& material_of(const SceneDev& S, int i)
@@ -1646,13 +1773,16 @@ __device__ __forceinline__ bool lane_work(const KParams& P, LaneWork& w)
 #define RT_MIN_WAVES_MEDIA 3
 #endif
 #ifndef RT_MIN_WAVES_FINAL
-#define RT_MIN_WAVES_FINAL 3
+// round 3: 4 (127 VGPRs, no spills, once machine LICM no longer pins the cold paths' f64
+// constants in VGPRs and the hit record is dead during the walk); round 2 measured 3 best
+// (4: 112.0 ms with 0.7 TB of scratch writes per launch, 3: 102.8, 2: 131.5 at 960x540x200)
+#define RT_MIN_WAVES_FINAL 4
 #endif
 // minimum waves per SIMD requested from the register allocator, per feature set
 template <class C>
 constexpr int min_waves()
 {
-    return Stack16Cfg<C>() ? 5
+    return Stack16Cfg<C>() && C::F == FEAT_SET_SPHERES ? 5
            : C::F == FEAT_SET_SPHERES ? RT_MIN_WAVES_SPHERES
            : C::F == FEAT_SET_RECTINST ? RT_MIN_WAVES_RECTINST
            : C::F == FEAT_SET_MEDIA    ? RT_MIN_WAVES_MEDIA
@@ -1754,6 +1884,27 @@ __global__ void __launch_bounds__(256, min_waves<C>()) trace_chunks(SceneDev S, 
 // [sample][pixel] buffer; reduce_samples then sums every pixel's samples in sample order,
 // so the image does not depend on which lane or wave computed a sample.
 // ---------------------------------------------------------------------------
+// The hit record's old contents are dead (RT_KILL_H): freeze(poison) for every field, so the
+// register allocator need not carry them through the walk that writes the next record.
+template <class R>
+__device__ __forceinline__ void forget(HitT<R>& h)
+{
+    h.t = __builtin_nondeterministic_value(h.t);
+    h.px = __builtin_nondeterministic_value(h.px);
+    h.py = __builtin_nondeterministic_value(h.py);
+    h.pz = __builtin_nondeterministic_value(h.pz);
+    h.nx = __builtin_nondeterministic_value(h.nx);
+    h.ny = __builtin_nondeterministic_value(h.ny);
+    h.nz = __builtin_nondeterministic_value(h.nz);
+    h.uv0 = __builtin_nondeterministic_value(h.uv0);
+    h.uv1 = __builtin_nondeterministic_value(h.uv1);
+    h.uv2 = __builtin_nondeterministic_value(h.uv2);
+    h.uv3 = __builtin_nondeterministic_value(h.uv3);
+    h.front = __builtin_nondeterministic_value(h.front);
+    h.mat = __builtin_nondeterministic_value(h.mat);
+    h.uvkind = __builtin_nondeterministic_value(h.uvkind);
+}
+
 __device__ __forceinline__ unsigned lanes_below(uint64_t mask)
 {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
@@ -1777,8 +1928,10 @@ __global__ void __launch_bounds__(256, min_waves<C>()) trace_pool(SceneDev S, co
     if constexpr (Stack16Cfg<C>()) stack.base = reinterpret_cast<short*>(rt_lds + lds_stack_offset<C>(S)) + threadIdx.x;
     else if constexpr (C::LDS) stack.base = rt_lds + lds_stack_offset<C>(S) + threadIdx.x;
     Count cnt{};
-    uint64_t t_cam = 0, t_trace = 0, t_shade = 0, t_prev = 0;
-    if (C::COUNT) t_prev = __builtin_amdgcn_s_memtime();
+    uint64_t t_cam = 0, t_trace = 0, t_shade = 0, t_prev = 0, t_start = 0;
+    if (C::COUNT) t_prev = t_start = __builtin_amdgcn_s_memtime();
+    (void)t_trace;
+    (void)t_start;
     const int lane = threadIdx.x & 63;
     const unsigned n_tiles = (unsigned)P.tiles_x * (unsigned)P.tiles_y;
     // a work block = one tile x block_chunks consecutive chunks (items chunk-major; the
@@ -1873,6 +2026,17 @@ __global__ void __launch_bounds__(256, min_waves<C>()) trace_pool(SceneDev S, co
         if (!__any(active)) break;
         if (C::COUNT && first_active_lane()) cnt.wave_steps++;
         if (!active) continue;
+        // (COUNT) refill and loop overhead since the last iteration's end stamp: lanes refilled this
+        // iteration were idle, so their stamp is old — take the wave's latest (max over lanes)
+        if (C::COUNT) {
+            unsigned long long tw = t_prev;
+            for (int off = 32; off > 0; off >>= 1) {
+                const unsigned long long o = __shfl_xor(tw, off);
+                tw = tw > o ? tw : o;
+            }
+            t_prev = tw;
+            RT_STAMP(cnt.t_refill, t_prev);
+        }
 #if RT_MERGED_DRAWS
         // Ray generation: the camera rays of new samples and the scattered rays of last
         // iteration's hits (pending), whose random_in_unit_disk / random_in_unit_sphere tries
@@ -1912,13 +2076,15 @@ __global__ void __launch_bounds__(256, min_waves<C>()) trace_pool(SceneDev S, co
                 if (go) depth -= 1;
             }
         }
-        if (C::COUNT) { const uint64_t t = __builtin_amdgcn_s_memtime(); t_cam += t - t_prev; t_prev = t; }
+        RT_STAMP(t_cam, t_prev);
         if (go && depth > 0) {  // main.rs:21-23: depth 0 is black
             key.bounce = (uint32_t)(P.max_depth - depth);
             if (C::COUNT) cnt.casts++;
             finish_ray<C>(r, S.has_spheres != 0);
+            if (RT_KILL_H) forget(h);
+            RT_STAMP(cnt.t_setup, t_prev);
             const bool hit = trace_world<C>(S, r, h, stack, key, cnt);
-            if (C::COUNT) { const uint64_t t = __builtin_amdgcn_s_memtime(); t_trace += t - t_prev; t_prev = t; }
+            if (C::COUNT) t_prev = __builtin_amdgcn_s_memtime();   // trace_world stamped its phases
             if (!hit) {  // main.rs:37: background
                 cr = cr + Tr * P.bg[0];
                 cg = cg + Tg * P.bg[1];
@@ -1930,8 +2096,9 @@ __global__ void __launch_bounds__(256, min_waves<C>()) trace_pool(SceneDev S, co
                 }
                 pending = shade_begin<C>(S, h, Tr, Tg, Tb, cr, cg, cb);
             }
+            RT_STAMP(t_shade, t_prev);
         }
-        if (C::COUNT) { const uint64_t t = __builtin_amdgcn_s_memtime(); t_shade += t - t_prev; t_prev = t; }
+        if (C::COUNT) t_prev = __builtin_amdgcn_s_memtime();   // lanes that did not trace
         if (pending) {
         } else if (ITEMS && left > 0) {  // the item's next sample: the lane takes it at the loop top
             active = false;
@@ -2013,13 +2180,21 @@ __global__ void __launch_bounds__(256, min_waves<C>()) trace_pool(SceneDev S, co
         atomicAdd(&counters[12], (unsigned long long)cnt.cam_steps);
         atomicAdd(&counters[13], (unsigned long long)cnt.shade_lanes);
         atomicAdd(&counters[14], (unsigned long long)cnt.shade_steps);
-        if (lane == 0) {  // every lane stays in the loop to the end: lane 0 saw the wave's whole time
-            atomicAdd(&counters[3], (unsigned long long)t_cam);
-            atomicAdd(&counters[4], (unsigned long long)t_trace);
-            atomicAdd(&counters[5], (unsigned long long)t_shade);
-            atomicAdd(&counters[8], (unsigned long long)cnt.t_nodes);
-            atomicAdd(&counters[9], (unsigned long long)cnt.t_leaves);
-        }
+        // phase times: each region's first active lane added its intervals, so every lane's
+        // share goes in (trace = everything from the ray set-up to the hit record)
+        const uint64_t trace = cnt.t_setup + cnt.t_pre + cnt.t_nodes + cnt.t_leaves + cnt.t_rec;
+        atomicAdd(&counters[3], (unsigned long long)t_cam);
+        atomicAdd(&counters[4], (unsigned long long)trace);
+        atomicAdd(&counters[5], (unsigned long long)t_shade);
+        atomicAdd(&counters[8], (unsigned long long)cnt.t_nodes);
+        atomicAdd(&counters[9], (unsigned long long)cnt.t_leaves);
+        atomicAdd(&counters[15], (unsigned long long)cnt.t_setup);
+        atomicAdd(&counters[16], (unsigned long long)cnt.t_pre);
+        atomicAdd(&counters[17], (unsigned long long)cnt.t_rec);
+        atomicAdd(&counters[18], (unsigned long long)cnt.t_med);
+        atomicAdd(&counters[19], (unsigned long long)cnt.t_inst);
+        atomicAdd(&counters[20], (unsigned long long)cnt.t_refill);
+        if (lane == 0) atomicAdd(&counters[21], (unsigned long long)(__builtin_amdgcn_s_memtime() - t_start));
     }
 }
 
@@ -2064,10 +2239,12 @@ template <uint32_t F, bool S32, bool LDS, bool COUNT, bool F32>
 static void launch_one(const Launch& L, hipStream_t stream, bool nall)
 {
     const SceneDev& S = *L.S;
-    const size_t node_bytes = nall && S32 ? sizeof(LdsNode) : sizeof(rt_bvh_node);   // lds_node_bytes
-    const bool s16 = RT_STACK16 && LDS && nall && S32 && F == FEAT_SET_SPHERES && !F32;   // Stack16Cfg
-    const size_t lds = (LDS ? (size_t)S.stack_entries * 256 * (s16 ? 2 : 4) : 0) + (size_t)S.n_lds_nodes * node_bytes +
-                       (F != FEAT_SET_SPHERES ? (size_t)S.n_lds_materials * 64 + (size_t)S.n_lds_textures * 96 : 0);
+    const int node_bytes = nall && S32 ? (int)sizeof(LdsNode) : (int)sizeof(rt_bvh_node);   // lds_node_bytes
+    const bool s16 = RT_STACK16 && LDS && nall && S32 && (F == FEAT_SET_SPHERES || (RT_STACK16_FINAL && F == FEAT_SET_FINAL)) &&
+                     !F32;   // Stack16Cfg
+    const bool stage = F != FEAT_SET_SPHERES;   // StageShade
+    const size_t lds = lds_layout(S.n_lds_nodes, node_bytes, LDS ? S.stack_entries : 0, s16 ? 2 : 4,
+                                  stage ? S.n_lds_materials : 0, stage ? S.n_lds_textures : 0).total;
     if (L.pool) {
         auto go = [&](auto kernel) {
             const unsigned nb = std::min<unsigned long long>(resident_blocks(L, kernel, lds), (L.n_blocks + 3) / 4);
@@ -2100,12 +2277,13 @@ static void launch_f(const Launch& L, int slab32, int lds, hipStream_t stream)
     bool nall = S.n_lds_nodes > 0 && S.n_lds_nodes == S.n_tlas_nodes;
     // the whole-TLAS spheres instantiation keeps 16-bit stack entries (Stack16Cfg): a scene
     // whose node addresses or leaf codes do not fit takes the partial-TLAS instantiation
-    if (RT_STACK16 && F == FEAT_SET_SPHERES && slab32 && lds && !S.stack16_ok) nall = false;
+    constexpr bool S16F = F == FEAT_SET_SPHERES || (RT_STACK16_FINAL && F == FEAT_SET_FINAL);   // Stack16Cfg's feature sets
+    if (RT_STACK16 && S16F && slab32 && lds && !S.stack16_ok) nall = false;
     // stack16_ok (abi.cpp) assumes the node records start at LDS address 0, i.e. that rt_lds is
     // the kernels' only __shared__ object: a static __shared__ variable would move the dynamic
     // base up, and 16-bit stack entries would truncate node addresses past 32 KB. Checked on the
     // compiled kernels: any static LDS in them sends the scene to the 32-bit-stack instantiation.
-    if (RT_STACK16 && F == FEAT_SET_SPHERES && slab32 && lds && nall) {
+    if (RT_STACK16 && S16F && slab32 && lds && nall) {
         static int static_lds = -1;
         if (static_lds < 0) {
             static_lds = 0;

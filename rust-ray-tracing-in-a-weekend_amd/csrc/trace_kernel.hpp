@@ -72,7 +72,9 @@ enum : uint32_t {
     FEAT_INST_MEDIUM = 128, // a medium inside an instance (nested Translate/RotateY over a ConstantMedium)
     FEAT_INST_BLAS = 256,   // an instance over a BVH (a nested walk; instances over one primitive need none)
     FEAT_SHUTTER = 512,     // a MovingSphere whose shutter is not [0, 1] (its centre needs a division)
-    FEAT_ALL = 1023,
+    FEAT_NEST_MOVING = 1024, // a MovingSphere (nonzero velocity) under an instance or in a medium boundary
+    FEAT_ALL = 2047,
+    FEAT_STATIC = 1u << 16,  // kernel-internal (InstC / BoundC): every sphere reached here is static
     FEAT_SET_SPHERES = 0,                                          // compiled variant: spheres + solid/checker
     FEAT_SET_RECTINST = FEAT_RECT | FEAT_INST | FEAT_INST_RECT,    // + rects, boxes, instances of one prim (Cornell)
     FEAT_SET_MEDIA = FEAT_SET_RECTINST | FEAT_MEDIUM | FEAT_MEDIUM_INST,  // + constant media (Cornell smoke)

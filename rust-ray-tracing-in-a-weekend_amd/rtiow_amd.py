@@ -52,7 +52,7 @@ EXPORTED = [
     "rt_world_box", "rt_world_translate", "rt_world_rotate_y", "rt_world_constant_medium",
     "rt_world_bvh", "rt_world_push", "rt_world_build_scene", "rt_world_info_get", "rt_camera_new",
     "rt_scene_preset_get", "rt_scene_camera", "rt_world_flatten", "rt_ctx_upload_soa",
-    "rt_ctx_upload_world", "rt_render", "rt_rows_in_shard", "rt_rows_in_band_shard", "rt_last_stats", "rt_write_ppm",
+    "rt_ctx_upload_world", "rt_render", "rt_rows_in_shard", "rt_rows_in_band_shard", "rt_last_stats", "rt_last_counters", "rt_write_ppm",
     "rt_ctx_set_variant", "rt_device_eval", "rt_accum_create", "rt_accum_destroy", "rt_accum_add",
     "rt_accum_get", "rt_accum_set", "rt_accum_resolve", "rt_render_progressive", "rt_ctx_set_schedule", "rt_ctx_set_precision",
     "rt_scene_validate",
@@ -169,6 +169,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
                                ctypes.POINTER(ctypes.c_int32)], I), "rt_ctx_upload_world": ([P, P, I], I),
         "rt_render": ([P, ctypes.POINTER(Camera), ctypes.POINTER(RenderParams), P], I),
         "rt_rows_in_shard": ([I, I, I], I), "rt_rows_in_band_shard": ([I, I, I, I], I), "rt_last_stats": ([P, ctypes.POINTER(Stats)], I),
+        "rt_last_counters": ([P, P, I], I),
         "rt_write_ppm": ([P, I, I, ctypes.c_char_p], I),
         "rt_device_eval": ([P, I, P, P, P, P, I], I), "rt_ctx_set_variant": ([P, I, I, I], I),
         "rt_accum_create": ([P, ctypes.POINTER(RenderParams), ctypes.POINTER(P)], I),
@@ -452,6 +453,14 @@ class Renderer:
 
     def set_variant(self, slab32: int = 1, lds_stack: int = 1, lds_nodes: int = 1):
         _check(self.lib.rt_ctx_set_variant(self.h, slab32, lds_stack, lds_nodes), "rt_ctx_set_variant")
+
+    def counters(self, n: int = 24) -> np.ndarray:
+        """The last count_work render's raw counters (rt_last_counters: phase wave-cycles etc.)."""
+        out = np.zeros(n, dtype=np.uint64)
+        rc = self.lib.rt_last_counters(self.h, out.ctypes.data, n)
+        if rc < 0:
+            _check(rc, "rt_last_counters")
+        return out[:rc]
 
     def stats(self) -> Stats:
         s = Stats()

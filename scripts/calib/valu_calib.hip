@@ -33,11 +33,11 @@
 
 enum Op { F64_FMA, F64_ADD, F64_MUL, F64_RCP, F64_SQRT, F32_FMA, F32_ADD, F32_RCP, I32_ADD, I32_MUL, B32_XOR,
           CNDMASK, MOV_B32, CNDMASK_VCC, CMP_F64, CMP_F32, MAX_F64, MIN_F32, LSHL_B64, CVT_F64_U32, BFE_U32,
-          N_OPS };
+          PK_FMA_F32, MAX3_F32, MED3_F32, N_OPS };
 static const char* kNames[N_OPS] = {"f64_fma", "f64_add", "f64_mul", "f64_rcp", "f64_sqrt", "f32_fma", "f32_add",
                                     "f32_rcp", "i32_add", "i32_mul", "b32_xor", "cndmask", "mov_b32", "cndmask_vcc",
                                     "cmp_f64", "cmp_f32", "max_f64", "min_f32", "lshl_b64", "cvt_f64_u32",
-                                    "bfe_u32"};
+                                    "bfe_u32", "pk_fma_f32", "max3_f32", "med3_f32"};
 
 // Each class as one exact instruction (inline asm): the compiler may not fold repeated
 // adds, pack f32 pairs into v_pk_* or strength-reduce, so the loop issues exactly
@@ -72,6 +72,12 @@ __device__ __forceinline__ void body(double (&d)[8], float (&f)[8], unsigned (&u
         if constexpr (OP == LSHL_B64) asm volatile("v_lshlrev_b64 %0, 1, %0" : "+v"(d[i]));
         if constexpr (OP == CVT_F64_U32) asm volatile("v_cvt_f64_u32 %0, %1" : "=v"(d[i]) : "v"(u[i]));
         if constexpr (OP == BFE_U32) asm volatile("v_bfe_u32 %0, %0, 3, 7" : "+v"(u[i]));
+        // packed f32 FMA, both halves of src1 / src2 from one register each (op_sel_hi): the
+        // slab-plane product of two BVH children per instruction
+        if constexpr (OP == PK_FMA_F32)
+            asm volatile("v_pk_fma_f32 %0, %0, %1, %1 op_sel:[0,0,1] op_sel_hi:[1,0,1]" : "+v"(d[i]) : "v"(db));
+        if constexpr (OP == MAX3_F32) asm volatile("v_max3_f32 %0, %0, %1, %2" : "+v"(f[i]) : "v"(fb), "v"(fc));
+        if constexpr (OP == MED3_F32) asm volatile("v_med3_f32 %0, %0, %1, %2" : "+v"(f[i]) : "v"(fb), "v"(fc));
     }
 }
 
@@ -207,6 +213,9 @@ int main(int argc, char** argv)
     if (want(LSHL_B64)) run_modes<LSHL_B64>(modes, cus, din, dout, dclk, iters);
     if (want(CVT_F64_U32)) run_modes<CVT_F64_U32>(modes, cus, din, dout, dclk, iters);
     if (want(BFE_U32)) run_modes<BFE_U32>(modes, cus, din, dout, dclk, iters);
+    if (want(PK_FMA_F32)) run_modes<PK_FMA_F32>(modes, cus, din, dout, dclk, iters);
+    if (want(MAX3_F32)) run_modes<MAX3_F32>(modes, cus, din, dout, dclk, iters);
+    if (want(MED3_F32)) run_modes<MED3_F32>(modes, cus, din, dout, dclk, iters);
     CHECK(hipFree(din));
     CHECK(hipFree(dout));
     CHECK(hipFree(dclk));

@@ -11,9 +11,10 @@ import sys
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(REPO, "rust-ray-tracing-in-a-weekend_amd", "csrc")
 src = os.path.join(CSRC, os.environ.get("RT_VARIANT_SRC", "trace_v_all.hip"))
-cmd = ["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math",
-       "--offload-arch=gfx950", "-I" + os.path.join(REPO, "include"), "--cuda-device-only", "-c", src,
-       "-o", "/tmp/res_usage.o", "-Rpass-analysis=kernel-resource-usage", *sys.argv[1:]]
+sys.path.insert(0, REPO)
+import __graft_entry__ as ge  # noqa: E402  (the library's own flags)
+cmd = ["/opt/rocm/bin/hipcc", *[f for f in ge.CXXFLAGS if f not in ("-Wall", "-Wno-unused-function")],
+       "--cuda-device-only", "-c", src, "-o", "/tmp/res_usage.o", "-Rpass-analysis=kernel-resource-usage", *sys.argv[1:]]
 out = subprocess.run(cmd, capture_output=True, text=True).stderr
 cur, rows = None, []
 for line in out.splitlines():

@@ -68,7 +68,7 @@ def test_nested_world_matches_oracle(rt, renderer):
     soa = tw.product.flatten()
     assert soa.n_media == 3 and soa.n_instances >= 5
     got, ref = _render_both(rt, renderer, tw, 48, 32, 6, (7.0, 4.0, 9.0), (0.0, 0.7, 0.0), (0.5, 0.6, 0.8))
-    assert renderer.stats().variant_features == 1023          # media under instances: the all-features variant
+    assert renderer.stats().variant_features == 2047          # media under instances: the all-features variant
     assert float(ref.max()) > 0.0
     assert_parity(got, ref, "nested world")
 
@@ -103,7 +103,7 @@ def _moving_world(rt, t0, t1):
     return tw
 
 
-@pytest.mark.parametrize("t0,t1,feat", [(0.0, 1.0, 0), (0.25, 0.75, 1023), (-1.0, 2.0, 1023)])
+@pytest.mark.parametrize("t0,t1,feat", [(0.0, 1.0, 0), (0.25, 0.75, 2047), (-1.0, 2.0, 2047)])
 def test_moving_sphere_shutters_match_oracle(rt, renderer, t0, t1, feat):
     """MovingSphere::center (hittable.rs:556-558) for any shutter: [0, 1] shutters (every
     reference scene) take the spheres variant, which loads no per-primitive shutter flag;
@@ -112,6 +112,46 @@ def test_moving_sphere_shutters_match_oracle(rt, renderer, t0, t1, feat):
     got, ref = _render_both(rt, renderer, tw, 40, 24, 6, (6.0, 2.0, 5.0), (0.0, 0.5, 0.0), (0.7, 0.8, 1.0))
     assert renderer.stats().variant_features == feat
     assert_parity(got, ref, f"moving spheres, shutter [{t0}, {t1}]")
+
+
+@pytest.mark.parametrize("moving", [False, True])
+def test_instanced_spheres_static_or_moving_match_oracle(rt, renderer, moving):
+    """Spheres under an instance (Translate(RotateY(BVH)), the final scene's cluster shape):
+    all static -> the final-scene variant, whose nested sphere tests load no velocity
+    (FEAT_STATIC); one moving sphere among them (FEAT_NEST_MOVING) -> the all-features
+    variant with the moving centre (hittable.rs:556-558). Both against the oracle."""
+    from tests.oracle_binding import TwinWorld
+    tw = TwinWorld(rt)
+    white = tw.lambertian(tw.solid(0.73, 0.73, 0.73))
+    red = tw.lambertian(tw.solid(0.65, 0.05, 0.05))
+    ids = [tw.sphere(white, (0.5 * i - 1.0, 0.3 + 0.1 * (i % 3), 0.2 * (i % 2)), 0.25) for i in range(6)]
+    if moving:
+        ids.append(tw.moving_sphere(red, (0.0, 1.0, 0.0), (0.3, 1.2, 0.0), 0.0, 1.0, 0.3))
+    tw.push(tw.translate(tw.rotate_y(tw.bvh(ids), 25.0), (0.2, 0.0, -0.5)))
+    tw.push(tw.sphere(white, (0.0, -100.0, 0.0), 100.0))
+    got, ref = _render_both(rt, renderer, tw, 40, 24, 6, (5.0, 2.0, 6.0), (0.0, 0.5, 0.0), (0.7, 0.8, 1.0))
+    assert renderer.stats().variant_features == (2047 if moving else 287)
+    assert_parity(got, ref, f"instanced spheres (moving={moving})")
+
+
+@pytest.mark.parametrize("n_spheres", [3, 40])
+def test_shared_blas_under_two_instances_matches_oracle(rt, renderer, n_spheres):
+    """Two instances over one BVH (a single-leaf BVH of 3 spheres, or a 40-sphere tree): the
+    upload rewrites a BLAS's leaf codes relative to its first slot once, keeps the base in the
+    device instance record for both instances (16-bit stack entries in the final-scene
+    variant), and both copies must render as the oracle does."""
+    tw = ob.TwinWorld(rt)
+    white = tw.lambertian(tw.solid(0.73, 0.73, 0.73))
+    glass = tw.dielectric(1.5)
+    ids = [tw.sphere(glass if i % 3 == 0 else white, (0.3 * (i % 8) - 1.0, 0.25 + 0.3 * (i // 8), 0.1 * (i % 2)), 0.14)
+           for i in range(n_spheres)]
+    balls = tw.bvh(ids)
+    tw.push(tw.translate(tw.rotate_y(balls, 30.0), (-0.8, 0.0, 0.0)))
+    tw.push(tw.translate(balls, (1.0, 0.0, -0.6)))
+    tw.push(tw.sphere(white, (0.0, -100.0, 0.0), 100.0))
+    got, ref = _render_both(rt, renderer, tw, 48, 32, 6, (3.0, 2.0, 6.0), (0.0, 0.6, 0.0), (0.7, 0.8, 1.0))
+    assert renderer.stats().variant_features == 287
+    assert_parity(got, ref, f"shared BLAS ({n_spheres} spheres)")
 
 
 def _sphere_field(rt, n):

@@ -208,7 +208,7 @@ def test_feature_set_variants_identical(rt, renderer, scene_id, W, H, feat):
     renderer.upload(world)
     img = renderer.render(cam, p)
     assert renderer.stats().variant_features == feat
-    os.environ["RT_EXTRA_FEATURES"] = "1023"
+    os.environ["RT_EXTRA_FEATURES"] = "2047"   # incl. FEAT_NEST_MOVING: nested spheres as moving
     try:
         big = rt.Renderer(0)
     finally:
@@ -216,7 +216,7 @@ def test_feature_set_variants_identical(rt, renderer, scene_id, W, H, feat):
     try:
         big.upload(world)
         img_all = big.render(cam, p)
-        assert big.stats().variant_features == 1023
+        assert big.stats().variant_features == 2047
     finally:
         big.close()
     assert np.array_equal(img, img_all)
