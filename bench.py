@@ -122,14 +122,38 @@ def pmc_entry(src_hash, workload):
     return None, doc.get("calibration")
 
 
-def valu_issue_cycles(counts, calib, other=None):
+ISA_JSON = os.path.join(REPO, "profiles", "isa_mix.json")
+VARIANT_NAMES = {0: "spheres", 35: "rectinst", 103: "media", 287: "final", 2047: "all"}
+
+
+def isa_prices(src_hash, variant_features, schedule, slab32=1, nall=1):
+    """Per-class issue prices from the trace kernel's own instruction mix (scripts/isa_mix.py,
+    profiles/isa_mix.json) for this build and kernel: {counter or 'other': (price, lo, hi)}."""
+    if not os.path.exists(ISA_JSON):
+        return None
+    e = json.load(open(ISA_JSON)).get(src_hash, {}).get(
+        "%s/%s/s%dn%d" % (VARIANT_NAMES.get(variant_features, "?"), "items" if schedule == 2 else "pool", slab32, nall))
+    if not e:
+        return None
+    return {c: (v["price"], v["range"][0], v["range"][1]) for c, v in e["classes"].items()}
+
+
+def valu_issue_cycles(counts, calib, other=None, isa=None, bound=0):
     """Issue cycles (summed over SIMDs) the launch's VALU instruction mix needs at the
     calibrated saturated rates: sum over classes of count x cycles per wave-instruction; the
     instructions no class counter covers (moves, compares, selects, bit ops) at the measured
-    rate of those (calib 'other', or `other` to price the bounds)."""
+    rate of those (calib 'other', or `other` to price the bounds). With `isa` (isa_prices),
+    every class — "other" included — is priced from the kernel's own static instruction mix
+    over the calibrated per-opcode costs; bound -1 / +1 takes each class's low / high price."""
     cyc = dict(calib["cycles_per_inst"])
     if other is not None:
         cyc["other"] = other
+    by_counter = {}
+    if isa:
+        k = {0: 0, -1: 1, 1: 2}[bound]
+        by_counter = {c: v[k] for c, v in isa.items()}
+        if "other" in isa:
+            cyc["other"] = isa["other"][k]
     total = counts["SQ_INSTS_VALU"]
     known, need = 0.0, 0.0
     for cls, key in calib["class_counters"].items():
@@ -137,7 +161,7 @@ def valu_issue_cycles(counts, calib, other=None):
         if n is None:
             continue
         known += n
-        need += n * cyc[cls]
+        need += n * by_counter.get(key[len("SQ_INSTS_VALU_"):], cyc[cls])
     need += max(0.0, total - known) * cyc["other"]
     return need
 
@@ -259,13 +283,18 @@ def main():
     roofline = {"bound": "valu", "achieved": None, "peak": None, "unit": "G SIMD-cycles/s", "frac": None,
                 "traffic": None, "src_hash": src_hash}
     if pmc is not None and calib is not None:
-        need = valu_issue_cycles(pmc["counters"], calib)         # SIMD-cycles of VALU issue per launch
+        isa = isa_prices(src_hash, last.variant_features, last.schedule, last.slab32, int(last.lds_nodes > 0))
+        need = valu_issue_cycles(pmc["counters"], calib, isa=isa)   # SIMD-cycles of VALU issue per launch
         clk = pmc["clock_ghz"]                                   # the clock the chip held in that pass
         achieved = need / (k_ms * 1e-3) / 1e9                    # per live-timed launch
         peak = N_SIMDS * clk
         dram = pmc["dram_bytes"]
-        lo, hi = (valu_issue_cycles(pmc["counters"], calib, o) / (k_ms * 1e-3) / 1e9 / peak
-                  for o in calib.get("other_range", [calib["cycles_per_inst"]["other"]] * 2))
+        if isa:   # each class at the low / high end of its static-mix price
+            lo, hi = (valu_issue_cycles(pmc["counters"], calib, isa=isa, bound=b) / (k_ms * 1e-3) / 1e9 / peak
+                      for b in (-1, 1))
+        else:
+            lo, hi = (valu_issue_cycles(pmc["counters"], calib, o) / (k_ms * 1e-3) / 1e9 / peak
+                      for o in calib.get("other_range", [calib["cycles_per_inst"]["other"]] * 2))
         roofline.update({
             "achieved": round(achieved, 1), "peak": round(peak, 1), "frac": round(achieved / peak, 4),
             "traffic": int(dram),
@@ -274,6 +303,11 @@ def main():
             "hbm": {"achieved": round(dram / (k_ms * 1e-3) / 1e9, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(dram / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)},
             "frac_range": [round(lo, 4), round(hi, 4)],
+            "useful_frac": round(achieved / peak * pmc["counters"]["SQ_THREAD_CYCLES_VALU"] /
+                                 (64.0 * pmc["counters"]["SQ_INSTS_VALU"]), 4),
+            "pricing": ("per-class prices from this kernel's instruction mix (profiles/isa_mix.json)" if isa
+                        else "calibration class means, 'other' bounded by its cheapest / dearest op"),
+            "model_check": calib.get("mix"),
             "pmc_tag": pmc.get("tag"), "pmc_kernel_ms": pmc.get("kernel_ms"), "clock_ghz": clk})
     else:
         roofline["note"] = "no PMC pass of this build (source hash) and workload in profiles/pmc_r02.json"

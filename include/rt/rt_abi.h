@@ -213,7 +213,8 @@ int rt_last_stats(rt_ctx* ctx, rt_stats* out);
  * exist). 0-14 as in rt_stats; wave-cycles (s_memtime) per phase of the pool kernels: 3 ray
  * generation, 4 trace, 5 shading, 8 node loops, 9 leaf tests (both of the top-level walk),
  * 15 ray set-up, 16 walk prologue (pre-leaf test), 17 hit record, 18 media and 19 instances
- * (inside the leaf tests), 20 refill, 21 kernel total (summed over waves). */
+ * (inside the leaf tests), 20 refill, 21 kernel total (summed over waves), 22 deferred instance
+ * walks (after the top-level walk). */
 int rt_last_counters(rt_ctx* ctx, uint64_t* out, int n);
 
 /* ---- progressive / resumable accumulation ------------------------------------ */

@@ -51,6 +51,11 @@ constexpr int kMaxLdsStack = 48;
 // TLAS nodes kept in LDS (32 KB per block): the first kMaxLdsNodes in BFS order, i.e.
 // the top levels; deeper ones are read from L1/L2
 constexpr int kMaxLdsNodes = 512;
+// instance BLAS nodes staged in LDS at most (64 B each)
+#ifndef RT_LDS_BLAS_MAX
+#define RT_LDS_BLAS_MAX 64   // C4 1920x1080x100: 64 staged 132.15 ms, 16 133.31, none 132.98 (r03h_ab_c4.log)
+#endif
+constexpr int kMaxLdsBlas = RT_LDS_BLAS_MAX;
 // material (64 B) and texture (96 B) tables staged in LDS when both are this small (10 KB)
 constexpr int kMaxLdsMaterials = 64;
 
@@ -757,6 +762,54 @@ int rt_ctx_upload_soa(rt_ctx* c, const rt_scene_soa* s)
             max_first = s->n_prim_refs;
         }
     }
+    // The largest instance BLAS in BFS order right after the TLAS prefix (device node order
+    // only): a launch stages its top levels in LDS (SceneDev.n_lds_blas), where the nested
+    // walk reads them instead of waiting on L2 for every level. Needs the TLAS prefix and a
+    // BLAS disjoint from it (validate_soa's n_tlas_nodes); otherwise nothing is staged.
+    int n_blas_bfs = 0;
+    {
+        int best_root = -1;
+        size_t best_n = 0;
+        std::vector<int> bfs;
+        for (const rt_instance& in : inst_dev) {
+            if (in.child_kind != RT_CHILD_BVH || in.child < n_tlas_nodes) continue;
+            std::vector<int> order{in.child};
+            std::vector<uint8_t> seen((size_t)s->n_nodes, 0);
+            seen[(size_t)in.child] = 1;
+            bool disjoint = true;
+            for (size_t i = 0; i < order.size(); ++i)
+                for (int ch : nodes_dev[(size_t)order[i]].child)
+                    if (ch >= 0 && !seen[(size_t)ch]) {
+                        seen[(size_t)ch] = 1;
+                        if (ch < n_tlas_nodes) disjoint = false;
+                        order.push_back(ch);
+                    }
+            if (disjoint && order.size() > best_n) {
+                best_n = order.size();
+                best_root = in.child;
+                bfs.swap(order);
+            }
+        }
+        if (best_root >= 0 && (n_tlas_nodes > 0 || s->tlas_root < 0)) {
+            std::vector<int> perm((size_t)s->n_nodes, -1);
+            for (int i = 0; i < n_tlas_nodes; ++i) perm[(size_t)i] = i;
+            int next = n_tlas_nodes;
+            for (int b : bfs) perm[(size_t)b] = next++;
+            for (int i = 0; i < s->n_nodes; ++i)
+                if (perm[(size_t)i] < 0) perm[(size_t)i] = next++;
+            std::vector<rt_bvh_node> moved((size_t)s->n_nodes);
+            for (int i = 0; i < s->n_nodes; ++i) {
+                rt_bvh_node nd = nodes_dev[(size_t)i];
+                for (int& ch : nd.child)
+                    if (ch >= 0) ch = perm[(size_t)ch];
+                moved[(size_t)perm[(size_t)i]] = nd;
+            }
+            nodes_dev.swap(moved);
+            for (rt_instance& in : inst_dev)
+                if (in.child_kind == RT_CHILD_BVH && in.child >= 0) in.child = perm[(size_t)in.child];
+            n_blas_bfs = (int)bfs.size();
+        }
+    }
     size_t off[10], bytes[10] = {
         (size_t)s->n_nodes * sizeof(rt_bvh_node), (size_t)s->n_prim_refs * 4, (size_t)s->n_prims * sizeof(rt_prim),
         (size_t)s->n_instances * sizeof(rt_instance), (size_t)s->n_materials * sizeof(rt_material),
@@ -801,6 +854,8 @@ int rt_ctx_upload_soa(rt_ctx* c, const rt_scene_soa* s)
     // relative, above) above the -32768 sentinel
     c->S.stack16_ok = (n_tlas_nodes * (int64_t)80 <= 32767 - 80 && max_first <= 1023 && s->n_nodes <= 32767) ? 1 : 0;
     c->S.n_lds_nodes = 0;
+    c->S.n_blas_bfs = n_blas_bfs;
+    c->S.n_lds_blas = 0;
     // traversal stack: TLAS walk, then a nested BLAS walk (instances) above it, sized from the
     // depths validate_soa measured (<= 32 each), each walk's bottom entry holding its RT_DONE
     // sentinel (traverse): the 66-entry scratch stack always fits
@@ -909,6 +964,9 @@ int rt_ctx_upload_soa(rt_ctx* c, const rt_scene_soa* s)
         if (nest) feat |= rtk::FEAT_NEST_MOVING;
     }
     c->features = feat;
+    c->S.has_lights = 0;   // any DiffuseLight: without one, a hit never emits (shade_begin skips its material read)
+    for (int i = 0; i < s->n_materials; ++i)
+        if (s->materials[i].kind == RT_MAT_DIFFUSE_LIGHT) c->S.has_lights = 1;
     c->S.has_spheres = 0;
     for (int i = 0; i < s->n_prims; ++i)
         if (s->prims[i].kind == RT_PRIM_SPHERE || s->prims[i].kind == RT_PRIM_MOVING_SPHERE) c->S.has_spheres = 1;
@@ -1039,7 +1097,9 @@ static int run_range(rt_ctx* c, const rt_camera* cam, const rt_render_params* p,
     o.lds_stack = c->opt_lds && c->S.stack_entries <= kMaxLdsStack;
     o.count = count;
     o.f32 = c->opt_precision == RT_PREC_F32;
-    if (o.f32 && count) return fail(RT_ERR_UNSUPPORTED, "count_work is an f64-mode diagnostic");
+    if (o.f32 && count && rtk::variant_features(o.features) != rtk::FEAT_SET_SPHERES &&
+        rtk::variant_features(o.features) != rtk::FEAT_SET_FINAL)
+        return fail(RT_ERR_UNSUPPORTED, "count_work in the f32 mode: the spheres and final-scene variants only");
     if (o.f32) o.slab32 = 1;   // statistical mode: f32 boxes whatever the camera
     // a scene with no BVH node (the Cornell scenes: one top-level leaf, instances over one
     // box) tests no slab: the f64-slab instantiation then, which holds no f32 ray terms
@@ -1055,6 +1115,24 @@ static int run_range(rt_ctx* c, const rt_camera* cam, const rt_render_params* p,
                        c->n_materials > 0;
     S.n_lds_materials = stage ? c->n_materials : 0;
     S.n_lds_textures = stage ? c->n_textures : 0;
+    // the top levels of the BFS-ordered instance BLAS in LDS too (variants with nested walks),
+    // as many as the LDS left over at the block count the rest of the layout allows
+    S.n_lds_blas = 0;
+    if (c->S.n_blas_bfs > 0 && c->opt_lds_nodes && !o.f32 &&
+        (rtk::variant_features(o.features) & rtk::FEAT_INST_BLAS) != 0) {
+        const bool oct = o.slab32 && S.n_lds_nodes == c->n_tlas_nodes && S.n_lds_nodes > 0;
+        const size_t base = (size_t)S.n_lds_nodes * (oct ? 80 : 64) +
+                            (o.lds_stack ? (size_t)c->S.stack_entries * 256 * 4 : 0) +
+                            (size_t)S.n_lds_materials * 64 + (size_t)S.n_lds_textures * 96;
+        // the CU's 160 KB shared by `blocks` workgroups, each allocation rounded up to the LDS
+        // granule (taken as 1 KB; the occupancy API does not round: a layout it rated at 3
+        // blocks per CU ran 2 and took 174 instead of 133 ms, r03g_ab_c4.log)
+        const size_t lds_cu = 160 * 1024, granule = 1024;
+        const size_t blocks = std::max<size_t>(1, lds_cu / (((std::max<size_t>(base, 1) + granule - 1) / granule) * granule));
+        const size_t budget = lds_cu / blocks / granule * granule;
+        const size_t spare = budget > base ? budget - base : 0;
+        S.n_lds_blas = (int32_t)std::min<size_t>({(size_t)c->S.n_blas_bfs, spare / 64, (size_t)kMaxLdsBlas});
+    }
     // work blocks of one tile: 16-sample chunks, per-sample pool one chunk per block, item pool
     // two (C2 kernel ms, pool 1/2/4 chunks: 99.8/100.2/103.2; items 1/2/4: 106.8/104.1/105.0;
     // profiles/r02f_*, r02g_*)

@@ -87,7 +87,7 @@ struct Count {
     // pool kernels, finer phases (wave-cycles; each added by the first active lane of the region
     // it times, so summed over lanes they are wave totals): ray set-up, the walk's prologue
     // (pre-leaf test, bounds), the hit record, and inside the leaf tests the media and instances
-    uint64_t t_setup, t_pre, t_rec, t_med, t_inst, t_refill;
+    uint64_t t_setup, t_pre, t_rec, t_med, t_inst, t_refill, t_defer;
 };
 // COUNT phase stamps: tp is the lane's last stamp; the first active lane adds the interval
 #define RT_STAMP(acc, tp)                                                   \
@@ -212,7 +212,7 @@ struct Stack<false> {
 #define RT_STACK16 1
 #endif
 #ifndef RT_STACK16_FINAL
-#define RT_STACK16_FINAL 1
+#define RT_STACK16_FINAL 0   // measured: the final variant with 16-bit entries (4 waves) 142.1 ms vs 132.7 with 32-bit (3 waves, LDS-bound); at 3 waves both ways 141.8 vs 132.4 (C4 1920x1080x100, r03f_ab_c4.log): the 16-bit stack itself costs ~7 % here
 #endif
 struct Stack16 {   // node records at LDS addresses < 32 KB, leaf codes > -32768 (SceneDev.stack16_ok)
     short* base;
@@ -698,6 +698,10 @@ __device__ __forceinline__ Node load_node(const rt_bvh_node* base, int i)
     return n;
 }
 
+// A node from LDS by byte address (four ds_read_b128 through an address-space-3 pointer: a
+// generic pointer that may be LDS or global would be read with flat loads)
+__device__ __forceinline__ Node load_node_lds(uint32_t addr);
+
 // The variants whose LDS node visits use packed-f32 plane products (v_pk_fma_f32 with op_sel:
 // 6 instead of 12 FMAs per visit, no extra registers; round 2's broadcast-pair form cost ~4
 // VGPRs and was rejected)
@@ -726,6 +730,54 @@ __device__ __forceinline__ const __attribute__((address_space(3))) T* lds_ptr(ui
 }
 template <class C>
 constexpr int lds_node_bytes() { return OctNodes<C>() ? (int)sizeof(LdsNode) : (int)sizeof(rt_bvh_node); }
+__device__ __forceinline__ Node load_node_lds(uint32_t addr)
+{
+    typedef unsigned u4v __attribute__((ext_vector_type(4)));
+    const auto q = lds_ptr<u4v>(addr);
+    const u4v a = q[0], b = q[1], c = q[2], d = q[3];
+    Node n;
+    n.lo0[0] = __uint_as_float(a.x); n.lo0[1] = __uint_as_float(a.y); n.lo0[2] = __uint_as_float(a.z);
+    n.hi0[0] = __uint_as_float(a.w); n.hi0[1] = __uint_as_float(b.x); n.hi0[2] = __uint_as_float(b.y);
+    n.lo1[0] = __uint_as_float(b.z); n.lo1[1] = __uint_as_float(b.w); n.lo1[2] = __uint_as_float(c.x);
+    n.hi1[0] = __uint_as_float(c.y); n.hi1[1] = __uint_as_float(c.z); n.hi1[2] = __uint_as_float(c.w);
+    n.child[0] = (int)d.x;
+    n.child[1] = (int)d.y;
+    return n;
+}
+
+// The material / texture table a shading step reads: staged in LDS by the block prologue
+// (north_star: "stages the top BVH levels and material table in LDS") when the variant
+// has rects or media and the tables are small (Cornell 4-6 materials, final scene 10), else
+// global memory (the random scene's 485 materials would cost the spheres variant blocks per
+// CU). The flag is per launch, so the choice is wave-uniform.
+template <class C>
+constexpr bool StageShade() { return C::F != FEAT_SET_SPHERES; }
+// The block's dynamic LDS: [TLAS nodes][BLAS nodes][stack: entries x 256 lanes][materials][textures], one
+// layout for the kernel's offsets and the launcher's allocation (launch_one)
+struct LdsLayout {
+    size_t blas, stack, shade, total;   // byte offsets of the BLAS nodes, the stack and the material table; bytes
+};
+__host__ __device__ constexpr LdsLayout lds_layout(int n_nodes, int node_bytes, int n_blas, int stack_entries,
+                                                   int entry_bytes, int n_materials, int n_textures)
+{
+    const size_t blas = (size_t)n_nodes * (size_t)node_bytes;
+    const size_t stack = blas + (size_t)n_blas * sizeof(rt_bvh_node);
+    const size_t shade = stack + (size_t)stack_entries * 256 * (size_t)entry_bytes;
+    return LdsLayout{blas, stack, shade, shade + (size_t)n_materials * 64 + (size_t)n_textures * 96};
+}
+// the variants that stage BLAS nodes (SceneDev.n_lds_blas; the host sets it only for them)
+#ifndef RT_STAGE_BLAS
+#define RT_STAGE_BLAS 1
+#endif
+template <class C>
+constexpr bool StageBlas() { return RT_STAGE_BLAS && (C::F & FEAT_INST_BLAS) != 0 && !C::F32; }
+template <class C>
+__device__ __forceinline__ LdsLayout lds_layout_of(const SceneDev& S)
+{
+    return lds_layout(S.n_lds_nodes, lds_node_bytes<C>(), StageBlas<C>() ? S.n_lds_blas : 0, C::LDS ? S.stack_entries : 0,
+                      Stack16Cfg<C>() ? 2 : 4, StageShade<C>() ? S.n_lds_materials : 0,
+                      StageShade<C>() ? S.n_lds_textures : 0);
+}
 
 // Closest hit in a BVH (nodes + leaf ranges of slots j, whose records are leaf_prims[j]).
 // `leaf(slot, t_max, best)` tests one primitive; on a closer hit it fills best (t and sub
@@ -773,6 +825,9 @@ __device__ __forceinline__ bool traverse(const SceneDev& S, int root, const RayT
     float ninf = -__builtin_inff();
     if constexpr (OCT && RT_MED3) asm("s_mov_b32 %0, 0xff800000" : "=s"(ninf));
     const char* const lb = reinterpret_cast<const char*>(lds_nodes);
+    uint32_t blas_lds_base = 0;   // LDS byte address of the staged BLAS nodes (nested walks)
+    if constexpr (!NL && StageBlas<C>()) blas_lds_base = lds_addr(lb) + (uint32_t)lds_layout_of<C>(S).blas;
+    (void)blas_lds_base;
     // t_min's f32 bound in a register set once per walk (an asm result: not rematerialized as a
     // v_mov inside the node loop, which machine LICM no longer hoists)
     float tmin_v = tmin_f;
@@ -846,8 +901,16 @@ __device__ __forceinline__ bool traverse(const SceneDev& S, int root, const RayT
             if (h1) return ch.y;
             return pop();
         }
-        const Node nd = (NL && (C::NALL || node < S.n_lds_nodes)) ? load_node(lds_nodes, node)
-                                                                  : load_node(S.nodes, node);
+        Node nd;
+        if constexpr (!NL && StageBlas<C>()) {
+            // a nested (BLAS) walk: its staged top levels from LDS (ds_read_b128 through an LDS
+            // pointer), the rest from L1/L2
+            const uint32_t j = (uint32_t)(node - S.n_tlas_nodes);
+            if (j < (uint32_t)S.n_lds_blas) nd = load_node_lds(blas_lds_base + j * (uint32_t)sizeof(rt_bvh_node));
+            else nd = load_node(S.nodes, node);
+        } else {
+            nd = (NL && (C::NALL || node < S.n_lds_nodes)) ? load_node(lds_nodes, node) : load_node(S.nodes, node);
+        }
         bool h0, h1, near0;
         if constexpr (C::S32) {
             float tn0, tn1;
@@ -1134,6 +1197,12 @@ __device__ __forceinline__ void medium_finish(const rt_prim& m, const RayT<R>& r
 // spills) and the Cornell variant would drop to 3 waves per SIMD.
 template <class C>
 constexpr bool PreLeaf() { return C::F == FEAT_SET_SPHERES; }
+#ifndef RT_DEFER_INST
+#define RT_DEFER_INST 1
+#endif
+// the variants whose instances can hold a BLAS (a nested walk) defer their first instance test
+template <class C>
+constexpr bool DeferInst() { return RT_DEFER_INST && (C::F & FEAT_INST_BLAS) != 0; }
 
 // HitRecord of the closest primitive.
 template <class C, class R = typename C::Real>
@@ -1144,10 +1213,23 @@ __device__ bool trace_world(const SceneDev& S, const RayT<R>& r, HitT<R>& h, Sta
     HitRefT<R> best;
     best.sub = 0;
     best.side = 0;
+    // DeferInst: the first instance a lane's walk reaches is tested after the walk (pend), so
+    // the lanes of a wave that have one walk its BLAS together, once, instead of each at its
+    // own step of the top-level walk while the others wait; its t_max is then the walk's final
+    // closest hit, which prunes it further. Closest hit does not depend on the order of the
+    // tests (the instance's t is the ray's t), so the image does not change.
+    int pend = -1;
+    (void)pend;
     auto leaf = [&](int slot, R tmax, HitRefT<R>& b) {
         const rt_prim& p = S.leaf_prims[slot];
         if constexpr ((C::F & FEAT_INST) != 0)
             if (p.kind == RT_PRIM_INSTANCE) {
+                if constexpr (DeferInst<C>()) {
+                    if (pend < 0) {
+                        pend = slot;
+                        return false;
+                    }
+                }
                 uint64_t ti = 0;
                 if (C::COUNT) ti = __builtin_amdgcn_s_memtime();
                 const bool hit = instance_t<C>(S, S.instances[p.a], r, t_min, tmax, b, stack, S.blas_base, key, cnt);
@@ -1199,6 +1281,22 @@ __device__ bool trace_world(const SceneDev& S, const RayT<R>& r, HitT<R>& h, Sta
         hit = traverse<C, true>(S, S.tlas_root, r, t_min, (R)RT_INF, best, stack, 0, cnt, leaf);
     }
     if (C::COUNT) tp = __builtin_amdgcn_s_memtime();   // the walk stamped its own phases
+    if constexpr (DeferInst<C>()) {
+        if (pend >= 0) {
+            const rt_prim& p = S.leaf_prims[pend];
+            HitRefT<R> b;
+            b.sub = 0;
+            b.side = 0;
+            // the top-level walk is done: its stack is free, the BLAS walk starts at entry 0
+            if (instance_t<C>(S, S.instances[p.a], r, t_min, hit ? best.t : (R)RT_INF, b, stack, 0, key, cnt)) {
+                best = b;
+                best.prim = pend;
+                hit = true;
+            }
+            RT_STAMP(cnt.t_defer, tp);
+        }
+        if (C::COUNT) tp = __builtin_amdgcn_s_memtime();   // lanes without one
+    }
     if (!hit) return false;
     const rt_prim& p = S.leaf_prims[best.prim];
     bool done = false;
@@ -1494,31 +1592,6 @@ __device__ __forceinline__ void camera_ray(const KParams& P, int x, int y, rt_ps
     camera_end(P, st, u, v, dxl, dyl, r);
 }
 
-// The material / texture table a shading step reads: staged in LDS by the block prologue
-// (north_star: "stages the top BVH levels and material table in LDS") when the variant
-// has rects or media and the tables are small (Cornell 4-6 materials, final scene 10), else
-// global memory (the random scene's 485 materials would cost the spheres variant blocks per
-// CU). The flag is per launch, so the choice is wave-uniform.
-template <class C>
-constexpr bool StageShade() { return C::F != FEAT_SET_SPHERES; }
-// The block's dynamic LDS: [TLAS nodes][stack: entries x 256 lanes][materials][textures], one
-// layout for the kernel's offsets and the launcher's allocation (launch_one)
-struct LdsLayout {
-    size_t stack, shade, total;   // byte offsets of the stack and of the material table; bytes
-};
-__host__ __device__ constexpr LdsLayout lds_layout(int n_nodes, int node_bytes, int stack_entries, int entry_bytes,
-                                                   int n_materials, int n_textures)
-{
-    const size_t stack = (size_t)n_nodes * (size_t)node_bytes;
-    const size_t shade = stack + (size_t)stack_entries * 256 * (size_t)entry_bytes;
-    return LdsLayout{stack, shade, shade + (size_t)n_materials * 64 + (size_t)n_textures * 96};
-}
-template <class C>
-__device__ __forceinline__ LdsLayout lds_layout_of(const SceneDev& S)
-{
-    return lds_layout(S.n_lds_nodes, lds_node_bytes<C>(), C::LDS ? S.stack_entries : 0, Stack16Cfg<C>() ? 2 : 4,
-                      StageShade<C>() ? S.n_lds_materials : 0, StageShade<C>() ? S.n_lds_textures : 0);
-}
 template <class C>
 __device__ __forceinline__ int lds_stack_offset(const SceneDev& S)   // in ints, after the TLAS nodes
 {
@@ -1578,6 +1651,14 @@ __device__ __forceinline__ void stage_lds(const SceneDev& S)
         }
         any = true;
     }
+    if constexpr (StageBlas<C>()) {
+        if (S.n_lds_blas > 0) {   // the BLAS's BFS prefix, nodes[n_tlas_nodes, ...) (abi.cpp)
+            uint4* db = reinterpret_cast<uint4*>(reinterpret_cast<char*>(rt_lds) + lds_layout_of<C>(S).blas);
+            const uint4* sb = reinterpret_cast<const uint4*>(S.nodes + S.n_tlas_nodes);
+            for (int i = threadIdx.x; i < S.n_lds_blas * 4; i += 256) db[i] = sb[i];
+            any = true;
+        }
+    }
     if constexpr (StageShade<C>()) {
         if (S.n_lds_materials > 0) {
             uint4* dm = reinterpret_cast<uint4*>(rt_lds + lds_shade_offset<C>(S));
@@ -1603,6 +1684,7 @@ template <class C, class R = typename C::Real>
 __device__ __forceinline__ bool shade_begin(const SceneDev& S, const HitT<R>& h, R Tr, R Tg, R Tb, double& sum_r,
                                             double& sum_g, double& sum_b)
 {
+    if (!S.has_lights) return true;   // wave-uniform: no material of the scene emits (no read needed)
     const rt_material& m = material_of<C>(S, h.mat);
     if (m.kind == RT_MAT_DIFFUSE_LIGHT) {  // material.rs:25-34 (emits on both faces, never scatters)
         R er, eg, eb;
@@ -2182,7 +2264,7 @@ __global__ void __launch_bounds__(256, min_waves<C>()) trace_pool(SceneDev S, co
         atomicAdd(&counters[14], (unsigned long long)cnt.shade_steps);
         // phase times: each region's first active lane added its intervals, so every lane's
         // share goes in (trace = everything from the ray set-up to the hit record)
-        const uint64_t trace = cnt.t_setup + cnt.t_pre + cnt.t_nodes + cnt.t_leaves + cnt.t_rec;
+        const uint64_t trace = cnt.t_setup + cnt.t_pre + cnt.t_nodes + cnt.t_leaves + cnt.t_defer + cnt.t_rec;
         atomicAdd(&counters[3], (unsigned long long)t_cam);
         atomicAdd(&counters[4], (unsigned long long)trace);
         atomicAdd(&counters[5], (unsigned long long)t_shade);
@@ -2194,6 +2276,7 @@ __global__ void __launch_bounds__(256, min_waves<C>()) trace_pool(SceneDev S, co
         atomicAdd(&counters[18], (unsigned long long)cnt.t_med);
         atomicAdd(&counters[19], (unsigned long long)cnt.t_inst);
         atomicAdd(&counters[20], (unsigned long long)cnt.t_refill);
+        atomicAdd(&counters[22], (unsigned long long)cnt.t_defer);
         if (lane == 0) atomicAdd(&counters[21], (unsigned long long)(__builtin_amdgcn_s_memtime() - t_start));
     }
 }
@@ -2242,9 +2325,10 @@ static void launch_one(const Launch& L, hipStream_t stream, bool nall)
     const int node_bytes = nall && S32 ? (int)sizeof(LdsNode) : (int)sizeof(rt_bvh_node);   // lds_node_bytes
     const bool s16 = RT_STACK16 && LDS && nall && S32 && (F == FEAT_SET_SPHERES || (RT_STACK16_FINAL && F == FEAT_SET_FINAL)) &&
                      !F32;   // Stack16Cfg
-    const bool stage = F != FEAT_SET_SPHERES;   // StageShade
-    const size_t lds = lds_layout(S.n_lds_nodes, node_bytes, LDS ? S.stack_entries : 0, s16 ? 2 : 4,
-                                  stage ? S.n_lds_materials : 0, stage ? S.n_lds_textures : 0).total;
+    const bool stage = F != FEAT_SET_SPHERES;                   // StageShade
+    const bool blas = RT_STAGE_BLAS && (F & FEAT_INST_BLAS) != 0 && !F32;   // StageBlas
+    const size_t lds = lds_layout(S.n_lds_nodes, node_bytes, blas ? S.n_lds_blas : 0, LDS ? S.stack_entries : 0,
+                                  s16 ? 2 : 4, stage ? S.n_lds_materials : 0, stage ? S.n_lds_textures : 0).total;
     if (L.pool) {
         auto go = [&](auto kernel) {
             const unsigned nb = std::min<unsigned long long>(resident_blocks(L, kernel, lds), (L.n_blocks + 3) / 4);
@@ -2324,6 +2408,17 @@ hipError_t launch_variant_f32(const Launch& L, const LaunchOpts& o, hipStream_t 
     else launch_one<F, true, false, false, true>(L, stream, nall);
     return hipGetLastError();
 }
+
+// The f32 mode's count_work variant (final scene and spheres: the f32-vs-f64 path-length and
+// step-cost comparison of DESIGN.md §5.6; trace_f32_*_count.hip)
+template <uint32_t F>
+hipError_t launch_variant_f32_count(const Launch& L, const LaunchOpts& o, hipStream_t stream)
+{
+    const bool nall = L.S->n_lds_nodes > 0 && L.S->n_lds_nodes == L.S->n_tlas_nodes;
+    if (o.lds_stack) launch_one<F, true, true, true, true>(L, stream, nall);
+    else launch_one<F, true, false, true, true>(L, stream, nall);
+    return hipGetLastError();
+}
 #define RT_VARIANT_DECL(F, COUNT) \
     extern template hipError_t launch_variant<F, COUNT>(const Launch&, const LaunchOpts&, hipStream_t);
 #define RT_VARIANT_F32_DECL(F) \
@@ -2343,6 +2438,8 @@ RT_VARIANT_F32_DECL(FEAT_SET_RECTINST)
 RT_VARIANT_F32_DECL(FEAT_SET_MEDIA)
 RT_VARIANT_F32_DECL(FEAT_SET_FINAL)
 RT_VARIANT_F32_DECL(FEAT_ALL)
+extern template hipError_t launch_variant_f32_count<FEAT_SET_SPHERES>(const Launch&, const LaunchOpts&, hipStream_t);
+extern template hipError_t launch_variant_f32_count<FEAT_SET_FINAL>(const Launch&, const LaunchOpts&, hipStream_t);
 #undef RT_VARIANT_DECL
 #undef RT_VARIANT_F32_DECL
 

@@ -182,6 +182,11 @@ hipError_t launch_trace(const SceneDev& S, const KParams& Ph, const KParams* P, 
         if (e != hipSuccess) return e;
     }
     const uint32_t f = variant_features(o.features);
+    if (o.f32 && o.count) {
+        if (f == FEAT_SET_SPHERES) return launch_variant_f32_count<FEAT_SET_SPHERES>(L, o, stream);
+        if (f == FEAT_SET_FINAL) return launch_variant_f32_count<FEAT_SET_FINAL>(L, o, stream);
+        return hipErrorNotSupported;
+    }
     if (o.f32) {
         if (f == FEAT_SET_SPHERES) return launch_variant_f32<FEAT_SET_SPHERES>(L, o, stream);
         if (f == FEAT_SET_RECTINST) return launch_variant_f32<FEAT_SET_RECTINST>(L, o, stream);

@@ -26,6 +26,7 @@ struct SceneDev {
     int32_t n_lds_nodes;    // the first n TLAS nodes (BFS order, nodes[0, n)) are copied into LDS
     int32_t n_tlas_nodes;   // TLAS size (its nodes are nodes[0, n_tlas_nodes))
     int32_t has_spheres;    // any Sphere / MovingSphere: rays need 1/|d|^2 for the root divisions
+    int32_t has_lights;     // any DiffuseLight material (else no hit emits: the random scene)
     int32_t n_lds_materials;  // > 0: the material and texture tables are staged in LDS after the
     int32_t n_lds_textures;   // TLAS nodes (the kernel variants with rects or media; small tables)
     // A leaf the cast tests before the TLAS walk (0: none): a root child holding a primitive
@@ -40,6 +41,11 @@ struct SceneDev {
     // the TLAS walk's stack entries fit 16 bits (Stack16: node records at LDS byte addresses
     // < 32 KB, i.e. <= 409 TLAS nodes, and leaf codes of <= 1023 leaf slots); set at upload
     int32_t stack16_ok;
+    // BLAS nodes staged in LDS after the TLAS records (variants with instanced BLASes): the device
+    // node array holds one instance BLAS's nodes in BFS order right after the TLAS prefix,
+    // nodes[n_tlas_nodes, n_tlas_nodes + n_blas_bfs) (abi.cpp), and a launch stages the first
+    // n_lds_blas of them (its LDS budget): the nested walk's top levels then read LDS
+    int32_t n_blas_bfs, n_lds_blas;
 };
 
 struct KParams {

@@ -33,18 +33,26 @@
 
 enum Op { F64_FMA, F64_ADD, F64_MUL, F64_RCP, F64_SQRT, F32_FMA, F32_ADD, F32_RCP, I32_ADD, I32_MUL, B32_XOR,
           CNDMASK, MOV_B32, CNDMASK_VCC, CMP_F64, CMP_F32, MAX_F64, MIN_F32, LSHL_B64, CVT_F64_U32, BFE_U32,
-          PK_FMA_F32, MAX3_F32, MED3_F32, N_OPS };
+          PK_FMA_F32, MAX3_F32, MED3_F32, AND_B32, OR_B32, LSHL_B32, LSHR_B32, ALIGNBIT, BITOP3, MOV_B64,
+          CMP_I32, LDEXP_F64, DIV_SCALE_F64, DIV_FMAS_F64, DIV_FIXUP_F64, MAD_U64_U32, LSHL_ADD_U64, LSHR_B64,
+          MBCNT_LO, MUL_HI_U32, CVT_F32_F64, CMP_CLASS_F64, SUB_U32, FMAC_F64, MUL_F32, RSQ_F64, CNDMASK_E32, MIX,
+          N_OPS };
 static const char* kNames[N_OPS] = {"f64_fma", "f64_add", "f64_mul", "f64_rcp", "f64_sqrt", "f32_fma", "f32_add",
                                     "f32_rcp", "i32_add", "i32_mul", "b32_xor", "cndmask", "mov_b32", "cndmask_vcc",
                                     "cmp_f64", "cmp_f32", "max_f64", "min_f32", "lshl_b64", "cvt_f64_u32",
-                                    "bfe_u32", "pk_fma_f32", "max3_f32", "med3_f32"};
+                                    "bfe_u32", "pk_fma_f32", "max3_f32", "med3_f32", "and_b32", "or_b32", "lshl_b32",
+                                    "lshr_b32", "alignbit_b32", "bitop3_b32", "mov_b64", "cmp_i32", "ldexp_f64",
+                                    "div_scale_f64", "div_fmas_f64", "div_fixup_f64", "mad_u64_u32", "lshl_add_u64",
+                                    "lshr_b64", "mbcnt_lo", "mul_hi_u32", "cvt_f32_f64", "cmp_class_f64", "sub_u32",
+                                    "fmac_f64", "mul_f32", "rsq_f64", "cndmask_e32", "mix"};
 
 // Each class as one exact instruction (inline asm): the compiler may not fold repeated
 // adds, pack f32 pairs into v_pk_* or strength-reduce, so the loop issues exactly
 // 8 x NACC wave-instructions of the class per iteration (plus two scalar loop ops).
 template <int OP, int NACC>
 __device__ __forceinline__ void body(double (&d)[8], float (&f)[8], unsigned (&u)[8], unsigned long long (&cm)[8],
-                                     double db, double dc, float fb, float fc, unsigned ub, unsigned long long mask)
+                                     unsigned (&cm2)[8], double db, double dc, float fb, float fc, unsigned ub,
+                                     unsigned long long mask)
 {
 #pragma unroll
     for (int i = 0; i < NACC; ++i) {
@@ -78,6 +86,40 @@ __device__ __forceinline__ void body(double (&d)[8], float (&f)[8], unsigned (&u
             asm volatile("v_pk_fma_f32 %0, %0, %1, %1 op_sel:[0,0,1] op_sel_hi:[1,0,1]" : "+v"(d[i]) : "v"(db));
         if constexpr (OP == MAX3_F32) asm volatile("v_max3_f32 %0, %0, %1, %2" : "+v"(f[i]) : "v"(fb), "v"(fc));
         if constexpr (OP == MED3_F32) asm volatile("v_med3_f32 %0, %0, %1, %2" : "+v"(f[i]) : "v"(fb), "v"(fc));
+        if constexpr (OP == AND_B32) asm volatile("v_and_b32 %0, %0, %1" : "+v"(u[i]) : "v"(ub));
+        if constexpr (OP == OR_B32) asm volatile("v_or_b32 %0, %0, %1" : "+v"(u[i]) : "v"(ub));
+        if constexpr (OP == LSHL_B32) asm volatile("v_lshlrev_b32 %0, 3, %0" : "+v"(u[i]));
+        if constexpr (OP == LSHR_B32) asm volatile("v_lshrrev_b32 %0, 3, %0" : "+v"(u[i]));
+        if constexpr (OP == ALIGNBIT) asm volatile("v_alignbit_b32 %0, %0, %1, 7" : "+v"(u[i]) : "v"(ub));
+        if constexpr (OP == BITOP3) asm volatile("v_bitop3_b32 %0, %0, %1, %1 bitop3:0x96" : "+v"(u[i]) : "v"(ub));
+        if constexpr (OP == MOV_B64) asm volatile("v_mov_b64 %0, %1" : "=v"(d[i]) : "v"(d[(i + 1) & 7]));
+        if constexpr (OP == CMP_I32) asm volatile("v_cmp_lt_i32 %0, %1, %2" : "=s"(cm[i]) : "v"(u[i]), "v"(ub));
+        if constexpr (OP == LDEXP_F64) asm volatile("v_ldexp_f64 %0, %0, 1" : "+v"(d[i]));
+        if constexpr (OP == DIV_SCALE_F64) asm volatile("v_div_scale_f64 %0, vcc, %0, %1, %0" : "+v"(d[i]) : "v"(db) : "vcc");
+        if constexpr (OP == DIV_FMAS_F64) asm volatile("v_div_fmas_f64 %0, %0, %1, %2" : "+v"(d[i]) : "v"(db), "v"(dc));
+        if constexpr (OP == DIV_FIXUP_F64) asm volatile("v_div_fixup_f64 %0, %0, %1, %2" : "+v"(d[i]) : "v"(db), "v"(dc));
+        if constexpr (OP == MAD_U64_U32) asm volatile("v_mad_u64_u32 %0, %1, %2, %3, %0" : "+v"(d[i]), "=s"(cm[i]) : "v"(u[i]), "v"(ub));
+        if constexpr (OP == LSHL_ADD_U64) asm volatile("v_lshl_add_u64 %0, %0, 1, %1" : "+v"(d[i]) : "v"(db));
+        if constexpr (OP == LSHR_B64) asm volatile("v_lshrrev_b64 %0, 1, %0" : "+v"(d[i]));
+        if constexpr (OP == MBCNT_LO) asm volatile("v_mbcnt_lo_u32_b32 %0, %1, %0" : "+v"(u[i]) : "v"(ub));
+        if constexpr (OP == MUL_HI_U32) asm volatile("v_mul_hi_u32 %0, %0, %1" : "+v"(u[i]) : "v"(ub));
+        if constexpr (OP == CVT_F32_F64) asm volatile("v_cvt_f32_f64 %0, %1" : "=v"(f[i]) : "v"(d[i]));
+        if constexpr (OP == CMP_CLASS_F64) asm volatile("v_cmp_class_f64 %0, %1, %2" : "=s"(cm[i]) : "v"(d[i]), "v"(ub));
+        if constexpr (OP == SUB_U32) asm volatile("v_sub_u32 %0, %0, %1" : "+v"(u[i]) : "v"(ub));
+        if constexpr (OP == FMAC_F64) asm volatile("v_fmac_f64 %0, %1, %2" : "+v"(d[i]) : "v"(db), "v"(dc));
+        if constexpr (OP == MUL_F32) asm volatile("v_mul_f32 %0, %0, %1" : "+v"(f[i]) : "v"(fb));
+        if constexpr (OP == RSQ_F64) asm volatile("v_rsq_f64 %0, %0" : "+v"(d[i]));
+        // a select reading vcc that a compare outside the unrolled body wrote (the compiler's
+        // v_cmp ... ; v_cndmask_b32_e32 pairs reuse vcc like this)
+        if constexpr (OP == CNDMASK_E32) asm volatile("v_cndmask_b32_e32 %0, %0, %1, vcc" : "+v"(u[i]) : "v"(ub));
+        // MIX: a fixed sequence of known composition (validates that per-class costs add up):
+        // 1 f64 fma, 1 f64 add, 2 f32 fma, 1 i32 add, 1 xor, 1 mov, 1 cndmask, 1 max3 per accumulator
+        if constexpr (OP == MIX)
+            asm volatile("v_fma_f64 %0, %0, %4, %5\n\tv_add_f64 %0, %0, %4\n\tv_fma_f32 %1, %1, %6, %7\n\t"
+                         "v_fma_f32 %1, %1, %6, %7\n\tv_add_u32 %2, %2, %8\n\tv_xor_b32 %2, %2, %8\n\t"
+                         "v_mov_b32 %3, %2\n\tv_cndmask_b32_e64 %2, %2, %8, %9\n\tv_max3_f32 %1, %1, %6, %7"
+                         : "+v"(d[i]), "+v"(f[i]), "+v"(u[i]), "=v"(cm2[i])
+                         : "v"(db), "v"(dc), "v"(fb), "v"(fc), "v"(ub), "s"(mask));
     }
 }
 
@@ -90,9 +132,11 @@ __global__ void __launch_bounds__(256) calib(const double* __restrict__ in, doub
     float f[8];
     unsigned u[8];
     unsigned long long cm[8];
+    unsigned cm2[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
         cm[i] = 0;
+        cm2[i] = 0;
         d[i] = in[(t + i) & 1023];
         f[i] = (float)d[i];
         u[i] = (unsigned)t * 2654435761u + i;
@@ -108,7 +152,7 @@ __global__ void __launch_bounds__(256) calib(const double* __restrict__ in, doub
     }
     for (int k = 0; k < iters; ++k) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) body<OP, NACC>(d, f, u, cm, db, dc, fb, fc, ub, mask);
+        for (int j = 0; j < 8; ++j) body<OP, NACC>(d, f, u, cm, cm2, db, dc, fb, fc, ub, mask);
     }
     if (threadIdx.x == 0 && blockIdx.x == 0) {
         clk[0] = __builtin_amdgcn_s_memtime() - c0;
@@ -116,7 +160,7 @@ __global__ void __launch_bounds__(256) calib(const double* __restrict__ in, doub
     }
     double acc = 0.0;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) acc += d[i] + (double)f[i] + (double)u[i] + (double)(cm[i] & 1u);
+    for (int i = 0; i < 8; ++i) acc += d[i] + (double)f[i] + (double)u[i] + (double)(cm[i] & 1u) + (double)cm2[i];
     out[t] = acc;
 }
 
@@ -160,6 +204,16 @@ static void run_modes(const std::vector<std::string>& modes, int cus, double* di
     for (const auto& m : modes) run<OP>(m.c_str(), cus, din, dout, dclk, m == "sat" ? iters : iters * 2);
 }
 
+template <int OP, class W>
+static void dispatch(const W& want, const std::vector<std::string>& modes, int cus, double* din, double* dout,
+                     unsigned long long* dclk, int iters)
+{
+    if constexpr (OP < N_OPS) {
+        if (want(OP)) run_modes<OP>(modes, cus, din, dout, dclk, iters);
+        dispatch<OP + 1>(want, modes, cus, din, dout, dclk, iters);
+    }
+}
+
 int main(int argc, char** argv)
 {
     // usage: valu_calib [ops,comma,separated|all] [modes: sat,one,lat] [iters]
@@ -192,30 +246,7 @@ int main(int argc, char** argv)
     CHECK(hipMalloc(&dclk, 2 * sizeof(unsigned long long)));
     CHECK(hipMemcpy(din, h.data(), h.size() * sizeof(double), hipMemcpyHostToDevice));
     auto want = [&](int op) { return ops == "all" || ("," + ops + ",").find("," + std::string(kNames[op]) + ",") != std::string::npos; };
-    if (want(F64_FMA)) run_modes<F64_FMA>(modes, cus, din, dout, dclk, iters);
-    if (want(F64_ADD)) run_modes<F64_ADD>(modes, cus, din, dout, dclk, iters);
-    if (want(F64_MUL)) run_modes<F64_MUL>(modes, cus, din, dout, dclk, iters);
-    if (want(F64_RCP)) run_modes<F64_RCP>(modes, cus, din, dout, dclk, iters);
-    if (want(F64_SQRT)) run_modes<F64_SQRT>(modes, cus, din, dout, dclk, iters);
-    if (want(F32_FMA)) run_modes<F32_FMA>(modes, cus, din, dout, dclk, iters);
-    if (want(F32_ADD)) run_modes<F32_ADD>(modes, cus, din, dout, dclk, iters);
-    if (want(F32_RCP)) run_modes<F32_RCP>(modes, cus, din, dout, dclk, iters);
-    if (want(I32_ADD)) run_modes<I32_ADD>(modes, cus, din, dout, dclk, iters);
-    if (want(I32_MUL)) run_modes<I32_MUL>(modes, cus, din, dout, dclk, iters);
-    if (want(B32_XOR)) run_modes<B32_XOR>(modes, cus, din, dout, dclk, iters);
-    if (want(CNDMASK)) run_modes<CNDMASK>(modes, cus, din, dout, dclk, iters);
-    if (want(MOV_B32)) run_modes<MOV_B32>(modes, cus, din, dout, dclk, iters);
-    if (want(CNDMASK_VCC)) run_modes<CNDMASK_VCC>(modes, cus, din, dout, dclk, iters);
-    if (want(CMP_F64)) run_modes<CMP_F64>(modes, cus, din, dout, dclk, iters);
-    if (want(CMP_F32)) run_modes<CMP_F32>(modes, cus, din, dout, dclk, iters);
-    if (want(MAX_F64)) run_modes<MAX_F64>(modes, cus, din, dout, dclk, iters);
-    if (want(MIN_F32)) run_modes<MIN_F32>(modes, cus, din, dout, dclk, iters);
-    if (want(LSHL_B64)) run_modes<LSHL_B64>(modes, cus, din, dout, dclk, iters);
-    if (want(CVT_F64_U32)) run_modes<CVT_F64_U32>(modes, cus, din, dout, dclk, iters);
-    if (want(BFE_U32)) run_modes<BFE_U32>(modes, cus, din, dout, dclk, iters);
-    if (want(PK_FMA_F32)) run_modes<PK_FMA_F32>(modes, cus, din, dout, dclk, iters);
-    if (want(MAX3_F32)) run_modes<MAX3_F32>(modes, cus, din, dout, dclk, iters);
-    if (want(MED3_F32)) run_modes<MED3_F32>(modes, cus, din, dout, dclk, iters);
+    dispatch<0>(want, modes, cus, din, dout, dclk, iters);
     CHECK(hipFree(din));
     CHECK(hipFree(dout));
     CHECK(hipFree(dclk));

@@ -13,7 +13,8 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 
 PHASES = [("refill", 20), ("ray generation (camera + scatter draws)", 3), ("ray set-up (finish_ray)", 15),
-          ("walk prologue (pre-leaf test)", 16), ("node loops", 8), ("leaf tests", 9), ("hit record", 17),
+          ("walk prologue (pre-leaf test)", 16), ("node loops", 8), ("leaf tests", 9),
+          ("deferred instance walks", 22), ("hit record", 17),
           ("shading (emission)", 5)]
 
 
@@ -32,12 +33,14 @@ def main():
     cam, bg = rt.scene_camera(a.scene, a.width, a.height)
     r = rt.Renderer(0)
     r.upload(world)
+    if a.precision == "f32":
+        r.set_precision(rt.RT_PREC_F32)
     p = rt.Renderer.params(a.width, a.height, a.spp, a.depth, bg, 1, count_work=1)
     r.render(cam, p)
     st = r.stats()
     c = [int(x) for x in r.counters()]
     tot = max(c[21], 1)
-    print(f"scene {a.scene} {a.width}x{a.height}x{a.spp} depth {a.depth}: waves/SIMD {st.waves_per_simd}, "
+    print(f"scene {a.scene} {a.width}x{a.height}x{a.spp} depth {a.depth} {a.precision}: waves/SIMD {st.waves_per_simd}, "
           f"casts/sample {st.casts / st.samples:.3f}, nodes/cast {st.node_visits / max(st.casts, 1):.2f}, "
           f"prims/cast {st.prim_tests / max(st.casts, 1):.2f}")
     acc = 0

@@ -45,7 +45,13 @@ CLASS_PROXY = {"f64_add": ["f64_add"], "f64_mul": ["f64_mul"], "f64_fma": ["f64_
 # the mean of the calibration ops that hit no class counter; bounds from their min / max
 CALIB_OPS = ["f64_fma", "f64_add", "f64_mul", "f64_rcp", "f64_sqrt", "f32_fma", "f32_add", "f32_rcp", "i32_add",
              "i32_mul", "b32_xor", "cndmask", "mov_b32", "cndmask_vcc", "cmp_f64", "cmp_f32", "max_f64", "min_f32",
-             "lshl_b64", "cvt_f64_u32", "bfe_u32"]
+             "lshl_b64", "cvt_f64_u32", "bfe_u32", "pk_fma_f32", "max3_f32", "med3_f32", "and_b32", "or_b32",
+             "lshl_b32", "lshr_b32", "alignbit_b32", "bitop3_b32", "mov_b64", "cmp_i32", "ldexp_f64", "div_scale_f64",
+             "div_fmas_f64", "div_fixup_f64", "mad_u64_u32", "lshl_add_u64", "lshr_b64", "mbcnt_lo", "mul_hi_u32",
+             "cvt_f32_f64", "cmp_class_f64", "sub_u32", "fmac_f64", "mul_f32", "rsq_f64", "cndmask_e32", "mix"]
+# the MIX kernel's composition per accumulator-step (scripts/calib/valu_calib.hip): the model's
+# prediction for it (sum of calibrated costs) against its measured rate validates additivity
+MIX = {"f64_fma": 1, "f64_add": 1, "f32_fma": 2, "i32_add": 1, "b32_xor": 1, "mov_b32": 1, "cndmask": 1, "max3_f32": 1}
 
 
 def read_counters(d, select):
@@ -97,7 +103,7 @@ def calib(d, tag):
              "clock / class instructions issued. 'one' = one wave per SIMD, 'lat' = one dependent chain.", "",
              "| op | cyc/inst PMC (sat) | clock GHz (PMC) | counters hit | ACTIVE_INST_VALU x4 / SIMD-cycles | "
              "cyc/inst timing sat | one | lat |", "|---|---|---|---|---|---|---|---|"]
-    rates, unclassed = {}, []
+    rates, unclassed, hit_map = {}, [], {}
     for op in CALIB_OPS:
         c = counters.get(op, {})
         t = {m: x for x in timing if x["op"] == op for m in [x["mode"]]}
@@ -111,23 +117,33 @@ def calib(d, tag):
                 if k.startswith("SQ_INSTS_VALU_") and v > 0.5 * c.get("SQ_INSTS_VALU", 1e30)]
         sat = t.get("sat", {}).get("cycles_per_inst_per_simd")
         rates[op] = cyc if cyc is not None else sat
-        if c and not hits and op != "cndmask_vcc":   # cndmask_vcc: a v_cmp + v_cndmask pair (2 instructions)
+        if c and not hits and op not in ("cndmask_vcc", "mix", "cndmask_e32"):   # pairs / mixes: not one op
             unclassed.append(op)
+        hit_map[op] = hits
         lines.append(f"| {op} | {cyc if cyc is None else round(cyc, 3)} | "
                      f"{'' if cyc is None else round(clk, 3)} | {', '.join(hits)} | "
                      f"{'' if cyc is None else round(busy, 3)} | {sat if sat is None else round(sat, 3)} | "
                      f"{round(t['one']['cycles_per_inst_per_simd'], 3) if 'one' in t else ''} | "
                      f"{round(t['lat']['cycles_per_inst_per_simd'], 3) if 'lat' in t else ''} |")
+    # the mix: predicted (sum of its instructions' calibrated costs) vs measured cycles per step
+    mix_line = None
+    if rates.get("mix") and all(rates.get(o) for o in MIX):
+        n = sum(MIX.values())
+        pred = sum(k * rates[o] for o, k in MIX.items()) / n   # per instruction
+        mix_line = (f"mix kernel ({n} instructions per step: {MIX}): measured {rates['mix']:.3f} cycles per "
+                    f"instruction, sum of calibrated costs {pred:.3f} -> ratio {rates['mix'] / pred:.3f}")
     proxies = dict(CLASS_PROXY, other=unclassed)
     cyc = {cls: statistics.mean(rates[o] for o in ps) for cls, ps in proxies.items()}
     other_range = [min(rates[o] for o in unclassed), max(rates[o] for o in unclassed)]
     lines += ["", "Cycles per wave-instruction used by the roofline (class <- calibration kernel(s)):", ""]
     lines += [f"- {cls}: {cyc[cls]:.3f} <- {', '.join(proxies[cls])}" for cls in proxies]
     lines += [f"- other: range {other_range[0]:.3f} .. {other_range[1]:.3f} (bounds of the roofline fraction)"]
+    if mix_line:
+        lines += ["", mix_line]
     doc = load()
     doc["calibration"] = {"tag": tag, "cycles_per_inst": cyc, "other_range": other_range,
                           "class_counters": CLASS_COUNTERS, "proxies": proxies,
-                          "raw": {o: rates[o] for o in CALIB_OPS}}
+                          "raw": {o: rates.get(o) for o in CALIB_OPS}, "hits": hit_map, "mix": mix_line}
     json.dump(doc, open(OUT_JSON, "w"), indent=1)
     open(os.path.join(REPO, "profiles", f"{tag}_valu_calib.md"), "w").write("\n".join(lines) + "\n")
     print("\n".join(lines))
@@ -188,9 +204,17 @@ def bench(d, tag, workload, note=""):
     if cal:
         import bench as bn
         need = bn.valu_issue_cycles(c, cal)
-        lines.append(f"VALU issue cycles the mix needs (calibration `{cal['tag']}`) = {need:.4g} SIMD-cycles; "
+        lines.append(f"VALU issue cycles the mix needs (calibration `{cal['tag']}` class means) = {need:.4g} SIMD-cycles; "
                      f"launch = {N_SIMDS} x {cycles:.4g} = {N_SIMDS * cycles:.4g} -> VALU issue roofline "
                      f"fraction {need / (N_SIMDS * cycles):.3f}")
+        m = re.search(r"Cfg<(\d+)u, (\w+), (\w+), (\w+), (\w+), (\w+)>, (true|false)>", knames[kern])
+        isa = (bn.isa_prices(entry["src_hash"], int(m.group(1)), 2 if m.group(7) == "true" else 1,
+                             int(m.group(2) == "true"), int(m.group(4) == "true")) if m else None)
+        if isa:
+            fr = [bn.valu_issue_cycles(c, cal, isa=isa, bound=b) / (N_SIMDS * cycles) for b in (0, -1, 1)]
+            lines.append(f"priced from the kernel's own instruction mix (profiles/isa_mix.json): fraction {fr[0]:.3f} "
+                         f"(classes at their low / high static-mix prices: {fr[1]:.3f} .. {fr[2]:.3f}); the additive "
+                         f"model's check on a saturated mixed stream: {cal.get('mix')}")
         lines.append(f"(naive 4 x SQ_ACTIVE_INST_VALU / SIMD-cycles = "
                      f"{4 * c.get('SQ_ACTIVE_INST_VALU', 0) / (N_SIMDS * cycles):.3f})")
     open(os.path.join(REPO, "profiles", f"{tag}_pmc.md"), "w").write("\n".join(lines) + "\n")

@@ -68,8 +68,16 @@ def test_f32_mode_all_scenes_and_schedules(rt, renderer):
             imgs.append(renderer.render(cam, rt.Renderer.params(40, 30, 8, 50, bg, 1, out_format=rt.RT_OUT_F64)))
         shard = renderer.render(cam, rt.Renderer.params(40, 30, 8, 50, bg, 1, row_begin=1, row_stride=3,
                                                         out_format=rt.RT_OUT_F64))
+        # count_work in the f32 mode: the final-scene (and spheres) variants have one
+        renderer.render(cam, rt.Renderer.params(40, 30, 8, 50, bg, 1, count_work=1, out_format=rt.RT_OUT_F64))
+        st = renderer.stats()
+        assert st.casts >= 40 * 30 * 8 and st.node_visits > 0 and st.prim_tests > 0
+        assert renderer.counters()[21] > 0   # phase timers ran
+        cornell = rt.World(1).build_scene(5)
+        renderer.upload(cornell)
         with pytest.raises(rt.RTError, match="UNSUPPORTED"):
             renderer.render(cam, rt.Renderer.params(40, 30, 8, 50, bg, 1, count_work=1, out_format=rt.RT_OUT_F64))
+        renderer.upload(world)
     finally:
         renderer.set_precision(rt.RT_PREC_F64)
         renderer.set_schedule(rt.RT_SCHED_AUTO)
