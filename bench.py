@@ -138,6 +138,16 @@ def isa_prices(src_hash, variant_features, schedule, slab32=1, nall=1):
     return {c: (v["price"], v["range"][0], v["range"][1]) for c, v in e["classes"].items()}
 
 
+KMIX_OF = {0: "kmix_c2", 287: "kmix_c4"}   # variant -> calibration replay of its VALU mix (scripts/calib/gen_kmix.py)
+
+
+def replay_price(calib, variant_features):
+    """Cycles per VALU instruction of the variant's own instruction mix replayed as a saturated
+    calibration stream (KMIX_*), or None."""
+    k = (calib.get("kmix") or {}).get(KMIX_OF.get(variant_features, ""))
+    return k["measured"] if k else None
+
+
 def valu_issue_cycles(counts, calib, other=None, isa=None, bound=0):
     """Issue cycles (summed over SIMDs) the launch's VALU instruction mix needs at the
     calibrated saturated rates: sum over classes of count x cycles per wave-instruction; the
@@ -284,17 +294,21 @@ def main():
                 "traffic": None, "src_hash": src_hash}
     if pmc is not None and calib is not None:
         isa = isa_prices(src_hash, last.variant_features, last.schedule, last.slab32, int(last.lds_nodes > 0))
-        need = valu_issue_cycles(pmc["counters"], calib, isa=isa)   # SIMD-cycles of VALU issue per launch
+        additive = valu_issue_cycles(pmc["counters"], calib, isa=isa)   # SIMD-cycles of VALU issue per launch
+        rp = replay_price(calib, last.variant_features)
+        # the kernel's mix replayed at saturation issues below the sum of its classes' costs
+        # (calibration 'kmix'): price the launch at the replay's measured rate when there is one
+        need = pmc["counters"]["SQ_INSTS_VALU"] * rp if rp else additive
         clk = pmc["clock_ghz"]                                   # the clock the chip held in that pass
         achieved = need / (k_ms * 1e-3) / 1e9                    # per live-timed launch
         peak = N_SIMDS * clk
         dram = pmc["dram_bytes"]
         if isa:   # each class at the low / high end of its static-mix price
-            lo, hi = (valu_issue_cycles(pmc["counters"], calib, isa=isa, bound=b) / (k_ms * 1e-3) / 1e9 / peak
-                      for b in (-1, 1))
+            ests = [valu_issue_cycles(pmc["counters"], calib, isa=isa, bound=b) for b in (-1, 0, 1)]
         else:
-            lo, hi = (valu_issue_cycles(pmc["counters"], calib, o) / (k_ms * 1e-3) / 1e9 / peak
-                      for o in calib.get("other_range", [calib["cycles_per_inst"]["other"]] * 2))
+            ests = [valu_issue_cycles(pmc["counters"], calib, o)
+                    for o in calib.get("other_range", [calib["cycles_per_inst"]["other"]] * 2)]
+        lo, hi = (x / (k_ms * 1e-3) / 1e9 / peak for x in (min(ests + [need]), max(ests + [need])))
         roofline.update({
             "achieved": round(achieved, 1), "peak": round(peak, 1), "frac": round(achieved / peak, 4),
             "traffic": int(dram),
@@ -305,9 +319,14 @@ def main():
             "frac_range": [round(lo, 4), round(hi, 4)],
             "useful_frac": round(achieved / peak * pmc["counters"]["SQ_THREAD_CYCLES_VALU"] /
                                  (64.0 * pmc["counters"]["SQ_INSTS_VALU"]), 4),
-            "pricing": ("per-class prices from this kernel's instruction mix (profiles/isa_mix.json)" if isa
+            "pricing": ("SQ_INSTS_VALU x the measured cycles per instruction of this kernel's VALU mix replayed "
+                        "at saturation (%s, %.3f); frac_range spans it and the additive per-class model" %
+                        (KMIX_OF[last.variant_features], rp) if rp else
+                        "per-class prices from this kernel's instruction mix (profiles/isa_mix.json)" if isa
                         else "calibration class means, 'other' bounded by its cheapest / dearest op"),
-            "model_check": calib.get("mix"),
+            "additive_frac": round(additive / (k_ms * 1e-3) / 1e9 / peak, 4),
+            "model_check": {"mix": calib.get("mix"),
+                            **{k: round(v["ratio"], 4) for k, v in (calib.get("kmix") or {}).items()}},
             "pmc_tag": pmc.get("tag"), "pmc_kernel_ms": pmc.get("kernel_ms"), "clock_ghz": clk})
     else:
         roofline["note"] = "no PMC pass of this build (source hash) and workload in profiles/pmc_r02.json"

@@ -36,7 +36,7 @@ enum Op { F64_FMA, F64_ADD, F64_MUL, F64_RCP, F64_SQRT, F32_FMA, F32_ADD, F32_RC
           PK_FMA_F32, MAX3_F32, MED3_F32, AND_B32, OR_B32, LSHL_B32, LSHR_B32, ALIGNBIT, BITOP3, MOV_B64,
           CMP_I32, LDEXP_F64, DIV_SCALE_F64, DIV_FMAS_F64, DIV_FIXUP_F64, MAD_U64_U32, LSHL_ADD_U64, LSHR_B64,
           MBCNT_LO, MUL_HI_U32, CVT_F32_F64, CMP_CLASS_F64, SUB_U32, FMAC_F64, MUL_F32, RSQ_F64, CNDMASK_E32, MIX,
-          N_OPS };
+          KMIX_C2, KMIX_C4, N_OPS };
 static const char* kNames[N_OPS] = {"f64_fma", "f64_add", "f64_mul", "f64_rcp", "f64_sqrt", "f32_fma", "f32_add",
                                     "f32_rcp", "i32_add", "i32_mul", "b32_xor", "cndmask", "mov_b32", "cndmask_vcc",
                                     "cmp_f64", "cmp_f32", "max_f64", "min_f32", "lshl_b64", "cvt_f64_u32",
@@ -44,18 +44,28 @@ static const char* kNames[N_OPS] = {"f64_fma", "f64_add", "f64_mul", "f64_rcp", 
                                     "lshr_b32", "alignbit_b32", "bitop3_b32", "mov_b64", "cmp_i32", "ldexp_f64",
                                     "div_scale_f64", "div_fmas_f64", "div_fixup_f64", "mad_u64_u32", "lshl_add_u64",
                                     "lshr_b64", "mbcnt_lo", "mul_hi_u32", "cvt_f32_f64", "cmp_class_f64", "sub_u32",
-                                    "fmac_f64", "mul_f32", "rsq_f64", "cndmask_e32", "mix"};
+                                    "fmac_f64", "mul_f32", "rsq_f64", "cndmask_e32", "mix", "kmix_c2",
+                                    "kmix_c4"};
+
+// KMIX_*: a trace kernel's own VALU mix replayed (scripts/calib/gen_kmix.py writes the op
+// sequences from its PMC class shares and ISA): each accumulator runs the whole sequence
+template <int... OPS>
+struct Seq {
+};
+#include "kmix_seq.h"
 
 // Each class as one exact instruction (inline asm): the compiler may not fold repeated
 // adds, pack f32 pairs into v_pk_* or strength-reduce, so the loop issues exactly
 // 8 x NACC wave-instructions of the class per iteration (plus two scalar loop ops).
-template <int OP, int NACC>
-__device__ __forceinline__ void body(double (&d)[8], float (&f)[8], unsigned (&u)[8], unsigned long long (&cm)[8],
-                                     unsigned (&cm2)[8], double db, double dc, float fb, float fc, unsigned ub,
-                                     unsigned long long mask)
+#define CALIB_ARGS                                                                                             \
+    double(&d)[8], float(&f)[8], unsigned(&u)[8], unsigned long long(&cm)[8], unsigned(&cm2)[8], double db,     \
+        double dc, float fb, float fc, unsigned ub, unsigned long long mask
+#define CALIB_PASS d, f, u, cm, cm2, db, dc, fb, fc, ub, mask
+
+template <int OP>
+__device__ __forceinline__ void one(int i, CALIB_ARGS)
 {
-#pragma unroll
-    for (int i = 0; i < NACC; ++i) {
+    {
         if constexpr (OP == F64_FMA) asm volatile("v_fma_f64 %0, %0, %1, %2" : "+v"(d[i]) : "v"(db), "v"(dc));
         if constexpr (OP == F64_ADD) asm volatile("v_add_f64 %0, %0, %1" : "+v"(d[i]) : "v"(db));
         if constexpr (OP == F64_MUL) asm volatile("v_mul_f64 %0, %0, %1" : "+v"(d[i]) : "v"(db));
@@ -121,6 +131,29 @@ __device__ __forceinline__ void body(double (&d)[8], float (&f)[8], unsigned (&u
                          : "+v"(d[i]), "+v"(f[i]), "+v"(u[i]), "=v"(cm2[i])
                          : "v"(db), "v"(dc), "v"(fb), "v"(fc), "v"(ub), "s"(mask));
     }
+}
+
+template <int OP, int NACC>
+__device__ __forceinline__ void each_acc(CALIB_ARGS)
+{
+#pragma unroll
+    for (int i = 0; i < NACC; ++i) one<OP>(i, CALIB_PASS);
+}
+
+// a sequence op by op, each over the accumulators (consecutive instructions independent: a
+// dependent chain across inline-asm statements gets a hazard s_nop after each one)
+template <int NACC, int... OPS>
+__device__ __forceinline__ void seq_all(Seq<OPS...>, CALIB_ARGS)
+{
+    (each_acc<OPS, NACC>(CALIB_PASS), ...);
+}
+
+template <int OP, int NACC>
+__device__ __forceinline__ void body(CALIB_ARGS)
+{
+    if constexpr (OP == KMIX_C2) seq_all<NACC>(Seq<KMIX_C2_SEQ>{}, CALIB_PASS);
+    else if constexpr (OP == KMIX_C4) seq_all<NACC>(Seq<KMIX_C4_SEQ>{}, CALIB_PASS);
+    else each_acc<OP, NACC>(CALIB_PASS);
 }
 
 template <int OP, int NACC>

@@ -48,7 +48,7 @@ CALIB_OPS = ["f64_fma", "f64_add", "f64_mul", "f64_rcp", "f64_sqrt", "f32_fma", 
              "lshl_b64", "cvt_f64_u32", "bfe_u32", "pk_fma_f32", "max3_f32", "med3_f32", "and_b32", "or_b32",
              "lshl_b32", "lshr_b32", "alignbit_b32", "bitop3_b32", "mov_b64", "cmp_i32", "ldexp_f64", "div_scale_f64",
              "div_fmas_f64", "div_fixup_f64", "mad_u64_u32", "lshl_add_u64", "lshr_b64", "mbcnt_lo", "mul_hi_u32",
-             "cvt_f32_f64", "cmp_class_f64", "sub_u32", "fmac_f64", "mul_f32", "rsq_f64", "cndmask_e32", "mix"]
+             "cvt_f32_f64", "cmp_class_f64", "sub_u32", "fmac_f64", "mul_f32", "rsq_f64", "cndmask_e32", "mix", "kmix_c2", "kmix_c4"]
 # the MIX kernel's composition per accumulator-step (scripts/calib/valu_calib.hip): the model's
 # prediction for it (sum of calibrated costs) against its measured rate validates additivity
 MIX = {"f64_fma": 1, "f64_add": 1, "f32_fma": 2, "i32_add": 1, "b32_xor": 1, "mov_b32": 1, "cndmask": 1, "max3_f32": 1}
@@ -117,7 +117,7 @@ def calib(d, tag):
                 if k.startswith("SQ_INSTS_VALU_") and v > 0.5 * c.get("SQ_INSTS_VALU", 1e30)]
         sat = t.get("sat", {}).get("cycles_per_inst_per_simd")
         rates[op] = cyc if cyc is not None else sat
-        if c and not hits and op not in ("cndmask_vcc", "mix", "cndmask_e32"):   # pairs / mixes: not one op
+        if c and not hits and op not in ("cndmask_vcc", "mix", "cndmask_e32", "kmix_c2", "kmix_c4"):   # pairs / mixes: not one op
             unclassed.append(op)
         hit_map[op] = hits
         lines.append(f"| {op} | {cyc if cyc is None else round(cyc, 3)} | "
@@ -132,6 +132,18 @@ def calib(d, tag):
         pred = sum(k * rates[o] for o, k in MIX.items()) / n   # per instruction
         mix_line = (f"mix kernel ({n} instructions per step: {MIX}): measured {rates['mix']:.3f} cycles per "
                     f"instruction, sum of calibrated costs {pred:.3f} -> ratio {rates['mix'] / pred:.3f}")
+    # kernel-mix replays (scripts/calib/gen_kmix.py): the additive model on a trace kernel's own mix
+    kmix = {}
+    kmeta = os.path.join(REPO, "scripts", "calib", "kmix_seq.json")
+    for op, meta in (json.load(open(kmeta)).items() if os.path.exists(kmeta) else []):
+        if rates.get(op) and all(rates.get(o) for o in meta["ops"]):
+            w = {o: k * (2 if o == "cndmask_vcc" else 1) for o, k in meta["ops"].items()}   # instructions
+            n = sum(w.values())
+            pred = sum(k * rates[o] for o, k in w.items()) / n
+            kmix[op] = dict(meta, measured=rates[op], predicted=pred, ratio=rates[op] / pred)
+            lines += ["", f"{op} (replay of `{meta['pmc_entry']}`'s VALU mix, {n} ops: {meta['ops']}): measured "
+                          f"{rates[op]:.3f} cycles per instruction, sum of calibrated costs {pred:.3f} -> ratio "
+                          f"{rates[op] / pred:.3f}"]
     proxies = dict(CLASS_PROXY, other=unclassed)
     cyc = {cls: statistics.mean(rates[o] for o in ps) for cls, ps in proxies.items()}
     other_range = [min(rates[o] for o in unclassed), max(rates[o] for o in unclassed)]
@@ -143,7 +155,8 @@ def calib(d, tag):
     doc = load()
     doc["calibration"] = {"tag": tag, "cycles_per_inst": cyc, "other_range": other_range,
                           "class_counters": CLASS_COUNTERS, "proxies": proxies,
-                          "raw": {o: rates.get(o) for o in CALIB_OPS}, "hits": hit_map, "mix": mix_line}
+                          "raw": {o: rates.get(o) for o in CALIB_OPS}, "hits": hit_map, "mix": mix_line,
+                          "kmix": kmix}
     json.dump(doc, open(OUT_JSON, "w"), indent=1)
     open(os.path.join(REPO, "profiles", f"{tag}_valu_calib.md"), "w").write("\n".join(lines) + "\n")
     print("\n".join(lines))
@@ -215,6 +228,11 @@ def bench(d, tag, workload, note=""):
             lines.append(f"priced from the kernel's own instruction mix (profiles/isa_mix.json): fraction {fr[0]:.3f} "
                          f"(classes at their low / high static-mix prices: {fr[1]:.3f} .. {fr[2]:.3f}); the additive "
                          f"model's check on a saturated mixed stream: {cal.get('mix')}")
+        rp = bn.replay_price(cal, int(m.group(1))) if m else None
+        if rp:
+            lines.append(f"priced at the measured rate of this kernel's mix replayed at saturation "
+                         f"({bn.KMIX_OF[int(m.group(1))]}: {rp:.3f} cycles per instruction): fraction "
+                         f"{c['SQ_INSTS_VALU'] * rp / (N_SIMDS * cycles):.3f}")
         lines.append(f"(naive 4 x SQ_ACTIVE_INST_VALU / SIMD-cycles = "
                      f"{4 * c.get('SQ_ACTIVE_INST_VALU', 0) / (N_SIMDS * cycles):.3f})")
     open(os.path.join(REPO, "profiles", f"{tag}_pmc.md"), "w").write("\n".join(lines) + "\n")
