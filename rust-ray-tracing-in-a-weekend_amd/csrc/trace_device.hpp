@@ -1197,9 +1197,6 @@ __device__ __forceinline__ void medium_finish(const rt_prim& m, const RayT<R>& r
 // spills) and the Cornell variant would drop to 3 waves per SIMD.
 template <class C>
 constexpr bool PreLeaf() { return C::F == FEAT_SET_SPHERES; }
-#ifndef RT_DEFER_INST
-#define RT_DEFER_INST 1
-#endif
 // the variants whose instances can hold a BLAS (a nested walk) defer their first instance test
 template <class C>
 constexpr bool DeferInst() { return RT_DEFER_INST && (C::F & FEAT_INST_BLAS) != 0; }

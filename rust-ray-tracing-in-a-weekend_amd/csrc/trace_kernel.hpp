@@ -5,6 +5,14 @@
 
 #include "rt/rt_scene.h"
 
+// The first instance a cast's top-level walk reaches is tested after that walk (trace_world's
+// DeferInst), its BLAS walk then starting at stack entry 0; shared with the host, which sizes the
+// stack from it (abi.cpp: a scene where no other nested walk can happen needs max(TLAS, BLAS)
+// entries instead of their sum)
+#ifndef RT_DEFER_INST
+#define RT_DEFER_INST 1
+#endif
+
 namespace rtk {
 
 // Device view of the uploaded rt_scene_soa tables.
@@ -21,8 +29,9 @@ struct SceneDev {
     const int32_t* perlin_perm;
     const uint8_t* image;
     int32_t tlas_root;
-    int32_t blas_base;      // first stack entry of a nested (instance) BLAS walk
-    int32_t stack_entries;  // traversal stack entries per lane (TLAS + BLAS walk)
+    int32_t blas_base;      // first stack entry of a BLAS walk nested in the top-level walk
+    int32_t stack_entries;  // traversal stack entries per lane (TLAS + nested BLAS walk, or the
+                            // larger of the two when every BLAS walk is a deferred one: abi.cpp)
     int32_t n_lds_nodes;    // the first n TLAS nodes (BFS order, nodes[0, n)) are copied into LDS
     int32_t n_tlas_nodes;   // TLAS size (its nodes are nodes[0, n_tlas_nodes))
     int32_t has_spheres;    // any Sphere / MovingSphere: rays need 1/|d|^2 for the root divisions
