@@ -123,7 +123,7 @@ def pmc_entry(src_hash, workload):
 
 
 ISA_JSON = os.path.join(REPO, "profiles", "isa_mix.json")
-VARIANT_NAMES = {0: "spheres", 35: "rectinst", 103: "media", 287: "final", 2047: "all"}
+VARIANT_NAMES = {0: "spheres", 35: "rectinst", 103: "media", 287: "final", 4095: "all"}
 
 
 def isa_prices(src_hash, variant_features, schedule, slab32=1, nall=1):

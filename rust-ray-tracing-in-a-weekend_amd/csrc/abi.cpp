@@ -941,6 +941,42 @@ int rt_ctx_upload_soa(rt_ctx* c, const rt_scene_soa* s)
         if (s->textures[i].kind == RT_TEX_NOISE) feat |= rtk::FEAT_NOISE;
         if (s->textures[i].kind == RT_TEX_IMAGE) feat |= rtk::FEAT_IMAGE;
     }
+    // FEAT_IMAGE_UV: an image-textured primitive whose hit record must carry its uv inputs (a rect
+    // or box, or anything under an instance); otherwise uv comes from a top-level sphere's normal
+    if (feat & rtk::FEAT_IMAGE) {
+        auto imaged = [&](const rt_prim& p) {
+            if (p.kind == RT_PRIM_INSTANCE || p.kind == RT_PRIM_MEDIUM) return false;
+            const int m = p.mat;
+            return m >= 0 && m < s->n_materials && s->materials[m].kind != RT_MAT_METAL &&
+                   s->materials[m].kind != RT_MAT_DIELECTRIC && s->materials[m].tex >= 0 &&
+                   s->materials[m].tex < s->n_textures && s->textures[s->materials[m].tex].kind == RT_TEX_IMAGE;
+        };
+        std::vector<uint8_t> under((size_t)s->n_prims, 0);   // reached through an instance
+        for (int i = 0; i < s->n_instances; ++i) {
+            const rt_instance& in = s->instances[i];
+            if (in.child_kind == RT_CHILD_PRIM) {
+                under[(size_t)in.child] = 1;
+                continue;
+            }
+            std::vector<int> todo{in.child};
+            while (!todo.empty()) {
+                const int ref = todo.back();
+                todo.pop_back();
+                if (ref >= 0) {
+                    todo.push_back(s->nodes[ref].child[0]);
+                    todo.push_back(s->nodes[ref].child[1]);
+                    continue;
+                }
+                const int code = ~ref;
+                for (int j = code >> 5; j < (code >> 5) + (code & 31); ++j) under[(size_t)s->prim_refs[j]] = 1;
+            }
+        }
+        for (int i = 0; i < s->n_prims; ++i) {
+            const rt_prim& p = s->prims[i];
+            if (imaged(p) && (under[(size_t)i] || (p.kind != RT_PRIM_SPHERE && p.kind != RT_PRIM_MOVING_SPHERE)))
+                feat |= rtk::FEAT_IMAGE_UV;
+        }
+    }
     if (general_shutter) feat |= rtk::FEAT_SHUTTER;
     // FEAT_NEST_MOVING: a sphere that really moves (nonzero velocity, or a shutter other than
     // [0, 1], whose centre may not be c0) under an instance or inside a medium boundary; without
@@ -1237,6 +1273,11 @@ static int run_range(rt_ctx* c, const rt_camera* cam, const rt_render_params* p,
         K.sample_begin = b0;
         K.spp = b1;
         K.n_chunks = (b1 - b0 + chunk - 1) / chunk;
+        {
+            const unsigned g = o.pool == RT_SCHED_ITEMS ? (unsigned)K.block_chunks : (unsigned)K.block_samples;
+            const unsigned n = o.pool == RT_SCHED_ITEMS ? (unsigned)K.n_chunks : (unsigned)(K.spp - K.sample_begin);
+            K.n_work_blocks = (unsigned)K.tiles_x * (unsigned)K.tiles_y * ((n + g - 1) / std::max(g, 1u));
+        }
         rtk::KParams* dK = c->params + c->param_slot;
         c->param_slot = (c->param_slot + 1) % kParamSlots;
         HIP_TRY(hipMemcpyAsync(dK, &K, sizeof K, hipMemcpyHostToDevice, stream));

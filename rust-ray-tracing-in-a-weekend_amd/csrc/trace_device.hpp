@@ -192,15 +192,38 @@ using InstMedC = CfgDropStatic<C, FEAT_INST_MEDIUM>;   // a medium under an inst
 // Traversal stack. LDS: a lane-interleaved dynamic LDS array [entry][256 threads]
 // (consecutive lanes hit consecutive banks) sized per scene by the host (TLAS depth +
 // BLAS depth); scratch: a private array (deep scenes).
-template <bool LDS>
+extern __shared__ int rt_lds[];  // [cached TLAS nodes] [stack entries x 256 lanes] [materials, textures]
+#ifndef RT_STACK_REMAT
+#define RT_STACK_REMAT 1
+#endif
+// The lane's index in its wave, recomputed where it is used (volatile: not CSE'd into one
+// value that stays live through the bounce loop; at 128 VGPRs the final variant spilled the
+// stack base it replaces and reloaded it from scratch at every walk)
+__device__ __forceinline__ int lane_remat()
+{
+    int l;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+    return l;
+}
+template <bool LDS, bool REMAT = false>
 struct Stack;
 template <>
-struct Stack<true> {
-    int* base;
-    __device__ __forceinline__ int& operator[](int i) const { return base[i * 256]; }
+struct Stack<true, true> {   // the variants with nested walks (128 VGPRs)
+    int wave0;   // rt_lds index of this wave's lane 0, entry 0 (wave-uniform: an SGPR)
+    __device__ __forceinline__ int& operator[](int i) const { return rt_lds[wave0 + lane_remat() + i * 256]; }
+    __device__ __forceinline__ void init(int stack_off)
+    {
+        wave0 = stack_off + __builtin_amdgcn_readfirstlane((int)threadIdx.x & ~63);
+    }
 };
 template <>
-struct Stack<false> {
+struct Stack<true, false> {   // (Cornell variants: the remat costs 0.3-0.9 %, nothing spills)
+    int* base;
+    __device__ __forceinline__ int& operator[](int i) const { return base[i * 256]; }
+    __device__ __forceinline__ void init(int stack_off) { base = rt_lds + stack_off + threadIdx.x; }
+};
+template <>
+struct Stack<false, false> {
     int v[66];   // 32 + 32 entries + the two walks' RT_DONE sentinels
     __device__ __forceinline__ int& operator[](int i) { return v[i]; }
 };
@@ -228,8 +251,8 @@ constexpr bool Stack16Cfg()
 // 45.8 to 33.3 KB, so 4 blocks (4 waves per SIMD) share a CU instead of 3; the BLAS walk's leaf
 // codes are relative to the BLAS's first slot, rt_instance.pad on the device, abi.cpp)
 template <class C>
-using StackT = typename std::conditional<Stack16Cfg<C>(), Stack16, Stack<C::LDS>>::type;
-extern __shared__ int rt_lds[];  // [cached TLAS nodes] [stack entries x 256 lanes] [materials, textures]
+using StackT = typename std::conditional<Stack16Cfg<C>(), Stack16,
+                                         Stack<C::LDS, C::LDS && RT_STACK_REMAT && (C::F & FEAT_INST_BLAS) != 0>>::type;
 
 // Division by a value b used many times, through its correctly rounded reciprocal
 // y = RN(1/b): q0 = RN(q*y), then one correction q1 = RN(q0 + RN-exact(q - b*q0) * y).
@@ -405,6 +428,16 @@ __device__ __forceinline__ bool sphere_t(double cx, double cy, double cz, double
     return true;
 }
 
+// Whether hit records carry the texture coordinates' inputs (uv0..uv3). Without FEAT_IMAGE_UV
+// the only image-textured primitives are top-level spheres, whose outward normal — the
+// sphere_uv input — is the record's normal, negated back when the hit was on the back face
+// (exact): the final scene's records then keep 8 VGPRs fewer live across the bounce loop.
+template <class C>
+constexpr bool UVStore()
+{
+    return (C::F & FEAT_IMAGE) != 0 && (C::F & FEAT_IMAGE_UV) != 0;
+}
+
 // hittable.rs:275-287
 template <class C, class R = typename C::Real>
 __device__ __forceinline__ void sphere_finish(R cx, R cy, R cz, R inv_r, const RayT<R>& r, R t, int mat, HitT<R>& h)
@@ -417,7 +450,7 @@ __device__ __forceinline__ void sphere_finish(R cx, R cy, R cz, R inv_r, const R
     set_face_normal(h, r.dx, r.dy, r.dz, onx, ony, onz);
     h.mat = mat;
     h.uvkind = 1;
-    if constexpr ((C::F & FEAT_IMAGE) != 0) {
+    if constexpr (UVStore<C>()) {
         h.uv0 = onx;
         h.uv1 = ony;
         h.uv2 = onz;
@@ -482,7 +515,7 @@ __device__ __forceinline__ void rect_finish(int axis, R a0, R a1, R b0, R b1, co
     R ok, dk, oa, da, ob, db;
     rect_axes(axis, r, ok, dk, oa, da, ob, db);
     h.uvkind = 2;
-    if constexpr ((C::F & FEAT_IMAGE) != 0) {
+    if constexpr (UVStore<C>()) {
         const R x = oa + t * da;
         const R y = ob + t * db;
         h.uv0 = x - a0;
@@ -1389,12 +1422,18 @@ __device__ __forceinline__ R clampd(R x, R mn, R mx)
     return x;
 }
 
-template <class R>
+template <class C, class R>
 __device__ void hit_uv(const HitT<R>& h, R& u, R& v)
 {
     if (h.uvkind == 1) {  // sphere_uv (math.rs:288-300)
-        const R theta = r_acos(-h.uv1);
-        const R phi = r_atan2(-h.uv2, h.uv0) + (R)RT_PI;
+        R ox = h.uv0, oy = h.uv1, oz = h.uv2;
+        if constexpr (!UVStore<C>()) {   // the outward normal (set_face_normal negated it on a back face)
+            ox = h.front ? h.nx : -h.nx;
+            oy = h.front ? h.ny : -h.ny;
+            oz = h.front ? h.nz : -h.nz;
+        }
+        const R theta = r_acos(-oy);
+        const R phi = r_atan2(-oz, ox) + (R)RT_PI;
         u = phi / ((R)2 * (R)RT_PI);
         v = theta / (R)RT_PI;
     } else if (h.uvkind == 2) {
@@ -1457,7 +1496,7 @@ __device__ void tex_value(const SceneDev& S, int ti, const HitT<R>& h, R& cr, R&
     default: {
         if (t.img_w <= 0 || t.img_h <= 0) { cr = (R)0; cg = (R)1; cb = (R)1; return; }
         R u, v;
-        hit_uv(h, u, v);
+        hit_uv<C>(h, u, v);
         u = clampd(u, (R)0, (R)1);
         v = (R)1 - clampd(v, (R)0, (R)1);
         uint64_t i = r_sat_u64(u * (R)t.img_w);
@@ -1881,7 +1920,7 @@ __global__ void __launch_bounds__(256, min_waves<C>()) trace_chunks(SceneDev S, 
     if (!lane_work(P, w)) return;
     StackT<C> stack;
     if constexpr (Stack16Cfg<C>()) stack.base = reinterpret_cast<short*>(rt_lds + lds_stack_offset<C>(S)) + threadIdx.x;
-    else if constexpr (C::LDS) stack.base = rt_lds + lds_stack_offset<C>(S) + threadIdx.x;
+    else if constexpr (C::LDS) stack.init((int)lds_stack_offset<C>(S));
     Count cnt{};
     uint64_t t_cam = 0, t_trace = 0, t_shade = 0, t_prev = 0;
     if (C::COUNT) t_prev = __builtin_amdgcn_s_memtime();
@@ -2005,7 +2044,7 @@ __global__ void __launch_bounds__(256, min_waves<C>()) trace_pool(SceneDev S, co
     stage_lds<C>(S);
     StackT<C> stack;
     if constexpr (Stack16Cfg<C>()) stack.base = reinterpret_cast<short*>(rt_lds + lds_stack_offset<C>(S)) + threadIdx.x;
-    else if constexpr (C::LDS) stack.base = rt_lds + lds_stack_offset<C>(S) + threadIdx.x;
+    else if constexpr (C::LDS) stack.init((int)lds_stack_offset<C>(S));
     Count cnt{};
     uint64_t t_cam = 0, t_trace = 0, t_shade = 0, t_prev = 0, t_start = 0;
     if (C::COUNT) t_prev = t_start = __builtin_amdgcn_s_memtime();
@@ -2019,9 +2058,7 @@ __global__ void __launch_bounds__(256, min_waves<C>()) trace_pool(SceneDev S, co
     // per-sample pool: a block = one tile x block_samples consecutive samples (any count: the
     // per-sample output does not depend on it)
     const unsigned group = ITEMS ? (unsigned)P.block_chunks : (unsigned)P.block_samples;
-    const unsigned n_groups = ITEMS ? ((unsigned)P.n_chunks + group - 1) / group
-                                    : ((unsigned)(P.spp - P.sample_begin) + group - 1) / group;
-    const unsigned n_blocks = n_tiles * n_groups;
+    const unsigned n_blocks = P.n_work_blocks;   // n_tiles x ceil(samples or chunks / group)
     const size_t n_px = (size_t)P.n_rows * (size_t)P.width;
     // current work block (wave-uniform)
     unsigned blk_units = 0, blk_next = 0, nvalid = 1;

@@ -114,6 +114,10 @@ __global__ void __launch_bounds__(256) accumulate_chunks(const double* __restric
     acc[3 * i + 2] = b;
 }
 
+struct StoredUV {   // hit_uv's config for the eval kernel: uv inputs held in the record
+    static constexpr uint32_t F = FEAT_ALL;
+};
+
 __global__ void eval_numerics(int fn, const double* x, const double* y, const double* z, double* out, int n)
 {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -130,7 +134,7 @@ __global__ void eval_numerics(int fn, const double* x, const double* y, const do
         h.uvkind = 1;
         h.uv0 = x[i]; h.uv1 = y[i]; h.uv2 = z[i];
         double u, v;
-        hit_uv(h, u, v);
+        hit_uv<StoredUV>(h, u, v);   // uv inputs held in the record
         r = fn == 5 ? u : v;
         break;
     }

@@ -73,6 +73,8 @@ struct KParams {
     int32_t sample_begin;       // chunk c covers samples [sample_begin + c*spp_chunk, ..) up to spp
     int32_t block_chunks;       // item pool: chunks per work block (a block = one tile x this many chunks)
     int32_t block_samples;      // per-sample pool: samples per work block (one tile x this many samples)
+    uint32_t n_work_blocks;     // pool schedules: tiles x sample groups of this launch (host-computed: in
+                                // the kernel the division's VGPR result stayed live through the loop)
 };
 
 // Scene features (which code a kernel variant must contain).
@@ -88,7 +90,9 @@ enum : uint32_t {
     FEAT_INST_BLAS = 256,   // an instance over a BVH (a nested walk; instances over one primitive need none)
     FEAT_SHUTTER = 512,     // a MovingSphere whose shutter is not [0, 1] (its centre needs a division)
     FEAT_NEST_MOVING = 1024, // a MovingSphere (nonzero velocity) under an instance or in a medium boundary
-    FEAT_ALL = 2047,
+    FEAT_IMAGE_UV = 2048,    // an image texture on a rect / box or an instanced primitive (its uv is stored at
+                             // the hit; else it is a top-level sphere's, recomputed from the hit normal)
+    FEAT_ALL = 4095,
     FEAT_STATIC = 1u << 16,  // kernel-internal (InstC / BoundC): every sphere reached here is static
     FEAT_SET_SPHERES = 0,                                          // compiled variant: spheres + solid/checker
     FEAT_SET_RECTINST = FEAT_RECT | FEAT_INST | FEAT_INST_RECT,    // + rects, boxes, instances of one prim (Cornell)

@@ -31,7 +31,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 OUT = os.path.join(REPO, "profiles", "isa_mix.json")
 PMC_JSON = os.path.join(REPO, "profiles", "pmc_r02.json")
-FEAT = {"spheres": 0, "rectinst": 35, "media": 103, "final": 287, "all": 2047}
+FEAT = {"spheres": 0, "rectinst": 35, "media": 103, "final": 287, "all": 4095}
 
 # mnemonic (regex on the opcode, without the _e32/_e64 suffix) -> calibration op
 OPMAP = [

@@ -28,10 +28,12 @@ for line in out.splitlines():
         cur[m.group(1).strip()] = int(m.group(2))
 for r in rows:
     n = r["name"]
-    m = re.search(r"(trace_chunks|trace_pool)INS_3CfgILj(\d+)ELb(\d)ELb(\d)ELb(\d)ELb(\d)E(?:Lb(\d)E)?", n)
+    m = re.search(r"(trace_chunks|trace_pool)INS_3CfgILj(\d+)ELb(\d)ELb(\d)ELb(\d)ELb(\d)E(?:Lb(\d)E)?EE(?:Lb(\d)E)?", n)
     if not m:
         continue
-    kern, f, s32, lds, nall, count, f32 = m.groups()
+    kern, f, s32, lds, nall, count, f32, items = m.groups()
+    if items == "1":
+        kern = "trace_items"
     if count == "1":
         continue
     print(f"{kern:12s} F={f:>2}{' f32' if f32 == '1' else ''} s32={s32} lds={lds} nall={nall}: VGPRs {r.get('VGPRs')} AGPRs {r.get('AGPRs')} "

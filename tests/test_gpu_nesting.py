@@ -68,7 +68,7 @@ def test_nested_world_matches_oracle(rt, renderer):
     soa = tw.product.flatten()
     assert soa.n_media == 3 and soa.n_instances >= 5
     got, ref = _render_both(rt, renderer, tw, 48, 32, 6, (7.0, 4.0, 9.0), (0.0, 0.7, 0.0), (0.5, 0.6, 0.8))
-    assert renderer.stats().variant_features == 2047          # media under instances: the all-features variant
+    assert renderer.stats().variant_features == 4095          # media under instances: the all-features variant
     assert float(ref.max()) > 0.0
     assert_parity(got, ref, "nested world")
 
@@ -103,7 +103,7 @@ def _moving_world(rt, t0, t1):
     return tw
 
 
-@pytest.mark.parametrize("t0,t1,feat", [(0.0, 1.0, 0), (0.25, 0.75, 2047), (-1.0, 2.0, 2047)])
+@pytest.mark.parametrize("t0,t1,feat", [(0.0, 1.0, 0), (0.25, 0.75, 4095), (-1.0, 2.0, 4095)])
 def test_moving_sphere_shutters_match_oracle(rt, renderer, t0, t1, feat):
     """MovingSphere::center (hittable.rs:556-558) for any shutter: [0, 1] shutters (every
     reference scene) take the spheres variant, which loads no per-primitive shutter flag;
@@ -130,7 +130,7 @@ def test_instanced_spheres_static_or_moving_match_oracle(rt, renderer, moving):
     tw.push(tw.translate(tw.rotate_y(tw.bvh(ids), 25.0), (0.2, 0.0, -0.5)))
     tw.push(tw.sphere(white, (0.0, -100.0, 0.0), 100.0))
     got, ref = _render_both(rt, renderer, tw, 40, 24, 6, (5.0, 2.0, 6.0), (0.0, 0.5, 0.0), (0.7, 0.8, 1.0))
-    assert renderer.stats().variant_features == (2047 if moving else 287)
+    assert renderer.stats().variant_features == (4095 if moving else 287)
     assert_parity(got, ref, f"instanced spheres (moving={moving})")
 
 

@@ -208,7 +208,7 @@ def test_feature_set_variants_identical(rt, renderer, scene_id, W, H, feat):
     renderer.upload(world)
     img = renderer.render(cam, p)
     assert renderer.stats().variant_features == feat
-    os.environ["RT_EXTRA_FEATURES"] = "2047"   # incl. FEAT_NEST_MOVING: nested spheres as moving
+    os.environ["RT_EXTRA_FEATURES"] = "4095"   # incl. FEAT_NEST_MOVING: nested spheres as moving
     try:
         big = rt.Renderer(0)
     finally:
@@ -216,7 +216,7 @@ def test_feature_set_variants_identical(rt, renderer, scene_id, W, H, feat):
     try:
         big.upload(world)
         img_all = big.render(cam, p)
-        assert big.stats().variant_features == 2047
+        assert big.stats().variant_features == 4095
     finally:
         big.close()
     assert np.array_equal(img, img_all)
@@ -227,8 +227,9 @@ def test_cornell_variant_occupancy(rt, renderer):
     """The Cornell scenes have no BVH node (one top-level leaf; instances over one box): they
     run the f64-slab instantiation of the rects + instances variant without the nested BLAS
     walk, whose registers fit 4 waves per SIMD; the spheres variant with the whole TLAS in
-    LDS and 16-bit stack entries (Stack16) runs at 5."""
-    for scene_id, waves in ((5, 4), (0, 5)):
+    LDS and 16-bit stack entries (Stack16) runs at 5; the final scene's variant (128 VGPRs) at 4,
+    its deferred instance walk sharing the top-level walk's LDS stack (13 entries, not 25)."""
+    for scene_id, waves in ((5, 4), (0, 5), (7, 4)):
         world = rt.World(1).build_scene(scene_id)
         cam, bg = rt.scene_camera(scene_id, 16, 16)
         renderer.upload(world)
