@@ -271,11 +271,12 @@ int rt_ctx_set_variant(rt_ctx* ctx, int slab32, int lds_stack, int lds_nodes);
  *           written as one partial per (pixel, chunk); the wave waits for its slowest lane.
  *   POOL:   persistent waves take (tile, chunk) blocks from a device counter and a lane
  *           whose path ended takes the block's next (pixel, sample) at once; every sample's
- *           radiance goes to a [sample][pixel] buffer summed per pixel in sample order.
+ *           radiance goes to a per-sample buffer ([8x8 tile][sample][pixel of the tile])
+ *           summed per pixel in sample order.
  *   ITEMS:  persistent waves as POOL, but a lane takes a whole (pixel, chunk) item, traces
  *           its samples in order and writes one partial, as CHUNKS does (1/chunk of POOL's
  *           buffer bytes); a lane whose item ended takes the next item at once.
- *   AUTO:   POOL when the render's [sample][pixel] buffer takes at most 4 batches (it is
+ *   AUTO:   POOL when the render's per-sample buffer takes at most 4 batches (it is
  *           the faster of the two), otherwise ITEMS; rt_stats.schedule reports which ran.
  * One launch's trace output is bounded by RT_SAMPLE_BUF_MB (default: sized at context
  * creation to 3/8 of the device's free memory, at most 128 GiB, at least 32 GiB where half

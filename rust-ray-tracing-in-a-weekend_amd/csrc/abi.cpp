@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
+#include <limits>
 #include <functional>
 #include <cmath>
 #include <cstdio>
@@ -490,6 +492,81 @@ static int walk_need(const rt_scene_soa* s, int ref, std::vector<int>& need, std
     return need[ref];
 }
 
+constexpr int RT_DONE_HOST = std::numeric_limits<int>::min();   // an empty W4 slot's reference (never hit)
+
+// The 4-wide TLAS (RT_WIDE; SceneDev.w4) from binary node `root`. Each W4 record starts from
+// a binary node's two children and, while it has fewer than four, replaces the internal child
+// of largest box surface by that child's two children (greedy collapse; boxes come from the
+// binary records, already padded). Records in BFS order, child references as record indices.
+// Returns the stack entries the walk needs: a visit pushes all but the nearest hit child, so
+// need(w) = (children - 1) + max need(internal child); + the RT_DONE sentinel and the
+// branch-free push's spare slot. 0 if there is nothing to build (root is a leaf).
+static int build_w4(const std::vector<rt_bvh_node>& nodes, int root, std::vector<rtk::W4Node>& out)
+{
+    out.clear();
+    if (root < 0) return 0;
+    struct Slot {
+        float lo[3], hi[3];
+        int ref;
+    };
+    auto area = [](const Slot& b) {
+        const double x = (double)b.hi[0] - b.lo[0], y = (double)b.hi[1] - b.lo[1], z = (double)b.hi[2] - b.lo[2];
+        return x * y + y * z + z * x;
+    };
+    auto kids_of = [&](int ref, Slot& a, Slot& b) {
+        const rt_bvh_node& n = nodes[(size_t)ref];
+        std::memcpy(a.lo, n.lo0, 12); std::memcpy(a.hi, n.hi0, 12); a.ref = n.child[0];
+        std::memcpy(b.lo, n.lo1, 12); std::memcpy(b.hi, n.hi1, 12); b.ref = n.child[1];
+    };
+    std::vector<int> src{root};   // binary node of each record
+    std::vector<std::array<int, 4>> kids;   // record index of internal children, else -1
+    for (size_t w = 0; w < src.size(); ++w) {
+        std::vector<Slot> slots(2);
+        kids_of(src[w], slots[0], slots[1]);
+        while (slots.size() < 4) {
+            int best = -1;
+            for (int i = 0; i < (int)slots.size(); ++i)
+                if (slots[(size_t)i].ref >= 0 && (best < 0 || area(slots[(size_t)i]) > area(slots[(size_t)best]))) best = i;
+            if (best < 0) break;
+            Slot a, b;
+            kids_of(slots[(size_t)best].ref, a, b);
+            slots[(size_t)best] = a;
+            slots.push_back(b);
+        }
+        rtk::W4Node o;
+        std::array<int, 4> kid{-1, -1, -1, -1};
+        const float inf = std::numeric_limits<float>::infinity();
+        for (int c = 0; c < 4; ++c) {
+            Slot sl{{inf, inf, inf}, {-inf, -inf, -inf}, RT_DONE_HOST};   // empty: never hit
+            if (c < (int)slots.size()) sl = slots[(size_t)c];
+            for (int a = 0; a < 3; ++a) {
+                o.ax[a][c] = sl.lo[a];
+                o.ax[a][4 + c] = sl.hi[a];
+                o.ax[a][8 + c] = sl.lo[a];
+            }
+            o.child[c] = sl.ref;
+            if (c < (int)slots.size() && sl.ref >= 0) {
+                kid[(size_t)c] = (int)src.size();
+                o.child[c] = (int)src.size();
+                src.push_back(sl.ref);
+            }
+        }
+        out.push_back(o);
+        kids.push_back(kid);
+    }
+    std::vector<int> need(out.size(), 0);
+    for (size_t w = out.size(); w-- > 0;) {
+        int k = 0, deep = 0;
+        for (int c = 0; c < 4; ++c) {
+            if (out[w].ax[0][c] > out[w].ax[0][4 + c]) continue;   // empty slot
+            ++k;
+            if (kids[w][(size_t)c] >= 0) deep = std::max(deep, need[(size_t)kids[w][(size_t)c]]);
+        }
+        need[w] = std::max(0, k - 1) + deep;
+    }
+    return need[0] + 2;
+}
+
 // SceneDev.pre_leaf: a root child that is a leaf of <= 2 primitives whose box holds at least
 // 8x the volume of its sibling's (a ground or fog sphere around the whole scene) is tested
 // before the walk, which then starts at the sibling (in the kernel variants that do this). The closest hit does not depend on the
@@ -810,15 +887,24 @@ int rt_ctx_upload_soa(rt_ctx* c, const rt_scene_soa* s)
             n_blas_bfs = (int)bfs.size();
         }
     }
-    size_t off[10], bytes[10] = {
+    // RT_WIDE: the 4-wide TLAS from the walk's start node (hoist_root_leaf's pre_root where it
+    // applies; the TLAS prefix keeps its indices and leaf codes in nodes_dev)
+    std::vector<rtk::W4Node> w4;
+    int w4_stack = 0;
+    if (RT_WIDE && n_tlas_nodes > 0) {
+        rtk::SceneDev hs{};
+        if (c->opt_hoist) hoist_root_leaf(s, hs);
+        w4_stack = build_w4(nodes_dev, hs.pre_leaf != 0 ? hs.pre_root : s->tlas_root, w4);
+    }
+    size_t off[11], bytes[11] = {
         (size_t)s->n_nodes * sizeof(rt_bvh_node), (size_t)s->n_prim_refs * 4, (size_t)s->n_prims * sizeof(rt_prim),
         (size_t)s->n_instances * sizeof(rt_instance), (size_t)s->n_materials * sizeof(rt_material),
         (size_t)s->n_textures * sizeof(rt_texture), (size_t)s->n_perlin * 768 * 8, (size_t)s->n_perlin * 768 * 4,
-        (size_t)s->image_bytes, (size_t)s->n_prim_refs * sizeof(rt_prim)};
-    const void* src[10] = {nodes_dev.data(), s->prim_refs, prims.data(), inst_dev.data(), s->materials, s->textures,
-                           s->perlin_ranvec, s->perlin_perm, s->image_data, leaf_prims.data()};
+        (size_t)s->image_bytes, (size_t)s->n_prim_refs * sizeof(rt_prim), w4.size() * sizeof(rtk::W4Node)};
+    const void* src[11] = {nodes_dev.data(), s->prim_refs, prims.data(), inst_dev.data(), s->materials, s->textures,
+                           s->perlin_ranvec, s->perlin_perm, s->image_data, leaf_prims.data(), w4.data()};
     size_t total = 0;
-    for (int i = 0; i < 10; ++i) {
+    for (int i = 0; i < 11; ++i) {
         off[i] = total;
         total = align_up(total + bytes[i], 256);
     }
@@ -834,7 +920,7 @@ int rt_ctx_upload_soa(rt_ctx* c, const rt_scene_soa* s)
         c->scene_bytes = total;
     }
     char* base = (char*)c->scene_buf;
-    for (int i = 0; i < 10; ++i)
+    for (int i = 0; i < 11; ++i)
         if (bytes[i]) HIP_TRY(hipMemcpy(base + off[i], src[i], bytes[i], hipMemcpyHostToDevice));
     c->S.nodes = (const rt_bvh_node*)(base + off[0]);
     c->S.prim_refs = (const int32_t*)(base + off[1]);
@@ -846,6 +932,9 @@ int rt_ctx_upload_soa(rt_ctx* c, const rt_scene_soa* s)
     c->S.perlin_perm = (const int32_t*)(base + off[7]);
     c->S.image = (const uint8_t*)(base + off[8]);
     c->S.leaf_prims = (const rt_prim*)(base + off[9]);
+    c->S.w4 = (const rtk::W4Node*)(base + off[10]);
+    c->S.n_w4 = (int32_t)w4.size();
+    c->S.w4_stack = w4_stack;
     c->S.tlas_root = s->tlas_root;
     c->S.pre_leaf = 0;
     if (c->opt_hoist) hoist_root_leaf(s, c->S);
@@ -853,6 +942,7 @@ int rt_ctx_upload_soa(rt_ctx* c, const rt_scene_soa* s)
     // indices < 32768, and leaf codes ((first slot << 5) | count, stored complemented; BLAS slots
     // relative, above) above the -32768 sentinel
     c->S.stack16_ok = (n_tlas_nodes * (int64_t)80 <= 32767 - 80 && max_first <= 1023 && s->n_nodes <= 32767) ? 1 : 0;
+    if (RT_WIDE && (w4.empty() || (int64_t)w4.size() * 160 > 32767 - 160 || w4_stack > kMaxLdsStack)) c->S.stack16_ok = 0;
     c->S.n_lds_nodes = 0;
     c->S.n_blas_bfs = n_blas_bfs;
     c->S.n_lds_blas = 0;
@@ -1169,9 +1259,15 @@ static int run_range(rt_ctx* c, const rt_camera* cam, const rt_render_params* p,
     if (c->n_nodes == 0 && !o.f32) o.slab32 = 0;
     const long long total = s_end - s_begin;
     const size_t px_bytes = px * 3 * sizeof(double);
+    // one sample's records in the per-sample buffer: whole 8x8 tiles (trace_kernel.hpp, tiled_record)
+    const rtk::SampleTiles tiles{p->width, n_rows, (p->width + 7) / 8};
+    const size_t sample_bytes = rtk::tiled_pixels(p->width, n_rows) * 3 * sizeof(double);
     // the TLAS in LDS (read-only, shared by the block) when it fits the per-block budget
     rtk::SceneDev S = c->S;
     S.n_lds_nodes = c->opt_lds_nodes ? std::min(c->n_tlas_nodes, kMaxLdsNodes) : 0;
+    // RT_WIDE: the spheres variant's whole-TLAS instantiation walks the 4-wide records
+    if (RT_WIDE && rtk::variant_features(o.features) == rtk::FEAT_SET_SPHERES && c->S.n_w4 > 0)
+        S.stack_entries = std::max(S.stack_entries, c->S.w4_stack);
     // small material and texture tables in LDS too (the variants with rects or media)
     const bool stage = c->opt_lds_nodes && c->n_materials <= kMaxLdsMaterials && c->n_textures <= kMaxLdsMaterials &&
                        c->n_materials > 0;
@@ -1211,17 +1307,17 @@ static int run_range(rt_ctx* c, const rt_camera* cam, const rt_render_params* p,
     double* open = nullptr;
     bool own_acc = false;
     for (;;) {
-        // AUTO: the per-sample pool when its [sample][pixel] buffer takes at most 4 batches (C2:
+        // AUTO: the per-sample pool when its per-sample buffer takes at most 4 batches (C2:
         // 11.5 GB in one, 101.6 vs 106.7 ms per frame for the item pool; C4: 49.8 GB in two,
         // 1492 vs 1571 ms; profiles/r02d_*, r02e_*), else the item pool, whose partials take
         // 1/chunk of those bytes and need no carried batches (C5: 1.6 TB of per-sample radiance)
         o.pool = c->opt_pool != RT_SCHED_AUTO ? c->opt_pool
-                 : ((size_t)total * px_bytes <= 4 * c->sample_buf_cap ? RT_SCHED_POOL : RT_SCHED_ITEMS);
+                 : ((size_t)total * sample_bytes <= 4 * c->sample_buf_cap ? RT_SCHED_POOL : RT_SCHED_ITEMS);
         // Buffer batches: the trace output of one launch is bounded by sample_buf_cap. Per-sample
         // pool: samples x pixels x 24 B; chunk and item schedules: chunks x pixels x 24 B, batches
         // on chunk boundaries (relative to s_begin), so the partials add in one-launch order.
         per_sample = o.pool == RT_SCHED_POOL;
-        const long long fit = (long long)std::max<size_t>(1, c->sample_buf_cap / px_bytes);
+        const long long fit = (long long)std::max<size_t>(1, c->sample_buf_cap / (per_sample ? sample_bytes : px_bytes));
         batch = std::min<long long>(total, per_sample ? fit : fit * chunk);
         n_batches = (int)((total + batch - 1) / batch);
         acc = sink.acc;
@@ -1244,10 +1340,10 @@ static int run_range(rt_ctx* c, const rt_camera* cam, const rt_render_params* p,
             own_acc = true;
         }
         const int max_chunks = (int)((batch + chunk - 1) / chunk);
-        const size_t need = per_sample ? (size_t)batch * px_bytes : (size_t)max_chunks * px_bytes;
+        const size_t need = per_sample ? (size_t)batch * sample_bytes : (size_t)max_chunks * px_bytes;
         rc = grow(c, stream, c->partial, c->partial_cap, need, &oom);
         if (rc == RT_OK) break;
-        if (!oom || c->sample_buf_cap <= ((size_t)1 << 20) || need <= px_bytes) return rc;
+        if (!oom || c->sample_buf_cap <= ((size_t)1 << 20) || need <= (per_sample ? sample_bytes : px_bytes)) return rc;
         c->sample_buf_cap = std::max<size_t>(c->sample_buf_cap / 2, (size_t)1 << 20);
     }
     if (own_acc) HIP_TRY(hipMemsetAsync(acc, 0, px_bytes, stream));
@@ -1287,9 +1383,9 @@ static int run_range(rt_ctx* c, const rt_camera* cam, const rt_render_params* p,
             if (acc) HIP_TRY(rtk::launch_accumulate(c->partial, acc, n_px, K.n_chunks, stream));
             else HIP_TRY(rtk::launch_reduce(c->partial, sink.out, sink.f64, n_px, K.n_chunks, sink.scale, stream));
         } else if (!open) {
-            HIP_TRY(rtk::launch_reduce_samples(c->partial, sink.out, sink.f64, n_px, b1 - b0, chunk, sink.scale, stream));
+            HIP_TRY(rtk::launch_reduce_samples(c->partial, sink.out, sink.f64, tiles, b1 - b0, chunk, sink.scale, stream));
         } else {
-            HIP_TRY(rtk::launch_reduce_samples_carry(c->partial, acc, open, n_px, b1 - b0, chunk,
+            HIP_TRY(rtk::launch_reduce_samples_carry(c->partial, acc, open, tiles, b1 - b0, chunk,
                                                      (int)(((long long)b0 - s_begin) % chunk), bi == n_batches - 1,
                                                      stream));
         }

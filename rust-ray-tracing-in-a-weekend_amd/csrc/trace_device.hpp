@@ -9,7 +9,7 @@
 //   * trace_pool (default): persistent waves take blocks from a device counter, and a
 //     lane whose path ended takes the block's next unit in the same bounce-loop
 //     iteration (ballot + mbcnt), so lanes do not idle until the last blocks run out;
-//     each sample's radiance goes to its slot of a [sample][pixel] buffer and
+//     each sample's radiance goes to its slot of a per-sample buffer (tiled) and
 //     reduce_samples sums every pixel's samples in sample order, chunk by chunk — the
 //     image does not depend on which lane computed a sample, on the launch geometry or
 //     on how rows are sharded over GPUs; trace_chunks (the first schedule, kept for A/B)
@@ -247,6 +247,9 @@ constexpr bool Stack16Cfg()
     return RT_STACK16 && C::LDS && C::NALL && C::S32 && (C::F == FEAT_SET_SPHERES || (RT_STACK16_FINAL && C::F == FEAT_SET_FINAL)) &&
            !C::F32;
 }
+// the 4-wide TLAS walk (RT_WIDE, SceneDev.w4): the spheres variant with the whole TLAS in LDS
+template <class C>
+constexpr bool Wide() { return RT_WIDE && Stack16Cfg<C>() && C::F == FEAT_SET_SPHERES; }
 // (final-scene variant: 25 entries x 256 lanes x 2 B instead of 4 take its LDS per block from
 // 45.8 to 33.3 KB, so 4 blocks (4 waves per SIMD) share a CU instead of 3; the BLAS walk's leaf
 // codes are relative to the BLAS's first slot, rt_instance.pad on the device, abi.cpp)
@@ -352,9 +355,15 @@ __device__ __forceinline__ void finish_ray(RayT<typename C::Real>& r, bool spher
         r.sz.y = -(float)r.oz * r.sz.x;
         // the LDS node (LdsNode): per axis [lo0 lo1 hi0 hi1 lo0 lo1] at bytes 0/24/48; the
         // near planes of both children at +0 (direction >= 0) or +8, the far ones 8 bytes on
-        r.onx = r.sx.x >= 0.0f ? 0u : 8u;
-        r.ony = r.sy.x >= 0.0f ? 24u : 32u;
-        r.onz = r.sz.x >= 0.0f ? 48u : 56u;
+        if constexpr (Wide<C>()) {   // W4Node: per axis 48 B, the near quadruple at +0 or +16
+            r.onx = r.sx.x >= 0.0f ? 0u : 16u;
+            r.ony = r.sy.x >= 0.0f ? 48u : 64u;
+            r.onz = r.sz.x >= 0.0f ? 96u : 112u;
+        } else {
+            r.onx = r.sx.x >= 0.0f ? 0u : 8u;
+            r.ony = r.sy.x >= 0.0f ? 24u : 32u;
+            r.onz = r.sz.x >= 0.0f ? 48u : 56u;
+        }
     } else {
         r.ix = (typename C::Real)1 / r.dx;
         r.iy = (typename C::Real)1 / r.dy;
@@ -762,7 +771,12 @@ __device__ __forceinline__ const __attribute__((address_space(3))) T* lds_ptr(ui
     return (const __attribute__((address_space(3))) T*)(uintptr_t)a;
 }
 template <class C>
-constexpr int lds_node_bytes() { return OctNodes<C>() ? (int)sizeof(LdsNode) : (int)sizeof(rt_bvh_node); }
+constexpr int lds_node_bytes()
+{
+    return Wide<C>() ? (int)sizeof(W4Node) : OctNodes<C>() ? (int)sizeof(LdsNode) : (int)sizeof(rt_bvh_node);
+}
+template <class C>
+__device__ __forceinline__ int lds_node_count(const SceneDev& S) { return Wide<C>() ? S.n_w4 : S.n_lds_nodes; }
 __device__ __forceinline__ Node load_node_lds(uint32_t addr)
 {
     typedef unsigned u4v __attribute__((ext_vector_type(4)));
@@ -807,7 +821,7 @@ constexpr bool StageBlas() { return RT_STAGE_BLAS && (C::F & FEAT_INST_BLAS) != 
 template <class C>
 __device__ __forceinline__ LdsLayout lds_layout_of(const SceneDev& S)
 {
-    return lds_layout(S.n_lds_nodes, lds_node_bytes<C>(), StageBlas<C>() ? S.n_lds_blas : 0, C::LDS ? S.stack_entries : 0,
+    return lds_layout(lds_node_count<C>(S), lds_node_bytes<C>(), StageBlas<C>() ? S.n_lds_blas : 0, C::LDS ? S.stack_entries : 0,
                       Stack16Cfg<C>() ? 2 : 4, StageShade<C>() ? S.n_lds_materials : 0,
                       StageShade<C>() ? S.n_lds_textures : 0);
 }
@@ -865,10 +879,54 @@ __device__ __forceinline__ bool traverse(const SceneDev& S, int root, const RayT
     // v_mov inside the node loop, which machine LICM no longer hoists)
     float tmin_v = tmin_f;
     if constexpr (OCT && PkSlab<C>()) asm("v_mov_b32 %0, %1" : "=v"(tmin_v) : "v"(tmin_f));
-    if constexpr (OCT) cur = cur >= 0 ? (int)(lds_addr(lb) + (uint32_t)cur * (uint32_t)sizeof(LdsNode)) : cur;
+    constexpr bool W4 = OCT && Wide<C>();   // the 4-wide TLAS: its root record (index 0) is the walk's start
+    if constexpr (W4) cur = cur >= 0 ? (int)lds_addr(lb) : cur;
+    else if constexpr (OCT) cur = cur >= 0 ? (int)(lds_addr(lb) + (uint32_t)cur * (uint32_t)sizeof(LdsNode)) : cur;
     // one node visit: test both children, continue with the nearer, push the farther
     auto visit = [&](int node) -> int {
         if (C::COUNT) cnt.nodes++;
+#if RT_SPTR
+        if constexpr (W4) {
+            // four children: near / far plane quadruples per axis (two ds_read_b128 each), the
+            // same conservative f32 slab test per child as the binary visit; the nearest hit child
+            // continues, the other hits are pushed (a two-round tournament on the entry distances:
+            // the winner of the other pair last, so it pops first) with branch-free pushes
+            const uint32_t nb = (uint32_t)node;
+            typedef float f4v __attribute__((ext_vector_type(4)));
+            typedef int i4v __attribute__((ext_vector_type(4)));
+            const f4v nx = *lds_ptr<f4v>(nb + r.onx), fx = *lds_ptr<f4v>(nb + r.onx + 16u);
+            const f4v ny = *lds_ptr<f4v>(nb + r.ony), fy = *lds_ptr<f4v>(nb + r.ony + 16u);
+            const f4v nz = *lds_ptr<f4v>(nb + r.onz), fz = *lds_ptr<f4v>(nb + r.onz + 16u);
+            const i4v ch = *lds_ptr<i4v>(nb + (uint32_t)offsetof(W4Node, child));
+            const float INF = __builtin_inff();
+            float k[4];
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                const float ax = __builtin_fmaf(nx[c], r.sx.x, r.sx.y), bx = __builtin_fmaf(fx[c], r.sx.x, r.sx.y);
+                const float ay = __builtin_fmaf(ny[c], r.sy.x, r.sy.y), by = __builtin_fmaf(fy[c], r.sy.x, r.sy.y);
+                const float az = __builtin_fmaf(nz[c], r.sz.x, r.sz.y), bz = __builtin_fmaf(fz[c], r.sz.x, r.sz.y);
+                const float tn = fmaxf(fmaxf(ax, ay), fmaxf(az, tmin_f));
+                const float tf = fminf(fminf(bx, by), __builtin_amdgcn_fmed3f(bz, tmax_f, ninf));
+                k[c] = tn <= tf ? tn : INF;
+            }
+            const bool a01 = k[0] <= k[1], a23 = k[2] <= k[3];
+            const float kA = a01 ? k[0] : k[1], lA = a01 ? k[1] : k[0];
+            const int rA = a01 ? ch.x : ch.y, qA = a01 ? ch.y : ch.x;
+            const float kB = a23 ? k[2] : k[3], lB = a23 ? k[3] : k[2];
+            const int rB = a23 ? ch.z : ch.w, qB = a23 ? ch.w : ch.z;
+            const bool aN = kA <= kB;
+            const float kN = aN ? kA : kB, kS = aN ? kB : kA;
+            const int rN = aN ? rA : rB, rS = aN ? rB : rA;
+            if (kN == INF) return pop();
+            *sptr = (SE)qA;
+            sptr += lA < INF ? SSTR : 0;
+            *sptr = (SE)qB;
+            sptr += lB < INF ? SSTR : 0;
+            *sptr = (SE)rS;
+            sptr += kS < INF ? SSTR : 0;
+            return rN;
+        }
+#endif
         if constexpr (OCT) {
             const uint32_t nb = (uint32_t)node;   // LDS address of the node
             typedef float f2v __attribute__((ext_vector_type(2)));
@@ -1663,7 +1721,16 @@ __device__ __forceinline__ void stage_lds(const SceneDev& S)
     bool any = false;
     const int off = 0;   // the TLAS nodes first (traverse)
     if (S.n_lds_nodes > 0) {
-        if constexpr (OctNodes<C>()) {   // one node per thread, rt_bvh_node -> LdsNode
+        if constexpr (Wide<C>()) {   // the 4-wide records, child indices -> LDS byte addresses
+            W4Node* dst = reinterpret_cast<W4Node*>(rt_lds + off);
+            for (int i = threadIdx.x; i < S.n_w4; i += 256) {
+                W4Node o = S.w4[i];
+#pragma unroll
+                for (int c = 0; c < 4; ++c)
+                    if (o.child[c] >= 0) o.child[c] = (int)(lds_addr(dst) + (uint32_t)o.child[c] * (uint32_t)sizeof(W4Node));
+                dst[i] = o;
+            }
+        } else if constexpr (OctNodes<C>()) {   // one node per thread, rt_bvh_node -> LdsNode
             LdsNode* dst = reinterpret_cast<LdsNode*>(rt_lds + off);
             for (int i = threadIdx.x; i < S.n_lds_nodes; i += 256) {
                 const rt_bvh_node n = S.nodes[i];
@@ -1998,8 +2065,8 @@ __global__ void __launch_bounds__(256, min_waves<C>()) trace_chunks(SceneDev S, 
 // Sample-pool schedule. Persistent waves take work blocks (one 8x8 tile x one chunk of
 // samples) from a global counter; inside the wave, a lane whose path ended takes the
 // block's next (pixel, sample) unit at once (ballot + mbcnt), so lanes do not idle until
-// the last blocks run out. Each sample's radiance goes to its own slot of a
-// [sample][pixel] buffer; reduce_samples then sums every pixel's samples in sample order,
+// the last blocks run out. Each sample's radiance goes to its own slot of a buffer
+// ([tile][sample][pixel of the tile], tiled_record); reduce_samples then sums every pixel's samples in sample order,
 // so the image does not depend on which lane or wave computed a sample.
 // ---------------------------------------------------------------------------
 // The hit record's old contents are dead (RT_KILL_H): freeze(poison) for every field, so the
@@ -2220,9 +2287,10 @@ __global__ void __launch_bounds__(256, min_waves<C>()) trace_pool(SceneDev S, co
             active = false;
             own = true;
         } else {
-            const size_t slot = ITEMS ? (size_t)((unsigned)(s - P.sample_begin) / (unsigned)P.spp_chunk)
-                                      : (size_t)(s - P.sample_begin);
-            double* o = samples + (slot * n_px + (size_t)k * P.width + x) * 3;
+            // items: the chunk's partial, [chunk][pixel]; per-sample pool: tiled_record order
+            double* o = ITEMS ? samples + ((size_t)((unsigned)(s - P.sample_begin) / (unsigned)P.spp_chunk) * n_px +
+                                           (size_t)k * P.width + x) * 3
+                              : samples + tiled_record(P.tiles_x, P.spp - P.sample_begin, x, k, s - P.sample_begin) * 3;
             o[0] = cr;
             o[1] = cg;
             o[2] = cb;
@@ -2273,11 +2341,11 @@ __global__ void __launch_bounds__(256, min_waves<C>()) trace_pool(SceneDev S, co
             active = false;
             own = true;
         } else {
-            // per-sample pool: this sample's radiance; items: the chunk's partial (the chunk of
-            // its last sample)
-            const size_t slot = ITEMS ? (size_t)((unsigned)(s - P.sample_begin) / (unsigned)P.spp_chunk)
-                                      : (size_t)(s - P.sample_begin);
-            double* o = samples + (slot * n_px + (size_t)k * P.width + x) * 3;
+            // per-sample pool: this sample's radiance (tiled_record order); items: the chunk's
+            // partial (the chunk of its last sample), [chunk][pixel]
+            double* o = ITEMS ? samples + ((size_t)((unsigned)(s - P.sample_begin) / (unsigned)P.spp_chunk) * n_px +
+                                           (size_t)k * P.width + x) * 3
+                              : samples + tiled_record(P.tiles_x, P.spp - P.sample_begin, x, k, s - P.sample_begin) * 3;
             o[0] = cr;
             o[1] = cg;
             o[2] = cb;
@@ -2356,12 +2424,13 @@ template <uint32_t F, bool S32, bool LDS, bool COUNT, bool F32>
 static void launch_one(const Launch& L, hipStream_t stream, bool nall)
 {
     const SceneDev& S = *L.S;
-    const int node_bytes = nall && S32 ? (int)sizeof(LdsNode) : (int)sizeof(rt_bvh_node);   // lds_node_bytes
     const bool s16 = RT_STACK16 && LDS && nall && S32 && (F == FEAT_SET_SPHERES || (RT_STACK16_FINAL && F == FEAT_SET_FINAL)) &&
                      !F32;   // Stack16Cfg
+    const bool wide = RT_WIDE && s16 && F == FEAT_SET_SPHERES;   // Wide
+    const int node_bytes = wide ? (int)sizeof(W4Node) : nall && S32 ? (int)sizeof(LdsNode) : (int)sizeof(rt_bvh_node);   // lds_node_bytes
     const bool stage = F != FEAT_SET_SPHERES;                   // StageShade
     const bool blas = RT_STAGE_BLAS && (F & FEAT_INST_BLAS) != 0 && !F32;   // StageBlas
-    const size_t lds = lds_layout(S.n_lds_nodes, node_bytes, blas ? S.n_lds_blas : 0, LDS ? S.stack_entries : 0,
+    const size_t lds = lds_layout(wide ? S.n_w4 : S.n_lds_nodes, node_bytes, blas ? S.n_lds_blas : 0, LDS ? S.stack_entries : 0,
                                   s16 ? 2 : 4, stage ? S.n_lds_materials : 0, stage ? S.n_lds_textures : 0).total;
     if (L.pool) {
         auto go = [&](auto kernel) {

@@ -5,32 +5,50 @@
 
 namespace rtk {
 
+// One thread per record slot of a tile (tiled_record order: a wave reads one tile's 64
+// consecutive records per sample); slots of an edge tile outside the image return. Sets the
+// pixel's output index and the record base of sample 0.
+__device__ __forceinline__ bool tile_slot(SampleTiles g, int n_samples, long long i, long long& px, size_t& rec)
+{
+    const long long tile = i >> 6;
+    const int lp = (int)(i & 63);
+    const int x = (int)(tile % g.tiles_x) * 8 + (lp & 7);
+    const int k = (int)(tile / g.tiles_x) * 8 + (lp >> 3);
+    if (x >= g.width || k >= g.n_rows) return false;
+    px = (long long)k * g.width + x;
+    rec = tiled_record(g.tiles_x, n_samples, x, k, 0);
+    return true;
+}
+
 // Per pixel: chunk sums of consecutive samples (chunk order, each from 0.0), added in
 // chunk order to 0.0 and scaled into out: the same additions, in the same order, as the
 // chunk schedule's lane sums + reduce_chunks.
 template <typename T>
 __global__ void __launch_bounds__(256) reduce_samples(const double* __restrict__ samples, T* __restrict__ out,
-                                                      long long n_px, int n_samples, int chunk, double scale)
+                                                      SampleTiles g, long long n_slots, int n_samples, int chunk,
+                                                      double scale)
 {
     const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n_px) return;
-    double r = 0.0, g = 0.0, b = 0.0;
+    long long px;
+    size_t rec;
+    if (i >= n_slots || !tile_slot(g, n_samples, i, px, rec)) return;
+    double r = 0.0, g_ = 0.0, b = 0.0;
     for (int c0 = 0; c0 < n_samples; c0 += chunk) {
         const int c1 = min(n_samples, c0 + chunk);
         double cr = 0.0, cg = 0.0, cb = 0.0;
         for (int j = c0; j < c1; ++j) {
-            const double* p = samples + ((size_t)j * n_px + i) * 3;
+            const double* p = samples + (rec + (size_t)j * 64) * 3;
             cr = cr + p[0];
             cg = cg + p[1];
             cb = cb + p[2];
         }
         r = r + cr;
-        g = g + cg;
+        g_ = g_ + cg;
         b = b + cb;
     }
-    out[3 * i + 0] = (T)(r * scale);
-    out[3 * i + 1] = (T)(g * scale);
-    out[3 * i + 2] = (T)(b * scale);
+    out[3 * px + 0] = (T)(r * scale);
+    out[3 * px + 1] = (T)(g_ * scale);
+    out[3 * px + 2] = (T)(b * scale);
 }
 
 // The same sums over a render split into buffer batches that need not end on a chunk
@@ -38,26 +56,28 @@ __global__ void __launch_bounds__(256) reduce_samples(const double* __restrict__
 // in at batch start, uniform); `close` ends the render's last chunk.
 __global__ void __launch_bounds__(256) reduce_samples_carry(const double* __restrict__ samples,
                                                             double* __restrict__ acc, double* __restrict__ open,
-                                                            long long n_px, int n_samples, int chunk, int pos,
-                                                            int close)
+                                                            SampleTiles g, long long n_slots, int n_samples,
+                                                            int chunk, int pos, int close)
 {
     const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n_px) return;
-    double r = acc[3 * i + 0], g = acc[3 * i + 1], b = acc[3 * i + 2];
+    long long px;
+    size_t rec;
+    if (i >= n_slots || !tile_slot(g, n_samples, i, px, rec)) return;
+    double r = acc[3 * px + 0], g_ = acc[3 * px + 1], b = acc[3 * px + 2];
     double cr = 0.0, cg = 0.0, cb = 0.0;
     if (pos > 0) {
-        cr = open[3 * i + 0];
-        cg = open[3 * i + 1];
-        cb = open[3 * i + 2];
+        cr = open[3 * px + 0];
+        cg = open[3 * px + 1];
+        cb = open[3 * px + 2];
     }
     for (int j = 0; j < n_samples; ++j) {
-        const double* p = samples + ((size_t)j * n_px + i) * 3;
+        const double* p = samples + (rec + (size_t)j * 64) * 3;
         cr = cr + p[0];
         cg = cg + p[1];
         cb = cb + p[2];
         if (++pos == chunk) {
             r = r + cr;
-            g = g + cg;
+            g_ = g_ + cg;
             b = b + cb;
             cr = cg = cb = 0.0;
             pos = 0;
@@ -65,15 +85,15 @@ __global__ void __launch_bounds__(256) reduce_samples_carry(const double* __rest
     }
     if (close && pos > 0) {
         r = r + cr;
-        g = g + cg;
+        g_ = g_ + cg;
         b = b + cb;
     }
-    acc[3 * i + 0] = r;
-    acc[3 * i + 1] = g;
-    acc[3 * i + 2] = b;
-    open[3 * i + 0] = cr;
-    open[3 * i + 1] = cg;
-    open[3 * i + 2] = cb;
+    acc[3 * px + 0] = r;
+    acc[3 * px + 1] = g_;
+    acc[3 * px + 2] = b;
+    open[3 * px + 0] = cr;
+    open[3 * px + 1] = cg;
+    open[3 * px + 2] = cb;
 }
 
 // sum of partials in chunk order, times 1/spp (math.rs:120-125 before sqrt).
@@ -213,27 +233,29 @@ hipError_t launch_trace(const SceneDev& S, const KParams& Ph, const KParams* P, 
 }
 
 
-hipError_t launch_reduce_samples(const double* samples, void* out, bool f64, long long n_px, int n_samples,
+hipError_t launch_reduce_samples(const double* samples, void* out, bool f64, SampleTiles g, int n_samples,
                                  int chunk, double scale, hipStream_t stream)
 {
-    const long long blocks = (n_px + 255) / 256;
+    const long long n_slots = (long long)tiled_pixels(g.width, g.n_rows);
+    const long long blocks = (n_slots + 255) / 256;
     if (blocks <= 0) return hipSuccess;
     if (f64)
         hipLaunchKernelGGL(reduce_samples<double>, dim3((unsigned)blocks), dim3(256), 0, stream, samples, (double*)out,
-                           n_px, n_samples, chunk, scale);
+                           g, n_slots, n_samples, chunk, scale);
     else
         hipLaunchKernelGGL(reduce_samples<float>, dim3((unsigned)blocks), dim3(256), 0, stream, samples, (float*)out,
-                           n_px, n_samples, chunk, scale);
+                           g, n_slots, n_samples, chunk, scale);
     return hipGetLastError();
 }
 
-hipError_t launch_reduce_samples_carry(const double* samples, double* acc, double* open, long long n_px,
+hipError_t launch_reduce_samples_carry(const double* samples, double* acc, double* open, SampleTiles g,
                                        int n_samples, int chunk, int pos, bool close, hipStream_t stream)
 {
-    const long long blocks = (n_px + 255) / 256;
+    const long long n_slots = (long long)tiled_pixels(g.width, g.n_rows);
+    const long long blocks = (n_slots + 255) / 256;
     if (blocks <= 0) return hipSuccess;
-    hipLaunchKernelGGL(reduce_samples_carry, dim3((unsigned)blocks), dim3(256), 0, stream, samples, acc, open, n_px,
-                       n_samples, chunk, pos, (int)close);
+    hipLaunchKernelGGL(reduce_samples_carry, dim3((unsigned)blocks), dim3(256), 0, stream, samples, acc, open, g,
+                       n_slots, n_samples, chunk, pos, (int)close);
     return hipGetLastError();
 }
 

@@ -13,7 +13,24 @@
 #define RT_DEFER_INST 1
 #endif
 
+// 4-wide TLAS in the spheres variant (A/B experiment): the binary SAH tree
+// collapsed two levels per node (W4Node), walked with one 4-child visit per step
+#ifndef RT_WIDE
+#define RT_WIDE 0
+#endif
+
 namespace rtk {
+
+// A 4-wide TLAS node (RT_WIDE): binary node n with each internal child replaced by that child's
+// two children. Per axis the four children's lower planes, upper planes and lower planes again,
+// so a ray reads its four near planes and four far planes as two 16-B reads at +0 (direction
+// >= 0) or +16; children as W4 indices (LDS byte addresses once staged), leaf codes, or an
+// empty slot (box +inf..-inf, never hit).
+struct W4Node {
+    float ax[3][12];
+    int32_t child[4];
+};
+static_assert(sizeof(W4Node) == 160, "W4Node layout");
 
 // Device view of the uploaded rt_scene_soa tables.
 struct SceneDev {
@@ -55,6 +72,11 @@ struct SceneDev {
     // nodes[n_tlas_nodes, n_tlas_nodes + n_blas_bfs) (abi.cpp), and a launch stages the first
     // n_lds_blas of them (its LDS budget): the nested walk's top levels then read LDS
     int32_t n_blas_bfs, n_lds_blas;
+    // RT_WIDE: the 4-wide TLAS from the walk's start node (pre_root with a hoisted leaf, else
+    // tlas_root), its record count and the stack entries its walk needs (+ sentinel, + the
+    // branch-free push's spare slot)
+    const W4Node* w4;
+    int32_t n_w4, w4_stack;
 };
 
 struct KParams {
@@ -111,18 +133,39 @@ struct LaunchOpts {
     int* waves_per_simd = nullptr;  // out (optional): resident waves per SIMD of the launched trace kernel
 };
 
+// Per-sample pool output: [8x8 tile][sample of the batch][64 pixels of the tile, row-major]
+// radiance records (f64 x 3). A wave's work block is one tile x consecutive samples and its
+// lanes take the block's units in order, so records written close in time lie close in memory
+// and fill whole cache lines while those sit in L2; the earlier [sample][pixel] layout spread
+// each (tile, sample)'s 64 records over 8 image rows written ~1 ms apart, and L2 evicted the
+// lines half written (C2 DRAM writes 1.22x the radiance bytes, C4 1.29x; profiles/r03o_*).
+// Edge tiles keep all 64 slots (unused ones are never written or read).
+struct SampleTiles {
+    int32_t width, n_rows, tiles_x;
+};
+__host__ __device__ inline size_t tiled_record(int tiles_x, int n_samples, int x, int k, int s)
+{
+    const size_t tile = (size_t)(k >> 3) * (size_t)tiles_x + (size_t)(x >> 3);
+    return (tile * (size_t)n_samples + (size_t)s) * 64 + (size_t)(((k & 7) << 3) | (x & 7));
+}
+__host__ __device__ inline size_t tiled_pixels(int width, int n_rows)   // records per sample, padded tiles
+{
+    return (size_t)((width + 7) / 8) * (size_t)((n_rows + 7) / 8) * 64;
+}
+
 uint32_t variant_features(uint32_t scene_features);
 // Ph: host copy of the params (grid size); P: the same params in device memory
 // chunk schedule: out = chunk partials [n_chunks][n_px][3]; pool schedule: out = per-sample
-// radiance [spp - sample_begin][n_px][3], work = one device counter
+// radiance, tiled_record order over spp - sample_begin samples; work = one device counter
 hipError_t launch_trace(const SceneDev& S, const KParams& Ph, const KParams* P, double* out,
                         unsigned long long* counters, unsigned* work, const LaunchOpts& o, hipStream_t stream);
 // pool schedule: per pixel, chunk sums of its samples (sample order) added to 0.0, scaled to out
-hipError_t launch_reduce_samples(const double* samples, void* out, bool f64, long long n_px, int n_samples,
+// (out and the carried sums are in pixel order k * width + x)
+hipError_t launch_reduce_samples(const double* samples, void* out, bool f64, SampleTiles g, int n_samples,
                                  int chunk, double scale, hipStream_t stream);
 // the same across buffer batches: acc = closed chunks' total, open = the chunk in progress
 // (pos of its samples seen before this batch); close ends the last chunk
-hipError_t launch_reduce_samples_carry(const double* samples, double* acc, double* open, long long n_px,
+hipError_t launch_reduce_samples_carry(const double* samples, double* acc, double* open, SampleTiles g,
                                        int n_samples, int chunk, int pos, bool close, hipStream_t stream);
 hipError_t launch_reduce(const double* partial, void* out, bool f64, long long n_px, int n_chunks, double scale,
                          hipStream_t stream);
