@@ -55,7 +55,9 @@ constexpr int kMaxLdsStack = 48;
 constexpr int kMaxLdsNodes = 512;
 // instance BLAS nodes staged in LDS at most (64 B each)
 #ifndef RT_LDS_BLAS_MAX
-#define RT_LDS_BLAS_MAX 64   // C4 1920x1080x100: 64 staged 132.15 ms, 16 133.31, none 132.98 (r03h_ab_c4.log)
+#define RT_LDS_BLAS_MAX 1024   // the LDS budget decides (512-thread final variant: 512 of the final scene's 548
+                               // BLAS nodes, 110.95 -> 108.23 ms at C4 1920x1080x100, r03r_ab_c4.log; with 256-thread
+                               // workgroups the budget held ~95: 64 staged 132.15 ms, 16 133.31, none 132.98, r03h)
 #endif
 constexpr int kMaxLdsBlas = RT_LDS_BLAS_MAX;
 // material (64 B) and texture (96 B) tables staged in LDS when both are this small (10 KB)
@@ -1279,14 +1281,20 @@ static int run_range(rt_ctx* c, const rt_camera* cam, const rt_render_params* p,
     if (c->S.n_blas_bfs > 0 && c->opt_lds_nodes && !o.f32 &&
         (rtk::variant_features(o.features) & rtk::FEAT_INST_BLAS) != 0) {
         const bool oct = o.slab32 && S.n_lds_nodes == c->n_tlas_nodes && S.n_lds_nodes > 0;
+        const uint32_t variant = rtk::variant_features(o.features);
+        const int bt = rtk::block_threads_of(variant, false);   // workgroup threads (RT_BLOCK_FINAL)
         const size_t base = (size_t)S.n_lds_nodes * (oct ? 80 : 64) +
-                            (o.lds_stack ? (size_t)c->S.stack_entries * 256 * 4 : 0) +
+                            (o.lds_stack ? (size_t)c->S.stack_entries * (size_t)bt * 4 : 0) +
                             (size_t)S.n_lds_materials * 64 + (size_t)S.n_lds_textures * 96;
         // the CU's 160 KB shared by `blocks` workgroups, each allocation rounded up to the LDS
         // granule (taken as 1 KB; the occupancy API does not round: a layout it rated at 3
-        // blocks per CU ran 2 and took 174 instead of 133 ms, r03g_ab_c4.log)
+        // blocks per CU ran 2 and took 174 instead of 133 ms, r03g_ab_c4.log), and no more
+        // workgroups than the variant's registers allow (final scene 4 waves per SIMD, the
+        // all-features variant 3: 16 or 12 waves per CU)
         const size_t lds_cu = 160 * 1024, granule = 1024;
-        const size_t blocks = std::max<size_t>(1, lds_cu / (((std::max<size_t>(base, 1) + granule - 1) / granule) * granule));
+        const size_t wave_blocks = std::max<size_t>(1, (size_t)(variant == rtk::FEAT_SET_FINAL ? 16 : 12) / (size_t)(bt / 64));
+        const size_t blocks = std::max<size_t>(1, std::min(wave_blocks,
+            lds_cu / (((std::max<size_t>(base, 1) + granule - 1) / granule) * granule)));
         const size_t budget = lds_cu / blocks / granule * granule;
         const size_t spare = budget > base ? budget - base : 0;
         S.n_lds_blas = (int32_t)std::min<size_t>({(size_t)c->S.n_blas_bfs, spare / 64, (size_t)kMaxLdsBlas});

@@ -170,6 +170,10 @@ struct Cfg {
 // The configuration of code reached only through an instance or a medium boundary: the
 // feature bits the scene does not need there are dropped (FEAT_INST_RECT / FEAT_MEDIUM_INST
 // clear), so e.g. the final scene's instanced BLAS of spheres compiles the sphere test only.
+// threads per workgroup (RT_BLOCK_FINAL; the LDS stack's lane stride)
+template <class C>
+constexpr int BlockThreads() { return block_threads_of(C::F, C::F32); }
+
 template <class C, uint32_t DROP>
 struct CfgDrop : C {
     static constexpr uint32_t F = C::F & ~DROP;
@@ -189,10 +193,10 @@ using BoundC = CfgDropStatic<C, FEAT_INST_MEDIUM | ((C::F & FEAT_MEDIUM_INST) ? 
 template <class C>
 using InstMedC = CfgDropStatic<C, FEAT_INST_MEDIUM>;   // a medium under an instance: no medium below it
 
-// Traversal stack. LDS: a lane-interleaved dynamic LDS array [entry][256 threads]
+// Traversal stack. LDS: a lane-interleaved dynamic LDS array [entry][block threads]
 // (consecutive lanes hit consecutive banks) sized per scene by the host (TLAS depth +
 // BLAS depth); scratch: a private array (deep scenes).
-extern __shared__ int rt_lds[];  // [cached TLAS nodes] [stack entries x 256 lanes] [materials, textures]
+extern __shared__ int rt_lds[];  // [cached TLAS nodes] [stack entries x block lanes] [materials, textures]
 #ifndef RT_STACK_REMAT
 #define RT_STACK_REMAT 1
 #endif
@@ -205,25 +209,25 @@ __device__ __forceinline__ int lane_remat()
     asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
     return l;
 }
-template <bool LDS, bool REMAT = false>
+template <bool LDS, bool REMAT = false, int BT = 256>
 struct Stack;
-template <>
-struct Stack<true, true> {   // the variants with nested walks (128 VGPRs)
+template <int BT>
+struct Stack<true, true, BT> {   // the variants with nested walks (128 VGPRs)
     int wave0;   // rt_lds index of this wave's lane 0, entry 0 (wave-uniform: an SGPR)
-    __device__ __forceinline__ int& operator[](int i) const { return rt_lds[wave0 + lane_remat() + i * 256]; }
+    __device__ __forceinline__ int& operator[](int i) const { return rt_lds[wave0 + lane_remat() + i * BT]; }
     __device__ __forceinline__ void init(int stack_off)
     {
         wave0 = stack_off + __builtin_amdgcn_readfirstlane((int)threadIdx.x & ~63);
     }
 };
-template <>
-struct Stack<true, false> {   // (Cornell variants: the remat costs 0.3-0.9 %, nothing spills)
+template <int BT>
+struct Stack<true, false, BT> {   // (Cornell variants: the remat costs 0.3-0.9 %, nothing spills)
     int* base;
-    __device__ __forceinline__ int& operator[](int i) const { return base[i * 256]; }
+    __device__ __forceinline__ int& operator[](int i) const { return base[i * BT]; }
     __device__ __forceinline__ void init(int stack_off) { base = rt_lds + stack_off + threadIdx.x; }
 };
-template <>
-struct Stack<false, false> {
+template <int BT>
+struct Stack<false, false, BT> {
     int v[66];   // 32 + 32 entries + the two walks' RT_DONE sentinels
     __device__ __forceinline__ int& operator[](int i) { return v[i]; }
 };
@@ -237,9 +241,10 @@ struct Stack<false, false> {
 #ifndef RT_STACK16_FINAL
 #define RT_STACK16_FINAL 0   // measured: the final variant with 16-bit entries (4 waves) 142.1 ms vs 132.7 with 32-bit (3 waves, LDS-bound); at 3 waves both ways 141.8 vs 132.4 (C4 1920x1080x100, r03f_ab_c4.log): the 16-bit stack itself costs ~7 % here
 #endif
+template <int BT>
 struct Stack16 {   // node records at LDS addresses < 32 KB, leaf codes > -32768 (SceneDev.stack16_ok)
     short* base;
-    __device__ __forceinline__ short& operator[](int i) const { return base[i * 256]; }
+    __device__ __forceinline__ short& operator[](int i) const { return base[i * BT]; }
 };
 template <class C>
 constexpr bool Stack16Cfg()
@@ -254,8 +259,9 @@ constexpr bool Wide() { return RT_WIDE && Stack16Cfg<C>() && C::F == FEAT_SET_SP
 // 45.8 to 33.3 KB, so 4 blocks (4 waves per SIMD) share a CU instead of 3; the BLAS walk's leaf
 // codes are relative to the BLAS's first slot, rt_instance.pad on the device, abi.cpp)
 template <class C>
-using StackT = typename std::conditional<Stack16Cfg<C>(), Stack16,
-                                         Stack<C::LDS, C::LDS && RT_STACK_REMAT && (C::F & FEAT_INST_BLAS) != 0>>::type;
+using StackT = typename std::conditional<Stack16Cfg<C>(), Stack16<BlockThreads<C>()>,
+                                         Stack<C::LDS, C::LDS && RT_STACK_REMAT && (C::F & FEAT_INST_BLAS) != 0,
+                                               BlockThreads<C>()>>::type;
 
 // Division by a value b used many times, through its correctly rounded reciprocal
 // y = RN(1/b): q0 = RN(q*y), then one correction q1 = RN(q0 + RN-exact(q - b*q0) * y).
@@ -799,17 +805,17 @@ __device__ __forceinline__ Node load_node_lds(uint32_t addr)
 // CU). The flag is per launch, so the choice is wave-uniform.
 template <class C>
 constexpr bool StageShade() { return C::F != FEAT_SET_SPHERES; }
-// The block's dynamic LDS: [TLAS nodes][BLAS nodes][stack: entries x 256 lanes][materials][textures], one
+// The block's dynamic LDS: [TLAS nodes][BLAS nodes][stack: entries x block lanes][materials][textures], one
 // layout for the kernel's offsets and the launcher's allocation (launch_one)
 struct LdsLayout {
     size_t blas, stack, shade, total;   // byte offsets of the BLAS nodes, the stack and the material table; bytes
 };
 __host__ __device__ constexpr LdsLayout lds_layout(int n_nodes, int node_bytes, int n_blas, int stack_entries,
-                                                   int entry_bytes, int n_materials, int n_textures)
+                                                   int entry_bytes, int n_materials, int n_textures, int lanes)
 {
     const size_t blas = (size_t)n_nodes * (size_t)node_bytes;
     const size_t stack = blas + (size_t)n_blas * sizeof(rt_bvh_node);
-    const size_t shade = stack + (size_t)stack_entries * 256 * (size_t)entry_bytes;
+    const size_t shade = stack + (size_t)stack_entries * (size_t)lanes * (size_t)entry_bytes;
     return LdsLayout{blas, stack, shade, shade + (size_t)n_materials * 64 + (size_t)n_textures * 96};
 }
 // the variants that stage BLAS nodes (SceneDev.n_lds_blas; the host sets it only for them)
@@ -823,7 +829,7 @@ __device__ __forceinline__ LdsLayout lds_layout_of(const SceneDev& S)
 {
     return lds_layout(lds_node_count<C>(S), lds_node_bytes<C>(), StageBlas<C>() ? S.n_lds_blas : 0, C::LDS ? S.stack_entries : 0,
                       Stack16Cfg<C>() ? 2 : 4, StageShade<C>() ? S.n_lds_materials : 0,
-                      StageShade<C>() ? S.n_lds_textures : 0);
+                      StageShade<C>() ? S.n_lds_textures : 0, BlockThreads<C>());
 }
 
 // Closest hit in a BVH (nodes + leaf ranges of slots j, whose records are leaf_prims[j]).
@@ -844,7 +850,7 @@ __device__ __forceinline__ bool traverse(const SceneDev& S, int root, const RayT
 #if RT_SPTR
     // the stack pointer as an address, pre-scaled by the entry stride: a push or pop is one
     // add (not an add plus a shift-add of the index)
-    constexpr int SSTR = C::LDS ? 256 : 1;
+    constexpr int SSTR = C::LDS ? BlockThreads<C>() : 1;
     auto* sptr = &stack[sp0];
     using SE = typename std::remove_reference<decltype(*sptr)>::type;
     *sptr = (SE)DONE;
@@ -1723,7 +1729,7 @@ __device__ __forceinline__ void stage_lds(const SceneDev& S)
     if (S.n_lds_nodes > 0) {
         if constexpr (Wide<C>()) {   // the 4-wide records, child indices -> LDS byte addresses
             W4Node* dst = reinterpret_cast<W4Node*>(rt_lds + off);
-            for (int i = threadIdx.x; i < S.n_w4; i += 256) {
+            for (int i = threadIdx.x; i < S.n_w4; i += BlockThreads<C>()) {
                 W4Node o = S.w4[i];
 #pragma unroll
                 for (int c = 0; c < 4; ++c)
@@ -1732,7 +1738,7 @@ __device__ __forceinline__ void stage_lds(const SceneDev& S)
             }
         } else if constexpr (OctNodes<C>()) {   // one node per thread, rt_bvh_node -> LdsNode
             LdsNode* dst = reinterpret_cast<LdsNode*>(rt_lds + off);
-            for (int i = threadIdx.x; i < S.n_lds_nodes; i += 256) {
+            for (int i = threadIdx.x; i < S.n_lds_nodes; i += BlockThreads<C>()) {
                 const rt_bvh_node n = S.nodes[i];
                 LdsNode o;
 #pragma unroll
@@ -1750,7 +1756,7 @@ __device__ __forceinline__ void stage_lds(const SceneDev& S)
         } else {
             uint4* dst = reinterpret_cast<uint4*>(rt_lds + off);
             const uint4* src = reinterpret_cast<const uint4*>(S.nodes);
-            for (int i = threadIdx.x; i < S.n_lds_nodes * 4; i += 256) dst[i] = src[i];
+            for (int i = threadIdx.x; i < S.n_lds_nodes * 4; i += BlockThreads<C>()) dst[i] = src[i];
         }
         any = true;
     }
@@ -1758,7 +1764,7 @@ __device__ __forceinline__ void stage_lds(const SceneDev& S)
         if (S.n_lds_blas > 0) {   // the BLAS's BFS prefix, nodes[n_tlas_nodes, ...) (abi.cpp)
             uint4* db = reinterpret_cast<uint4*>(reinterpret_cast<char*>(rt_lds) + lds_layout_of<C>(S).blas);
             const uint4* sb = reinterpret_cast<const uint4*>(S.nodes + S.n_tlas_nodes);
-            for (int i = threadIdx.x; i < S.n_lds_blas * 4; i += 256) db[i] = sb[i];
+            for (int i = threadIdx.x; i < S.n_lds_blas * 4; i += BlockThreads<C>()) db[i] = sb[i];
             any = true;
         }
     }
@@ -1766,10 +1772,10 @@ __device__ __forceinline__ void stage_lds(const SceneDev& S)
         if (S.n_lds_materials > 0) {
             uint4* dm = reinterpret_cast<uint4*>(rt_lds + lds_shade_offset<C>(S));
             const uint4* sm = reinterpret_cast<const uint4*>(S.materials);
-            for (int i = threadIdx.x; i < S.n_lds_materials * 4; i += 256) dm[i] = sm[i];
+            for (int i = threadIdx.x; i < S.n_lds_materials * 4; i += BlockThreads<C>()) dm[i] = sm[i];
             uint4* dt = dm + S.n_lds_materials * 4;
             const uint4* stx = reinterpret_cast<const uint4*>(S.textures);
-            for (int i = threadIdx.x; i < S.n_lds_textures * 6; i += 256) dt[i] = stx[i];
+            for (int i = threadIdx.x; i < S.n_lds_textures * 6; i += BlockThreads<C>()) dt[i] = stx[i];
             any = true;
         }
     }
@@ -1977,7 +1983,7 @@ constexpr int min_waves()
 // KParams comes by pointer: read where used (scalar loads) instead of pinning ~70 SGPRs
 // for the whole kernel (by value it spilled SGPRs into VGPR lanes).
 template <class C>
-__global__ void __launch_bounds__(256, min_waves<C>()) trace_chunks(SceneDev S, const KParams* __restrict__ Pp,
+__global__ void __launch_bounds__(BlockThreads<C>(), min_waves<C>()) trace_chunks(SceneDev S, const KParams* __restrict__ Pp,
                                                                     double* __restrict__ partial,
                                                                     unsigned long long* __restrict__ counters)
 {
@@ -2102,7 +2108,7 @@ __device__ __forceinline__ unsigned lanes_below(uint64_t mask)
 // per-sample pool, so lanes still do not idle. Output: chunk partials for
 // reduce_chunks, 1/chunk of the per-sample buffer's bytes.
 template <class C, bool ITEMS>
-__global__ void __launch_bounds__(256, min_waves<C>()) trace_pool(SceneDev S, const KParams* __restrict__ Pp,
+__global__ void __launch_bounds__(BlockThreads<C>(), min_waves<C>()) trace_pool(SceneDev S, const KParams* __restrict__ Pp,
                                                                   double* __restrict__ samples,
                                                                   unsigned long long* __restrict__ counters,
                                                                   unsigned* __restrict__ work)
@@ -2397,19 +2403,19 @@ struct Launch {
     int* waves_per_simd;           // out (optional): resident blocks per CU = waves per SIMD (4-wave blocks)
 };
 
-// Resident 256-thread blocks per CU of a kernel (registers, LDS), reported to the caller.
+// Resident blocks per CU of a kernel (registers, LDS); waves per SIMD reported to the caller.
 template <class K>
-static int blocks_per_cu(const Launch& L, K kernel, size_t lds)
+static int blocks_per_cu(const Launch& L, K kernel, size_t lds, int bt)
 {
     int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, 256, lds) != hipSuccess || per_cu <= 0) per_cu = 1;
-    if (L.waves_per_simd) *L.waves_per_simd = per_cu;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, bt, lds) != hipSuccess || per_cu <= 0) per_cu = 1;
+    if (L.waves_per_simd) *L.waves_per_simd = per_cu * (bt / 256);   // 4 SIMDs per CU
     return per_cu;
 }
 
 // Persistent grid for the pool schedule: as many blocks as fit on the device at once.
 template <class K>
-static unsigned resident_blocks(const Launch& L, K kernel, size_t lds)
+static unsigned resident_blocks(const Launch& L, K kernel, size_t lds, int bt)
 {
     static int cus = 0;
     if (!cus) {
@@ -2417,7 +2423,7 @@ static unsigned resident_blocks(const Launch& L, K kernel, size_t lds)
         (void)hipGetDevice(&dev);
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
     }
-    return (unsigned)(cus * blocks_per_cu(L, kernel, lds));
+    return (unsigned)(cus * blocks_per_cu(L, kernel, lds, bt));
 }
 
 template <uint32_t F, bool S32, bool LDS, bool COUNT, bool F32>
@@ -2430,12 +2436,13 @@ static void launch_one(const Launch& L, hipStream_t stream, bool nall)
     const int node_bytes = wide ? (int)sizeof(W4Node) : nall && S32 ? (int)sizeof(LdsNode) : (int)sizeof(rt_bvh_node);   // lds_node_bytes
     const bool stage = F != FEAT_SET_SPHERES;                   // StageShade
     const bool blas = RT_STAGE_BLAS && (F & FEAT_INST_BLAS) != 0 && !F32;   // StageBlas
+    constexpr int bt = block_threads_of(F, F32), wpb = bt / 64;   // BlockThreads
     const size_t lds = lds_layout(wide ? S.n_w4 : S.n_lds_nodes, node_bytes, blas ? S.n_lds_blas : 0, LDS ? S.stack_entries : 0,
-                                  s16 ? 2 : 4, stage ? S.n_lds_materials : 0, stage ? S.n_lds_textures : 0).total;
+                                  s16 ? 2 : 4, stage ? S.n_lds_materials : 0, stage ? S.n_lds_textures : 0, bt).total;
     if (L.pool) {
         auto go = [&](auto kernel) {
-            const unsigned nb = std::min<unsigned long long>(resident_blocks(L, kernel, lds), (L.n_blocks + 3) / 4);
-            hipLaunchKernelGGL(kernel, dim3(nb), dim3(256), lds, stream, S, L.P, L.out, L.counters, L.work);
+            const unsigned nb = std::min<unsigned long long>(resident_blocks(L, kernel, lds, bt), (L.n_blocks + wpb - 1) / wpb);
+            hipLaunchKernelGGL(kernel, dim3(nb), dim3(bt), lds, stream, S, L.P, L.out, L.counters, L.work);
         };
         if (L.pool == 2) {
             if (nall) go(trace_pool<Cfg<F, S32, LDS, true, COUNT, F32>, true>);
@@ -2446,10 +2453,10 @@ static void launch_one(const Launch& L, hipStream_t stream, bool nall)
         }
         return;
     }
-    const unsigned nb = (unsigned)((L.n_blocks + 3) / 4);
+    const unsigned nb = (unsigned)((L.n_blocks + wpb - 1) / wpb);
     auto go = [&](auto kernel) {
-        if (L.waves_per_simd) (void)blocks_per_cu(L, kernel, lds);
-        hipLaunchKernelGGL(kernel, dim3(nb), dim3(256), lds, stream, S, L.P, L.out, L.counters);
+        if (L.waves_per_simd) (void)blocks_per_cu(L, kernel, lds, bt);
+        hipLaunchKernelGGL(kernel, dim3(nb), dim3(bt), lds, stream, S, L.P, L.out, L.counters);
     };
     if (nall) go(trace_chunks<Cfg<F, S32, LDS, true, COUNT, F32>>);
     else go(trace_chunks<Cfg<F, S32, LDS, false, COUNT, F32>>);

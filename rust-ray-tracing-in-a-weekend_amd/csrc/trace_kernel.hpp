@@ -19,7 +19,22 @@
 #define RT_WIDE 0
 #endif
 
+// Threads per workgroup of the final-scene variant's kernels (the others: 256). 512 (8 waves)
+// shares one LDS copy of the TLAS and materials among twice the waves, which leaves room for
+// the instanced BLAS in LDS (SceneDev.n_lds_blas; the host sizes that budget with it): the
+// final scene's 1000-sphere BLAS 512 of 548 nodes staged instead of 64, C4 1920x1080x100
+// 110.95 -> 108.23 ms; 512 threads with 64 staged 111.27 (profiles/r03r_ab_c4.log)
+#ifndef RT_BLOCK_FINAL
+#define RT_BLOCK_FINAL 512
+#endif
+
 namespace rtk {
+
+// workgroup threads of a kernel variant (host and device): see RT_BLOCK_FINAL
+__host__ __device__ constexpr int block_threads_of(uint32_t variant_features, bool f32)
+{
+    return variant_features == 287u /* FEAT_SET_FINAL */ && !f32 ? RT_BLOCK_FINAL : 256;
+}
 
 // A 4-wide TLAS node (RT_WIDE): binary node n with each internal child replaced by that child's
 // two children. Per axis the four children's lower planes, upper planes and lower planes again,
@@ -122,6 +137,7 @@ enum : uint32_t {
     // + Perlin and image textures, instances over spheres, media bounded by spheres (final scene)
     FEAT_SET_FINAL = FEAT_RECT | FEAT_INST | FEAT_MEDIUM | FEAT_NOISE | FEAT_IMAGE | FEAT_INST_BLAS
 };
+static_assert(FEAT_SET_FINAL == 287u, "block_threads_of");
 
 struct LaunchOpts {
     uint32_t features;  // scene features (FEAT_*)
