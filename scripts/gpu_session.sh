@@ -12,7 +12,7 @@
 #   f32_c2..c4       bench.py --config Cn --precision f32
 #   prof_c2..c5      scripts/profile_r02.sh on that config (kernel trace + PMC passes)
 #   calib            scripts/calib_r02.sh (VALU issue-rate calibration through rocprofv3)
-# env: PREFIX (log-name prefix, e.g. r03a_)
+# env: PREFIX (log-name prefix, e.g. r03a_). Round 3 sessions: scripts/sessions_r03.sh
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 P=${PREFIX:-}
 NB="--no-cpu-baseline --no-count"
