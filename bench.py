@@ -2,10 +2,11 @@
 """Headline benchmark: Msamples/s (pixels x spp per second) on the 1200x800 random-spheres
 scene, 500 spp, max depth 50 (BASELINE.json configs[1] = SURVEY C2), at N GPUs.
 
-One step = one full render of the frame: every rank traces its interleaved row shard
-(rows y = rank + k*N) through the HIP megakernel (C ABI, librtiow_amd.so); for N > 1
-the shards are gathered to rank 0 over RCCL (torch.distributed "nccl") and put back
-in row order — inside the timed region. The scene is built and uploaded before timing.
+One step = one full render of the frame: every rank traces its shard through the HIP
+megakernel (C ABI, librtiow_amd.so) — at N > 1 the frame's 8x8 tiles t = rank + k*N
+(rt_render_params.tile_shard; --shard rows: rows y = rank + k*N) — and the shards are
+gathered to rank 0 over RCCL (torch.distributed "nccl") and put back in image order —
+inside the timed region. The scene is built and uploaded before timing.
 
 Prints ONE JSON line (rank 0). Besides the contract fields it carries
   roofline:     the binding resource, VALU issue: the issue cycles the launch's VALU
@@ -73,6 +74,9 @@ def parse():
     ap.add_argument("--no-count", action="store_true", help="skip the count_work pass (profiling runs)")
     ap.add_argument("--ppm", default="", help="write the rendered frame (rank 0) as a P3 PPM")
     ap.add_argument("--frame-npy", default="", help="save the rendered f32 frame (rank 0) as .npy")
+    ap.add_argument("--shard", default="tiles", choices=["tiles", "rows"],
+                    help="N > 1 partition: the frame's 8x8 tiles round-robin (rt_render_params.tile_shard) or "
+                         "single rows round-robin")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="N > 1: nccl (RCCL over xGMI, the product) or gloo (host-staged slabs; lets several "
                          "ranks share one GPU, for tests of this N > 1 path on a 1-GPU box)")
@@ -215,13 +219,23 @@ def main():
         renderer.set_precision(rt.RT_PREC_F32)
     t_build = time.perf_counter() - t_build
 
-    # ranks take rows round-robin (ROW_BLOCK 1). 8-row bands (row_block 8) keep every 8x8
-    # work tile contiguous in the image and raise a shard's per-sample rate ~3 % at 8 GPUs,
-    # but 100 bands over 8 ranks leave ranks of 13 and 12 bands: the job is slower
-    # (scripts/shard_coherence.py, profiles/r02p_shard.log)
-    rows = rt.rows_in_shard(H, rank, world, ROW_BLOCK)
-    rows_max = max(rt.rows_in_shard(H, r, world, ROW_BLOCK) for r in range(world))
-    slab = torch.zeros((rows_max, W, 3), dtype=torch.float32, device=device)
+    # N > 1: ranks take the frame's 8x8 tiles round-robin (tile shards: every work tile stays a
+    # compact 8x8 block of the image and every rank gets the same tile count to within one).
+    # Rank 0's C2 shard at N = 8 runs at 6,202 Msamples/s in 8x8 tiles against 5,993 as single
+    # rows 8 apart (8-row bands, the other compact layout, leave 13 vs 12 bands per rank;
+    # scripts/shard_coherence.py, profiles/r03u_shard.log). --shard rows keeps the row partition.
+    tiles = world > 1 and args.shard == "tiles"
+    if tiles:
+        n_mine = rt.tiles_in_shard(W, H, rank, world)
+        n_max = max(rt.tiles_in_shard(W, H, r, world) for r in range(world))
+        px_mine, slab_shape = 64 * n_mine, (8, 8 * n_max, 3)
+    else:
+        rows = rt.rows_in_shard(H, rank, world, ROW_BLOCK)
+        rows_max = max(rt.rows_in_shard(H, r, world, ROW_BLOCK) for r in range(world))
+        px_mine, slab_shape = rows * W, (rows_max, W, 3)
+    # the render writes its shard contiguously at the start of the slab (a tile shard's 8 x 8n
+    # layout is then a prefix of the padded 8 x 8n_max buffer, read back with the same view)
+    slab = torch.zeros(slab_shape, dtype=torch.float32, device=device)
     # gloo gathers host copies of the slabs (staged through pinned memory), RCCL device slabs
     stage = torch.empty(slab.shape, dtype=slab.dtype, pin_memory=True) if gloo else None
     gathered = ([torch.empty_like(stage if gloo else slab) for _ in range(world)]
@@ -233,7 +247,16 @@ def main():
     # op of a step runs under this stream; NCCL orders its gather after it.
     stream = torch.cuda.Stream(device)
     params = rt.Renderer.params(W, H, spp, depth, bg, args.seed, row_begin=rank, row_stride=world,
-                                spp_chunk=args.spp_chunk, out_format=rt.RT_OUT_F32, row_block=ROW_BLOCK)
+                                spp_chunk=args.spp_chunk, out_format=rt.RT_OUT_F32,
+                                row_block=1 if tiles else ROW_BLOCK, tile_shard=int(tiles))
+
+    def assemble(slabs):
+        if tiles:
+            views = [g.reshape(-1)[: 3 * 64 * rt.tiles_in_shard(W, H, r, world)].view(8, -1, 3)
+                     for r, g in enumerate(slabs)]
+            rt.assemble_tiles(views, W, H, world, out=frame)
+        else:
+            rt.assemble_rows(slabs, H, world, out=frame, row_block=ROW_BLOCK)
     kernel_ms = []
 
     def step():
@@ -244,12 +267,11 @@ def main():
                 stream.synchronize()
                 dist.gather(stage, gathered if rank == 0 else None, dst=0)
                 if rank == 0:
-                    dev = [g.to(device, non_blocking=True) for g in gathered]
-                    rt.assemble_rows(dev, H, world, out=frame, row_block=ROW_BLOCK)
+                    assemble([g.to(device, non_blocking=True) for g in gathered])
             elif world > 1:
                 dist.gather(slab, gathered if rank == 0 else None, dst=0)
                 if rank == 0:
-                    rt.assemble_rows(gathered, H, world, out=frame, row_block=ROW_BLOCK)
+                    assemble(gathered)
             else:
                 frame[:] = slab[:H]
 
@@ -336,7 +358,7 @@ def main():
     cs = None
     if not args.no_count and not f32:   # count_work is an f64-mode diagnostic
         cp = rt.Renderer.params(W, H, count_spp, depth, bg, args.seed, row_begin=rank, row_stride=world,
-                                row_block=ROW_BLOCK,
+                                row_block=1 if tiles else ROW_BLOCK, tile_shard=int(tiles),
                                 spp_chunk=min(args.spp_chunk, count_spp), out_format=rt.RT_OUT_F32, count_work=1)
         renderer.render(cam, cp)
         cs = renderer.stats()
@@ -345,7 +367,7 @@ def main():
         bytes_per_sample = (cs.node_visits * cs.node_bytes + cs.prim_tests * cs.prim_bytes +
                             cs.casts * cs.material_bytes) / max(cs.samples, 1)
         alg = {"bytes_per_sample": round(bytes_per_sample, 1),
-               "gbs": round(bytes_per_sample * rows * W * spp / (k_ms * 1e-3) / 1e9, 1),
+               "gbs": round(bytes_per_sample * px_mine * spp / (k_ms * 1e-3) / 1e9, 1),
                "casts_per_sample": round(cs.casts / max(cs.samples, 1), 4),
                "nodes_per_cast": round(cs.node_visits / max(cs.casts, 1), 3),
                "prims_per_cast": round(cs.prim_tests / max(cs.casts, 1), 3),
@@ -431,12 +453,13 @@ def main():
             "vs_baseline": None,
             "dtype": args.precision,
             "data": "synthetic (seeded scene builders, scene_seed=render_seed=%d)" % args.seed,
-            "config": {"workload": "%s %s %dx%d, %d spp, max depth %d, row-sharded over %d GPU"
+            "config": {"workload": "%s %s %dx%d, %d spp, max depth %d, %s-sharded over %d GPU"
                                    % (args.config, SCENE_NAMES.get(args.scene, "scene %d" % args.scene), W, H, spp,
-                                      depth, world),
+                                      depth, "tile" if tiles else "row", world),
                        "scene": args.scene, "width": W, "height": H, "spp": spp, "max_depth": depth,
-                       "parallelism": "rows interleaved over %d rank(s), %s gather"
-                                      % (world, "gloo (host-staged)" if gloo else "RCCL")},
+                       "parallelism": "%s interleaved over %d rank(s), %s gather"
+                                      % ("8x8 tiles" if tiles else "rows", world,
+                                         "gloo (host-staged)" if gloo else "RCCL")},
             "roofline": roofline,
             "cpu_baseline": cpu,
             "parity": parity,

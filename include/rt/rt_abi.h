@@ -160,18 +160,28 @@ typedef struct rt_render_params {
                                     into bands of B rows and the shard is bands j = row_begin +
                                     m*row_stride (rows jB .. jB+B-1 < height): row-band interleave, so
                                     a multi-GPU shard keeps 8x8 work tiles contiguous in the image */
-    int32_t reserved_;
+    int32_t tile_shard;          /* 0: rows as above. 1 (row_block 0 / 1): the shard is the 8x8 pixel tiles
+                                    t = row_begin + m*row_stride of the frame's tile grid (ceil(width/8)
+                                    tiles per tile row, t = ty*ceil(width/8) + tx), written side by side
+                                    as one 8-row slab: out row k holds rows 8*ty + k of the shard's
+                                    tiles, tile m in columns 8m .. 8m+7 (rt_tiles_in_shard tiles; the
+                                    pixels of an edge tile past the image are rendered and meaningless).
+                                    Every shard is whole 8x8 tiles, so a multi-GPU shard keeps the
+                                    kernel's work tiles compact in the image at any GPU count. */
 } rt_render_params;
 
-/* Renders the selected rows into out (rows_local x width x 3, row k = the k-th
- * selected row) as the per-pixel mean radiance sum * (1/spp). Synchronous unless
- * out_on_device is set, in which case the work is only enqueued on `stream`. */
+/* Renders the selected rows (or tiles) into out (rows_local x width x 3, row k = the k-th
+ * selected row; tile shards: 8 x (8 * tiles_local) x 3) as the per-pixel mean radiance
+ * sum * (1/spp). Synchronous unless out_on_device is set, in which case the work is only
+ * enqueued on `stream`. */
 int rt_render(rt_ctx* ctx, const rt_camera* cam, const rt_render_params* p, void* out);
 
 /* Rows rendered for (height, row_begin, row_stride). */
 int rt_rows_in_shard(int height, int row_begin, int row_stride);
 /* Rows rendered for (height, row_begin, row_stride, row_block) (rt_render_params.row_block). */
 int rt_rows_in_band_shard(int height, int row_begin, int row_stride, int row_block);
+/* 8x8 tiles rendered for (width, height, row_begin, row_stride) with tile_shard = 1. */
+int rt_tiles_in_shard(int width, int height, int tile_begin, int tile_stride);
 
 typedef struct rt_stats {
     double kernel_ms;            /* last rt_render: trace kernel time (HIP events) */

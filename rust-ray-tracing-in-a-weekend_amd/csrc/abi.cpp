@@ -1160,17 +1160,39 @@ int rt_rows_in_band_shard(int height, int row_begin, int row_stride, int row_blo
     return (mine - 1) * row_block + std::min(row_block, height - last * row_block);
 }
 
+int rt_tiles_in_shard(int width, int height, int tile_begin, int tile_stride)
+{
+    if (width <= 0 || height <= 0) return 0;
+    const long long tiles = (long long)((width + 7) / 8) * ((height + 7) / 8);
+    if (tiles > 0x7fffffffLL) return 0;
+    return rt_rows_in_shard((int)tiles, tile_begin, tile_stride);
+}
+
 static int row_block_of(const rt_render_params* p) { return p->row_block > 1 ? p->row_block : 1; }
 static int shard_rows(const rt_render_params* p)
 {
     return rt_rows_in_band_shard(p->height, p->row_begin, p->row_stride, row_block_of(p));
+}
+// The shard's output layout (the kernel's pixel grid): its rows of the image, or (tile_shard)
+// its 8x8 tiles side by side in one 8-row slab
+struct Layout {
+    int w, rows;
+};
+static Layout layout_of(const rt_render_params* p)
+{
+    if (p->tile_shard) {
+        const int n = rt_tiles_in_shard(p->width, p->height, p->row_begin, p->row_stride);
+        return Layout{8 * n, n > 0 ? 8 : 0};
+    }
+    return Layout{p->width, shard_rows(p)};
 }
 
 static bool bad_geometry(const rt_render_params* p)
 {
     const int b = row_block_of(p);
     return p->width < 2 || p->height < 2 || p->row_stride < 1 || p->row_begin < 0 || p->spp_chunk < 0 ||
-           (b & (b - 1)) || b > 64 || (long long)p->width * p->height > 0xffffffffLL;
+           (b & (b - 1)) || b > 64 || (long long)p->width * p->height > 0xffffffffLL ||
+           (p->tile_shard != 0 && (p->tile_shard != 1 || b > 1));
 }
 
 static int grow(rt_ctx* c, hipStream_t stream, double*& buf, size_t& cap, size_t need, bool* oom = nullptr)
@@ -1211,8 +1233,9 @@ struct Sink {
 static int run_range(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, int s_begin, int s_end, int chunk,
                      hipStream_t stream, const Sink& sink)
 {
-    const int n_rows = shard_rows(p);
-    const long long n_px = (long long)n_rows * p->width;
+    const Layout lay = layout_of(p);
+    const int n_rows = lay.rows;
+    const long long n_px = (long long)n_rows * lay.w;
     const size_t px = (size_t)std::max<long long>(n_px, 1);
 
     rtk::KParams K;
@@ -1226,16 +1249,19 @@ static int run_range(rt_ctx* c, const rt_camera* cam, const rt_render_params* p,
     K.inv_wm1 = 1.0 / K.wm1;
     K.inv_hm1 = 1.0 / K.hm1;
     K.seed = p->render_seed;
-    K.width = p->width;
+    K.width = lay.w;
     K.height = p->height;
+    K.img_width = p->width;
     K.max_depth = p->max_depth;
     K.spp_chunk = chunk;
     K.row_begin = p->row_begin;
     K.row_stride = p->row_stride;
     K.row_block_shift = 0;
     while ((1 << K.row_block_shift) < row_block_of(p)) K.row_block_shift++;
+    K.tile_shard = p->tile_shard;
+    K.img_tiles_x = (p->width + 7) / 8;
     K.n_rows = n_rows;
-    K.tiles_x = (p->width + 7) / 8;
+    K.tiles_x = (lay.w + 7) / 8;
     K.tiles_y = (n_rows + 7) / 8;
 
     const bool count = p->count_work != 0;
@@ -1262,8 +1288,8 @@ static int run_range(rt_ctx* c, const rt_camera* cam, const rt_render_params* p,
     const long long total = s_end - s_begin;
     const size_t px_bytes = px * 3 * sizeof(double);
     // one sample's records in the per-sample buffer: whole 8x8 tiles (trace_kernel.hpp, tiled_record)
-    const rtk::SampleTiles tiles{p->width, n_rows, (p->width + 7) / 8};
-    const size_t sample_bytes = rtk::tiled_pixels(p->width, n_rows) * 3 * sizeof(double);
+    const rtk::SampleTiles tiles{lay.w, n_rows, (lay.w + 7) / 8};
+    const size_t sample_bytes = rtk::tiled_pixels(lay.w, n_rows) * 3 * sizeof(double);
     // the TLAS in LDS (read-only, shared by the block) when it fits the per-block budget
     rtk::SceneDev S = c->S;
     S.n_lds_nodes = c->opt_lds_nodes ? std::min(c->n_tlas_nodes, kMaxLdsNodes) : 0;
@@ -1484,9 +1510,9 @@ int rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, void* 
     if (!c->has_scene) return fail(RT_ERR_NO_SCENE, "no scene uploaded");
     if (bad_geometry(p) || p->spp < 1 || p->max_depth < 0 || (p->out_format != RT_OUT_F32 && p->out_format != RT_OUT_F64))
         return fail(RT_ERR_INVALID, "bad render params");
-    const int n_rows = shard_rows(p);
+    const Layout lay = layout_of(p);
     const int chunk = p->spp_chunk > 0 ? std::min(p->spp_chunk, p->spp) : auto_chunk(p->spp);
-    const long long n_px = (long long)n_rows * p->width;
+    const long long n_px = (long long)lay.rows * lay.w;
 
     HIP_TRY(hipSetDevice(c->device));
     hipStream_t stream = p->stream ? (hipStream_t)p->stream : c->stream;
@@ -1515,7 +1541,7 @@ int rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, void* 
 // ---- progressive accumulation -----------------------------------------------------------------
 struct rt_accum {
     rt_ctx* ctx = nullptr;
-    int width = 0, height = 0, row_begin = 0, row_stride = 1, row_block = 1, n_rows = 0, chunk = 1;
+    int width = 0, height = 0, row_begin = 0, row_stride = 1, row_block = 1, tile_shard = 0, n_rows = 0, chunk = 1;
     long long n_px = 0;
     int64_t done = 0;
     double* sums = nullptr;             // device, n_px x 3
@@ -1536,9 +1562,11 @@ int rt_accum_create(rt_ctx* c, const rt_render_params* p, rt_accum** out)
     a->row_begin = p->row_begin;
     a->row_stride = p->row_stride;
     a->row_block = row_block_of(p);
-    a->n_rows = shard_rows(p);
+    a->tile_shard = p->tile_shard;
+    const Layout lay = layout_of(p);
+    a->n_rows = lay.rows;
     a->chunk = p->spp_chunk > 0 ? p->spp_chunk : auto_chunk(p->spp);
-    a->n_px = (long long)a->n_rows * p->width;
+    a->n_px = (long long)lay.rows * lay.w;
     a->last_stream = c->stream;
     const size_t bytes = (size_t)std::max<long long>(a->n_px, 1) * 3 * sizeof(double);
     hipError_t e = hipSetDevice(c->device);
@@ -1568,7 +1596,7 @@ int rt_accum_add(rt_ctx* c, rt_accum* a, const rt_camera* cam, const rt_render_p
     if (a->ctx != c) return fail(RT_ERR_INVALID, "accumulator belongs to another context");
     if (!c->has_scene) return fail(RT_ERR_NO_SCENE, "no scene uploaded");
     if (p->width != a->width || p->height != a->height || p->row_begin != a->row_begin ||
-        p->row_stride != a->row_stride || row_block_of(p) != a->row_block)
+        p->row_stride != a->row_stride || row_block_of(p) != a->row_block || p->tile_shard != a->tile_shard)
         return fail(RT_ERR_INVALID, "render params do not match the accumulator's shard");
     if (sample_count < 0 || p->max_depth < 0 || a->done + sample_count > 0x7fffffffLL)
         return fail(RT_ERR_INVALID, "bad sample range");

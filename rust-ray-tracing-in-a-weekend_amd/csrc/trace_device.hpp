@@ -1631,7 +1631,7 @@ __device__ __forceinline__ void camera_begin(const KParams& P, int x, int y, rt_
 __device__ __forceinline__ void camera_begin(const KParams& P, int x, int y, rt_pstream& st, double& u, double& v)
 {
 #ifdef RT_PROBE_FAST_CAMERA  // timing probe: NOT the product
-    u = ((double)x + rt_unit53(ds_u64(st))) * __builtin_amdgcn_rcp((double)P.width - 1.0);
+    u = ((double)x + rt_unit53(ds_u64(st))) * __builtin_amdgcn_rcp((double)P.img_width - 1.0);
     v = ((double)y + rt_unit53(ds_u64(st))) * __builtin_amdgcn_rcp((double)P.height - 1.0);
 #else
     u = div_rcp((double)x + rt_unit53(ds_u64(st)), P.wm1, P.inv_wm1);
@@ -1920,10 +1920,25 @@ __device__ __forceinline__ int image_row(const KParams& P, int k)
     const int s = P.row_block_shift;
     return ((P.row_begin + (k >> s) * P.row_stride) << s) + (k & ((1 << s) - 1));
 }
+// image pixel (X, Y) of the shard's grid pixel (x, k): a row shard's x and image_row(k); a tile
+// shard's grid is its tiles side by side (tile m = the frame's tile row_begin + m*row_stride)
+__device__ __forceinline__ void image_xy(const KParams& P, int x, int k, int& X, int& Y)
+{
+    if (P.tile_shard) {   // wave-uniform
+        const unsigned t = (unsigned)P.row_begin + (unsigned)(x >> 3) * (unsigned)P.row_stride;
+        const unsigned ty = t / (unsigned)P.img_tiles_x;
+        X = (int)(t - ty * (unsigned)P.img_tiles_x) * 8 + (x & 7);
+        Y = (int)ty * 8 + k;
+    } else {
+        X = x;
+        Y = image_row(P, k);
+    }
+}
 
 // lane -> (chunk, pixel): a wave64 owns an 8x8 tile of one chunk
 struct LaneWork {
-    int x, y, k, chunk, s_begin, s_end;
+    int x, y, k, chunk, s_begin, s_end;   // x, k: the shard's grid; y: image row
+    int ix;                               // image column
     uint32_t pixel;
 };
 __device__ __forceinline__ bool lane_work(const KParams& P, LaneWork& w)
@@ -1937,8 +1952,10 @@ __device__ __forceinline__ bool lane_work(const KParams& P, LaneWork& w)
     w.x = (tile % P.tiles_x) * 8 + (lane & 7);
     w.k = (tile / P.tiles_x) * 8 + (lane >> 3);
     if (w.x >= P.width || w.k >= P.n_rows) return false;
-    w.y = image_row(P, w.k);
-    w.pixel = (uint32_t)w.y * (uint32_t)P.width + (uint32_t)w.x;
+    int ix;
+    image_xy(P, w.x, w.k, ix, w.y);
+    w.pixel = (uint32_t)w.y * (uint32_t)P.img_width + (uint32_t)ix;
+    w.ix = ix;
     w.s_begin = P.sample_begin + w.chunk * P.spp_chunk;
     w.s_end = min(P.spp, w.s_begin + P.spp_chunk);
     return true;
@@ -2012,7 +2029,7 @@ __global__ void __launch_bounds__(BlockThreads<C>(), min_waves<C>()) trace_chunk
             new_sample = false;
             ds_start(st, P.seed, w.pixel, (uint32_t)s);
             key.sample = (uint32_t)s;
-            camera_ray(P, w.x, w.y, st, r);
+            camera_ray(P, w.ix, w.y, st, r);
             finish_ray<C>(r, S.has_spheres != 0);
             Tr = Tg = Tb = (R)1;
             depth = P.max_depth;
@@ -2240,11 +2257,12 @@ __global__ void __launch_bounds__(BlockThreads<C>(), min_waves<C>()) trace_pool(
                     cnt.cam_lanes++;
                     if (first_active_lane()) cnt.cam_steps++;
                 }
-                const int y = image_row(P, k);
-                key.pixel = (uint32_t)y * (uint32_t)P.width + (uint32_t)x;
+                int ix, y;
+                image_xy(P, x, k, ix, y);
+                key.pixel = (uint32_t)y * (uint32_t)P.img_width + (uint32_t)ix;
                 key.sample = (uint32_t)s;
                 ds_start(st, P.seed, key.pixel, (uint32_t)s);
-                camera_begin(P, x, y, st, u, v);
+                camera_begin(P, ix, y, st, u, v);
                 Tr = Tg = Tb = (R)1;
                 if constexpr (!ITEMS) cr = cg = cb = 0.0;  // ITEMS: the chunk's running sum
                 depth = P.max_depth;
@@ -2309,11 +2327,12 @@ __global__ void __launch_bounds__(BlockThreads<C>(), min_waves<C>()) trace_pool(
                 if (first_active_lane()) cnt.cam_steps++;
             }
             new_sample = false;
-            const int y = image_row(P, k);
-            key.pixel = (uint32_t)y * (uint32_t)P.width + (uint32_t)x;
+            int ix, y;
+            image_xy(P, x, k, ix, y);
+            key.pixel = (uint32_t)y * (uint32_t)P.img_width + (uint32_t)ix;
             key.sample = (uint32_t)s;
             ds_start(st, P.seed, key.pixel, (uint32_t)s);
-            camera_ray(P, x, y, st, r);
+            camera_ray(P, ix, y, st, r);
             if constexpr (!RT_FINISH_AT_TRACE) finish_ray<C>(r, S.has_spheres != 0);
             Tr = Tg = Tb = (R)1;
             if constexpr (!ITEMS) cr = cg = cb = 0.0;  // ITEMS: the chunk's running sum

@@ -102,7 +102,7 @@ struct KParams {
     double wm1, hm1;    // width - 1, height - 1 (the jitter divisors of main.rs:517-518)
     double inv_wm1, inv_hm1;  // 1 / (width - 1), 1 / (height - 1), correctly rounded
     uint64_t seed;
-    int32_t width, height, spp, max_depth;
+    int32_t width, height, spp, max_depth;   // width: of the shard's pixel grid (the image's, or a tile slab's)
     int32_t spp_chunk, n_chunks;
     int32_t row_begin, row_stride, n_rows;
     int32_t row_block_shift;    // rows in bands of 2^shift (rt_render_params.row_block); 0: single rows
@@ -112,6 +112,9 @@ struct KParams {
     int32_t block_samples;      // per-sample pool: samples per work block (one tile x this many samples)
     uint32_t n_work_blocks;     // pool schedules: tiles x sample groups of this launch (host-computed: in
                                 // the kernel the division's VGPR result stayed live through the loop)
+    int32_t img_width;          // the image's width (pixel keys)
+    int32_t tile_shard;         // rt_render_params.tile_shard: grid tile m = the frame's tile row_begin + m*row_stride
+    int32_t img_tiles_x;        // tiles per tile row of the image
 };
 
 // Scene features (which code a kernel variant must contain).

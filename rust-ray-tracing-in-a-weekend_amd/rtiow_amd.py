@@ -52,7 +52,7 @@ EXPORTED = [
     "rt_world_box", "rt_world_translate", "rt_world_rotate_y", "rt_world_constant_medium",
     "rt_world_bvh", "rt_world_push", "rt_world_build_scene", "rt_world_info_get", "rt_camera_new",
     "rt_scene_preset_get", "rt_scene_camera", "rt_world_flatten", "rt_ctx_upload_soa",
-    "rt_ctx_upload_world", "rt_render", "rt_rows_in_shard", "rt_rows_in_band_shard", "rt_last_stats", "rt_last_counters", "rt_write_ppm",
+    "rt_ctx_upload_world", "rt_render", "rt_rows_in_shard", "rt_rows_in_band_shard", "rt_tiles_in_shard", "rt_last_stats", "rt_last_counters", "rt_write_ppm",
     "rt_ctx_set_variant", "rt_device_eval", "rt_accum_create", "rt_accum_destroy", "rt_accum_add",
     "rt_accum_get", "rt_accum_set", "rt_accum_resolve", "rt_render_progressive", "rt_ctx_set_schedule", "rt_ctx_set_precision",
     "rt_scene_validate",
@@ -107,7 +107,7 @@ class RenderParams(ctypes.Structure):
                 ("row_stride", ctypes.c_int32), ("out_format", ctypes.c_int32),
                 ("out_on_device", ctypes.c_int32), ("count_work", ctypes.c_int32),
                 ("background", ctypes.c_double * 3), ("render_seed", ctypes.c_uint64),
-                ("stream", ctypes.c_void_p), ("row_block", ctypes.c_int32), ("reserved_", ctypes.c_int32)]
+                ("stream", ctypes.c_void_p), ("row_block", ctypes.c_int32), ("tile_shard", ctypes.c_int32)]
 
 
 class Stats(ctypes.Structure):
@@ -168,7 +168,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "rt_scene_validate": ([ctypes.POINTER(SceneSoA), ctypes.POINTER(ctypes.c_int32),
                                ctypes.POINTER(ctypes.c_int32)], I), "rt_ctx_upload_world": ([P, P, I], I),
         "rt_render": ([P, ctypes.POINTER(Camera), ctypes.POINTER(RenderParams), P], I),
-        "rt_rows_in_shard": ([I, I, I], I), "rt_rows_in_band_shard": ([I, I, I, I], I), "rt_last_stats": ([P, ctypes.POINTER(Stats)], I),
+        "rt_rows_in_shard": ([I, I, I], I), "rt_rows_in_band_shard": ([I, I, I, I], I),
+        "rt_tiles_in_shard": ([I, I, I, I], I), "rt_last_stats": ([P, ctypes.POINTER(Stats)], I),
         "rt_last_counters": ([P, P, I], I),
         "rt_write_ppm": ([P, I, I, ctypes.c_char_p], I),
         "rt_device_eval": ([P, I, P, P, P, P, I], I), "rt_ctx_set_variant": ([P, I, I, I], I),
@@ -335,6 +336,14 @@ def rows_in_shard(height: int, row_begin: int, row_stride: int, row_block: int =
     return load_library().rt_rows_in_shard(height, row_begin, row_stride)
 
 
+def shard_shape(params) -> tuple:
+    """(rows, width) of a render's output: its rows of the image, or a tile shard's slab."""
+    if params.tile_shard:
+        n = tiles_in_shard(params.width, params.height, params.row_begin, params.row_stride)
+        return (8 if n else 0), 8 * n
+    return rows_in_shard(params.height, params.row_begin, params.row_stride, params.row_block), params.width
+
+
 def shard_rows(height: int, rank: int, world: int, row_block: int = 1):
     """Image rows of rank `rank` in the N-way partition, in the shard's order: single rows
     y = rank + k*world, or bands of row_block rows interleaved the same way."""
@@ -342,6 +351,37 @@ def shard_rows(height: int, rank: int, world: int, row_block: int = 1):
         return list(range(rank, height, world))
     return [y for band in range(rank, (height + row_block - 1) // row_block, world)
             for y in range(band * row_block, min(height, (band + 1) * row_block))]
+
+
+def tiles_in_shard(width: int, height: int, tile_begin: int, tile_stride: int) -> int:
+    """8x8 tiles of a tile shard (rt_render_params.tile_shard = 1)."""
+    return load_library().rt_tiles_in_shard(width, height, tile_begin, tile_stride)
+
+
+def _perm(a, axes):
+    return a.permute(*axes) if hasattr(a, "permute") else a.transpose(axes)
+
+
+def assemble_tiles(slabs, width: int, height: int, world: int, out=None):
+    """Inverse of the tile partition: slabs[r] is rank r's 8 x (8 * n_r) x 3 tile slab (tiles
+    t = r + m*world of the frame's tile grid side by side; wider padding is ignored). Works on
+    numpy arrays and torch tensors alike; returns the height x width x 3 frame."""
+    tx, ty = (width + 7) // 8, (height + 7) // 8
+    like = slabs[0]
+    if hasattr(like, "new_empty"):
+        tiles = like.new_empty((ty * tx, 8, 8, like.shape[-1]))
+    else:
+        import numpy as _np
+        tiles = _np.empty((ty * tx, 8, 8, like.shape[-1]), dtype=like.dtype)
+    for r in range(world):
+        n = len(range(r, ty * tx, world))
+        if n:
+            tiles[r::world] = _perm(slabs[r][:, :8 * n].reshape(8, n, 8, like.shape[-1]), (1, 0, 2, 3))
+    frame = _perm(tiles.reshape(ty, tx, 8, 8, like.shape[-1]), (0, 2, 1, 3, 4)).reshape(ty * 8, tx * 8, like.shape[-1])
+    if out is None:
+        return frame[:height, :width]
+    out[...] = frame[:height, :width]
+    return out
 
 
 def assemble_rows(slabs, height: int, world: int, out=None, row_block: int = 1):
@@ -400,9 +440,10 @@ class Renderer:
     @staticmethod
     def params(width, height, spp, max_depth=50, background=(0.0, 0.0, 0.0), render_seed=1, row_begin=0,
                row_stride=1, spp_chunk=0, out_format=RT_OUT_F32, out_on_device=0, count_work=0, stream=None,
-               row_block=1):
+               row_block=1, tile_shard=0):
         p = RenderParams()
         p.row_block = row_block
+        p.tile_shard = tile_shard
         p.width, p.height, p.spp, p.max_depth = width, height, spp, max_depth
         p.spp_chunk, p.row_begin, p.row_stride = spp_chunk, row_begin, row_stride
         p.out_format, p.out_on_device, p.count_work = out_format, out_on_device, count_work
@@ -412,13 +453,14 @@ class Renderer:
         return p
 
     def render(self, camera: Camera, params: RenderParams, out=None) -> np.ndarray:
-        """Host-output render: returns rows_local x width x 3 mean radiance (row k = k-th selected row)."""
-        n_rows = rows_in_shard(params.height, params.row_begin, params.row_stride, params.row_block)
+        """Host-output render: returns rows_local x width x 3 mean radiance (row k = k-th selected
+        row), or for a tile shard its 8 x (8 * tiles_local) x 3 slab."""
+        n_rows, width = shard_shape(params)
         dt = np.float64 if params.out_format == RT_OUT_F64 else np.float32
         if out is None:
-            out = np.empty((n_rows, params.width, 3), dtype=dt)
-        if out.dtype != dt or out.size < n_rows * params.width * 3 or not out.flags.c_contiguous:
-            raise RTError(f"output buffer too small or of the wrong type for {n_rows} x {params.width} x 3 {dt}")
+            out = np.empty((n_rows, width, 3), dtype=dt)
+        if out.dtype != dt or out.size < n_rows * width * 3 or not out.flags.c_contiguous:
+            raise RTError(f"output buffer too small or of the wrong type for {n_rows} x {width} x 3 {dt}")
         params.out_on_device = 0
         _check(self.lib.rt_render(self.h, ctypes.byref(camera), ctypes.byref(params), out.ctypes.data), "rt_render")
         return out
@@ -432,9 +474,9 @@ class Renderer:
 
     def render_progressive(self, camera: Camera, params: RenderParams, batch_spp: int, progress=None) -> np.ndarray:
         """rt_render in sample batches; progress(samples_done, samples_total) -> truthy stops early."""
-        n_rows = rows_in_shard(params.height, params.row_begin, params.row_stride, params.row_block)
+        n_rows, width = shard_shape(params)
         dt = np.float64 if params.out_format == RT_OUT_F64 else np.float32
-        out = np.empty((n_rows, params.width, 3), dtype=dt)
+        out = np.empty((n_rows, width, 3), dtype=dt)
         params.out_on_device = 0
         cb = PROGRESS_FN(lambda _u, done, total: int(bool(progress(done, total)))) if progress else PROGRESS_FN()
         _check(self.lib.rt_render_progressive(self.h, ctypes.byref(camera), ctypes.byref(params), batch_spp, cb,
@@ -482,8 +524,7 @@ class Accumulator:
 
     def __init__(self, renderer: Renderer, params: RenderParams):
         self.r, self.lib = renderer, renderer.lib
-        self.rows = rows_in_shard(params.height, params.row_begin, params.row_stride, params.row_block)
-        self.width = params.width
+        self.rows, self.width = shard_shape(params)
         h = ctypes.c_void_p()
         _check(self.lib.rt_accum_create(renderer.h, ctypes.byref(params), ctypes.byref(h)), "rt_accum_create")
         self.h = h

@@ -130,5 +130,25 @@ t)
       "600:r03t_ab_c4:python scripts/ab_builds.py $L/librtiow_exp_r03s.so $L/librtiow_amd.so $L/librtiow_exp_rcpf.so --scene 7 --width 1920 --height 1080 --spp 100 --rounds 2" \
       "400:r03t_ab_c3:python scripts/ab_builds.py $L/librtiow_exp_r03s.so $L/librtiow_amd.so --scene 5 --width 800 --height 800 --spp 200 --rounds 2"
     ;;
+u)
+    # round-3 session U: rank 0's row shard of C2 for N = 1, 2, 4, 8 on one GPU (the multi-GPU
+    # scaling loss from tile coherence, apart from the gather), rows and 8-row bands
+    scripts/gpu_session.sh "400:r03u_shard:python scripts/shard_coherence.py --spp 500 --reps 3"
+    ;;
+v)
+    # round-3 session V: rank 0's row shard of C2 for 2-, 4- and 8-row bands (N = 2, 4, 8)
+    scripts/gpu_session.sh "400:r03v_shard:python scripts/shard_coherence.py --spp 500 --reps 3 --row-blocks 2 4 8"
+    ;;
+w)
+    # round-3 session W: tile shards (rt_render_params.tile_shard) — rank 0's C2 shard at N = 2, 4, 8
+    # against row shards; GPU tests (tile-shard reassembly, bench.py N = 2 tiles / N = 3 rows)
+    scripts/gpu_session.sh "400:r03w_shard:python scripts/shard_coherence.py --spp 500 --reps 3 --row-blocks 1 --tiles" \
+      "900:r03w_gpu_tests:python -u -m pytest tests -m gpu -v --maxfail=8 --timeout 300 --timeout-method thread"
+    ;;
+x)
+    # round-3 session X: the final build end to end — smoke, bench lines (C2 default, C4), PMC profiles
+    # of C2 and C4 at this source hash (the roofline bench.py quotes)
+    PREFIX=r03x_ scripts/gpu_session.sh smoke bench bench_c4 prof_c2 prof_c4
+    ;;
 *) echo "usage: scripts/sessions_r03.sh <session letter>" >&2; exit 2 ;;
 esac

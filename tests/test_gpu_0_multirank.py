@@ -71,17 +71,20 @@ def _bench(tmp_path, world, tag, extra=()):
 
 @pytest.mark.timeout(1300)
 def test_bench_py_n2_branch_equals_n1(tmp_path):
-    """bench.py --gpus 2 (two ranks on device 0, gloo gather of the interleaved shards) writes
-    the N = 1 frame bit for bit, and its JSON line reports n_gpus 2 (runs before this test
-    process touches the GPU: every GPU user here is a child process)."""
+    """bench.py --gpus 2 (two ranks on device 0, gloo gather of the 8x8 tile shards, 90 rows:
+    a cut last tile row) and --gpus 3 --shard rows (interleaved rows) write the N = 1 frame bit
+    for bit, and their JSON lines report n_gpus (runs before this test process touches the
+    GPU: every GPU user here is a child process)."""
     j2, f2, p2 = _bench(tmp_path, 2, "n2")
+    j3, f3, p3 = _bench(tmp_path, 3, "n3", extra=("--shard", "rows"))
     j1, f1, p1 = _bench(tmp_path, 1, "n1")
-    assert j2["n_gpus"] == 2 and j1["n_gpus"] == 1
+    assert j2["n_gpus"] == 2 and j3["n_gpus"] == 3 and j1["n_gpus"] == 1
     assert j2["steps"] == 2 and j2["value"] > 0 and j2["ms_per_step"] > 0
-    assert "gloo" in j2["config"]["parallelism"]
-    assert f2.shape == f1.shape == (90, 160, 3)
-    assert np.array_equal(f2, f1)
-    assert p2 == p1
+    assert "gloo" in j2["config"]["parallelism"] and "8x8 tiles" in j2["config"]["parallelism"]
+    assert "rows" in j3["config"]["parallelism"]
+    assert f2.shape == f3.shape == f1.shape == (90, 160, 3)
+    assert np.array_equal(f2, f1) and np.array_equal(f3, f1)
+    assert p2 == p1 and p3 == p1
 
 
 @pytest.mark.timeout(900)

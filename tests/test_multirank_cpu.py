@@ -1,7 +1,9 @@
 """The N > 1 path on CPU: world_size-2 (and 3) gloo process groups, each rank renders its
 interleaved row shard (with the CPU oracle, no GPU here), rank 0 gathers the padded slabs
 the way bench.py does over RCCL and re-interleaves them; the frame must equal the
-single-process render bit-for-bit (every draw is keyed by pixel and sample)."""
+single-process render bit-for-bit (every draw is keyed by pixel and sample). Tile shards
+(rt_render_params.tile_shard, bench.py's default for N > 1): the documented slab layout,
+gathered and reassembled the same way."""
 import os
 import socket
 
@@ -42,6 +44,66 @@ def _rank_main(rank, world, port, out_path):
         np.save(out_path, frame)
     dist.barrier()
     dist.destroy_process_group()
+
+
+def tile_slab(frame, rank, world):
+    """Rank `rank`'s tile shard of a frame in the layout rt_render writes (rt_abi.h tile_shard):
+    tiles t = rank + m*world of the 8x8 tile grid side by side in one 8-row slab."""
+    H, W = frame.shape[:2]
+    tx, ty = (W + 7) // 8, (H + 7) // 8
+    pad = np.zeros((ty * 8, tx * 8) + frame.shape[2:], frame.dtype)
+    pad[:H, :W] = frame
+    ts = list(range(rank, tx * ty, world))
+    slab = np.zeros((8, 8 * len(ts)) + frame.shape[2:], frame.dtype)
+    for m, t in enumerate(ts):
+        y0, x0 = (t // tx) * 8, (t % tx) * 8
+        slab[:, 8 * m:8 * m + 8] = pad[y0:y0 + 8, x0:x0 + 8]
+    return slab
+
+
+def _rank_main_tiles(rank, world, port, out_path):
+    import __graft_entry__ as ge
+    rt = ge.import_binding()
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    n_max = max(rt.tiles_in_shard(W, H, r, world) for r in range(world))
+    mine = tile_slab(ob.render(SCENE, W, H, SPP, threads=1), rank, world)
+    assert mine.shape[1] == 8 * rt.tiles_in_shard(W, H, rank, world)
+    slab = torch.zeros((8, 8 * n_max, 3), dtype=torch.float64)
+    slab[:, : mine.shape[1]] = torch.from_numpy(mine)
+    gathered = [torch.empty_like(slab) for _ in range(world)] if rank == 0 else None
+    dist.gather(slab, gathered, dst=0)
+    if rank == 0:
+        np.save(out_path, rt.assemble_tiles(gathered, W, H, world).numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_tile_sharded_gather_equals_single_render(tmp_path, world):
+    out = str(tmp_path / "frame.npy")
+    mp.start_processes(_rank_main_tiles, args=(world, _free_port(), out), nprocs=world, join=True,
+                       start_method="spawn")
+    assert np.array_equal(np.load(out), ob.render(SCENE, W, H, SPP, threads=2))
+
+
+def test_tile_shards_partition_and_assemble():
+    """The C ABI's tile count per shard and assemble_tiles (numpy and torch) invert tile_slab."""
+    import __graft_entry__ as ge
+    rt = ge.import_binding()
+    for (h, w) in ((800, 1200), (19, 24), (9, 17), (8, 8)):
+        img = np.arange(h * w * 3, dtype=np.float64).reshape(h, w, 3)
+        tiles = ((w + 7) // 8) * ((h + 7) // 8)
+        for world in (1, 2, 3, 8):
+            n = [rt.tiles_in_shard(w, h, r, world) for r in range(world)]
+            assert sum(n) == tiles and n == [len(range(r, tiles, world)) for r in range(world)]
+            slabs = [tile_slab(img, r, world) for r in range(world)]
+            assert np.array_equal(rt.assemble_tiles(slabs, w, h, world), img)
+            wide = max(n) * 8   # slabs padded to the largest shard, as gathered
+            padded = [torch.from_numpy(np.pad(s, ((0, 0), (0, wide - s.shape[1]), (0, 0)))) for s in slabs]
+            assert np.array_equal(rt.assemble_tiles(padded, w, h, world).numpy(), img)
+    assert rt.tiles_in_shard(24, 19, 8, 4) == 1 and rt.tiles_in_shard(24, 19, 9, 4) == 0   # 9 tiles
 
 
 @pytest.mark.parametrize("world", [2, 3])
