@@ -150,5 +150,18 @@ x)
     # of C2 and C4 at this source hash (the roofline bench.py quotes)
     PREFIX=r03x_ scripts/gpu_session.sh smoke bench bench_c4 prof_c2 prof_c4
     ;;
+y)
+    # round-3 session Y: the final variant testing the huge root-child leaf (the r = 5000 fog medium)
+    # before its walk with the whole wave (RT_PRELEAF_FINAL; 126 VGPRs, 6 spilled) vs HEAD, C4
+    scripts/gpu_session.sh \
+      "600:r03y_ab_c4:python scripts/ab_builds.py $L/librtiow_amd.so $L/librtiow_exp_prefinal.so --scene 7 --width 1920 --height 1080 --spp 100 --rounds 2"
+    ;;
+z)
+    # round-3 session Z: session Y's A/B (librtiow_exp_prefinal.so built with -DRT_PRELEAF_FINAL=1 on
+    # the flag's definition, not kept in the tree) then session X (smoke, bench lines, PMC at HEAD)
+    scripts/gpu_session.sh \
+      "600:r03z_ab_c4:python scripts/ab_builds.py $L/librtiow_amd.so $L/librtiow_exp_prefinal.so --scene 7 --width 1920 --height 1080 --spp 100 --rounds 2" && \
+    PREFIX=r03x_ scripts/gpu_session.sh smoke bench bench_c4 prof_c2 prof_c4
+    ;;
 *) echo "usage: scripts/sessions_r03.sh <session letter>" >&2; exit 2 ;;
 esac
