@@ -34,6 +34,19 @@
 #include <string.h>
 #include <time.h>
 
+#ifdef ORC_LIBM
+/* The independent-numerics build (liboracle_libm.so, tests/test_oracle.py): the platform libm's
+ * transcendentals in place of rt_numerics.h's restatements, which the kernel and this oracle
+ * share. A bug in those restatements would be invisible to GPU-vs-oracle parity; against this
+ * build it would show (the two agree wherever glibc and the restatement round alike). */
+#define rt_sin(x) sin(x)
+#define rt_cos(x) cos(x)
+#define rt_log(x) log(x)
+#define rt_acos(x) acos(x)
+#define rt_atan2(y, x) atan2(y, x)
+#define rt_pow5(x) pow((x), 5.0)   /* (1 - cosine).powf(5.0), material.rs:93 */
+#endif
+
 /* ------------------------------------------------------------------------- */
 /* math.rs — Vector3                                                          */
 /* ------------------------------------------------------------------------- */
