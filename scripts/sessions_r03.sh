@@ -163,5 +163,9 @@ z)
       "600:r03z_ab_c4:python scripts/ab_builds.py $L/librtiow_amd.so $L/librtiow_exp_prefinal.so --scene 7 --width 1920 --height 1080 --spp 100 --rounds 2" && \
     PREFIX=r03x_ scripts/gpu_session.sh smoke bench bench_c4 prof_c2 prof_c4
     ;;
+final)
+    # round-3 closing check of HEAD as the driver runs it: GPU tests, smoke, bench.py with no arguments
+    PREFIX=r03_final_ scripts/gpu_session.sh tests smoke bench
+    ;;
 *) echo "usage: scripts/sessions_r03.sh <session letter>" >&2; exit 2 ;;
 esac
