@@ -164,6 +164,9 @@ struct Cfg {
     static constexpr bool COUNT = COUNT_;
     static constexpr bool F32 = F32_;
     static constexpr int LOOP = RT_TRACE_LOOP;
+    // threads per workgroup (RT_BLOCK_FINAL): a property of the launched kernel, inherited by the
+    // reduced configurations of nested code (CfgDrop), which share its LDS stack
+    static constexpr int BT = block_threads_of(F_, F32_);
     using Real = typename std::conditional<F32_, float, double>::type;
 };
 
@@ -172,7 +175,7 @@ struct Cfg {
 // clear), so e.g. the final scene's instanced BLAS of spheres compiles the sphere test only.
 // threads per workgroup (RT_BLOCK_FINAL; the LDS stack's lane stride)
 template <class C>
-constexpr int BlockThreads() { return block_threads_of(C::F, C::F32); }
+constexpr int BlockThreads() { return C::BT; }
 
 template <class C, uint32_t DROP>
 struct CfgDrop : C {

@@ -164,8 +164,9 @@ z)
     PREFIX=r03x_ scripts/gpu_session.sh smoke bench bench_c4 prof_c2 prof_c4
     ;;
 final)
-    # round-3 closing check of HEAD as the driver runs it: GPU tests, smoke, bench.py with no arguments
-    PREFIX=r03_final_ scripts/gpu_session.sh tests smoke bench
+    # round-3 closing check of HEAD as the driver runs it (GPU tests, smoke, bench.py with no
+    # arguments), C4's bench line, and the PMC passes of C2 / C4 at this source hash
+    PREFIX=r03_final_ scripts/gpu_session.sh tests smoke bench bench_c4 prof_c2 prof_c4
     ;;
 *) echo "usage: scripts/sessions_r03.sh <session letter>" >&2; exit 2 ;;
 esac
