@@ -168,5 +168,9 @@ final)
     # arguments), C4's bench line, and the PMC passes of C2 / C4 at this source hash
     PREFIX=r03_final_ scripts/gpu_session.sh tests smoke bench bench_c4 prof_c2 prof_c4
     ;;
+final2)
+    # the remaining bench lines at HEAD's source hash: C1, C3, C5 (f64), C2-C4 (f32), C3's PMC passes
+    PREFIX=r03_final_ scripts/gpu_session.sh bench_c1 bench_c3 bench_c5 f32_c2 f32_c3 f32_c4 prof_c3
+    ;;
 *) echo "usage: scripts/sessions_r03.sh <session letter>" >&2; exit 2 ;;
 esac
