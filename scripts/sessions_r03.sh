@@ -172,5 +172,12 @@ final2)
     # the remaining bench lines at HEAD's source hash: C1, C3, C5 (f64), C2-C4 (f32), C3's PMC passes
     PREFIX=r03_final_ scripts/gpu_session.sh bench_c1 bench_c3 bench_c5 f32_c2 f32_c3 f32_c4 prof_c3
     ;;
+probe)
+    # timing probes (NOT the product; built from a copy of csrc with RT_PROBE_NO_NOISE /
+    # RT_PROBE_NO_IMAGE: the noise / image texture returns a constant; paths unchanged): the share
+    # of the final scene's time its Perlin and image textures take, C4 1920x1080x100
+    scripts/gpu_session.sh \
+      "700:r03_probe_tex_c4:python scripts/ab_builds.py $L/librtiow_amd.so $L/librtiow_probe_nonoise.so $L/librtiow_probe_noimage.so $L/librtiow_probe_notex.so --scene 7 --width 1920 --height 1080 --spp 100 --rounds 2"
+    ;;
 *) echo "usage: scripts/sessions_r03.sh <session letter>" >&2; exit 2 ;;
 esac
