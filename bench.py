@@ -73,7 +73,7 @@ def parse():
     ap.add_argument("--spp-chunk", type=int, default=0, help="samples per chunk (0: the library's automatic choice)")
     ap.add_argument("--no-count", action="store_true", help="skip the count_work pass (profiling runs)")
     ap.add_argument("--ppm", default="", help="write the rendered frame (rank 0) as a P3 PPM")
-    ap.add_argument("--frame-npy", default="", help="save the rendered f32 frame (rank 0) as .npy")
+    ap.add_argument("--frame-npy", default="", help="save the rendered f64 frame (rank 0) as .npy")
     ap.add_argument("--shard", default="tiles", choices=["tiles", "rows"],
                     help="N > 1 partition: the frame's 8x8 tiles round-robin (rt_render_params.tile_shard) or "
                          "single rows round-robin")
@@ -82,6 +82,10 @@ def parse():
                          "ranks share one GPU, for tests of this N > 1 path on a 1-GPU box)")
     ap.add_argument("--device", type=int, default=None,
                     help="GPU index for every rank (default: LOCAL_RANK); with --dist-backend gloo, ranks may share one")
+    ap.add_argument("--force-dist", action="store_true",
+                    help="take the distributed branch (process group, device gather of the shard slab, "
+                         "reassembly, barrier, MAX all-reduce) even at world size 1, so the RCCL path runs on a "
+                         "1-GPU box: launch as torch.distributed.run --nproc-per-node 1 ... --gpus 1 --force-dist")
     ap.add_argument("--precision", default="f64", choices=["f64", "f32"],
                     help="f64: the reference's arithmetic (the headline); f32: the fast mode (SURVEY §8 f3)")
     args = ap.parse_args()
@@ -192,13 +196,17 @@ def main():
     if world != args.gpus:
         if world == 1 and args.gpus > 1:
             raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run (one rank per GPU)")
-    gloo = world > 1 and args.dist_backend == "gloo"
+    # the distributed branch: N > 1, or N = 1 under --force-dist (the RCCL code path on one GPU)
+    dist_on = world > 1 or args.force_dist
+    if args.force_dist and "MASTER_ADDR" not in os.environ:
+        raise SystemExit("--force-dist needs torch.distributed.run (MASTER_ADDR / RANK / WORLD_SIZE in the env)")
+    gloo = dist_on and args.dist_backend == "gloo"
     if args.device is not None:
         if world > 1 and not gloo:
             raise SystemExit("--device with N > 1 needs --dist-backend gloo (RCCL needs one GPU per rank)")
         local = args.device
     torch.cuda.set_device(local)
-    if world > 1:
+    if dist_on:
         if gloo:
             dist.init_process_group("gloo")
         else:
@@ -224,7 +232,7 @@ def main():
     # Rank 0's C2 shard at N = 8 runs at 6,202 Msamples/s in 8x8 tiles against 5,993 as single
     # rows 8 apart (8-row bands, the other compact layout, leave 13 vs 12 bands per rank;
     # scripts/shard_coherence.py, profiles/r03u_shard.log). --shard rows keeps the row partition.
-    tiles = world > 1 and args.shard == "tiles"
+    tiles = dist_on and args.shard == "tiles"
     if tiles:
         n_mine = rt.tiles_in_shard(W, H, rank, world)
         n_max = max(rt.tiles_in_shard(W, H, r, world) for r in range(world))
@@ -235,19 +243,21 @@ def main():
         px_mine, slab_shape = rows * W, (rows_max, W, 3)
     # the render writes its shard contiguously at the start of the slab (a tile shard's 8 x 8n
     # layout is then a prefix of the padded 8 x 8n_max buffer, read back with the same view)
-    slab = torch.zeros(slab_shape, dtype=torch.float32, device=device)
+    # f64 output (sum * (1/spp), the reference's `self.x * scale`, math.rs:120-125): the frame the
+    # PPM writer turns into the reference's bytes (rt_write_ppm_f64); 23 MB for C2
+    slab = torch.zeros(slab_shape, dtype=torch.float64, device=device)
     # gloo gathers host copies of the slabs (staged through pinned memory), RCCL device slabs
     stage = torch.empty(slab.shape, dtype=slab.dtype, pin_memory=True) if gloo else None
     gathered = ([torch.empty_like(stage if gloo else slab) for _ in range(world)]
-                if (world > 1 and rank == 0) else None)
-    frame = torch.empty((H, W, 3), dtype=torch.float32, device=device) if rank == 0 else None
+                if (dist_on and rank == 0) else None)
+    frame = torch.empty((H, W, 3), dtype=torch.float64, device=device) if rank == 0 else None
     # A stream of our own: torch's default stream has the null handle, which the C ABI reads
     # as "the context's stream" (a non-blocking stream the default stream does not wait
     # for), so the frame copy / RCCL gather would not be ordered after the render. Every
     # op of a step runs under this stream; NCCL orders its gather after it.
     stream = torch.cuda.Stream(device)
     params = rt.Renderer.params(W, H, spp, depth, bg, args.seed, row_begin=rank, row_stride=world,
-                                spp_chunk=args.spp_chunk, out_format=rt.RT_OUT_F32,
+                                spp_chunk=args.spp_chunk, out_format=rt.RT_OUT_F64,
                                 row_block=1 if tiles else ROW_BLOCK, tile_shard=int(tiles))
 
     def assemble(slabs):
@@ -258,18 +268,32 @@ def main():
         else:
             rt.assemble_rows(slabs, H, world, out=frame, row_block=ROW_BLOCK)
     kernel_ms = []
+    gather_ev = []    # (before, after) events on `stream` around the RCCL gather of each timed step
+    gather_host_ms = []
 
-    def step():
+    def step(timed=False):
         with torch.cuda.stream(stream):
             renderer.render_device(cam, params, slab.data_ptr(), stream.cuda_stream)
             if gloo:
                 stage.copy_(slab, non_blocking=True)
                 stream.synchronize()
+                tg = time.perf_counter()
                 dist.gather(stage, gathered if rank == 0 else None, dst=0)
+                if timed:
+                    gather_host_ms.append((time.perf_counter() - tg) * 1e3)
                 if rank == 0:
                     assemble([g.to(device, non_blocking=True) for g in gathered])
-            elif world > 1:
+            elif dist_on:
+                # the events bracket the gather on the render's stream: from the end of this rank's
+                # render to the gather's completion (the wait for slower ranks included)
+                e0 = torch.cuda.Event(enable_timing=True) if timed else None
+                e1 = torch.cuda.Event(enable_timing=True) if timed else None
+                if timed:
+                    e0.record(stream)
                 dist.gather(slab, gathered if rank == 0 else None, dst=0)
+                if timed:
+                    e1.record(stream)
+                    gather_ev.append((e0, e1))
                 if rank == 0:
                     assemble(gathered)
             else:
@@ -284,23 +308,32 @@ def main():
         torch.cuda.synchronize(device)
         progress(f"warmup {i + 1}/{args.warmup}")
     torch.cuda.synchronize(device)
-    if world > 1:
+    if dist_on:
         dist.barrier()
     torch.cuda.synchronize(device)
     t0 = time.perf_counter()
     for i in range(args.steps):
-        step()
+        step(timed=True)
         kernel_ms.append(renderer.stats().kernel_ms)   # HIP events around the trace kernel on `stream`
         progress(f"step {i + 1}/{args.steps}: kernel {kernel_ms[-1]:.1f} ms")
     torch.cuda.synchronize(device)
-    if world > 1:
+    if dist_on:
         dist.barrier()
     torch.cuda.synchronize(device)
     elapsed = time.perf_counter() - t0
-    if world > 1:
+    per_rank = None
+    if dist_on:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if gloo else device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+        # per-rank kernel and gather times, so a multi-GPU line says where its time went
+        g_ms = ([a.elapsed_time(b) for a, b in gather_ev] if not gloo else gather_host_ms) or [float("nan")]
+        mine = torch.tensor([float(np.mean(kernel_ms)) if kernel_ms else float("nan"), float(np.mean(g_ms)),
+                             float(px_mine * spp)], dtype=torch.float64, device="cpu" if gloo else device)
+        allr = [torch.empty_like(mine) for _ in range(world)]
+        dist.all_gather(allr, mine)
+        per_rank = [{"rank": r, "kernel_ms": round(float(v[0]), 3), "gather_ms": round(float(v[1]), 3),
+                     "samples": int(v[2])} for r, v in enumerate(a.cpu() for a in allr)]
     last = renderer.stats()
 
     samples_per_step = W * H * spp
@@ -375,16 +408,16 @@ def main():
                "node_lane_occupancy": round(cs.node_visits / max(64 * cs.wave_node_steps, 1), 3),
                "leaf_lane_occupancy": round(cs.prim_tests / max(64 * cs.wave_leaf_steps, 1), 3)}
 
-    frame_np = frame.cpu().numpy() if rank == 0 else None
+    frame_np = frame.cpu().numpy() if rank == 0 else None   # f64 mean radiance, row 0 = bottom
     if args.ppm and rank == 0:
-        rt.write_ppm(frame_np, args.ppm)
+        rt.write_ppm(frame_np, args.ppm)   # f64: rt_write_ppm_f64, the reference's bytes
     if args.frame_npy and rank == 0:
         np.save(args.frame_npy, frame_np)
 
     progress("timed steps done; count pass, CPU baseline and parity")
     # ---- CPU baseline + parity (rank 0, N = 1 only)
     cpu, parity = None, None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and not dist_on and not args.no_cpu_baseline:
         from tests import oracle_binding as ob
         cores, n_aff, quota = usable_cores()
         # calibrate on `cores` interleaved rows at low spp, then take an interleaved row
@@ -422,7 +455,7 @@ def main():
             "comparable_to": "README.md:6 (1200x800x500 in 1 h 10 min on 10 threads = 0.114 Msamples/s; "
                              "older book-1 scene revision, unknown CPU)"}
         # parity: the GPU renders exactly those rows and samples (f64 output) and the timed
-        # f32 frame's same rows (full spp only) are compared as well
+        # frame's same rows (full spp only) are compared as well
         gp = rt.Renderer.params(W, H, spp_cpu, depth, bg, args.seed, row_begin=0, row_stride=stride,
                                 out_format=rt.RT_OUT_F64)
         gimg = renderer.render(cam, gp)
@@ -436,7 +469,10 @@ def main():
             parity.update({"mode": "statistical (f32)", "mean_rel": mean_rel, "tolerance": 0.01,
                            "pass": bool(mean_rel < 0.01)})
         if spp_cpu == spp and not f32:
-            parity["linf_timed_f32_frame"] = float(np.abs(frame_np[0::stride].astype(np.float64) - ref_img).max())
+            parity["linf_timed_frame"] = float(np.abs(frame_np[0::stride] - ref_img).max())
+            # the timed frame's PPM bytes (rt_write_color) against the oracle's write_color of its image
+            parity["ppm_bytes_equal_on_rows"] = bool(np.array_equal(rt.write_color(frame_np[0::stride]),
+                                                                    ob.write_color(ref_img)))
 
     if rank == 0:
         out = {
@@ -459,7 +495,7 @@ def main():
                        "scene": args.scene, "width": W, "height": H, "spp": spp, "max_depth": depth,
                        "parallelism": "%s interleaved over %d rank(s), %s gather"
                                       % ("8x8 tiles" if tiles else "rows", world,
-                                         "gloo (host-staged)" if gloo else "RCCL")},
+                                         "gloo (host-staged)" if gloo else "RCCL" if dist_on else "no")},
             "roofline": roofline,
             "cpu_baseline": cpu,
             "parity": parity,
@@ -468,8 +504,12 @@ def main():
                        "scene_bytes": int(last.scene_bytes), "scene_build_upload_s": round(t_build, 3),
                        "algorithmic_bytes_survey_8d": alg},
         }
+        if per_rank is not None:
+            out["per_rank"] = per_rank
+            out["distributed"] = {"backend": "gloo" if gloo else "nccl (RCCL)", "world_size": world,
+                                  "forced_at_world_1": bool(args.force_dist and world == 1)}
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if dist_on:
         dist.destroy_process_group()
 
 

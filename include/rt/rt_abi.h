@@ -261,9 +261,19 @@ int rt_render_progressive(rt_ctx* ctx, const rt_camera* cam, const rt_render_par
                           rt_progress_fn progress, void* user, void* out);
 
 /* ---- output ------------------------------------------------------------------------------ */
-/* P3 PPM exactly as the reference writes it: header "P3\nW H\n255\n\n", rows top to
- * bottom, each channel (int)(256 * clamp(sqrt(mean), 0, 0.999)) with NaN -> 0.
- * mean_rgb is height x width x 3 f32 with row 0 = bottom (y = 0). */
+/* P3 PPM byte for byte as the reference writes it (write_color, math.rs:119-132; main.rs:472,
+ * 591-596): header "P3\nW H\n255\n\n", rows top to bottom, each channel
+ * (int)(256 * clamp(sqrt(x * (1.0 / samples_per_pixel)), 0, 0.999)) in f64, with Rust's
+ * saturating `as i32` (NaN -> 0). rgb is height x width x 3 f64 with row 0 = bottom (y = 0):
+ * per-pixel sums over samples_per_pixel samples (rt_accum_get), or rt_render's RT_OUT_F64 mean
+ * (already sum * (1/spp)) with samples_per_pixel = 1 — x * 1.0 == x, so both give the
+ * reference's bytes. */
+int rt_write_ppm_f64(const double* rgb, int samples_per_pixel, int width, int height, const char* path);
+/* The same channel values without the file: out[i] for the 3n channels of n pixels, in memory order. */
+int rt_write_color(const double* rgb, int samples_per_pixel, int64_t n, int32_t* out);
+/* The f32 frame's writer (RT_OUT_F32 output, the f32 mode): as rt_write_ppm_f64 with spp = 1, but
+ * the mean was rounded to f32 before the sqrt, so a channel whose 256*sqrt(mean) lies within
+ * ~1e-5 of an integer can differ by one from the reference's f64 write_color. */
 int rt_write_ppm(const float* mean_rgb, int width, int height, const char* path);
 
 /* Kernel variant knobs of a context: slab32 (conservative f32 BVH slab tests),

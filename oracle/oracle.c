@@ -30,6 +30,7 @@
 
 #include <math.h>
 #include <pthread.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 #include <time.h>
@@ -1493,4 +1494,49 @@ int orc_world_render(const orc_world* o, const orc_params* p, const double* cam2
     cam.time0 = cam24[22];
     cam.time1 = cam24[23];
     return render_world(p, &o->w, &cam, v3(bg[0], bg[1], bg[2]), out_mean, stats);
+}
+
+/* ---- output: Vector3::write_color (math.rs:119-132) and the P3 writer (main.rs:472,591-596) ---- */
+
+/* Rust's `f64 as i32` (saturating since Rust 1.45): NaN -> 0, out of range -> the nearest
+ * bound, otherwise truncation toward zero. Restated here independently of rt_numerics.h's
+ * rt_sat_i32, which the product uses. */
+static int rust_as_i32(double x)
+{
+    if (isnan(x)) return 0;
+    if (x >= 2147483647.0) return 2147483647;
+    if (x <= -2147483648.0) return -2147483647 - 1;
+    return (int)trunc(x);
+}
+
+/* write_color(samples_per_pixel) of one channel: scale = 1.0 / spp (math.rs:120),
+ * (x * scale).sqrt() (:123-125), clamp(_, 0.0, 0.999) (:127-129, clamp math.rs:282-286:
+ * NaN passes through), 256.0 * c as i32. */
+static int write_color_channel(double x, int samples_per_pixel)
+{
+    const double scale = 1.0 / (double)samples_per_pixel;
+    const double r = sqrt(x * scale);
+    return rust_as_i32(256.0 * clampd(r, 0.0, 0.999));
+}
+
+int orc_write_color(const double* rgb, int samples_per_pixel, int64_t n, int32_t* out)
+{
+    if (!rgb || !out || n < 0 || samples_per_pixel < 1) return -1;
+    for (int64_t i = 0; i < 3 * n; ++i) out[i] = write_color_channel(rgb[i], samples_per_pixel);
+    return 0;
+}
+
+int orc_write_ppm(const double* rgb, int samples_per_pixel, int width, int height, const char* path)
+{
+    if (!rgb || !path || width < 1 || height < 1 || samples_per_pixel < 1) return -1;
+    FILE* f = fopen(path, "wb");
+    if (!f) return -1;
+    fprintf(f, "P3\n%d %d\n255\n\n", width, height);             /* main.rs:472: println! adds "\n" */
+    for (int j = height - 1; j >= 0; --j)                              /* main.rs:591: rows top to bottom */
+        for (int i = 0; i < width; ++i) {                              /* main.rs:592 */
+            const double* px = rgb + ((size_t)j * width + i) * 3;
+            fprintf(f, "%d %d %d\n", write_color_channel(px[0], samples_per_pixel),
+                    write_color_channel(px[1], samples_per_pixel), write_color_channel(px[2], samples_per_pixel));
+        }
+    return fclose(f) == 0 ? 0 : -1;
 }

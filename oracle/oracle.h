@@ -111,6 +111,15 @@ int orc_world_push(orc_world* w, int id);
 int orc_world_render(const orc_world* w, const orc_params* p, const double* cam24, const double bg[3],
                      double* out_mean, orc_stats* stats);
 
+/* Output (math.rs:119-132, main.rs:472,591-596). rgb is height x width x 3 f64, row 0 =
+ * the bottom image row (y = 0), holding per-pixel sums taken over samples_per_pixel samples;
+ * each channel is written as (int)(256 * clamp(sqrt(x * (1.0 / spp)), 0, 0.999)) with Rust's
+ * saturating `as i32` (NaN -> 0). Pass orc_render's out_mean (already sum * (1/spp)) with
+ * spp = 1: x * 1.0 == x, so that equals write_color(spp) of the sums.
+ * orc_write_color: the 3n channel values of n pixels, in memory order, into out. */
+int orc_write_color(const double* rgb, int samples_per_pixel, int64_t n, int32_t* out);
+int orc_write_ppm(const double* rgb, int samples_per_pixel, int width, int height, const char* path);
+
 #ifdef __cplusplus
 }
 #endif

@@ -12,6 +12,8 @@
 #include <cstring>
 #include <new>
 #include <string>
+#include <unordered_map>
+#include <unordered_set>
 #include <vector>
 
 #include "rt/rt_abi.h"
@@ -116,6 +118,8 @@ struct rt_ctx {
     size_t acc_tmp_cap = 0;
     int n_tlas_nodes = 0;
     int n_nodes = 0;                    // BVH nodes of the uploaded scene (TLAS + BLASes)
+    size_t lds_per_cu = 160 * 1024;     // the device's LDS per CU and per workgroup (read at creation)
+    size_t lds_per_block = 160 * 1024;
 };
 
 extern "C" {
@@ -168,6 +172,14 @@ int rt_ctx_create(int device, rt_ctx** out)
             cap = std::max(cap, std::min((size_t)32 << 30, fr / 2));
             c->sample_buf_cap = std::max(cap >> 20, (size_t)1) << 20;
         }
+    }
+    {
+        int v = 0;
+        if (hipDeviceGetAttribute(&v, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, device) == hipSuccess && v > 0)
+            c->lds_per_cu = (size_t)v;
+        if (hipDeviceGetAttribute(&v, hipDeviceAttributeMaxSharedMemoryPerBlock, device) == hipSuccess && v > 0)
+            c->lds_per_block = (size_t)v;
+        c->lds_per_block = std::min(c->lds_per_block, c->lds_per_cu);
     }
     hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     for (int i = 0; i < 3 && e == hipSuccess; ++i) e = hipEventCreate(&c->ev[i]);
@@ -779,14 +791,14 @@ int rt_ctx_upload_soa(rt_ctx* c, const rt_scene_soa* s)
     std::vector<rt_bvh_node> nodes_dev(s->nodes, s->nodes + s->n_nodes);
     std::vector<rt_instance> inst_dev(s->instances, s->instances + s->n_instances);
     for (rt_instance& in : inst_dev) in.pad = 0;
-    int max_first = 0;            // the largest leaf-code first slot either walk pushes
+    int max_code = 0;             // the largest leaf code ((first slot << 5) | count) either walk pushes
     bool rel_ok = true;
     {
         auto leaf_first = [](int ref) { return (~ref) >> 5; };
         std::vector<int> owner((size_t)s->n_nodes, -1);   // -2: TLAS; else the BLAS base
         std::vector<int> todo;
         if (s->tlas_root >= 0) todo.push_back(s->tlas_root);
-        else max_first = std::max(max_first, leaf_first(s->tlas_root));
+        else max_code = std::max(max_code, ~s->tlas_root);
         while (!todo.empty()) {   // validate_soa checked refs and acyclicity
             const int i = todo.back();
             todo.pop_back();
@@ -794,22 +806,35 @@ int rt_ctx_upload_soa(rt_ctx* c, const rt_scene_soa* s)
             owner[(size_t)i] = -2;
             for (int ch : s->nodes[i].child) {
                 if (ch >= 0) todo.push_back(ch);
-                else max_first = std::max(max_first, leaf_first(ch));
+                else max_code = std::max(max_code, ~ch);
             }
         }
+        // each BLAS root is walked once however many instances share it (memo: root -> base),
+        // over one epoch-stamped visited array
+        std::unordered_map<int, int> root_base;
+        std::vector<uint32_t> seen((size_t)s->n_nodes, 0);
+        uint32_t epoch = 0;
         for (size_t ii = 0; ii < inst_dev.size() && rel_ok; ++ii) {
             rt_instance& in = inst_dev[ii];
             if (in.child_kind != RT_CHILD_BVH) continue;
+            if (in.child >= 0) {
+                const auto m = root_base.find(in.child);
+                if (m != root_base.end()) {
+                    in.pad = m->second;
+                    continue;
+                }
+            }
             std::vector<int> blas;   // the BLAS's nodes, and its smallest leaf slot
             int base = 1 << 30;
+            const int root = in.child;
             if (in.child < 0) base = leaf_first(in.child);
             else todo.push_back(in.child);
-            std::vector<uint8_t> seen((size_t)s->n_nodes, 0);
+            ++epoch;
             while (!todo.empty()) {
                 const int i = todo.back();
                 todo.pop_back();
-                if (seen[(size_t)i]) continue;
-                seen[(size_t)i] = 1;
+                if (seen[(size_t)i] == epoch) continue;
+                seen[(size_t)i] = epoch;
                 blas.push_back(i);
                 for (int ch : s->nodes[i].child) {
                     if (ch >= 0) todo.push_back(ch);
@@ -822,8 +847,9 @@ int rt_ctx_upload_soa(rt_ctx* c, const rt_scene_soa* s)
             auto rel = [&](int ref) {
                 const int code = ~ref;
                 const int first = (code >> 5) - base;
-                max_first = std::max(max_first, first);
-                return ~((first << 5) | (code & 31));
+                const int rcode = (first << 5) | (code & 31);
+                max_code = std::max(max_code, rcode);
+                return ~rcode;
             };
             for (int i : blas) {
                 if (owner[(size_t)i] == base) continue;   // shared with an instance already rewritten
@@ -832,13 +858,14 @@ int rt_ctx_upload_soa(rt_ctx* c, const rt_scene_soa* s)
                     if (ch < 0) ch = rel(ch);
             }
             if (in.child < 0) in.child = rel(in.child);
+            else root_base.emplace(root, base);
             in.pad = base;
         }
         if (!rel_ok) {   // absolute codes everywhere
             nodes_dev.assign(s->nodes, s->nodes + s->n_nodes);
             inst_dev.assign(s->instances, s->instances + s->n_instances);
             for (rt_instance& in : inst_dev) in.pad = 0;
-            max_first = s->n_prim_refs;
+            max_code = (s->n_prim_refs << 5) | 31;
         }
     }
     // The largest instance BLAS in BFS order right after the TLAS prefix (device node order
@@ -850,16 +877,20 @@ int rt_ctx_upload_soa(rt_ctx* c, const rt_scene_soa* s)
         int best_root = -1;
         size_t best_n = 0;
         std::vector<int> bfs;
+        std::unordered_set<int> walked;   // each BLAS root once, over one epoch-stamped array
+        std::vector<uint32_t> seen((size_t)s->n_nodes, 0);
+        uint32_t epoch = 0;
         for (const rt_instance& in : inst_dev) {
             if (in.child_kind != RT_CHILD_BVH || in.child < n_tlas_nodes) continue;
+            if (!walked.insert(in.child).second) continue;
             std::vector<int> order{in.child};
-            std::vector<uint8_t> seen((size_t)s->n_nodes, 0);
-            seen[(size_t)in.child] = 1;
+            ++epoch;
+            seen[(size_t)in.child] = epoch;
             bool disjoint = true;
             for (size_t i = 0; i < order.size(); ++i)
                 for (int ch : nodes_dev[(size_t)order[i]].child)
-                    if (ch >= 0 && !seen[(size_t)ch]) {
-                        seen[(size_t)ch] = 1;
+                    if (ch >= 0 && seen[(size_t)ch] != epoch) {
+                        seen[(size_t)ch] = epoch;
                         if (ch < n_tlas_nodes) disjoint = false;
                         order.push_back(ch);
                     }
@@ -942,8 +973,9 @@ int rt_ctx_upload_soa(rt_ctx* c, const rt_scene_soa* s)
     if (c->opt_hoist) hoist_root_leaf(s, c->S);
     // Stack16 (trace_device.hpp): node records at LDS addresses < 32 KB (80 B each), BLAS node
     // indices < 32768, and leaf codes ((first slot << 5) | count, stored complemented; BLAS slots
-    // relative, above) above the -32768 sentinel
-    c->S.stack16_ok = (n_tlas_nodes * (int64_t)80 <= 32767 - 80 && max_first <= 1023 && s->n_nodes <= 32767) ? 1 : 0;
+    // relative, above) strictly above the -32768 = ~32767 sentinel: every code < 32767 (a leaf
+    // at first slot 1023 holding 31 primitives would complement to the sentinel itself)
+    c->S.stack16_ok = (n_tlas_nodes * (int64_t)80 <= 32767 - 80 && max_code < 32767 && s->n_nodes <= 32767) ? 1 : 0;
     if (RT_WIDE && (w4.empty() || (int64_t)w4.size() * 160 > 32767 - 160 || w4_stack > kMaxLdsStack)) c->S.stack16_ok = 0;
     c->S.n_lds_nodes = 0;
     c->S.n_blas_bfs = n_blas_bfs;
@@ -1237,6 +1269,20 @@ static int run_range(rt_ctx* c, const rt_camera* cam, const rt_render_params* p,
     const int n_rows = lay.rows;
     const long long n_px = (long long)n_rows * lay.w;
     const size_t px = (size_t)std::max<long long>(n_px, 1);
+    if (n_px == 0 || s_end <= s_begin) {
+        // an empty shard (rt_rows_in_shard / rt_tiles_in_shard 0: a rank past the tile count)
+        // or an empty sample range: nothing to trace or write; the events still bracket the
+        // (empty) work so rt_last_stats resolves
+        for (int i = 0; i < 3; ++i) HIP_TRY(hipEventRecord(c->ev[i], stream));
+        c->stats.n_batches = 0;
+        c->stats.samples = 0;
+        c->stats.n_items = 0;
+        c->stats.n_chunks = 0;
+        c->stats.spp_chunk = chunk;
+        c->pending_stats = true;
+        c->pending_counts = false;
+        return RT_OK;
+    }
 
     rtk::KParams K;
     std::memset(&K, 0, sizeof K);
@@ -1317,11 +1363,11 @@ static int run_range(rt_ctx* c, const rt_camera* cam, const rt_render_params* p,
         // blocks per CU ran 2 and took 174 instead of 133 ms, r03g_ab_c4.log), and no more
         // workgroups than the variant's registers allow (final scene 4 waves per SIMD, the
         // all-features variant 3: 16 or 12 waves per CU)
-        const size_t lds_cu = 160 * 1024, granule = 1024;
+        const size_t lds_cu = c->lds_per_cu, granule = 1024;
         const size_t wave_blocks = std::max<size_t>(1, (size_t)(variant == rtk::FEAT_SET_FINAL ? 16 : 12) / (size_t)(bt / 64));
         const size_t blocks = std::max<size_t>(1, std::min(wave_blocks,
             lds_cu / (((std::max<size_t>(base, 1) + granule - 1) / granule) * granule)));
-        const size_t budget = lds_cu / blocks / granule * granule;
+        const size_t budget = std::min(lds_cu / blocks, c->lds_per_block) / granule * granule;
         const size_t spare = budget > base ? budget - base : 0;
         S.n_lds_blas = (int32_t)std::min<size_t>({(size_t)c->S.n_blas_bfs, spare / 64, (size_t)kMaxLdsBlas});
     }
@@ -1340,18 +1386,21 @@ static int run_range(rt_ctx* c, const rt_camera* cam, const rt_render_params* p,
     double* acc = sink.acc;
     double* open = nullptr;
     bool own_acc = false;
+    // halved on an out-of-memory retry for this render only: the context's bound stays, so a
+    // later render on it uses the memory freed since
+    size_t buf_cap = c->sample_buf_cap;
     for (;;) {
         // AUTO: the per-sample pool when its per-sample buffer takes at most 4 batches (C2:
         // 11.5 GB in one, 101.6 vs 106.7 ms per frame for the item pool; C4: 49.8 GB in two,
         // 1492 vs 1571 ms; profiles/r02d_*, r02e_*), else the item pool, whose partials take
         // 1/chunk of those bytes and need no carried batches (C5: 1.6 TB of per-sample radiance)
         o.pool = c->opt_pool != RT_SCHED_AUTO ? c->opt_pool
-                 : ((size_t)total * sample_bytes <= 4 * c->sample_buf_cap ? RT_SCHED_POOL : RT_SCHED_ITEMS);
+                 : ((size_t)total * sample_bytes <= 4 * buf_cap ? RT_SCHED_POOL : RT_SCHED_ITEMS);
         // Buffer batches: the trace output of one launch is bounded by sample_buf_cap. Per-sample
         // pool: samples x pixels x 24 B; chunk and item schedules: chunks x pixels x 24 B, batches
         // on chunk boundaries (relative to s_begin), so the partials add in one-launch order.
         per_sample = o.pool == RT_SCHED_POOL;
-        const long long fit = (long long)std::max<size_t>(1, c->sample_buf_cap / (per_sample ? sample_bytes : px_bytes));
+        const long long fit = (long long)std::max<size_t>(1, buf_cap / (per_sample ? sample_bytes : px_bytes));
         batch = std::min<long long>(total, per_sample ? fit : fit * chunk);
         n_batches = (int)((total + batch - 1) / batch);
         acc = sink.acc;
@@ -1377,8 +1426,10 @@ static int run_range(rt_ctx* c, const rt_camera* cam, const rt_render_params* p,
         const size_t need = per_sample ? (size_t)batch * sample_bytes : (size_t)max_chunks * px_bytes;
         rc = grow(c, stream, c->partial, c->partial_cap, need, &oom);
         if (rc == RT_OK) break;
-        if (!oom || c->sample_buf_cap <= ((size_t)1 << 20) || need <= (per_sample ? sample_bytes : px_bytes)) return rc;
-        c->sample_buf_cap = std::max<size_t>(c->sample_buf_cap / 2, (size_t)1 << 20);
+        if (!oom) return rc;
+        if (buf_cap <= ((size_t)1 << 20) || need <= (per_sample ? sample_bytes : px_bytes))
+            return hip_fail(hipErrorOutOfMemory, "trace output buffer (smallest batch)");
+        buf_cap = std::max<size_t>(buf_cap / 2, (size_t)1 << 20);
     }
     if (own_acc) HIP_TRY(hipMemsetAsync(acc, 0, px_bytes, stream));
     // per-sample pool blocks: the chunk's 16 samples per tile while that leaves >= 160 k blocks
@@ -1755,6 +1806,45 @@ int rt_last_counters(rt_ctx* c, uint64_t* out, int n)
 }
 
 // ---- output ---------------------------------------------------------------------------------
+// write_color (math.rs:119-131) of one f64 channel summed over spp samples: scale = 1.0/spp,
+// sqrt(x * scale), clamp to [0, 0.999] (NaN passes through, math.rs:282-286), 256 * c with
+// Rust's saturating `as i32` (NaN -> 0). All in f64, as the reference: with rt_render's
+// RT_OUT_F64 mean (sum * (1/spp)) and spp = 1 this is write_color(spp) of the sums bit for bit.
+static inline int write_color_f64(double x, double scale)
+{
+    const double r = std::sqrt(x * scale);
+    const double c = r < 0.0 ? 0.0 : r > 0.999 ? 0.999 : r;
+    return (int)rt_sat_i32(256.0 * c);
+}
+
+int rt_write_color(const double* rgb, int samples_per_pixel, int64_t n, int32_t* out)
+{
+    if (!rgb || !out || n < 0 || samples_per_pixel < 1) return fail(RT_ERR_INVALID, "bad argument");
+    const double scale = 1.0 / (double)samples_per_pixel;
+    for (int64_t i = 0; i < 3 * n; ++i) out[i] = write_color_f64(rgb[i], scale);
+    return RT_OK;
+}
+
+int rt_write_ppm_f64(const double* rgb, int samples_per_pixel, int width, int height, const char* path)
+{
+    if (!rgb || !path || width < 1 || height < 1 || samples_per_pixel < 1) return fail(RT_ERR_INVALID, "bad argument");
+    FILE* f = std::fopen(path, "wb");
+    if (!f) return fail(RT_ERR_INVALID, std::string("cannot open ") + path);
+    const double scale = 1.0 / (double)samples_per_pixel;           // math.rs:120
+    std::fprintf(f, "P3\n%d %d\n255\n\n", width, height);          // main.rs:472 (println! adds the blank line)
+    for (int j = height - 1; j >= 0; --j)                          // main.rs:591-596: rows top to bottom
+        for (int i = 0; i < width; ++i) {
+            const double* px = rgb + ((size_t)j * width + i) * 3;
+            std::fprintf(f, "%d %d %d\n", write_color_f64(px[0], scale), write_color_f64(px[1], scale),
+                         write_color_f64(px[2], scale));
+        }
+    if (std::fclose(f) != 0) return fail(RT_ERR_INVALID, std::string("cannot write ") + path);
+    return RT_OK;
+}
+
+// The f32 frame's writer (RT_OUT_F32 renders, the f32 mode): the mean is rounded to f32
+// before the sqrt, so a channel whose 256*sqrt(mean) lies within ~1e-5 of an integer may
+// differ by one from the reference's f64 write_color; rt_write_ppm_f64 is the exact one.
 int rt_write_ppm(const float* mean, int width, int height, const char* path)
 {
     if (!mean || !path || width < 1 || height < 1) return fail(RT_ERR_INVALID, "bad argument");

@@ -34,8 +34,9 @@
 
 namespace rtk {
 
-// R: the path's arithmetic type — double (the reference's f64, math.rs:13-17; bit-exact
-// against the oracle) or float (the f32 fast mode; statistically equal).
+// R: the path's arithmetic type — double (the reference's f64, math.rs:13-17; path-identical
+// to the oracle: the same rays, hits and draws, per-pixel means within last-ulp summation
+// differences) or float (the f32 fast mode; statistically equal).
 typedef float f2v __attribute__((ext_vector_type(2)));
 template <class R>
 struct RayT {

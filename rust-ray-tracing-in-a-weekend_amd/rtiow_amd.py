@@ -53,6 +53,7 @@ EXPORTED = [
     "rt_world_bvh", "rt_world_push", "rt_world_build_scene", "rt_world_info_get", "rt_camera_new",
     "rt_scene_preset_get", "rt_scene_camera", "rt_world_flatten", "rt_ctx_upload_soa",
     "rt_ctx_upload_world", "rt_render", "rt_rows_in_shard", "rt_rows_in_band_shard", "rt_tiles_in_shard", "rt_last_stats", "rt_last_counters", "rt_write_ppm",
+    "rt_write_ppm_f64", "rt_write_color",
     "rt_ctx_set_variant", "rt_device_eval", "rt_accum_create", "rt_accum_destroy", "rt_accum_add",
     "rt_accum_get", "rt_accum_set", "rt_accum_resolve", "rt_render_progressive", "rt_ctx_set_schedule", "rt_ctx_set_precision",
     "rt_scene_validate",
@@ -172,6 +173,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "rt_tiles_in_shard": ([I, I, I, I], I), "rt_last_stats": ([P, ctypes.POINTER(Stats)], I),
         "rt_last_counters": ([P, P, I], I),
         "rt_write_ppm": ([P, I, I, ctypes.c_char_p], I),
+        "rt_write_ppm_f64": ([P, I, I, I, ctypes.c_char_p], I),
+        "rt_write_color": ([P, I, ctypes.c_int64, P], I),
         "rt_device_eval": ([P, I, P, P, P, P, I], I), "rt_ctx_set_variant": ([P, I, I, I], I),
         "rt_accum_create": ([P, ctypes.POINTER(RenderParams), ctypes.POINTER(P)], I),
         "rt_ctx_set_schedule": ([P, I], I),
@@ -403,11 +406,31 @@ def assemble_rows(slabs, height: int, world: int, out=None, row_block: int = 1):
     return out
 
 
-def write_ppm(mean_rgb: np.ndarray, path: str) -> None:
-    """P3 writer with the reference's write_color semantics (math.rs:119-132)."""
+def write_ppm(rgb: np.ndarray, path: str, samples_per_pixel: int = 1) -> None:
+    """P3 writer of the reference (write_color, math.rs:119-132; main.rs:472, 591-596):
+    height x width x 3, row 0 = bottom. An f64 array takes rt_write_ppm_f64 — the reference's
+    bytes exactly: pass rt_render's RT_OUT_F64 mean with samples_per_pixel=1, or per-pixel sums
+    (Accumulator.get) with their spp. An f32 array (the f32 frame) takes rt_write_ppm, whose
+    f32-rounded mean can move a channel at a rounding boundary by one."""
     lib = load_library()
-    a = np.ascontiguousarray(mean_rgb, dtype=np.float32)
+    if np.asarray(rgb).dtype == np.float64:
+        a = np.ascontiguousarray(rgb, dtype=np.float64)
+        _check(lib.rt_write_ppm_f64(a.ctypes.data, samples_per_pixel, a.shape[1], a.shape[0], str(path).encode()),
+               "rt_write_ppm_f64")
+        return
+    if samples_per_pixel != 1:
+        raise RTError("an f32 frame is a mean: samples_per_pixel must be 1")
+    a = np.ascontiguousarray(rgb, dtype=np.float32)
     _check(lib.rt_write_ppm(a.ctypes.data, a.shape[1], a.shape[0], str(path).encode()), "rt_write_ppm")
+
+
+def write_color(rgb: np.ndarray, samples_per_pixel: int = 1) -> np.ndarray:
+    """The reference's write_color channel values (int32, same shape) of f64 sums / means."""
+    lib = load_library()
+    a = np.ascontiguousarray(rgb, dtype=np.float64)
+    out = np.empty(a.shape, dtype=np.int32)
+    _check(lib.rt_write_color(a.ctypes.data, samples_per_pixel, a.size // 3, out.ctypes.data), "rt_write_color")
+    return out
 
 
 class Renderer:
@@ -490,7 +513,8 @@ class Renderer:
         _check(self.lib.rt_ctx_set_schedule(self.h, schedule), "rt_ctx_set_schedule")
 
     def set_precision(self, precision: int):
-        """RT_PREC_F64 (default, bit-exact against the oracle) or RT_PREC_F32 (fast mode)."""
+        """RT_PREC_F64 (default: path-identical to the oracle, last-ulp summation differences) or
+        RT_PREC_F32 (fast mode, statistical parity)."""
         _check(self.lib.rt_ctx_set_precision(self.h, precision), "rt_ctx_set_precision")
 
     def set_variant(self, slab32: int = 1, lds_stack: int = 1, lds_nodes: int = 1):

@@ -66,6 +66,10 @@ def lib() -> ctypes.CDLL:
         getattr(l, name).restype = I
     l.orc_world_destroy.argtypes = [P]
     l.orc_world_destroy.restype = None
+    l.orc_write_color.argtypes = [P, I, ctypes.c_int64, P]
+    l.orc_write_color.restype = I
+    l.orc_write_ppm.argtypes = [P, I, I, I, ctypes.c_char_p]
+    l.orc_write_ppm.restype = I
     return l
 
 
@@ -93,6 +97,22 @@ def render(scene_id: int, width: int, height: int, spp: int, max_depth: int = 50
     if rc != 0:
         raise RuntimeError(f"orc_render failed: {rc}")
     return (out, st) if return_stats else out
+
+
+def write_color(rgb, samples_per_pixel: int = 1) -> np.ndarray:
+    """The oracle's write_color (math.rs:119-132) channel values of f64 sums / means."""
+    a = np.ascontiguousarray(rgb, dtype=np.float64)
+    out = np.empty(a.shape, dtype=np.int32)
+    if lib().orc_write_color(a.ctypes.data, samples_per_pixel, a.size // 3, out.ctypes.data) != 0:
+        raise ValueError("orc_write_color")
+    return out
+
+
+def write_ppm(rgb, path: str, samples_per_pixel: int = 1) -> None:
+    """The oracle's P3 writer (main.rs:472, 591-596): rgb height x width x 3, row 0 = bottom."""
+    a = np.ascontiguousarray(rgb, dtype=np.float64)
+    if lib().orc_write_ppm(a.ctypes.data, samples_per_pixel, a.shape[1], a.shape[0], str(path).encode()) != 0:
+        raise RuntimeError("orc_write_ppm")
 
 
 def scene_info(scene_id: int, scene_seed: int = 1):

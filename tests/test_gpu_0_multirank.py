@@ -47,14 +47,18 @@ def _run_ranks(world, scene, W, H, spp, out, block=1):
     return rcs
 
 
-def _bench(tmp_path, world, tag, extra=()):
+def _bench(tmp_path, world, tag, extra=(), rccl=False):
     """bench.py as child processes (N > 1: torch.distributed.run, one child per rank), a
-    small random-scene workload; returns (JSON line of rank 0, frame, PPM bytes)."""
+    small random-scene workload; returns (JSON line of rank 0, frame, PPM bytes). rccl: one
+    rank under torch.distributed.run with --force-dist and the default nccl backend."""
     frame, ppm = str(tmp_path / f"{tag}.npy"), str(tmp_path / f"{tag}.ppm")
     args = ["bench.py", "--gpus", str(world), "--device", "0", "--scene", "0", "--width", "160", "--height", "90",
             "--spp", "8", "--depth", "50", "--steps", "2", "--warmup", "1", "--no-cpu-baseline", "--no-count",
             "--frame-npy", frame, "--ppm", ppm, *extra]
-    if world > 1:
+    if rccl:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
+               "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), *args, "--force-dist"]
+    elif world > 1:
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
                "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), *args, "--dist-backend", "gloo"]
     else:
@@ -85,6 +89,27 @@ def test_bench_py_n2_branch_equals_n1(tmp_path):
     assert f2.shape == f3.shape == f1.shape == (90, 160, 3)
     assert np.array_equal(f2, f1) and np.array_equal(f3, f1)
     assert p2 == p1 and p3 == p1
+
+
+@pytest.mark.timeout(900)
+def test_bench_py_rccl_branch_at_world_size_1(tmp_path):
+    """bench.py's distributed branch with the product's backend, RCCL
+    (torch.distributed "nccl"), executed at world size 1 on the box's one GPU:
+    init_process_group("nccl"), the render into the tile-shard slab, the device dist.gather of
+    the slab, assemble_tiles on the gathered device slab, the barriers and the MAX all-reduce.
+    Its frame and PPM equal the plain N = 1 run bit for bit; the JSON line says n_gpus 1, an
+    RCCL gather and the per-rank kernel / gather times."""
+    jd, fd, pd = _bench(tmp_path, 1, "rccl1", rccl=True)
+    j1, f1, p1 = _bench(tmp_path, 1, "plain1")
+    assert jd["n_gpus"] == 1 and "RCCL" in jd["config"]["parallelism"]
+    assert "8x8 tiles" in jd["config"]["parallelism"]
+    assert jd["distributed"] == {"backend": "nccl (RCCL)", "world_size": 1, "forced_at_world_1": True}
+    pr = jd["per_rank"]
+    assert len(pr) == 1 and pr[0]["kernel_ms"] > 0 and pr[0]["gather_ms"] >= 0 and pr[0]["samples"] >= 160 * 90 * 8
+    assert "per_rank" not in j1 and "no gather" in j1["config"]["parallelism"]
+    assert fd.dtype == np.float64 and fd.shape == f1.shape == (90, 160, 3)
+    assert np.array_equal(fd, f1)
+    assert pd == p1
 
 
 @pytest.mark.timeout(900)

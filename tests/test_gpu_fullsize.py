@@ -76,9 +76,41 @@ def test_baseline_configs_full_spp_against_oracle(rt, renderer, cfg):
     img, st = rt.render_scene(scene_id, W, H, spp, depth, row_begin=row_begin, row_stride=stride,
                               out_format=rt.RT_OUT_F64, renderer=renderer)
     assert st.samples == img.shape[0] * W * spp
-    ref = ob.render(scene_id, W, H, spp, depth, row_begin=row_begin, row_stride=stride, threads=16)
+    ref = _full_ref(cfg)
     assert img.shape == ref.shape == (len(range(row_begin, H, stride)), W, 3)
     _parity(img, ref, cfg + " full spp")
+
+
+_FULL_REF = {}
+
+
+def _full_ref(cfg):
+    if cfg not in _FULL_REF:
+        scene_id, W, H, spp, depth, row_begin, stride = FULL[cfg]
+        _FULL_REF[cfg] = ob.render(scene_id, W, H, spp, depth, row_begin=row_begin, row_stride=stride, threads=16)
+    return _FULL_REF[cfg]
+
+
+@pytest.mark.timeout(300)
+def test_c1_whole_frame_ppm_bytes_equal_oracle(rt, renderer, tmp_path):
+    """VERDICT r03 item 1 (a22/f1): the product's PPM of C1's whole 1200x800x10 frame (depth 8)
+    is byte-identical to the oracle's write_color (math.rs:119-132, main.rs:472,591-596) of the
+    product's own f64 means AND to the oracle's PPM of the oracle's own render of the frame. The
+    frame is rendered through rt_render with RT_OUT_F64 (sum * (1/spp) in f64, the reference's
+    `self.x * scale`) and written by rt_write_ppm_f64."""
+    scene_id, W, H, spp, depth, _, _ = FULL["C1"]
+    img, _ = rt.render_scene(scene_id, W, H, spp, depth, out_format=rt.RT_OUT_F64, renderer=renderer)
+    assert img.shape == (H, W, 3) and img.dtype == np.float64
+    mine, own, ref = tmp_path / "product.ppm", tmp_path / "oracle_of_product.ppm", tmp_path / "oracle.ppm"
+    rt.write_ppm(img, str(mine))
+    ob.write_ppm(img, str(own))
+    ob.write_ppm(_full_ref("C1"), str(ref))
+    b = mine.read_bytes()
+    assert b.startswith(b"P3\n1200 800\n255\n\n") and b.count(b"\n") == 4 + W * H
+    assert b == own.read_bytes(), "product write_color != oracle write_color of the same means"
+    assert b == ref.read_bytes(), "product PPM != oracle PPM of the oracle's render"
+    # and channel by channel (a mismatch would name its pixel)
+    assert np.array_equal(rt.write_color(img), ob.write_color(_full_ref("C1")))
 
 
 _C5_REF = {}

@@ -464,3 +464,43 @@ def test_renders_on_two_streams_are_ordered(rt, renderer):
     torch.cuda.synchronize()
     assert np.array_equal(got_b, ref_b)
     assert np.array_equal(slab.cpu().numpy(), ref_a)
+
+
+@pytest.mark.parametrize("sched", ["AUTO", "POOL", "ITEMS", "CHUNKS"])
+def test_empty_shards_render_nothing(rt, renderer, sched):
+    """a shard with no tiles (a rank past the frame's tile count) or no rows is
+    valid input. rt_render (host and device output, the bench's padded slab), rt_accum_add /
+    resolve and rt_render_progressive return RT_OK and write nothing; no division by the shard's
+    size. The next non-empty render on the same context is unaffected."""
+    import torch
+    W, H, spp = 16, 16, 4                        # 2 x 2 = 4 tiles
+    world = rt.World(1).build_scene(0)
+    cam, bg = rt.scene_camera(0, W, H)
+    renderer.upload(world)
+    renderer.set_schedule(getattr(rt, "RT_SCHED_" + sched))
+    try:
+        assert rt.tiles_in_shard(W, H, 5, 8) == 0 and rt.rows_in_shard(H, 17, 4) == 0
+        shards = [dict(row_begin=5, row_stride=8, tile_shard=1), dict(row_begin=17, row_stride=4)]
+        for sh in shards:
+            p = rt.Renderer.params(W, H, spp, 50, bg, 1, out_format=rt.RT_OUT_F64, **sh)
+            img = renderer.render(cam, p)
+            assert img.size == 0
+            st = renderer.stats()
+            assert st.samples == 0
+            # device output into a non-empty padded slab (bench.py at N > 1): left untouched
+            slab = torch.full((8, 16, 3), 7.0, dtype=torch.float64, device="cuda:0")
+            stream = torch.cuda.Stream()
+            renderer.render_device(cam, p, slab.data_ptr(), stream.cuda_stream)
+            stream.synchronize()
+            assert bool((slab == 7.0).all())
+            acc = renderer.accumulator(p)
+            acc.add(cam, p, spp)
+            assert acc.samples_done == spp
+            assert acc.resolve(out_format=rt.RT_OUT_F64).size == 0
+            acc.close()
+            assert renderer.render_progressive(cam, p, 2).size == 0
+        full = renderer.render(cam, rt.Renderer.params(W, H, spp, 50, bg, 1, out_format=rt.RT_OUT_F64))
+        ref = ob.render(0, W, H, spp)
+        assert np.abs(full - ref).max() <= 1e-12
+    finally:
+        renderer.set_schedule(rt.RT_SCHED_AUTO)
