@@ -35,7 +35,9 @@ enum {
     RT_PRIM_YZ_RECT = 4,       /* p: y0 y1 z0 z1 k */
     RT_PRIM_BOX = 5,           /* p: minxyz maxxyz (6 rects, hittable.rs:132-145); b = 1: p[6..8] hold
                                   the box's f32 bounds (lo xyz, hi xyz), padded and rounded outward
-                                  like a node's, for a conservative pre-test (b = 0: none) */
+                                  like a node's, for the kernel's conservative candidate-side test
+                                  (b = 0: none, all six sides tested). The upload derives the face
+                                  slabs' width from that padding (device copy: b = 2, p[9]). */
     RT_PRIM_INSTANCE = 6,      /* a: instance index */
     RT_PRIM_MEDIUM = 7         /* a: boundary prim index (SPHERE/BOX/INSTANCE), b: medium id, p[0]: -1/density */
 };

@@ -110,6 +110,7 @@ struct rt_ctx {
     int opt_lds = 1;                    // rt_ctx_set_variant / RT_LDS_STACK
     int opt_lds_nodes = 1;              // RT_LDS_NODES: keep the TLAS in LDS when it fits
     int opt_hoist = RT_HOIST_DEFAULT;   // RT_HOIST: test a huge root-child leaf before the walk (pre_leaf)
+    int opt_box_cand = 1;               // RT_BOX_CAND: boxes take the candidate-side test (0: six exact sides; A/B)
     int opt_pool = RT_SCHED_AUTO;       // rt_ctx_set_schedule / RT_SCHEDULE: RT_SCHED_*
     int opt_precision = RT_PREC_F64;    // rt_ctx_set_precision / RT_PRECISION: RT_PREC_*
     size_t sample_buf_cap = (size_t)32 << 30;  // RT_SAMPLE_BUF_MB: bound of one launch's trace output
@@ -118,6 +119,8 @@ struct rt_ctx {
     size_t acc_tmp_cap = 0;
     int n_tlas_nodes = 0;
     int n_nodes = 0;                    // BVH nodes of the uploaded scene (TLAS + BLASes)
+    rtk::WalkSave* walk_save = nullptr; // RT_PAUSE builds: suspended walks, one slot per thread of a full grid
+    int n_cus = 256;
     size_t lds_per_cu = 160 * 1024;     // the device's LDS per CU and per workgroup (read at creation)
     size_t lds_per_block = 160 * 1024;
 };
@@ -155,6 +158,7 @@ int rt_ctx_create(int device, rt_ctx** out)
     if (const char* e = std::getenv("RT_LDS_STACK")) c->opt_lds = std::atoi(e) != 0;
     if (const char* e = std::getenv("RT_LDS_NODES")) c->opt_lds_nodes = std::atoi(e) != 0;
     if (const char* e = std::getenv("RT_HOIST")) c->opt_hoist = std::atoi(e) != 0;
+    if (const char* e = std::getenv("RT_BOX_CAND")) c->opt_box_cand = std::atoi(e) != 0;
     if (const char* e = std::getenv("RT_SCHEDULE")) c->opt_pool = std::min(3, std::max(0, std::atoi(e)));
     if (const char* e = std::getenv("RT_PRECISION")) c->opt_precision = std::atoi(e) == RT_PREC_F32 ? RT_PREC_F32 : RT_PREC_F64;
     if (const char* e = std::getenv("RT_BLOCK_CHUNKS")) c->block_chunks = std::min(64, std::max(1, std::atoi(e)));
@@ -179,6 +183,8 @@ int rt_ctx_create(int device, rt_ctx** out)
             c->lds_per_cu = (size_t)v;
         if (hipDeviceGetAttribute(&v, hipDeviceAttributeMaxSharedMemoryPerBlock, device) == hipSuccess && v > 0)
             c->lds_per_block = (size_t)v;
+        if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && v > 0)
+            c->n_cus = v;
         c->lds_per_block = std::min(c->lds_per_block, c->lds_per_cu);
     }
     hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
@@ -208,6 +214,7 @@ void rt_ctx_destroy(rt_ctx* c)
     (void)hipFree(c->params);
     (void)hipFree(c->work);
     (void)hipFree(c->acc_tmp);
+    (void)hipFree(c->walk_save);
     for (auto& e : c->ev)
         if (e) (void)hipEventDestroy(e);
     if (c->ev_done) (void)hipEventDestroy(c->ev_done);
@@ -778,6 +785,28 @@ int rt_ctx_upload_soa(rt_ctx* c, const rt_scene_soa* s)
         } else if (p.kind == RT_PRIM_MOVING_SPHERE) {
             p.a = (p.p[8] == 0.0 && p.p[9] == 1.0) ? 1 : 0;
             if (!p.a) general_shutter = true;
+        } else if (p.kind == RT_PRIM_BOX && p.b != 0 && c->opt_box_cand) {
+            // The kernel's candidate-side test (box_candidates) takes thin slabs around each face
+            // plane as wide as the padding of the box's f32 bounds on the outer side: w = twice
+            // the largest padding, stored after the bounds (p[9], b = 2). Bounds that do not
+            // contain the box (a foreign SoA) or are not finite leave b = 0: six exact sides.
+            const float* fb = reinterpret_cast<const float*>(&p.p[6]);
+            double pad = 0.0;
+            bool ok = true;
+            for (int a = 0; a < 3; ++a) {
+                const double lo = (double)fb[a], hi = (double)fb[3 + a];
+                if (!std::isfinite(lo) || !std::isfinite(hi) || lo > p.p[a] || hi < p.p[3 + a]) ok = false;
+                else pad = std::max({pad, p.p[a] - lo, hi - p.p[3 + a]});
+            }
+            float w = (float)(2.0 * pad);
+            if ((double)w < 2.0 * pad) w = std::nextafter(w, INFINITY);
+            if (!ok || !std::isfinite(w)) {
+                p.b = 0;
+            } else {
+                p.b = 2;
+                float wv[2] = {w, 0.0f};
+                std::memcpy(&p.p[9], wv, sizeof wv);
+            }
         }
     }
     std::vector<rt_prim> leaf_prims((size_t)s->n_prim_refs);
@@ -1307,6 +1336,14 @@ static int run_range(rt_ctx* c, const rt_camera* cam, const rt_render_params* p,
     K.tile_shard = p->tile_shard;
     K.img_tiles_x = (p->width + 7) / 8;
     K.n_rows = n_rows;
+    if (RT_PAUSE > 0) {   // suspended walks (trace_kernel.hpp RT_PAUSE): a slot per thread the grid can hold
+        if (!c->walk_save) {
+            HIP_TRY(hipStreamSynchronize(stream));
+            HIP_TRY(hipMalloc((void**)&c->walk_save,
+                              (size_t)c->n_cus * rtk::kWalkSaveThreadsPerCU * sizeof(rtk::WalkSave)));
+        }
+        K.walk_save = c->walk_save;
+    }
     K.tiles_x = (lay.w + 7) / 8;
     K.tiles_y = (n_rows + 7) / 8;
 

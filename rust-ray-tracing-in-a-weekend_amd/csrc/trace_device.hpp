@@ -149,6 +149,20 @@ __device__ __forceinline__ bool first_active_lane()
 #ifndef RT_PERLIN_ROLLED
 #define RT_PERLIN_ROLLED 0   // rolled: C4 143.3 vs 136.9 ms unrolled (r03b_ab_c4.log); no spills either way without machine LICM
 #endif
+#ifndef RT_TRY_LEFT
+// pool schedules (RT_MERGED_DRAWS): the wave leaves its rejection loop (random_in_unit_disk /
+// random_in_unit_sphere tries, math.rs:51-76) once at most RT_TRY_LEFT lanes still reject, after
+// at least RT_TRY_MIN tries; those lanes keep their stream position and candidate state and go
+// on drawing in the next bounce-loop iteration instead of tracing in this one. Each lane's draws
+// stay in its own stream order, so the bits do not change; the wave no longer runs as many
+// tries as its unluckiest lane (E[max of 64 geometric(0.52)] ~ 6.9 against a mean of 1.9).
+// 0: the loop runs until every lane accepted (round 3). C2 1200x800x100 (profiles/r04b_ab_c2.log):
+// off 15.28 ms, 2 15.12, 4 15.07, 8 15.37, 4 after one try 15.22; images identical.
+#define RT_TRY_LEFT 4
+#endif
+#ifndef RT_TRY_MIN
+#define RT_TRY_MIN 2
+#endif
 #ifndef RT_KILL_H
 // pool schedules: the hit record carried across the loop edge (RT_MERGED_DRAWS) is marked dead
 // before the next trace (trace_world writes only the fields its primitive kind has, so the
@@ -602,10 +616,82 @@ __device__ __forceinline__ void box_side(const rt_prim& p, int side, int& axis, 
     else { axis = 2; a0 = mny; a1 = mxy; b0 = mnz; b1 = mxz; k = side == 4 ? mxx : mnx; }
 }
 
+#ifndef RT_BOX_CAND
+// Box candidate sides: a conservative f32 test per side first, the exact
+// f64 rect test only on the sides that can pass it. Measured slower and off: C4 1920x1080x100
+// 111.30 vs 107.23 ms with six sides, leaf-test share 0.338 vs 0.329 (profiles/r04b_ab_c4.log,
+// r04b_phases_c4*.log): a wave enters an axis's block when any lane has a candidate there, and
+// the lanes testing a box are mostly the ones that hit it (entry and exit sides on two or three
+// axes), so the wave still runs about three exact tests and a reciprocal per axis, plus the
+// candidate test itself.
+#define RT_BOX_CAND 0
+#endif
+// The variants that take it: the final scene's (400 boxes at the top level, f32 slab terms
+// in every ray). In the Cornell variants (f64 slabs, boxes under instances) its values cost a
+// wave per SIMD (rects + instances 122 -> 137 VGPRs, media 121 -> 141: 4 -> 3 waves).
+template <class C>
+constexpr bool BoxCand() { return RT_BOX_CAND && C::S32 && !C::F32 && C::F == FEAT_SET_FINAL; }
+// The sides of a Box whose exact rect test (hittable.rs:308-384) can pass, as a bit mask
+// (bit s = side s of box_side). The box record holds its bounds padded outward and rounded
+// to f32 (lo', hi': flatten.cpp, the padding a BVH node box gets) and w = twice the largest
+// padding (upload, rt_prim.b = 2). Side s lies on the plane k of axis A; take the thin slab
+// [k - pad, k + pad] on A (lo face: [lo', lo' + w], hi face: [hi' - w, hi']). If the exact
+// test of side s passes at t*, the point o + t* d lies on the side's rect (to f64 rounding),
+// so t* lies inside the padded slabs of the two other axes and inside the thin slab of A, the
+// padding covering the f32 rounding of the slab products exactly as it does for a BVH node
+// (|o| <= 2M); and t* is in [t_min, t_max]. So s is a candidate when the intersection of those
+// three t intervals with [t_min, t_max] (rounded outward) is non-empty: a slab test of the
+// side's padded flat box. A side that is not a candidate fails its exact test (with this
+// t_max, and with any smaller one), so testing the candidates only, in side order with the
+// same t_max updates, gives the reference's (t, side) bit for bit.
+template <bool S32, class R>
+__device__ __forceinline__ uint32_t box_candidates(const rt_prim& p, const RayT<R>& r, R t_min, R t_max)
+{
+    using T = typename std::conditional<S32, float, R>::type;
+    const float* fb = reinterpret_cast<const float*>(&p.p[6]);
+    const T w = (T)reinterpret_cast<const float*>(&p.p[9])[0];
+    // t of plane x on axis a: f32 x * (1/d) - o/d with the ray's slab terms (finish_ray), or f64
+    auto tp = [&](int a, T x) -> T {
+        if constexpr (S32) {
+            const f2v sa = a == 0 ? r.sx : a == 1 ? r.sy : r.sz;
+            return __builtin_fmaf(x, sa.x, sa.y);
+        } else {
+            return (x - (a == 0 ? r.ox : a == 1 ? r.oy : r.oz)) * (a == 0 ? r.ix : a == 1 ? r.iy : r.iz);
+        }
+    };
+    T nr[3], fr[3];   // the padded box's slab per axis
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        const T tl = tp(a, (T)fb[a]), th = tp(a, (T)fb[3 + a]);
+        nr[a] = fmin(tl, th);
+        fr[a] = fmax(tl, th);
+    }
+    T tmn, tmx;
+    if constexpr (S32) {
+        tmn = f32_down(t_min);
+        tmx = f32_up(t_max);
+    } else {
+        tmn = t_min;
+        tmx = t_max;
+    }
+    uint32_t m = 0;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {   // axis a = x, y, z: its hi side 4 - 2a, lo side 5 - 2a
+        const int b = a == 0 ? 1 : 0, c = a == 2 ? 1 : 2;
+        const T tn = fmax(fmax(nr[b], nr[c]), tmn), tf = fmin(fmin(fr[b], fr[c]), tmx);
+        // the face slabs [lo', lo' + w] and [hi' - w, hi'] (plane products recomputed: fewer live values)
+        const T tl = tp(a, (T)fb[a]), tli = tp(a, (T)fb[a] + w);
+        const T th = tp(a, (T)fb[3 + a]), thi = tp(a, (T)fb[3 + a] - w);
+        if (fmax(fmin(th, thi), tn) <= fmin(fmax(th, thi), tf)) m |= 1u << (4 - 2 * a);
+        if (fmax(fmin(tl, tli), tn) <= fmin(fmax(tl, tli), tf)) m |= 1u << (5 - 2 * a);
+    }
+    return m;
+}
+
 // Box::hit = hit_hittables over its sides (hittable.rs:229-231): closest, ties to the later side.
 // The reference has no bounding-box pre-test (Q8); a conservative one on the box's padded
 // f32 bounds (flatten.cpp) only skips rect tests that cannot hit, like a BVH node box does.
-template <bool RCP = false, bool S32 = true, bool LRCP = false, class R>
+template <bool RCP = false, bool S32 = true, bool LRCP = false, bool CAND = false, class R>
 __device__ __forceinline__ bool box_t(const rt_prim& p, const RayT<R>& r, R t_min, R t_max, R& t, int& side)
 {
     if (RT_BOX_PRETEST && p.b) {
@@ -627,6 +713,45 @@ __device__ __forceinline__ bool box_t(const rt_prim& p, const RayT<R>& r, R t_mi
     // direction component outside [2^-900, 2^900], e.g. an exact 0, divides as the reference).
     constexpr bool LOCAL_RCP = LRCP && !RCP && std::is_same<R, double>::value;
     auto in_range = [](R d) { const R m = r_fabs(d); return m >= (R)0x1.0p-900 && m <= (R)0x1.0p+900; };
+    if constexpr (CAND && std::is_same<R, double>::value) {
+        // candidate sides only (box_candidates), with every direction component in [2^-60, 2^60]
+        // (finite f32 slab terms; outside, e.g. an exact 0, all six sides run below). Per axis
+        // one block, entered by the wave when any lane has a candidate on that axis: a lane
+        // tests its pair's first candidate, and the second only in the rare case that both are
+        // (a box thinner than its padding); the sides keep their order 0..5.
+        auto cand_range = [](R d) { const R m = r_fabs(d); return m >= (R)0x1.0p-60 && m <= (R)0x1.0p+60; };
+        if (p.b == 2 && cand_range(r.dx) && cand_range(r.dy) && cand_range(r.dz)) {
+            const uint32_t m = box_candidates<S32>(p, r, t_min, t_max);
+            const R mnx = (R)p.p[0], mny = (R)p.p[1], mnz = (R)p.p[2], mxx = (R)p.p[3], mxy = (R)p.p[4], mxz = (R)p.p[5];
+#pragma unroll
+            for (int ax = 0; ax < 3; ++ax) {   // rect axis: 0 XY (k on z, sides 0/1), 1 XZ (y, 2/3), 2 YZ (x, 4/5)
+                const uint32_t bits = (m >> (2 * ax)) & 3u;
+                if (bits == 0) continue;
+                const R a0 = ax == 2 ? mny : mnx, a1 = ax == 2 ? mxy : mxx;
+                const R b0 = ax == 0 ? mny : mnz, b1 = ax == 0 ? mxy : mxz;
+                const R kmax = ax == 0 ? mxz : ax == 1 ? mxy : mxx, kmin = ax == 0 ? mnz : ax == 1 ? mny : mnx;
+                const R dk = ax == 0 ? r.dz : ax == 1 ? r.dy : r.dx;
+                R y = (R)0;
+                if constexpr (RCP) y = ax == 0 ? r.yz : ax == 1 ? r.yy : r.yx;
+                else if constexpr (LOCAL_RCP) y = (R)1 / dk;
+                auto test = [&](int s, R k) {
+                    R ts;
+                    bool ok;
+                    if constexpr (RCP || LOCAL_RCP) ok = rect_t_y(ax, a0, a1, b0, b1, k, r, y, t_min, t_max, ts);
+                    else ok = rect_t<false>(ax, a0, a1, b0, b1, k, r, t_min, t_max, ts);
+                    if (ok) {
+                        t_max = ts;
+                        t = ts;
+                        side = s;
+                        any = true;
+                    }
+                };
+                test((bits & 1u) ? 2 * ax : 2 * ax + 1, (bits & 1u) ? kmax : kmin);
+                if (bits == 3u) test(2 * ax + 1, kmin);
+            }
+            return any;
+        }
+    }
     if (LOCAL_RCP && in_range(r.dx) && in_range(r.dy) && in_range(r.dz)) {
         R y = (R)0;   // of the side pair's direction (sides 2a, 2a+1 share axis a)
 #pragma unroll
@@ -699,7 +824,7 @@ __device__ __forceinline__ bool simple_t(const rt_prim& p, const RayT<R>& r, R t
         case RT_PRIM_XY_RECT: return rect_t<RectRcp<C>()>(0, q0, q1, q2, q3, q4, r, t_min, t_max, t);
         case RT_PRIM_XZ_RECT: return rect_t<RectRcp<C>()>(1, q0, q1, q2, q3, q4, r, t_min, t_max, t);
         case RT_PRIM_YZ_RECT: return rect_t<RectRcp<C>()>(2, q0, q1, q2, q3, q4, r, t_min, t_max, t);
-        case RT_PRIM_BOX: return box_t<RectRcp<C>(), C::S32, BoxRcp<C>()>(p, r, t_min, t_max, t, side);
+        case RT_PRIM_BOX: return box_t<RectRcp<C>(), C::S32, BoxRcp<C>(), BoxCand<C>()>(p, r, t_min, t_max, t, side);
         default: return false;
         }
     }
@@ -839,15 +964,19 @@ __device__ __forceinline__ LdsLayout lds_layout_of(const SceneDev& S)
 // Closest hit in a BVH (nodes + leaf ranges of slots j, whose records are leaf_prims[j]).
 // `leaf(slot, t_max, best)` tests one primitive; on a closer hit it fills best (t and sub
 // ids) and returns true; best.prim is then the slot.
-template <class C, bool NL = false, class LeafFn, class R = typename C::Real>
+// PAUSE (RT_PAUSE): the walk may be suspended (see RT_PAUSE) into *ws, *paused set, and
+// resumed from it (resume: root, t_max and best come from *ws instead).
+template <class C, bool NL = false, bool PAUSE = false, class LeafFn, class R = typename C::Real>
 __device__ __forceinline__ bool traverse(const SceneDev& S, int root, const RayT<R>& r, R t_min, R t_max,
-                                         HitRefT<R>& best, StackT<C>& stack, int sp0, Count& cnt, LeafFn&& leaf)
+                                         HitRefT<R>& best, StackT<C>& stack, int sp0, Count& cnt, LeafFn&& leaf,
+                                         WalkSave* ws = nullptr, bool resume = false, bool* paused = nullptr,
+                                         bool may_pause = false, bool pre_any = false)
 {
     // NL: this is the TLAS, whose first S.n_lds_nodes nodes (BFS order) were copied into
     // LDS at block start; deeper nodes are read from L1/L2
     const rt_bvh_node* lds_nodes =
         reinterpret_cast<const rt_bvh_node*>(rt_lds);   // at LDS address 0: node offsets are addresses
-    bool any = false;
+    bool any = PAUSE && pre_any;   // PAUSE: the caller's pre-leaf hit travels with the walk's state
     // the walk's bottom entry is RT_DONE (the host reserves it: SceneDev.stack_entries,
     // blas_base), so a pop needs no empty-stack test: popping it ends the walk
     constexpr int DONE = Stack16Cfg<C>() ? -32768 : RT_DONE;   // the walk's bottom entry
@@ -857,8 +986,10 @@ __device__ __forceinline__ bool traverse(const SceneDev& S, int root, const RayT
     constexpr int SSTR = C::LDS ? BlockThreads<C>() : 1;
     auto* sptr = &stack[sp0];
     using SE = typename std::remove_reference<decltype(*sptr)>::type;
-    *sptr = (SE)DONE;
-    sptr += SSTR;
+    if (!(PAUSE && resume)) {
+        *sptr = (SE)DONE;
+        sptr += SSTR;
+    }
     auto push = [&](int v) { *sptr = (SE)v; sptr += SSTR; };
     auto pop = [&]() -> int { sptr -= SSTR; return (int)*sptr; };
 #else
@@ -868,6 +999,22 @@ __device__ __forceinline__ bool traverse(const SceneDev& S, int root, const RayT
     auto pop = [&]() -> int { return stack[--sp]; };
 #endif
     int cur = root;
+    if constexpr (PAUSE) {
+        // ws: the block's slots; the lane's is its thread index, recovered from its stack column's
+        // address where that is an LDS column (no register held for it through the bounce loop)
+        if constexpr (Stack16Cfg<C>())
+            ws += (int)(stack.base - reinterpret_cast<short*>(rt_lds + lds_stack_offset<C>(S)));
+        else
+            ws += threadIdx.x;
+        if (resume) {   // the suspended walk: its node (already an LDS address), stack depth, t_max, hit
+            cur = ws->cur;
+            sptr += ws->sp;
+            t_max = (R)ws->t_max;
+            best.t = (R)ws->best_t;
+            best.prim = ws->best_prim;
+            any = ws->any != 0;
+        }
+    }
     float tmin_f = 0.0f, tmax_f = 0.0f;
     if constexpr (C::S32) {
         tmin_f = f32_down(t_min);
@@ -890,8 +1037,10 @@ __device__ __forceinline__ bool traverse(const SceneDev& S, int root, const RayT
     float tmin_v = tmin_f;
     if constexpr (OCT && PkSlab<C>()) asm("v_mov_b32 %0, %1" : "=v"(tmin_v) : "v"(tmin_f));
     constexpr bool W4 = OCT && Wide<C>();   // the 4-wide TLAS: its root record (index 0) is the walk's start
-    if constexpr (W4) cur = cur >= 0 ? (int)lds_addr(lb) : cur;
-    else if constexpr (OCT) cur = cur >= 0 ? (int)(lds_addr(lb) + (uint32_t)cur * (uint32_t)sizeof(LdsNode)) : cur;
+    if (!(PAUSE && resume)) {
+        if constexpr (W4) cur = cur >= 0 ? (int)lds_addr(lb) : cur;
+        else if constexpr (OCT) cur = cur >= 0 ? (int)(lds_addr(lb) + (uint32_t)cur * (uint32_t)sizeof(LdsNode)) : cur;
+    }
     // one node visit: test both children, continue with the nearer, push the farther
     auto visit = [&](int node) -> int {
         if (C::COUNT) cnt.nodes++;
@@ -1057,7 +1206,22 @@ __device__ __forceinline__ bool traverse(const SceneDev& S, int root, const RayT
         }
     } else if constexpr (C::LOOP == 1) {
         uint64_t t0 = 0;
+        int leaves = 0;
+        (void)leaves;
         while (cur != DONE) {
+            if constexpr (PAUSE) {
+                // every lane still walking is here (the wave's outer-loop head): few enough left?
+                if (may_pause && ++leaves > RT_PAUSE_MIN && __popcll(__ballot(1)) <= RT_PAUSE) {
+                    ws->cur = cur;
+                    ws->sp = (int32_t)(sptr - &stack[sp0]);
+                    ws->t_max = (double)t_max;
+                    ws->best_t = (double)best.t;
+                    ws->best_prim = best.prim;
+                    ws->any = any ? 1 : 0;
+                    *paused = true;
+                    break;
+                }
+            }
             if (C::COUNT && NL) t0 = __builtin_amdgcn_s_memtime();
             while (cur >= 0) {
                 if (C::COUNT && first_active_lane()) cnt.wave_nodes++;
@@ -1302,10 +1466,16 @@ constexpr bool PreLeaf() { return C::F == FEAT_SET_SPHERES; }
 template <class C>
 constexpr bool DeferInst() { return RT_DEFER_INST && (C::F & FEAT_INST_BLAS) != 0; }
 
-// HitRecord of the closest primitive.
+// the variants whose top-level walk may be suspended (RT_PAUSE): the spheres ones (C2, C5)
+template <class C>
+constexpr bool Pause() { return RT_PAUSE > 0 && C::F == FEAT_SET_SPHERES && !C::F32; }
+
+// HitRecord of the closest primitive. Pause<C>(): with ws, the top-level walk may be
+// suspended (*paused: no record; the lane resumes it with resume = true next iteration).
 template <class C, class R = typename C::Real>
 __device__ bool trace_world(const SceneDev& S, const RayT<R>& r, HitT<R>& h, StackT<C>& stack, const Keyed& key,
-                            Count& cnt)
+                            Count& cnt, WalkSave* ws = nullptr, bool resume = false, bool* paused = nullptr,
+                            bool may_pause = false)
 {
     const R t_min = (R)0.001;
     HitRefT<R> best;
@@ -1351,7 +1521,7 @@ __device__ bool trace_world(const SceneDev& S, const RayT<R>& r, HitT<R>& h, Sta
         R t_max = (R)RT_INF;
         hit = false;
         int root = S.tlas_root;
-        if (S.pre_leaf != 0) {   // wave-uniform: the huge root-child leaf first (SceneDev.pre_leaf)
+        if (S.pre_leaf != 0 && !(Pause<C>() && resume)) {   // wave-uniform: the huge root-child leaf first (SceneDev.pre_leaf)
             root = S.pre_root;
             bool in_box;
             if constexpr (C::S32) {
@@ -1372,8 +1542,19 @@ __device__ bool trace_world(const SceneDev& S, const RayT<R>& r, HitT<R>& h, Sta
                 }
             }
         }
+        if (S.pre_leaf != 0) root = S.pre_root;
         RT_STAMP(cnt.t_pre, tp);
-        hit |= traverse<C, true>(S, root, r, t_min, t_max, best, stack, 0, cnt, leaf);
+        if constexpr (Pause<C>()) {   // (ws is NULL only without a walk_save buffer: no suspension then)
+            bool susp = false;
+            hit = traverse<C, true, true>(S, root, r, t_min, t_max, best, stack, 0, cnt, leaf, ws, resume, &susp,
+                                          may_pause && ws != nullptr, hit);
+            if (susp) {
+                *paused = true;
+                return false;
+            }
+        } else {
+            hit |= traverse<C, true>(S, root, r, t_min, t_max, best, stack, 0, cnt, leaf);
+        }
     } else {
         RT_STAMP(cnt.t_pre, tp);
         hit = traverse<C, true>(S, S.tlas_root, r, t_min, (R)RT_INF, best, stack, 0, cnt, leaf);
@@ -2172,6 +2353,16 @@ __global__ void __launch_bounds__(BlockThreads<C>(), min_waves<C>()) trace_pool(
     HitT<R> h;             // RT_MERGED_DRAWS: a hit whose scattered ray the next iteration draws
     bool pending = false;
     (void)pending;
+    bool cam_wait = false;  // RT_TRY_LEFT: camera_begin ran, the disk tries go on (u, v in r.dx, r.dy)
+    (void)cam_wait;
+    // RT_PAUSE: the lane's suspended top-level walk (the block's slots in KParams.walk_save)
+    bool walk_paused = false;
+    WalkSave* ws = nullptr;
+    if constexpr (Pause<C>()) {
+        if (P.walk_save) ws = P.walk_save + (size_t)blockIdx.x * BlockThreads<C>();
+    }
+    (void)walk_paused;
+    (void)ws;
     for (;;) {
         if (ITEMS && own) {
             own = false;
@@ -2253,32 +2444,59 @@ __global__ void __launch_bounds__(BlockThreads<C>(), min_waves<C>()) trace_pool(
         // run in one rejection loop (the wave used to run the two loops one after the other).
         // Each lane's draws keep their order (its stream is its own), so the bits do not change.
         bool go = true;   // the lane traces this iteration
+        bool gen_wait = false;   // RT_TRY_LEFT: the lane's tries go on in the next iteration
         {
             R u = 0, v = 0;
             bool tries = false;
-            if (new_sample) {
-                if (C::COUNT) {
-                    cnt.cam_lanes++;
-                    if (first_active_lane()) cnt.cam_steps++;
+            if (Pause<C>() && walk_paused) {
+                // the lane's walk resumes in the trace step (its ray kept in r)
+            } else if (new_sample) {
+                if (RT_TRY_LEFT > 0 && cam_wait) {   // camera_begin ran: the jitter waits in r.dx / r.dy
+                    u = r.dx;
+                    v = r.dy;
+                    cam_wait = false;
+                } else {
+                    if (C::COUNT) {
+                        cnt.cam_lanes++;
+                        if (first_active_lane()) cnt.cam_steps++;
+                    }
+                    int ix, y;
+                    image_xy(P, x, k, ix, y);
+                    key.pixel = (uint32_t)y * (uint32_t)P.img_width + (uint32_t)ix;
+                    key.sample = (uint32_t)s;
+                    ds_start(st, P.seed, key.pixel, (uint32_t)s);
+                    camera_begin(P, ix, y, st, u, v);
+                    Tr = Tg = Tb = (R)1;
+                    if constexpr (!ITEMS) cr = cg = cb = 0.0;  // ITEMS: the chunk's running sum
+                    depth = P.max_depth;
                 }
-                int ix, y;
-                image_xy(P, x, k, ix, y);
-                key.pixel = (uint32_t)y * (uint32_t)P.img_width + (uint32_t)ix;
-                key.sample = (uint32_t)s;
-                ds_start(st, P.seed, key.pixel, (uint32_t)s);
-                camera_begin(P, ix, y, st, u, v);
-                Tr = Tg = Tb = (R)1;
-                if constexpr (!ITEMS) cr = cg = cb = 0.0;  // ITEMS: the chunk's running sum
-                depth = P.max_depth;
                 tries = true;
             } else if (pending) {
                 tries = shade_draws<C>(S, h.mat);
             }
             R qx = (R)0, qy = (R)0, qz = (R)0, l2 = (R)1;
             const bool three = !new_sample;
+#if RT_TRY_LEFT > 0
+            bool accepted = !tries;
+            for (int n = 1;; ++n) {
+                if (!accepted) accepted = unit_try(st, (R)P.scale_m11, three, qx, qy, qz, l2);
+                const uint64_t rejecting = __ballot(!accepted);
+                if (rejecting == 0 || (n >= RT_TRY_MIN && __popcll(rejecting) <= RT_TRY_LEFT)) break;
+            }
+            gen_wait = !accepted;
+#else
             while (tries && !unit_try(st, (R)P.scale_m11, three, qx, qy, qz, l2)) {
             }
-            if (new_sample) {
+#endif
+            if (Pause<C>() && walk_paused) {
+            } else if (gen_wait) {   // (RT_TRY_LEFT) no trace this iteration; pending / new_sample stay set
+                go = false;
+                if (new_sample) {
+                    cam_wait = true;
+                    r.dx = u;
+                    r.dy = v;
+                }
+            } else if (new_sample) {
                 new_sample = false;
                 camera_end(P, st, u, v, qx, qy, r);
             } else if (pending) {
@@ -2290,13 +2508,17 @@ __global__ void __launch_bounds__(BlockThreads<C>(), min_waves<C>()) trace_pool(
         RT_STAMP(t_cam, t_prev);
         if (go && depth > 0) {  // main.rs:21-23: depth 0 is black
             key.bounce = (uint32_t)(P.max_depth - depth);
-            if (C::COUNT) cnt.casts++;
+            if (C::COUNT && !walk_paused) cnt.casts++;
             finish_ray<C>(r, S.has_spheres != 0);
             if (RT_KILL_H) forget(h);
             RT_STAMP(cnt.t_setup, t_prev);
-            const bool hit = trace_world<C>(S, r, h, stack, key, cnt);
+            bool suspended = false;
+            // no suspension once the grid's work is exhausted: no new walks would fill the lanes
+            const bool hit = trace_world<C>(S, r, h, stack, key, cnt, ws, walk_paused, &suspended, !exhausted);
+            walk_paused = suspended;
             if (C::COUNT) t_prev = __builtin_amdgcn_s_memtime();   // trace_world stamped its phases
-            if (!hit) {  // main.rs:37: background
+            if (Pause<C>() && suspended) {
+            } else if (!hit) {  // main.rs:37: background
                 cr = cr + Tr * P.bg[0];
                 cg = cg + Tg * P.bg[1];
                 cb = cb + Tb * P.bg[2];
@@ -2310,7 +2532,7 @@ __global__ void __launch_bounds__(BlockThreads<C>(), min_waves<C>()) trace_pool(
             RT_STAMP(t_shade, t_prev);
         }
         if (C::COUNT) t_prev = __builtin_amdgcn_s_memtime();   // lanes that did not trace
-        if (pending) {
+        if (pending || gen_wait || walk_paused) {
         } else if (ITEMS && left > 0) {  // the item's next sample: the lane takes it at the loop top
             active = false;
             own = true;

@@ -94,6 +94,29 @@ struct SceneDev {
     int32_t n_w4, w4_stack;
 };
 
+#ifndef RT_PAUSE
+// Walk suspension (regrouping live rays across bounce iterations): in the
+// spheres variant's top-level walk, once at most RT_PAUSE lanes of the wave are still walking
+// (checked at each leaf, after RT_PAUSE_MIN of them), those lanes store their walk state (node,
+// stack pointer, t_max, closest hit so far) to a per-thread slot in global memory and leave
+// the walk; the wave goes on to shade and generate rays for its other lanes, and the suspended
+// lanes resume their walk in the next iteration's trace step beside the new walks, so the
+// wave no longer idles behind its longest walks. The stack stays in the lane's LDS column; the
+// ray stays in its registers (it is live across the loop edge anyway). Closest hit does not
+// depend on when the steps run, so the bits do not change. 0: off.
+#define RT_PAUSE 0
+#endif
+#ifndef RT_PAUSE_MIN
+#define RT_PAUSE_MIN 2
+#endif
+// A suspended top-level walk (RT_PAUSE, trace_device.hpp): 32 B per thread of the persistent
+// grid (KParams.walk_save, allocated by the context: walk_save_threads() slots)
+struct WalkSave {
+    double t_max, best_t;
+    int32_t cur, sp, best_prim, any;
+};
+constexpr int kWalkSaveThreadsPerCU = 2048;   // the most threads a CU holds at once
+
 struct KParams {
     rt_camera cam;
     double bg[3];
@@ -115,6 +138,7 @@ struct KParams {
     int32_t img_width;          // the image's width (pixel keys)
     int32_t tile_shard;         // rt_render_params.tile_shard: grid tile m = the frame's tile row_begin + m*row_stride
     int32_t img_tiles_x;        // tiles per tile row of the image
+    WalkSave* walk_save;        // RT_PAUSE builds: one slot per thread of the persistent grid (NULL: no suspension)
 };
 
 // Scene features (which code a kernel variant must contain).

@@ -11,6 +11,28 @@ a)
     # round-4 session A: the byte-exact output / RCCL-branch / empty-shard build — GPU tests, smoke, default bench
     PREFIX=r04a_ scripts/gpu_session.sh tests smoke bench
     ;;
+b)
+    # round-4 session B: GPU tests with the Box candidate-side test; A/B of the rejection-loop cap
+    # (RT_TRY_LEFT 2/4/8, RT_TRY_MIN 1) on C2 and of the candidate sides on C4; phase timers of
+    # C4 (candidates) and of C2 under the cap
+    scripts/gpu_session.sh tests \
+      "600:r04b_ab_c2:python scripts/ab_builds.py $L/librtiow_amd.so $L/librtiow_exp_try2.so $L/librtiow_exp_try4.so $L/librtiow_exp_try8.so $L/librtiow_exp_try4m1.so --scene 0 --width 1200 --height 800 --spp 100 --rounds 3" \
+      "600:r04b_ab_c4:python scripts/ab_builds.py $L/librtiow_amd.so $L/librtiow_exp_nocand.so --scene 7 --width 1920 --height 1080 --spp 100 --rounds 3" \
+      "200:r04b_phases_c4:python scripts/phases.py --scene 7 --width 1920 --height 1080 --spp 8" \
+      "200:r04b_phases_c4_nocand:RT_LIB_PATH=$L/librtiow_exp_nocand.so python scripts/phases.py --scene 7 --width 1920 --height 1080 --spp 8" \
+      "200:r04b_phases_c2:python scripts/phases.py --scene 0 --width 1200 --height 800 --spp 16" \
+      "200:r04b_phases_c2_try4:RT_LIB_PATH=$L/librtiow_exp_try4.so python scripts/phases.py --scene 0 --width 1200 --height 800 --spp 16"
+    ;;
+c)
+    # round-4 session C: GPU tests (RT_TRY_LEFT 4 default, box candidates off); A/B of walk suspension
+    # (RT_PAUSE 4/8/16/32) and of the rejection cap off on C2; the cap on C4; phase timers under suspension
+    scripts/gpu_session.sh tests \
+      "600:r04c_ab_c2:python scripts/ab_builds.py $L/librtiow_amd.so $L/librtiow_exp_try0.so $L/librtiow_exp_pause4.so $L/librtiow_exp_pause8.so $L/librtiow_exp_pause16.so $L/librtiow_exp_pause32.so --scene 0 --width 1200 --height 800 --spp 100 --rounds 3" \
+      "600:r04c_ab_c4:python scripts/ab_builds.py $L/librtiow_amd.so $L/librtiow_exp_try0.so --scene 7 --width 1920 --height 1080 --spp 100 --rounds 3" \
+      "200:r04c_phases_c2:python scripts/phases.py --scene 0 --width 1200 --height 800 --spp 16" \
+      "200:r04c_phases_c2_pause8:RT_LIB_PATH=$L/librtiow_exp_pause8.so python scripts/phases.py --scene 0 --width 1200 --height 800 --spp 16" \
+      "200:r04c_phases_c2_pause16:RT_LIB_PATH=$L/librtiow_exp_pause16.so python scripts/phases.py --scene 0 --width 1200 --height 800 --spp 16"
+    ;;
 *)
     echo "unknown session: $1" >&2; exit 2 ;;
 esac

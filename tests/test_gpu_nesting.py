@@ -177,3 +177,67 @@ def test_sphere_fields_both_stack_widths_match_oracle(rt, renderer, n):
     got, ref = _render_both(rt, renderer, tw, 32, 20, 3, (7.0, 2.0, 6.0), (0.0, 0.0, 0.0), (0.7, 0.8, 1.0))
     assert renderer.stats().variant_features == 0
     assert_parity(got, ref, f"sphere field of {n}")
+
+
+def _box_world(rt):
+    """Top-level boxes that stress the candidate-side test (trace_device.hpp box_candidates):
+    a grid of unit boxes on integer coordinates (shared edge planes, exact ties at edges), boxes
+    of thickness 0, 1e-12, 1e-7 and 1e-3 (thinner than their padding: both sides of an axis are
+    candidates), boxes near the scene extent, a box the camera's rays start inside (exit sides
+    win), metal and glass boxes (rays leave from and re-enter box faces) and a light."""
+    tw = ob.TwinWorld(rt, 9)
+    white = tw.lambertian(tw.solid(0.73, 0.73, 0.73))
+    red = tw.lambertian(tw.checker((0.65, 0.05, 0.05), (0.9, 0.9, 0.9)))
+    metal = tw.metal((0.8, 0.8, 0.9), 0.05)
+    glass = tw.dielectric(1.5)
+    light = tw.diffuse_light(tw.solid(5.0, 5.0, 5.0))
+    for i in range(-5, 5):
+        for j in range(-5, 5):
+            h = 1.0 + ((i * 7 + j * 3) % 4)
+            tw.push(tw.box((float(i), 0.0, float(j)), (float(i + 1), h, float(j + 1)),
+                           (white, red, metal)[(i + j) % 3]))
+    for k, th in enumerate((0.0, 1e-12, 1e-7, 1e-3)):
+        tw.push(tw.box((-6.0 + 3.0 * k, 5.0, -7.0), (-4.0 + 3.0 * k, 5.0 + th, -5.0), white))
+        tw.push(tw.box((6.5, 1.0 + 1.5 * k, -3.0 + 2.0 * k), (6.5 + th, 2.0 + 1.5 * k, -1.5 + 2.0 * k), red))
+    tw.push(tw.box((-2.0, 5.5, -2.0), (2.0, 6.0, 2.0), glass))
+    tw.push(tw.box((990.0, -10.0, -10.0), (1000.0, 300.0, 10.0), white))     # near the extent
+    tw.push(tw.box((-30.0, -1.0, -30.0), (30.0, 40.0, 30.0), white))         # encloses everything
+    tw.push(tw.xz_rect(light, -3.0, 3.0, -3.0, 3.0, 12.0))
+    return tw
+
+
+@pytest.mark.parametrize("look_from,look_at", [((13.0, 9.0, 11.0), (0.0, 1.0, 0.0)), ((0.5, 3.0, 0.5), (0.7, 0.0, 0.2)),
+                                               ((-8.0, 5.0, -6.0), (6.5, 2.5, -2.0))])
+def test_box_world_on_final_variant_matches_oracle(rt, look_from, look_at):
+    """Boxes on the final-scene variant (the one C4's 400 ground boxes run on; RT_EXTRA_FEATURES
+    adds the noise bit so a world of boxes selects it): grid-aligned edges, boxes thinner than
+    their padding, rays starting inside a box. With the candidate-side build (RT_BOX_CAND=1,
+    trace_device.hpp box_candidates; measured slower, off by default) the context's runtime
+    switch RT_BOX_CAND=0 gives the six-side test: both images equal bit for bit, and the oracle's
+    to the parity bar."""
+    import os
+    tw = _box_world(rt)
+    W, H, spp = 64, 40, 6
+    cam = rt.camera_new(look_from, look_at, (0.0, 1.0, 0.0), 50.0, W / H, 0.1, 10.0, 0.0, 1.0)
+    bg = (0.3, 0.35, 0.4)
+    p = rt.Renderer.params(W, H, spp, 50, bg, 1, out_format=rt.RT_OUT_F64)
+    imgs = []
+    for cand in ("1", "0"):
+        os.environ["RT_EXTRA_FEATURES"] = "8"
+        os.environ["RT_BOX_CAND"] = cand
+        try:
+            r = rt.Renderer(0)
+        finally:
+            del os.environ["RT_EXTRA_FEATURES"]
+            del os.environ["RT_BOX_CAND"]
+        try:
+            r.upload(tw.product)
+            imgs.append(r.render(cam, p))
+            assert r.stats().variant_features == 287 and r.stats().slab32 == 1
+        finally:
+            r.close()
+    same = imgs[0] == imgs[1]
+    assert same.all(), f"{int((~same.all(axis=2)).sum())} px differ"
+    ref = tw.oracle.render(_cam24(cam), bg, W, H, spp)
+    assert float(ref.max()) > 0.0
+    assert_parity(imgs[0], ref, "box world")
