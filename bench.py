@@ -146,7 +146,7 @@ def isa_prices(src_hash, variant_features, schedule, slab32=1, nall=1):
     return {c: (v["price"], v["range"][0], v["range"][1]) for c, v in e["classes"].items()}
 
 
-KMIX_OF = {0: "kmix_c2", 287: "kmix_c4"}   # variant -> calibration replay of its VALU mix (scripts/calib/gen_kmix.py)
+KMIX_OF = {0: "kmix_c2", 287: "kmix_c4", 35: "kmix_c3"}   # variant -> calibration replay of its VALU mix (scripts/calib/gen_kmix.py)
 
 
 def replay_price(calib, variant_features):
@@ -501,6 +501,7 @@ def main():
             "parity": parity,
             "detail": {"kernel_ms_mean": round(k_ms, 3), "reduce_ms": round(last.reduce_ms, 3),
                        "schedule": last.schedule, "n_batches": last.n_batches, "waves_per_simd": last.waves_per_simd, "spp_chunk": last.spp_chunk,
+                       "trace_buf_bytes": int(last.trace_buf_bytes), "batches_overlapped": bool(last.overlapped),
                        "scene_bytes": int(last.scene_bytes), "scene_build_upload_s": round(t_build, 3),
                        "algorithmic_bytes_survey_8d": alg},
         }

@@ -217,6 +217,9 @@ typedef struct rt_stats {
     uint64_t shade_steps;        /*   wave iterations in which any lane did (shade_steps) */
     int32_t precision;           /* RT_PREC_* the last render ran with */
     int32_t waves_per_simd;      /* resident waves per SIMD of the last trace kernel (occupancy) */
+    int64_t trace_buf_bytes;     /* the trace-output buffer the last render used (both halves when overlapped) */
+    int32_t overlapped;          /* 1 if its buffer batches ran overlapped (two trace streams) */
+    int32_t pad0;
 } rt_stats;
 int rt_last_stats(rt_ctx* ctx, rt_stats* out);
 /* Diagnostic: the raw count_work counters of the last render (n entries; returns how many
@@ -296,12 +299,13 @@ int rt_ctx_set_variant(rt_ctx* ctx, int slab32, int lds_stack, int lds_nodes);
  *   ITEMS:  persistent waves as POOL, but a lane takes a whole (pixel, chunk) item, traces
  *           its samples in order and writes one partial, as CHUNKS does (1/chunk of POOL's
  *           buffer bytes); a lane whose item ended takes the next item at once.
- *   AUTO:   POOL when the render's per-sample buffer takes at most 4 batches (it is
+ *   AUTO:   POOL when the render's per-sample radiance is at most 16 x the buffer bound (it is
  *           the faster of the two), otherwise ITEMS; rt_stats.schedule reports which ran.
- * One launch's trace output is bounded by RT_SAMPLE_BUF_MB (default: sized at context
- * creation to 3/8 of the device's free memory, at most 128 GiB, at least 32 GiB where half
- * the free memory allows; allocated lazily, as large as a render needs); a larger render
- * runs in buffer batches (on chunk boundaries) whose sums are carried across. */
+ * The trace-output buffer is bounded by RT_SAMPLE_BUF_MB (default 4 GB, at most a quarter of
+ * the device's free memory; allocated lazily, as large as a render needs). A larger render
+ * runs in buffer batches whose sums are carried across, in two halves of the bound: batch k
+ * traces into half k & 1 on one of two context streams while the render's stream reduces
+ * batch k - 1, so consecutive traces overlap (RT_BATCH_OVERLAP=0: one buffer, in order). */
 enum { RT_SCHED_CHUNKS = 0, RT_SCHED_POOL = 1, RT_SCHED_ITEMS = 2, RT_SCHED_AUTO = 3 };
 int rt_ctx_set_schedule(rt_ctx* ctx, int schedule);
 

@@ -113,8 +113,13 @@ struct rt_ctx {
     int opt_box_cand = 1;               // RT_BOX_CAND: boxes take the candidate-side test (0: six exact sides; A/B)
     int opt_pool = RT_SCHED_AUTO;       // rt_ctx_set_schedule / RT_SCHEDULE: RT_SCHED_*
     int opt_precision = RT_PREC_F64;    // rt_ctx_set_precision / RT_PRECISION: RT_PREC_*
-    size_t sample_buf_cap = (size_t)32 << 30;  // RT_SAMPLE_BUF_MB: bound of one launch's trace output
-    unsigned* work = nullptr;           // pool / item schedules: work-block counter
+    size_t sample_buf_cap = (size_t)4000000000;  // RT_SAMPLE_BUF_MB: bound of the trace-output buffer (4 GB)
+    unsigned* work = nullptr;           // pool / item schedules: work-block counters (one per overlapped batch)
+    // Overlapped buffer batches (RT_BATCH_OVERLAP): batch k traces on tstream[k & 1] into half k & 1
+    // of the trace-output buffer while the caller's stream reduces batch k - 1
+    hipStream_t tstream[2] = {nullptr, nullptr};
+    hipEvent_t ev_in = nullptr, ev_tr[2] = {nullptr, nullptr}, ev_rd[2] = {nullptr, nullptr};
+    int opt_overlap = 1;
     double* acc_tmp = nullptr;          // running sums when a render takes several buffer batches
     size_t acc_tmp_cap = 0;
     int n_tlas_nodes = 0;
@@ -159,6 +164,7 @@ int rt_ctx_create(int device, rt_ctx** out)
     if (const char* e = std::getenv("RT_LDS_NODES")) c->opt_lds_nodes = std::atoi(e) != 0;
     if (const char* e = std::getenv("RT_HOIST")) c->opt_hoist = std::atoi(e) != 0;
     if (const char* e = std::getenv("RT_BOX_CAND")) c->opt_box_cand = std::atoi(e) != 0;
+    if (const char* e = std::getenv("RT_BATCH_OVERLAP")) c->opt_overlap = std::atoi(e) != 0;
     if (const char* e = std::getenv("RT_SCHEDULE")) c->opt_pool = std::min(3, std::max(0, std::atoi(e)));
     if (const char* e = std::getenv("RT_PRECISION")) c->opt_precision = std::atoi(e) == RT_PREC_F32 ? RT_PREC_F32 : RT_PREC_F64;
     if (const char* e = std::getenv("RT_BLOCK_CHUNKS")) c->block_chunks = std::min(64, std::max(1, std::atoi(e)));
@@ -167,15 +173,13 @@ int rt_ctx_create(int device, rt_ctx** out)
     if (const char* e = std::getenv("RT_SAMPLE_BUF_MB")) {
         c->sample_buf_cap = (size_t)std::max(1L, std::atol(e)) << 20;
     } else {
-        // sized for the device: 3/8 of its free HBM, at most 128 GiB (an MI355X: ~107 GB, so
-        // C4's 49.8 GB of per-sample radiance is one launch), at least 32 GiB where half the
-        // free memory allows it (allocated lazily, only as large as a render needs)
+        // 4 GB (round 3 took 3/8 of the free HBM, ~107 GB on an MI355X, so that
+        // C4's 49.8 GB of per-sample radiance was one launch): a render larger than that runs in
+        // buffer batches whose traces overlap (run_range), at most a quarter of the free memory
+        // on a smaller device (allocated lazily, only as large as a render needs)
         size_t fr = 0, tot = 0;
-        if (hipMemGetInfo(&fr, &tot) == hipSuccess && fr > 0) {
-            size_t cap = std::min(fr / 8 * 3, (size_t)128 << 30);
-            cap = std::max(cap, std::min((size_t)32 << 30, fr / 2));
-            c->sample_buf_cap = std::max(cap >> 20, (size_t)1) << 20;
-        }
+        if (hipMemGetInfo(&fr, &tot) == hipSuccess && fr > 0)
+            c->sample_buf_cap = std::max<size_t>(std::min(c->sample_buf_cap, fr / 4), (size_t)1 << 20);
     }
     {
         int v = 0;
@@ -192,7 +196,11 @@ int rt_ctx_create(int device, rt_ctx** out)
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_done, hipEventDisableTiming);
     if (e == hipSuccess) e = hipMalloc((void**)&c->counters, kCounters * sizeof(unsigned long long));
     if (e == hipSuccess) e = hipMalloc((void**)&c->params, kParamSlots * sizeof(rtk::KParams));
-    if (e == hipSuccess) e = hipMalloc((void**)&c->work, sizeof(unsigned));
+    if (e == hipSuccess) e = hipMalloc((void**)&c->work, 2 * sizeof(unsigned));
+    for (int i = 0; i < 2 && e == hipSuccess; ++i) e = hipStreamCreateWithFlags(&c->tstream[i], hipStreamNonBlocking);
+    for (int i = 0; i < 2 && e == hipSuccess; ++i) e = hipEventCreateWithFlags(&c->ev_tr[i], hipEventDisableTiming);
+    for (int i = 0; i < 2 && e == hipSuccess; ++i) e = hipEventCreateWithFlags(&c->ev_rd[i], hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_in, hipEventDisableTiming);
     if (e != hipSuccess) {
         rt_ctx_destroy(c);
         return hip_fail(e, "rt_ctx_create");
@@ -218,6 +226,13 @@ void rt_ctx_destroy(rt_ctx* c)
     for (auto& e : c->ev)
         if (e) (void)hipEventDestroy(e);
     if (c->ev_done) (void)hipEventDestroy(c->ev_done);
+    for (int i = 0; i < 2; ++i) {
+        if (c->tstream[i]) (void)hipStreamSynchronize(c->tstream[i]);
+        if (c->tstream[i]) (void)hipStreamDestroy(c->tstream[i]);
+        if (c->ev_tr[i]) (void)hipEventDestroy(c->ev_tr[i]);
+        if (c->ev_rd[i]) (void)hipEventDestroy(c->ev_rd[i]);
+    }
+    if (c->ev_in) (void)hipEventDestroy(c->ev_in);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -1304,6 +1319,8 @@ static int run_range(rt_ctx* c, const rt_camera* cam, const rt_render_params* p,
         // (empty) work so rt_last_stats resolves
         for (int i = 0; i < 3; ++i) HIP_TRY(hipEventRecord(c->ev[i], stream));
         c->stats.n_batches = 0;
+        c->stats.trace_buf_bytes = 0;
+        c->stats.overlapped = 0;
         c->stats.samples = 0;
         c->stats.n_items = 0;
         c->stats.n_chunks = 0;
@@ -1426,19 +1443,29 @@ static int run_range(rt_ctx* c, const rt_camera* cam, const rt_render_params* p,
     // halved on an out-of-memory retry for this render only: the context's bound stays, so a
     // later render on it uses the memory freed since
     size_t buf_cap = c->sample_buf_cap;
+    bool overlap = false;
     for (;;) {
-        // AUTO: the per-sample pool when its per-sample buffer takes at most 4 batches (C2:
-        // 11.5 GB in one, 101.6 vs 106.7 ms per frame for the item pool; C4: 49.8 GB in two,
-        // 1492 vs 1571 ms; profiles/r02d_*, r02e_*), else the item pool, whose partials take
-        // 1/chunk of those bytes and need no carried batches (C5: 1.6 TB of per-sample radiance)
+        // AUTO: the per-sample pool when its per-sample buffer takes at most 16 of the bound (C2
+        // 11.5 GB, C4 49.8 GB at 4 GB: overlapped batches; round 2 pool vs items, C2: 101.6 vs
+        // 106.7 ms per frame, C4: 1492 vs 1571 ms; profiles/r02d_*, r02e_*), else the item pool,
+        // whose partials take 1/chunk of those bytes (C5: 1.6 TB of per-sample radiance)
         o.pool = c->opt_pool != RT_SCHED_AUTO ? c->opt_pool
-                 : ((size_t)total * sample_bytes <= 4 * buf_cap ? RT_SCHED_POOL : RT_SCHED_ITEMS);
-        // Buffer batches: the trace output of one launch is bounded by sample_buf_cap. Per-sample
-        // pool: samples x pixels x 24 B; chunk and item schedules: chunks x pixels x 24 B, batches
-        // on chunk boundaries (relative to s_begin), so the partials add in one-launch order.
+                 : ((size_t)total * sample_bytes <= 16 * buf_cap ? RT_SCHED_POOL : RT_SCHED_ITEMS);
+        // Buffer batches: the trace output is bounded by sample_buf_cap. Per-sample pool: samples x
+        // pixels x 24 B; chunk and item schedules: chunks x pixels x 24 B, batches on chunk
+        // boundaries (relative to s_begin), so the partials add in one-launch order. A render that
+        // does not fit in one batch takes two buffers of half the bound: batch k traces into half
+        // k & 1 on stream tstream[k & 1] while the caller's stream reduces batch k - 1, so the
+        // next trace fills the CUs its predecessor's last waves leave (no tail per batch).
         per_sample = o.pool == RT_SCHED_POOL;
-        const long long fit = (long long)std::max<size_t>(1, buf_cap / (per_sample ? sample_bytes : px_bytes));
+        const size_t unit = per_sample ? sample_bytes : px_bytes;
+        long long fit = (long long)std::max<size_t>(1, buf_cap / unit);
         batch = std::min<long long>(total, per_sample ? fit : fit * chunk);
+        overlap = c->opt_overlap && batch < total && o.pool != RT_SCHED_CHUNKS;
+        if (overlap) {
+            fit = (long long)std::max<size_t>(1, buf_cap / 2 / unit);
+            batch = std::min<long long>(total, per_sample ? fit : fit * chunk);
+        }
         n_batches = (int)((total + batch - 1) / batch);
         acc = sink.acc;
         open = nullptr;
@@ -1460,7 +1487,8 @@ static int run_range(rt_ctx* c, const rt_camera* cam, const rt_render_params* p,
             own_acc = true;
         }
         const int max_chunks = (int)((batch + chunk - 1) / chunk);
-        const size_t need = per_sample ? (size_t)batch * sample_bytes : (size_t)max_chunks * px_bytes;
+        const size_t half = per_sample ? (size_t)batch * sample_bytes : (size_t)max_chunks * px_bytes;
+        const size_t need = overlap ? 2 * half : half;
         rc = grow(c, stream, c->partial, c->partial_cap, need, &oom);
         if (rc == RT_OK) break;
         if (!oom) return rc;
@@ -1485,6 +1513,14 @@ static int run_range(rt_ctx* c, const rt_camera* cam, const rt_render_params* p,
     int waves_per_simd = 0;
     o.waves_per_simd = &waves_per_simd;
     HIP_TRY(hipEventRecord(c->ev[0], stream));
+    // overlapped batches: both trace streams start after everything enqueued on `stream` so far
+    if (overlap) {
+        HIP_TRY(hipEventRecord(c->ev_in, stream));
+        for (int i = 0; i < 2; ++i) HIP_TRY(hipStreamWaitEvent(c->tstream[i], c->ev_in, 0));
+    }
+    const size_t half_elems = overlap ? (per_sample ? (size_t)batch * sample_bytes
+                                                    : (size_t)((batch + chunk - 1) / chunk) * px_bytes) / sizeof(double)
+                                      : 0;
     for (int bi = 0; bi < n_batches; ++bi) {
         const int b0 = s_begin + (int)(bi * batch);
         const int b1 = (int)std::min<long long>(s_end, b0 + batch);
@@ -1496,21 +1532,31 @@ static int run_range(rt_ctx* c, const rt_camera* cam, const rt_render_params* p,
             const unsigned n = o.pool == RT_SCHED_ITEMS ? (unsigned)K.n_chunks : (unsigned)(K.spp - K.sample_begin);
             K.n_work_blocks = (unsigned)K.tiles_x * (unsigned)K.tiles_y * ((n + g - 1) / std::max(g, 1u));
         }
+        // batch bi's buffer half, trace stream and work counter (one of each per overlapped batch)
+        const int h = overlap ? (bi & 1) : 0;
+        double* buf = c->partial + (size_t)h * half_elems;
+        hipStream_t ts = overlap ? c->tstream[h] : stream;
+        if (overlap && bi >= 2) HIP_TRY(hipStreamWaitEvent(ts, c->ev_rd[h], 0));   // batch bi - 2 reduced: half free
         rtk::KParams* dK = c->params + c->param_slot;
         c->param_slot = (c->param_slot + 1) % kParamSlots;
-        HIP_TRY(hipMemcpyAsync(dK, &K, sizeof K, hipMemcpyHostToDevice, stream));
-        HIP_TRY(rtk::launch_trace(S, K, dK, c->partial, c->counters, c->work, o, stream));
-        if (bi == n_batches - 1) HIP_TRY(hipEventRecord(c->ev[1], stream));
+        HIP_TRY(hipMemcpyAsync(dK, &K, sizeof K, hipMemcpyHostToDevice, ts));
+        HIP_TRY(rtk::launch_trace(S, K, dK, buf, c->counters, c->work + h, o, ts));
+        if (bi == n_batches - 1) HIP_TRY(hipEventRecord(c->ev[1], ts));
+        if (overlap) {   // reduce in batch order on `stream`, after this batch's trace
+            HIP_TRY(hipEventRecord(c->ev_tr[h], ts));
+            HIP_TRY(hipStreamWaitEvent(stream, c->ev_tr[h], 0));
+        }
         if (!per_sample) {
-            if (acc) HIP_TRY(rtk::launch_accumulate(c->partial, acc, n_px, K.n_chunks, stream));
-            else HIP_TRY(rtk::launch_reduce(c->partial, sink.out, sink.f64, n_px, K.n_chunks, sink.scale, stream));
+            if (acc) HIP_TRY(rtk::launch_accumulate(buf, acc, n_px, K.n_chunks, stream));
+            else HIP_TRY(rtk::launch_reduce(buf, sink.out, sink.f64, n_px, K.n_chunks, sink.scale, stream));
         } else if (!open) {
-            HIP_TRY(rtk::launch_reduce_samples(c->partial, sink.out, sink.f64, tiles, b1 - b0, chunk, sink.scale, stream));
+            HIP_TRY(rtk::launch_reduce_samples(buf, sink.out, sink.f64, tiles, b1 - b0, chunk, sink.scale, stream));
         } else {
-            HIP_TRY(rtk::launch_reduce_samples_carry(c->partial, acc, open, tiles, b1 - b0, chunk,
+            HIP_TRY(rtk::launch_reduce_samples_carry(buf, acc, open, tiles, b1 - b0, chunk,
                                                      (int)(((long long)b0 - s_begin) % chunk), bi == n_batches - 1,
                                                      stream));
         }
+        if (overlap) HIP_TRY(hipEventRecord(c->ev_rd[h], stream));
     }
     if (own_acc)  // resolve the running sums: 0.0 + sum, times scale, as one batch does
         HIP_TRY(rtk::launch_reduce(acc, sink.out, sink.f64, n_px, 1, sink.scale, stream));
@@ -1524,6 +1570,10 @@ static int run_range(rt_ctx* c, const rt_camera* cam, const rt_render_params* p,
     c->stats.precision = o.f32 ? RT_PREC_F32 : RT_PREC_F64;
     c->stats.waves_per_simd = waves_per_simd;
     c->stats.n_batches = n_batches;
+    c->stats.trace_buf_bytes = (int64_t)(overlap ? 2 * half_elems * sizeof(double)
+                                                 : (per_sample ? (size_t)batch * sample_bytes
+                                                               : (size_t)((batch + chunk - 1) / chunk) * px_bytes));
+    c->stats.overlapped = overlap ? 1 : 0;
     c->stats.samples = (uint64_t)n_px * (uint64_t)total;
     c->stats.n_chunks = (int32_t)((total + chunk - 1) / chunk);
     c->stats.n_items = (uint64_t)n_px * (uint64_t)c->stats.n_chunks;

@@ -160,9 +160,18 @@ __device__ __forceinline__ bool first_active_lane()
 // off 15.28 ms, 2 15.12, 4 15.07, 8 15.37, 4 after one try 15.22; images identical.
 #define RT_TRY_LEFT 4
 #endif
+#ifndef RT_TRY_ALL
+// the variants it applies to: the spheres ones (C2, C5) and the Cornell box's (C3 800x800x200
+// 46.00 -> 45.80 ms, profiles/r04d_ab_c3.log). The final scene's is 1-2 % slower with it (C4
+// 1920x1080x100 106.84 -> 109.04 ms, r04c_ab_c4.log; 107.83 -> 109.19, r04d_ab_c4.log): its
+// iterations are long, so a lane that sits one out loses more than the wave saves on tries
+#define RT_TRY_ALL 0
+#endif
 #ifndef RT_TRY_MIN
 #define RT_TRY_MIN 2
 #endif
+template <class C>
+constexpr bool TryLeft() { return RT_TRY_LEFT > 0 && (RT_TRY_ALL || C::F == FEAT_SET_SPHERES || C::F == FEAT_SET_RECTINST); }
 #ifndef RT_KILL_H
 // pool schedules: the hit record carried across the loop edge (RT_MERGED_DRAWS) is marked dead
 // before the next trace (trace_world writes only the fields its primitive kind has, so the
@@ -1211,7 +1220,11 @@ __device__ __forceinline__ bool traverse(const SceneDev& S, int root, const RayT
         while (cur != DONE) {
             if constexpr (PAUSE) {
                 // every lane still walking is here (the wave's outer-loop head): few enough left?
-                if (may_pause && ++leaves > RT_PAUSE_MIN && __popcll(__ballot(1)) <= RT_PAUSE) {
+                // RT_PAUSE_ONCE: a resumed walk is not suspended again; while one is still walking the
+                // wave walks on anyway, so then no lane is suspended
+                const bool eligible = !(RT_PAUSE_ONCE && resume);
+                if (may_pause && ++leaves > RT_PAUSE_MIN && __popcll(__ballot(1)) <= RT_PAUSE &&
+                    __ballot(!eligible) == 0) {
                     ws->cur = cur;
                     ws->sp = (int32_t)(sptr - &stack[sp0]);
                     ws->t_max = (double)t_max;
@@ -2451,7 +2464,7 @@ __global__ void __launch_bounds__(BlockThreads<C>(), min_waves<C>()) trace_pool(
             if (Pause<C>() && walk_paused) {
                 // the lane's walk resumes in the trace step (its ray kept in r)
             } else if (new_sample) {
-                if (RT_TRY_LEFT > 0 && cam_wait) {   // camera_begin ran: the jitter waits in r.dx / r.dy
+                if (TryLeft<C>() && cam_wait) {   // camera_begin ran: the jitter waits in r.dx / r.dy
                     u = r.dx;
                     v = r.dy;
                     cam_wait = false;
@@ -2476,18 +2489,18 @@ __global__ void __launch_bounds__(BlockThreads<C>(), min_waves<C>()) trace_pool(
             }
             R qx = (R)0, qy = (R)0, qz = (R)0, l2 = (R)1;
             const bool three = !new_sample;
-#if RT_TRY_LEFT > 0
-            bool accepted = !tries;
-            for (int n = 1;; ++n) {
-                if (!accepted) accepted = unit_try(st, (R)P.scale_m11, three, qx, qy, qz, l2);
-                const uint64_t rejecting = __ballot(!accepted);
-                if (rejecting == 0 || (n >= RT_TRY_MIN && __popcll(rejecting) <= RT_TRY_LEFT)) break;
+            if constexpr (TryLeft<C>()) {
+                bool accepted = !tries;
+                for (int n = 1;; ++n) {
+                    if (!accepted) accepted = unit_try(st, (R)P.scale_m11, three, qx, qy, qz, l2);
+                    const uint64_t rejecting = __ballot(!accepted);
+                    if (rejecting == 0 || (n >= RT_TRY_MIN && __popcll(rejecting) <= RT_TRY_LEFT)) break;
+                }
+                gen_wait = !accepted;
+            } else {
+                while (tries && !unit_try(st, (R)P.scale_m11, three, qx, qy, qz, l2)) {
+                }
             }
-            gen_wait = !accepted;
-#else
-            while (tries && !unit_try(st, (R)P.scale_m11, three, qx, qy, qz, l2)) {
-            }
-#endif
             if (Pause<C>() && walk_paused) {
             } else if (gen_wait) {   // (RT_TRY_LEFT) no trace this iteration; pending / new_sample stay set
                 go = false;

@@ -109,6 +109,9 @@ struct SceneDev {
 #ifndef RT_PAUSE_MIN
 #define RT_PAUSE_MIN 2
 #endif
+#ifndef RT_PAUSE_ONCE
+#define RT_PAUSE_ONCE 0
+#endif
 // A suspended top-level walk (RT_PAUSE, trace_device.hpp): 32 B per thread of the persistent
 // grid (KParams.walk_save, allocated by the context: walk_save_threads() slots)
 struct WalkSave {

@@ -125,7 +125,8 @@ class Stats(ctypes.Structure):
                 ("schedule", ctypes.c_int32), ("n_batches", ctypes.c_int32),
                 ("wave_leaf_steps", ctypes.c_uint64), ("camera_lanes", ctypes.c_uint64),
                 ("camera_steps", ctypes.c_uint64), ("shade_lanes", ctypes.c_uint64),
-                ("shade_steps", ctypes.c_uint64), ("precision", ctypes.c_int32), ("waves_per_simd", ctypes.c_int32)]
+                ("shade_steps", ctypes.c_uint64), ("precision", ctypes.c_int32), ("waves_per_simd", ctypes.c_int32),
+                ("trace_buf_bytes", ctypes.c_int64), ("overlapped", ctypes.c_int32), ("pad0", ctypes.c_int32)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

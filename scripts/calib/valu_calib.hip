@@ -36,7 +36,7 @@ enum Op { F64_FMA, F64_ADD, F64_MUL, F64_RCP, F64_SQRT, F32_FMA, F32_ADD, F32_RC
           PK_FMA_F32, MAX3_F32, MED3_F32, AND_B32, OR_B32, LSHL_B32, LSHR_B32, ALIGNBIT, BITOP3, MOV_B64,
           CMP_I32, LDEXP_F64, DIV_SCALE_F64, DIV_FMAS_F64, DIV_FIXUP_F64, MAD_U64_U32, LSHL_ADD_U64, LSHR_B64,
           MBCNT_LO, MUL_HI_U32, CVT_F32_F64, CMP_CLASS_F64, SUB_U32, FMAC_F64, MUL_F32, RSQ_F64, CNDMASK_E32, MIX,
-          KMIX_C2, KMIX_C4, N_OPS };
+          KMIX_C2, KMIX_C4, KMIX_C3, N_OPS };
 static const char* kNames[N_OPS] = {"f64_fma", "f64_add", "f64_mul", "f64_rcp", "f64_sqrt", "f32_fma", "f32_add",
                                     "f32_rcp", "i32_add", "i32_mul", "b32_xor", "cndmask", "mov_b32", "cndmask_vcc",
                                     "cmp_f64", "cmp_f32", "max_f64", "min_f32", "lshl_b64", "cvt_f64_u32",
@@ -45,7 +45,7 @@ static const char* kNames[N_OPS] = {"f64_fma", "f64_add", "f64_mul", "f64_rcp", 
                                     "div_scale_f64", "div_fmas_f64", "div_fixup_f64", "mad_u64_u32", "lshl_add_u64",
                                     "lshr_b64", "mbcnt_lo", "mul_hi_u32", "cvt_f32_f64", "cmp_class_f64", "sub_u32",
                                     "fmac_f64", "mul_f32", "rsq_f64", "cndmask_e32", "mix", "kmix_c2",
-                                    "kmix_c4"};
+                                    "kmix_c4", "kmix_c3"};
 
 // KMIX_*: a trace kernel's own VALU mix replayed (scripts/calib/gen_kmix.py writes the op
 // sequences from its PMC class shares and ISA): each accumulator runs the whole sequence
@@ -53,6 +53,9 @@ template <int... OPS>
 struct Seq {
 };
 #include "kmix_seq.h"
+#ifndef KMIX_C3_SEQ   // until gen_kmix.py has a C3 entry (kmix_seq.json then lists kmix_c3; pmc_r02.py reports only those)
+#define KMIX_C3_SEQ F64_FMA
+#endif
 
 // Each class as one exact instruction (inline asm): the compiler may not fold repeated
 // adds, pack f32 pairs into v_pk_* or strength-reduce, so the loop issues exactly
@@ -153,6 +156,7 @@ __device__ __forceinline__ void body(CALIB_ARGS)
 {
     if constexpr (OP == KMIX_C2) seq_all<NACC>(Seq<KMIX_C2_SEQ>{}, CALIB_PASS);
     else if constexpr (OP == KMIX_C4) seq_all<NACC>(Seq<KMIX_C4_SEQ>{}, CALIB_PASS);
+    else if constexpr (OP == KMIX_C3) seq_all<NACC>(Seq<KMIX_C3_SEQ>{}, CALIB_PASS);
     else each_acc<OP, NACC>(CALIB_PASS);
 }
 

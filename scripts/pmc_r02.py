@@ -48,7 +48,8 @@ CALIB_OPS = ["f64_fma", "f64_add", "f64_mul", "f64_rcp", "f64_sqrt", "f32_fma", 
              "lshl_b64", "cvt_f64_u32", "bfe_u32", "pk_fma_f32", "max3_f32", "med3_f32", "and_b32", "or_b32",
              "lshl_b32", "lshr_b32", "alignbit_b32", "bitop3_b32", "mov_b64", "cmp_i32", "ldexp_f64", "div_scale_f64",
              "div_fmas_f64", "div_fixup_f64", "mad_u64_u32", "lshl_add_u64", "lshr_b64", "mbcnt_lo", "mul_hi_u32",
-             "cvt_f32_f64", "cmp_class_f64", "sub_u32", "fmac_f64", "mul_f32", "rsq_f64", "cndmask_e32", "mix", "kmix_c2", "kmix_c4"]
+             "cvt_f32_f64", "cmp_class_f64", "sub_u32", "fmac_f64", "mul_f32", "rsq_f64", "cndmask_e32", "mix", "kmix_c2", "kmix_c4",
+             "kmix_c3"]
 # the MIX kernel's composition per accumulator-step (scripts/calib/valu_calib.hip): the model's
 # prediction for it (sum of calibrated costs) against its measured rate validates additivity
 MIX = {"f64_fma": 1, "f64_add": 1, "f32_fma": 2, "i32_add": 1, "b32_xor": 1, "mov_b32": 1, "cndmask": 1, "max3_f32": 1}
@@ -117,7 +118,7 @@ def calib(d, tag):
                 if k.startswith("SQ_INSTS_VALU_") and v > 0.5 * c.get("SQ_INSTS_VALU", 1e30)]
         sat = t.get("sat", {}).get("cycles_per_inst_per_simd")
         rates[op] = cyc if cyc is not None else sat
-        if c and not hits and op not in ("cndmask_vcc", "mix", "cndmask_e32", "kmix_c2", "kmix_c4"):   # pairs / mixes: not one op
+        if c and not hits and op not in ("cndmask_vcc", "mix", "cndmask_e32", "kmix_c2", "kmix_c4", "kmix_c3"):   # pairs / mixes: not one op
             unclassed.append(op)
         hit_map[op] = hits
         lines.append(f"| {op} | {cyc if cyc is None else round(cyc, 3)} | "

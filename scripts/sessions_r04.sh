@@ -33,6 +33,37 @@ c)
       "200:r04c_phases_c2_pause8:RT_LIB_PATH=$L/librtiow_exp_pause8.so python scripts/phases.py --scene 0 --width 1200 --height 800 --spp 16" \
       "200:r04c_phases_c2_pause16:RT_LIB_PATH=$L/librtiow_exp_pause16.so python scripts/phases.py --scene 0 --width 1200 --height 800 --spp 16"
     ;;
+d)
+    # round-4 session D: walk suspension refined (a resumed walk is not suspended again; later
+    # first suspension) on C2; the rejection cap on every variant (RT_TRY_ALL) on C3 / C4; VALU lane
+    # counters (SQ pass) of the default build and of the best suspension build on C2; GPU tests
+    export TMPDIR=/tmp
+    SQA="SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAVES SQ_INSTS_SALU SQ_INSTS_LDS GRBM_GUI_ACTIVE"
+    B="--steps 2 --warmup 1 --no-cpu-baseline --no-count"
+    scripts/gpu_session.sh \
+      "600:r04d_ab_c2:python scripts/ab_builds.py $L/librtiow_amd.so $L/librtiow_exp_p8once.so $L/librtiow_exp_p8once_m5.so $L/librtiow_exp_p16once.so $L/librtiow_exp_p8m6.so --scene 0 --width 1200 --height 800 --spp 100 --rounds 3" \
+      "600:r04d_ab_c3:python scripts/ab_builds.py $L/librtiow_amd.so $L/librtiow_exp_tryall.so --scene 5 --width 800 --height 800 --spp 200 --rounds 3" \
+      "600:r04d_ab_c4:python scripts/ab_builds.py $L/librtiow_amd.so $L/librtiow_exp_tryall.so --scene 7 --width 1920 --height 1080 --spp 100 --rounds 2" \
+      "200:r04d_phases_c2_p8once:RT_LIB_PATH=$L/librtiow_exp_p8once.so python scripts/phases.py --scene 0 --width 1200 --height 800 --spp 16" \
+      "300:r04d_sqa_default:timeout -s KILL 240 rocprofv3 --pmc $SQA --output-format csv -d gpurun_out/r04d_sqa_default -o sqa -- python3 bench.py $B" \
+      "300:r04d_sqa_p8once:RT_LIB_PATH=$L/librtiow_exp_p8once.so timeout -s KILL 240 rocprofv3 --pmc $SQA --output-format csv -d gpurun_out/r04d_sqa_p8once -o sqa -- python3 bench.py $B" \
+      "300:r04d_sqa_pause8:RT_LIB_PATH=$L/librtiow_exp_p8m6.so timeout -s KILL 240 rocprofv3 --pmc $SQA --output-format csv -d gpurun_out/r04d_sqa_p8m6 -o sqa -- python3 bench.py $B" \
+      tests
+    ;;
+e)
+    # round-4 session E: the bounded trace-output buffer (4 GB default, overlapped batches) — GPU tests;
+    # C2 and C4 bench lines at the default bound, at a 128 GB bound (one batch, round 3's behaviour)
+    # and at 4 GB without overlap (batches in order)
+    NB="--no-cpu-baseline --no-count"
+    scripts/gpu_session.sh tests \
+      "300:r04e_c2_bound4g:python bench.py --steps 10 --warmup 2 $NB" \
+      "300:r04e_c2_onebatch:RT_SAMPLE_BUF_MB=131072 python bench.py --steps 10 --warmup 2 $NB" \
+      "300:r04e_c2_serial:RT_BATCH_OVERLAP=0 python bench.py --steps 10 --warmup 2 $NB" \
+      "300:r04e_c2_bound4g_b:python bench.py --steps 10 --warmup 2 $NB" \
+      "400:r04e_c4_bound4g:python bench.py --config C4 --steps 3 --warmup 1 $NB" \
+      "400:r04e_c4_onebatch:RT_SAMPLE_BUF_MB=131072 python bench.py --config C4 --steps 3 --warmup 1 $NB" \
+      "400:r04e_c4_serial:RT_BATCH_OVERLAP=0 python bench.py --config C4 --steps 3 --warmup 1 $NB"
+    ;;
 *)
     echo "unknown session: $1" >&2; exit 2 ;;
 esac

@@ -400,3 +400,33 @@ def test_validate_rejects_a_chain_deeper_than_the_stack(rt):
     soa.nodes, soa.n_nodes, soa.tlas_root, soa.n_tlas_nodes = deep.ctypes.data, n, 0, n
     with pytest.raises(rt.RTError, match="UNSUPPORTED"):
         rt.validate_soa(soa)
+
+
+def test_ctypes_structs_match_the_c_header(rt, tmp_path):
+    """The Python binding's ctypes mirrors of the ABI's structs (rt_stats, rt_render_params,
+    rt_camera, rt_scene_preset, rt_world_info, rt_scene_soa) have the C header's size and field
+    offsets (compiled here with gcc against include/rt/rt_abi.h)."""
+    import subprocess
+    import ctypes
+    structs = {"rt_stats": rt.Stats, "rt_render_params": rt.RenderParams, "rt_camera": rt.Camera,
+               "rt_scene_preset": rt.ScenePreset, "rt_world_info": rt.WorldInfo, "rt_scene_soa": rt.SceneSoA}
+    src = ['#include <stdio.h>', '#include <stddef.h>', '#include "rt/rt_abi.h"', "int main(void) {"]
+    for cname, py in structs.items():
+        src.append(f'printf("{cname} size %zu\\n", sizeof({cname}));')
+        for f, _ in py._fields_:
+            if not f.startswith("pad"):
+                src.append(f'printf("{cname} {f} %zu\\n", offsetof({cname}, {f}));')
+    src.append("return 0; }")
+    c = tmp_path / "layout.c"
+    c.write_text("\n".join(src))
+    exe = tmp_path / "layout"
+    inc = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include")
+    subprocess.run(["gcc", "-I" + inc, str(c), "-o", str(exe)], check=True)
+    out = subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split("\n")
+    for line in out:
+        if not line:
+            continue
+        cname, field, val = line.split()
+        py = structs[cname]
+        got = ctypes.sizeof(py) if field == "size" else getattr(py, field).offset
+        assert got == int(val), (cname, field, got, int(val))

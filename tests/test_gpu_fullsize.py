@@ -279,3 +279,44 @@ def test_device_output_on_a_torch_stream_matches_host_render(rt, renderer):
     torch.cuda.synchronize()
     host = renderer.render(cam, rt.Renderer.params(W, H, spp, 50, bg, 1, out_format=rt.RT_OUT_F32))
     assert np.array_equal(frame.cpu().numpy(), host)
+
+
+@pytest.mark.parametrize("sched", ["POOL", "ITEMS"])
+def test_overlapped_buffer_batches_at_c2_size(rt, renderer, sched):
+    """the trace-output buffer is bounded (default 4 GB); a render larger than
+    the bound runs in batches traced on two streams into the bound's two halves while the
+    render's stream reduces the previous batch. The whole C2 frame at 48 spp under a 256 MB bound
+    (per-sample pool: 5 samples per half, 10 batches; item pool: chunks of 3, 5 chunks per half,
+    4 batches) equals the one-batch render bit for bit, and so does the same bound without
+    overlap (RT_BATCH_OVERLAP=0: 11 samples or chunks per batch, 5 and 2 batches)."""
+    import os
+    W, H, spp = 1200, 800, 48
+    world = rt.World(1).build_scene(0)
+    cam, bg = rt.scene_camera(0, W, H)
+    p = rt.Renderer.params(W, H, spp, 50, bg, 1, out_format=rt.RT_OUT_F64)
+    renderer.upload(world)
+    renderer.set_schedule(getattr(rt, "RT_SCHED_" + sched))
+    try:
+        one = renderer.render(cam, p)
+        assert renderer.stats().n_batches == 1
+    finally:
+        renderer.set_schedule(rt.RT_SCHED_AUTO)
+    for overlap in ("1", "0"):
+        os.environ["RT_SAMPLE_BUF_MB"] = "256"
+        os.environ["RT_BATCH_OVERLAP"] = overlap
+        try:
+            r = rt.Renderer(0)
+        finally:
+            os.environ.pop("RT_SAMPLE_BUF_MB")
+            os.environ.pop("RT_BATCH_OVERLAP")
+        try:
+            r.set_schedule(getattr(rt, "RT_SCHED_" + sched))
+            r.upload(world)
+            img = r.render(cam, p)
+            st = r.stats()
+        finally:
+            r.close()
+        expect = {("POOL", "1"): 10, ("POOL", "0"): 5, ("ITEMS", "1"): 4, ("ITEMS", "0"): 2}[(sched, overlap)]
+        assert st.n_batches == expect, (overlap, st.n_batches)
+        same = img == one
+        assert same.all(), f"overlap {overlap}: {int((~same.all(axis=2)).sum())} px differ"

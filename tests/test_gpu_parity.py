@@ -404,9 +404,17 @@ def test_schedules_render_identically(rt, scene_id, W, H, spp):
     finally:
         os.environ.pop("RT_BLOCK_CHUNKS")
         os.environ.pop("RT_BLOCK_SAMPLES")
+    os.environ["RT_SAMPLE_BUF_MB"] = "1"
+    os.environ["RT_BATCH_OVERLAP"] = "0"
+    try:
+        serial = rt.Renderer(0)                      # buffer batches one after another in one buffer
+    finally:
+        os.environ.pop("RT_SAMPLE_BUF_MB")
+        os.environ.pop("RT_BATCH_OVERLAP")
     r = rt.Renderer(0)
     runs = [(r, rt.RT_SCHED_CHUNKS), (r, rt.RT_SCHED_POOL), (r, rt.RT_SCHED_ITEMS), (small, rt.RT_SCHED_POOL),
-            (small, rt.RT_SCHED_ITEMS), (grouped, rt.RT_SCHED_ITEMS), (r, rt.RT_SCHED_AUTO)]
+            (small, rt.RT_SCHED_ITEMS), (grouped, rt.RT_SCHED_ITEMS), (r, rt.RT_SCHED_AUTO),
+            (serial, rt.RT_SCHED_POOL), (serial, rt.RT_SCHED_ITEMS)]
     for rr, sched in runs:
         rr.set_schedule(sched)
         rr.upload(world)
@@ -421,8 +429,12 @@ def test_schedules_render_identically(rt, scene_id, W, H, spp):
     assert r.stats().n_batches == 1
     small.set_schedule(rt.RT_SCHED_POOL)
     batched = small.render(cam, q)
-    assert small.stats().n_batches == 3              # 14 + 14 + 12 samples; chunks of 3 straddle batches
+    assert small.stats().n_batches == 6              # 5 x 7 + 5 samples in the bound's halves; chunks of 3 straddle batches
     assert np.array_equal(batched, one)
+    serial.set_schedule(rt.RT_SCHED_POOL)
+    assert np.array_equal(serial.render(cam, q), one)
+    assert serial.stats().n_batches == 3             # 14 + 14 + 12 samples in the whole bound, in order
+    serial.close()
     acc = small.accumulator(q)                       # an accumulator batch straddling buffer batches
     acc.add(cam, q, 21)
     acc.add(cam, q, 19)
