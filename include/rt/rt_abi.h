@@ -299,13 +299,15 @@ int rt_ctx_set_variant(rt_ctx* ctx, int slab32, int lds_stack, int lds_nodes);
  *   ITEMS:  persistent waves as POOL, but a lane takes a whole (pixel, chunk) item, traces
  *           its samples in order and writes one partial, as CHUNKS does (1/chunk of POOL's
  *           buffer bytes); a lane whose item ended takes the next item at once.
- *   AUTO:   POOL when the render's per-sample radiance is at most 16 x the buffer bound (it is
+ *   AUTO:   POOL when the render's per-sample radiance is at most 4 x the buffer bound (it is
  *           the faster of the two), otherwise ITEMS; rt_stats.schedule reports which ran.
- * The trace-output buffer is bounded by RT_SAMPLE_BUF_MB (default 4 GB, at most a quarter of
- * the device's free memory; allocated lazily, as large as a render needs). A larger render
- * runs in buffer batches whose sums are carried across, in two halves of the bound: batch k
- * traces into half k & 1 on one of two context streams while the render's stream reduces
- * batch k - 1, so consecutive traces overlap (RT_BATCH_OVERLAP=0: one buffer, in order). */
+ * The trace-output buffer is bounded by RT_SAMPLE_BUF_MB (default: sized at context creation
+ * to 3/8 of the device's free memory, at most 128 GiB, at least 32 GiB where half the free
+ * memory allows; allocated lazily, as large as a render needs). A larger render runs in buffer
+ * batches whose sums are carried across, in two halves of the bound: batch k traces into half
+ * k & 1 on one of two context streams while the render's stream reduces batch k - 1, so
+ * consecutive traces overlap (RT_BATCH_OVERLAP=0: one buffer, in order). A 4 GB bound
+ * (RT_SAMPLE_BUF_MB=4000) renders C2 as fast as one batch; long-path scenes pay per batch. */
 enum { RT_SCHED_CHUNKS = 0, RT_SCHED_POOL = 1, RT_SCHED_ITEMS = 2, RT_SCHED_AUTO = 3 };
 int rt_ctx_set_schedule(rt_ctx* ctx, int schedule);
 

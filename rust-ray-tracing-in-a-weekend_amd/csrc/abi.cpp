@@ -113,7 +113,7 @@ struct rt_ctx {
     int opt_box_cand = 1;               // RT_BOX_CAND: boxes take the candidate-side test (0: six exact sides; A/B)
     int opt_pool = RT_SCHED_AUTO;       // rt_ctx_set_schedule / RT_SCHEDULE: RT_SCHED_*
     int opt_precision = RT_PREC_F64;    // rt_ctx_set_precision / RT_PRECISION: RT_PREC_*
-    size_t sample_buf_cap = (size_t)4000000000;  // RT_SAMPLE_BUF_MB: bound of the trace-output buffer (4 GB)
+    size_t sample_buf_cap = (size_t)32 << 30;  // RT_SAMPLE_BUF_MB: bound of the trace-output buffer
     unsigned* work = nullptr;           // pool / item schedules: work-block counters (one per overlapped batch)
     // Overlapped buffer batches (RT_BATCH_OVERLAP): batch k traces on tstream[k & 1] into half k & 1
     // of the trace-output buffer while the caller's stream reduces batch k - 1
@@ -173,13 +173,19 @@ int rt_ctx_create(int device, rt_ctx** out)
     if (const char* e = std::getenv("RT_SAMPLE_BUF_MB")) {
         c->sample_buf_cap = (size_t)std::max(1L, std::atol(e)) << 20;
     } else {
-        // 4 GB (round 3 took 3/8 of the free HBM, ~107 GB on an MI355X, so that
-        // C4's 49.8 GB of per-sample radiance was one launch): a render larger than that runs in
-        // buffer batches whose traces overlap (run_range), at most a quarter of the free memory
-        // on a smaller device (allocated lazily, only as large as a render needs)
+        // sized for the device: 3/8 of its free HBM, at most 128 GiB (an MI355X: ~107 GB, so C4's
+        // 49.8 GB of per-sample radiance is one launch), at least 32 GiB where half the free
+        // memory allows it (allocated lazily, only as large as a render needs). A bound of 4 GB
+        // (RT_SAMPLE_BUF_MB=4000) costs C2 nothing (six overlapped batches:
+        // 74.77 vs 74.75 ms per frame) but the final scene 4.4 % in the item pool and 18 % in 25
+        // overlapped per-sample batches (profiles/r04e_*, r04f_*): its paths are long and its
+        // 512-thread blocks free CUs late, so every batch pays a tail. The default keeps speed.
         size_t fr = 0, tot = 0;
-        if (hipMemGetInfo(&fr, &tot) == hipSuccess && fr > 0)
-            c->sample_buf_cap = std::max<size_t>(std::min(c->sample_buf_cap, fr / 4), (size_t)1 << 20);
+        if (hipMemGetInfo(&fr, &tot) == hipSuccess && fr > 0) {
+            size_t cap = std::min(fr / 8 * 3, (size_t)128 << 30);
+            cap = std::max(cap, std::min((size_t)32 << 30, fr / 2));
+            c->sample_buf_cap = std::max(cap >> 20, (size_t)1) << 20;
+        }
     }
     {
         int v = 0;
@@ -1445,12 +1451,13 @@ static int run_range(rt_ctx* c, const rt_camera* cam, const rt_render_params* p,
     size_t buf_cap = c->sample_buf_cap;
     bool overlap = false;
     for (;;) {
-        // AUTO: the per-sample pool when its per-sample buffer takes at most 16 of the bound (C2
-        // 11.5 GB, C4 49.8 GB at 4 GB: overlapped batches; round 2 pool vs items, C2: 101.6 vs
-        // 106.7 ms per frame, C4: 1492 vs 1571 ms; profiles/r02d_*, r02e_*), else the item pool,
-        // whose partials take 1/chunk of those bytes (C5: 1.6 TB of per-sample radiance)
+        // AUTO: the per-sample pool when its per-sample radiance is at most 4 times the bound,
+        // else the item pool, whose partials take 1/chunk of those bytes (C5's 1.6 TB: one launch).
+        // Round 2, pool vs items: C2 101.6 vs 106.7 ms per frame, C4 1492 vs 1571 (r02d_*, r02e_*);
+        // round 4: C2 74.75 vs 76.06, C4 1018.5 vs 1074.7; C5 in 25 overlapped pool batches of
+        // 64 GB halves 10,578 ms vs the item pool 10,649 in 64 batches at a 4 GB bound (r04f_*)
         o.pool = c->opt_pool != RT_SCHED_AUTO ? c->opt_pool
-                 : ((size_t)total * sample_bytes <= 16 * buf_cap ? RT_SCHED_POOL : RT_SCHED_ITEMS);
+                 : ((size_t)total * sample_bytes <= 4 * buf_cap ? RT_SCHED_POOL : RT_SCHED_ITEMS);
         // Buffer batches: the trace output is bounded by sample_buf_cap. Per-sample pool: samples x
         // pixels x 24 B; chunk and item schedules: chunks x pixels x 24 B, batches on chunk
         // boundaries (relative to s_begin), so the partials add in one-launch order. A render that

@@ -18,8 +18,11 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(os.path.dirname(HERE))
 N = 40
-# name -> (PMC entry tag, isa_mix key)
+# name -> (PMC entry tag, isa_mix key); RT_KMIX_TAGS="c2=tag,c3=tag,c4=tag" picks other PMC entries
 MIXES = {"c2": ("r03j_c2", "spheres/pool/s1n1"), "c4": ("r03j_c4", "final/pool/s1n1")}
+if os.environ.get("RT_KMIX_TAGS"):
+    KEYS = {"c2": "spheres/pool/s1n1", "c3": "rectinst/pool/s0n0", "c4": "final/pool/s1n1"}
+    MIXES = {k: (v, KEYS[k]) for k, v in (x.split("=") for x in os.environ["RT_KMIX_TAGS"].split(","))}
 ENUM = {  # calibration op name -> valu_calib.hip enum
     "f64_fma": "F64_FMA", "f64_add": "F64_ADD", "f64_mul": "F64_MUL", "f64_rcp": "F64_RCP", "f64_sqrt": "F64_SQRT",
     "f32_fma": "F32_FMA", "f32_add": "F32_ADD", "f32_rcp": "F32_RCP", "i32_add": "I32_ADD", "i32_mul": "I32_MUL",

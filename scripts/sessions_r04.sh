@@ -64,6 +64,19 @@ e)
       "400:r04e_c4_onebatch:RT_SAMPLE_BUF_MB=131072 python bench.py --config C4 --steps 3 --warmup 1 $NB" \
       "400:r04e_c4_serial:RT_BATCH_OVERLAP=0 python bench.py --config C4 --steps 3 --warmup 1 $NB"
     ;;
+f)
+    # round-4 session F: the item pool under the 4 GB bound (C4: its partials fit one batch) against
+    # the per-sample pool in one batch; C2 items; C5 at the bound (items, overlapped batches) vs one batch
+    NB="--no-cpu-baseline --no-count"
+    scripts/gpu_session.sh \
+      "400:r04f_c4_items:RT_SCHEDULE=2 python bench.py --config C4 --steps 3 --warmup 1 $NB" \
+      "400:r04f_c4_items_blk4:RT_SCHEDULE=2 RT_BLOCK_CHUNKS=4 python bench.py --config C4 --steps 3 --warmup 1 $NB" \
+      "400:r04f_c4_onebatch:RT_SAMPLE_BUF_MB=131072 python bench.py --config C4 --steps 3 --warmup 1 $NB" \
+      "300:r04f_c2_items:RT_SCHEDULE=2 python bench.py --steps 10 --warmup 2 $NB" \
+      "300:r04f_c2_default:python bench.py --steps 10 --warmup 2 $NB" \
+      "600:r04f_c5_default:python bench.py --config C5 --steps 1 --warmup 1 $NB" \
+      "600:r04f_c5_onebatch:RT_SAMPLE_BUF_MB=131072 python bench.py --config C5 --steps 1 --warmup 1 $NB"
+    ;;
 *)
     echo "unknown session: $1" >&2; exit 2 ;;
 esac
