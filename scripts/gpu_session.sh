@@ -10,7 +10,7 @@
 #   bench            bench.py with no arguments (the driver's bench line)
 #   bench_c1..c5     bench.py --config Cn (f64)
 #   f32_c2..c4       bench.py --config Cn --precision f32
-#   prof_c2..c5      scripts/profile_r02.sh on that config (kernel trace + PMC passes)
+#   prof_c1..c5      scripts/profile_r02.sh on that config (kernel trace + PMC passes)
 #   calib            scripts/calib_r02.sh (VALU issue-rate calibration through rocprofv3)
 # env: PREFIX (log-name prefix, e.g. r03a_). Round 3 sessions: scripts/sessions_r03.sh
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -30,6 +30,7 @@ for s in "$@"; do
     f32_c2) specs+=("300:${P}f32_c2:python bench.py --steps 10 --warmup 2 --precision f32 $NB") ;;
     f32_c3) specs+=("300:${P}f32_c3:python bench.py --config C3 --steps 5 --warmup 1 --precision f32 $NB") ;;
     f32_c4) specs+=("300:${P}f32_c4:python bench.py --config C4 --steps 2 --warmup 1 --precision f32 $NB") ;;
+    prof_c1) specs+=("500:${P}prof_c1:PROF_DIR=${P}prof_c1 BENCH_ARGS='--config C1 --steps 2 --warmup 1 $NB' scripts/profile_r02.sh") ;;
     prof_c2) specs+=("700:${P}prof_c2:PROF_DIR=${P}prof_c2 scripts/profile_r02.sh") ;;
     prof_c3) specs+=("700:${P}prof_c3:PROF_DIR=${P}prof_c3 BENCH_ARGS='--config C3 --steps 1 --warmup 0 $NB' scripts/profile_r02.sh") ;;
     prof_c4) specs+=("900:${P}prof_c4:PROF_DIR=${P}prof_c4 BENCH_ARGS='--config C4 --steps 1 --warmup 0 $NB' scripts/profile_r02.sh") ;;

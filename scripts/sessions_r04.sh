@@ -77,6 +77,19 @@ f)
       "600:r04f_c5_default:python bench.py --config C5 --steps 1 --warmup 1 $NB" \
       "600:r04f_c5_onebatch:RT_SAMPLE_BUF_MB=131072 python bench.py --config C5 --steps 1 --warmup 1 $NB"
     ;;
+g)
+    # round-4 session G (final build): GPU tests, smoke, rocprofv3 kernel trace + PMC passes of C1-C5
+    PREFIX=r04g_ scripts/gpu_session.sh tests smoke prof_c1 prof_c2 prof_c3 prof_c4 prof_c5
+    ;;
+h)
+    # round-4 session H: VALU calibration incl. the kmix replays of C2 / C3 / C4 (gen_kmix.py on r04g's PMC)
+    scripts/gpu_session.sh "600:r04h_calib:scripts/calib_r02.sh r04h_calib"
+    ;;
+i)
+    # round-4 session I: the final bench lines (roofline from r04g's PMC and r04h's calibration), C1-C5 f64,
+    # the default bench line the driver runs, f32 lines of C2-C4
+    PREFIX=r04i_ scripts/gpu_session.sh bench bench_c1 bench_c2 bench_c3 bench_c4 bench_c5 f32_c2 f32_c3 f32_c4
+    ;;
 *)
     echo "unknown session: $1" >&2; exit 2 ;;
 esac
