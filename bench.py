@@ -11,7 +11,7 @@ inside the timed region. The scene is built and uploaded before timing.
 Prints ONE JSON line (rank 0). Besides the contract fields it carries
   roofline:     the binding resource, VALU issue: the issue cycles the launch's VALU
                 instruction mix needs (per-class counts from a rocprofv3 PMC pass of THIS
-                build and workload, profiles/pmc_r02.json keyed by the source hash; cycles
+                build and workload, profiles/pmc.json keyed by the source hash; cycles
                 per instruction class calibrated on the box, scripts/calib) against the
                 SIMD-cycles of the live-timed kernel; `traffic` = DRAM bytes per launch from
                 the same PMC pass; the DRAM fraction and the SURVEY §8(d) algorithmic
@@ -37,7 +37,7 @@ sys.path.insert(0, REPO)
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 N_SIMDS = 1024                 # 256 CUs x 4 SIMDs
-PMC_JSON = os.path.join(REPO, "profiles", "pmc_r02.json")
+PMC_JSON = os.path.join(REPO, "profiles", "pmc.json")
 ROW_BLOCK = 1                  # multi-GPU shards: single rows round-robin over the ranks
 
 
@@ -384,7 +384,7 @@ def main():
                             **{k: round(v["ratio"], 4) for k, v in (calib.get("kmix") or {}).items()}},
             "pmc_tag": pmc.get("tag"), "pmc_kernel_ms": pmc.get("kernel_ms"), "clock_ghz": clk})
     else:
-        roofline["note"] = "no PMC pass of this build (source hash) and workload in profiles/pmc_r02.json"
+        roofline["note"] = "no PMC pass of this build (source hash) and workload in profiles/pmc.json"
 
     # ---- SURVEY §8(d) algorithmic bytes per sample (LDS/L1/L2-served; not an HBM figure)
     count_spp = min(args.count_spp, spp)

@@ -4,7 +4,7 @@
 The roofline prices the kernel's VALU instructions class by class at the issue cost each
 class has alone at saturation (scripts/calib). Whether those costs add up for a *mix* is what
 this checks, on the kernel's own mix: the dynamic class shares come from the kernel's PMC
-pass (profiles/pmc_r02.json entry), the instructions inside each class from its ISA
+pass (profiles/pmc.json entry), the instructions inside each class from its ISA
 (profiles/isa_mix.json, loop depth >= 1), and a sequence of N calibration ops with those
 shares (largest remainder, spread out by a stride schedule) becomes the KMIX_<name> kernel of
 valu_calib.hip. Its measured cycles per instruction against the sum of its ops' calibrated
@@ -93,7 +93,7 @@ def sequence(shares, n=N):
 
 
 def main():
-    pmc = json.load(open(os.path.join(REPO, "profiles", "pmc_r02.json")))
+    pmc = json.load(open(os.path.join(REPO, "profiles", "pmc.json")))
     isa_doc = json.load(open(os.path.join(REPO, "profiles", "isa_mix.json")))
     out, meta = [], {}
     for name, (tag, key) in MIXES.items():

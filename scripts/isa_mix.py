@@ -30,7 +30,7 @@ import sys
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 OUT = os.path.join(REPO, "profiles", "isa_mix.json")
-PMC_JSON = os.path.join(REPO, "profiles", "pmc_r02.json")
+PMC_JSON = os.path.join(REPO, "profiles", "pmc.json")
 FEAT = {"spheres": 0, "rectinst": 35, "media": 103, "final": 287, "all": 4095}
 
 # mnemonic (regex on the opcode, without the _e32/_e64 suffix) -> calibration op

@@ -2,10 +2,10 @@
 """Summarise rocprofv3 runs into profiles/ (round 2 format).
 
   python scripts/pmc_r02.py calib <gpurun_out dir> <tag>
-      scripts/calib_r02.sh output -> the VALU calibration block of profiles/pmc_r02.json
+      scripts/calib_r02.sh output -> the VALU calibration block of profiles/pmc.json
       and profiles/<tag>_valu_calib.md
   python scripts/pmc_r02.py bench <gpurun_out dir> <tag> <scene,W,H,spp,depth,n_gpus,schedule> [note]
-      scripts/profile_r02.sh output -> one entry of profiles/pmc_r02.json (keyed by the
+      scripts/profile_r02.sh output -> one entry of profiles/pmc.json (keyed by the
       source hash of this tree and the workload), profiles/<tag>_pmc.md and
       profiles/<tag>_kernel_stats.csv
 
@@ -28,7 +28,7 @@ import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
-OUT_JSON = os.path.join(REPO, "profiles", "pmc_r02.json")
+OUT_JSON = os.path.join(REPO, "profiles", "pmc.json")
 N_SIMDS = 1024
 
 # trace-kernel VALU classes (rocprofv3 counter) -> the calibration kernel measuring its rate

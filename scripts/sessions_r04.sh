@@ -79,7 +79,10 @@ f)
     ;;
 g)
     # round-4 session G (final build): GPU tests, smoke, rocprofv3 kernel trace + PMC passes of C1-C5
-    PREFIX=r04g_ scripts/gpu_session.sh tests smoke prof_c1 prof_c2 prof_c3 prof_c4 prof_c5
+    PREFIX=r04g_ scripts/gpu_session.sh tests smoke prof_c1 prof_c2 prof_c3 prof_c4
+    ;;
+g2)
+    PREFIX=r04g_ scripts/gpu_session.sh prof_c5
     ;;
 h)
     # round-4 session H: VALU calibration incl. the kmix replays of C2 / C3 / C4 (gen_kmix.py on r04g's PMC)
