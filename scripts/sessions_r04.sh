@@ -93,6 +93,25 @@ i)
     # the default bench line the driver runs, f32 lines of C2-C4
     PREFIX=r04i_ scripts/gpu_session.sh bench bench_c1 bench_c2 bench_c3 bench_c4 bench_c5 f32_c2 f32_c3 f32_c4
     ;;
+j)
+    # round-4 session J: walk suspension with the parked state in LDS (12 B per lane after the stack; built
+    # from a copy of csrc, scripts/sessions_r04.sh j) against the default on C2; phases and SQ pass of K = 8
+    export TMPDIR=/tmp
+    SQA="SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAVES SQ_INSTS_SALU SQ_INSTS_LDS GRBM_GUI_ACTIVE"
+    B="--steps 2 --warmup 1 --no-cpu-baseline --no-count"
+    scripts/gpu_session.sh \
+      "600:r04j_ab_c2:python scripts/ab_builds.py $L/librtiow_amd.so $L/librtiow_exp_ldsp8.so $L/librtiow_exp_ldsp8once.so $L/librtiow_exp_ldsp16once.so $L/librtiow_exp_ldsp4.so --scene 0 --width 1200 --height 800 --spp 100 --rounds 3" \
+      "200:r04j_phases_c2_ldsp8:RT_LIB_PATH=$L/librtiow_exp_ldsp8.so python scripts/phases.py --scene 0 --width 1200 --height 800 --spp 16" \
+      "300:r04j_sqa_ldsp8:RT_LIB_PATH=$L/librtiow_exp_ldsp8.so timeout -s KILL 240 rocprofv3 --pmc $SQA --output-format csv -d gpurun_out/r04j_sqa_ldsp8 -o sqa -- python3 bench.py $B"
+    ;;
+jg)
+    # sessions J and G in one call (boxes are scarce): the LDS suspension A/B, then the final-build passes
+    "$0" j && "$0" g
+    ;;
+g2h)
+    # sessions G2 (C5's passes) and H (calibration with the r04 kmix replays) in one call
+    "$0" g2 && "$0" h
+    ;;
 *)
     echo "unknown session: $1" >&2; exit 2 ;;
 esac
