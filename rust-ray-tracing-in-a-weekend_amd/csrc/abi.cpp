@@ -806,6 +806,10 @@ int rt_ctx_upload_soa(rt_ctx* c, const rt_scene_soa* s)
         } else if (p.kind == RT_PRIM_MOVING_SPHERE) {
             p.a = (p.p[8] == 0.0 && p.p[9] == 1.0) ? 1 : 0;
             if (!p.a) general_shutter = true;
+        } else if (p.kind == RT_PRIM_INSTANCE) {
+            // b = 1: the instance's child is a BVH (the kernel defers the first such walk of a
+            // cast, RT_DEFER_INST); a single child primitive is tested where the walk meets it
+            p.b = s->instances[p.a].child_kind == RT_CHILD_BVH ? 1 : 0;
         } else if (p.kind == RT_PRIM_BOX && p.b != 0 && c->opt_box_cand) {
             // The kernel's candidate-side test (box_candidates) takes thin slabs around each face
             // plane as wide as the padding of the box's f32 bounds on the outer side: w = twice
@@ -1035,11 +1039,12 @@ int rt_ctx_upload_soa(rt_ctx* c, const rt_scene_soa* s)
     // sentinel (traverse): the 66-entry scratch stack always fits
     c->S.blas_base = tlas_depth + 1;
     c->S.stack_entries = tlas_depth + 1 + (blas_depth > 0 ? blas_depth + 1 : 0);
-    // A BLAS walk nests in the top-level walk only for a cast's second instance (the first is
-    // deferred until the top-level walk ends, then walks from entry 0: RT_DEFER_INST) or for a
-    // medium whose boundary is an instance. A scene whose top level holds one instance and no
-    // such medium (the final scene) needs the larger of the two walks, not their sum: 13
-    // entries instead of 25 per lane, 12 KB less LDS per block.
+    // A BLAS walk nests in the top-level walk only for a cast's second instance over a BVH (the
+    // first is deferred until the top-level walk ends, then walks from entry 0: RT_DEFER_INST),
+    // an instance over a medium, or a medium whose boundary is an instance. A scene whose top
+    // level holds one instance over a BVH and none of the others (the final scene) needs the
+    // larger of the two walks, not their sum: 13 entries instead of 25 per lane, 12 KB less LDS
+    // per block.
     if (RT_DEFER_INST && blas_depth > 0) {
         int n_inst = 0;
         bool inst_boundary = false;
@@ -1055,7 +1060,11 @@ int rt_ctx_upload_soa(rt_ctx* c, const rt_scene_soa* s)
             const int code = ~ref;
             for (int j = code >> 5; j < (code >> 5) + (code & 31); ++j) {
                 const rt_prim& p = s->prims[s->prim_refs[j]];
-                if (p.kind == RT_PRIM_INSTANCE) ++n_inst;
+                if (p.kind == RT_PRIM_INSTANCE) {   // an instance that may walk a BLAS
+                    const rt_instance& in = s->instances[p.a];
+                    if (in.child_kind == RT_CHILD_BVH) ++n_inst;
+                    else if (s->prims[in.child].kind == RT_PRIM_MEDIUM) inst_boundary = true;   // never deferred
+                }
                 if (p.kind == RT_PRIM_MEDIUM && s->prims[p.a].kind == RT_PRIM_INSTANCE) inst_boundary = true;
             }
         }

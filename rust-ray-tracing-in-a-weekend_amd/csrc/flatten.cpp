@@ -182,6 +182,28 @@ struct Builder {
         return b;
     }
 
+    // The world box of a primitive under ops: a static sphere's centre mapped to world space
+    // (the same per-op formulas) +- r (tighter than its rotated object box); others box_through.
+    AABB world_box(const Ops& ops, int hid) const
+    {
+        const HNode& h = w.nodes[hid];
+        if (h.kind != HKind::Sphere) return box_through(ops, box_of(hid));
+        double x = h.c0.x, y = h.c0.y, z = h.c0.z;
+        for (int i = ops.n - 1; i >= 0; --i) {
+            if (ops.kind[i] == RT_OP_TRANSLATE) {
+                x += ops.op[i][0]; y += ops.op[i][1]; z += ops.op[i][2];
+                continue;
+            }
+            const double sn = ops.op[i][0], cs = ops.op[i][1];
+            const double nx = cs * x + sn * z, nz = -sn * x + cs * z;
+            x = nx;
+            z = nz;
+        }
+        // the mapped centre is off by a few ulps of the coordinates; to_f32_box pads by far more
+        const double r = std::fabs(h.radius);
+        return AABB{v3(x - r, y - r, z - r), v3(x + r, y + r, z + r)};
+    }
+
     Item item_box(int prim, const AABB& b)
     {
         Item it;
@@ -288,7 +310,13 @@ struct Builder {
         }
         std::vector<int> simple, complex;
         collect_split(child, simple, complex);
-        if (!simple.empty()) {
+        if (!simple.empty() && dissolve_inst && accel == RT_ACCEL_SAH) {
+            // Dissolved: one instance per leaf of the BVH, each with the whole chain, in the
+            // enclosing hierarchy under its world box — the walk then crosses the cluster's
+            // boxes in the same node loop as everything else instead of in a nested walk.
+            for (int hid : simple)
+                items.push_back(item_box(make_instance(ops, RT_CHILD_PRIM, lower_simple_in(ops, hid)), world_box(ops, hid)));
+        } else if (!simple.empty()) {
             AABB b = box_of(simple[0]);
             for (int hid : simple) {
                 const AABB bi = box_of(hid);
@@ -558,6 +586,9 @@ struct Builder {
     }
 
     int blas_depth = 0;   // max over instance BLASes
+    // RT_INST_DISSOLVE=1: an instance over a BVH of simple primitives becomes one instance per
+    // primitive in the enclosing SAH hierarchy (lower_instance)
+    bool dissolve_inst = false;
 
     // LINEAR / MEDIAN: the list in order. Runs of primitives become <=31-prim leaves, a
     // subtree stays a child; node k = (segment k, node k+1), both boxes unbounded, so the
@@ -644,6 +675,7 @@ int flatten(World& w, int accel, std::string& err)
     if (const char* e = std::getenv("RT_BVH_MAXLEAF")) bld.max_leaf = std::min(31, std::max(2, std::atoi(e)));
     if (const char* e = std::getenv("RT_BVH_LEAFN")) bld.force_leaf = std::min(31, std::max(1, std::atoi(e)));
     if (const char* e = std::getenv("RT_BVH_ROOTLEAF")) bld.root_leaf = std::min(31, std::max(0, std::atoi(e)));
+    if (const char* e = std::getenv("RT_INST_DISSOLVE")) bld.dissolve_inst = std::atoi(e) != 0;
     std::vector<Item> top;
     for (int id : w.hittables) {  // M for the f32-slab padding (see to_f32_box)
         AABB b;

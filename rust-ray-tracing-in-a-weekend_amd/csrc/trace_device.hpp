@@ -368,8 +368,9 @@ constexpr bool BoxRcp()
     return RT_BOX_RCP && !C::F32 && (RT_BOX_RCP_ALL || (C::F & (FEAT_NOISE | FEAT_IMAGE)) != 0);
 }
 
-// spheres: the scene has spheres (wave-uniform); otherwise no root division needs 1/a
-template <class C>
+// spheres: the scene has spheres (wave-uniform); otherwise no root division needs 1/a.
+// SLABS = false: no node-slab terms (a ray that meets one primitive, e.g. an instance's child)
+template <class C, bool SLABS = true>
 __device__ __forceinline__ void finish_ray(RayT<typename C::Real>& r, bool spheres)
 {
     r.a = r.dx * r.dx + r.dy * r.dy + r.dz * r.dz;
@@ -379,7 +380,8 @@ __device__ __forceinline__ void finish_ray(RayT<typename C::Real>& r, bool spher
         r.yy = rcp_for_div(r.dy);
         r.yz = rcp_for_div(r.dz);
     }
-    if constexpr (C::S32) {
+    if constexpr (!SLABS) {
+    } else if constexpr (C::S32) {
         r.sx.x = f32_inv_dir(r.dx);
         r.sy.x = f32_inv_dir(r.dy);
         r.sz.x = f32_inv_dir(r.dz);
@@ -1317,17 +1319,19 @@ __device__ bool instance_t(const SceneDev& S, const rt_instance& in, const RayT<
 {
     RayT<R> r = ray;
     instance_ray(in, r);
-    finish_ray<C>(r, S.has_spheres != 0);
     if (in.child_kind == RT_CHILD_PRIM) {
         if constexpr ((C::F & FEAT_INST_MEDIUM) != 0) {
             const rt_prim& cp = S.prims[in.child];
             if (cp.kind == RT_PRIM_MEDIUM) {   // the medium in object space (its boundary walks at sp0)
+                finish_ray<C>(r, S.has_spheres != 0);
                 if (!medium_t<InstMedC<C>>(S, cp, r, t_min, t_max, ref.t, stack, sp0, key, cnt)) return false;
                 ref.sub = in.child;
                 ref.side = 0;
                 return true;
             }
         }
+        // one primitive: no node-slab terms (the candidate-side box test reads them)
+        finish_ray<C, BoxCand<InstC<C>>()>(r, S.has_spheres != 0);
         int side = 0;
         if (!simple_t<InstC<C>>(S.prims[in.child], r, t_min, t_max, ref.t, side, cnt, (C::F & FEAT_SHUTTER) != 0)) return false;
         ref.sub = in.child;
@@ -1337,6 +1341,7 @@ __device__ bool instance_t(const SceneDev& S, const rt_instance& in, const RayT<
     // an instance over a BVH: a nested walk (its state on top of the TLAS walk's is what
     // set the Cornell variants' register count, 157 vs 125 VGPRs: 3 vs 4 waves per SIMD)
     if constexpr ((C::F & FEAT_INST_BLAS) == 0) return false;
+    finish_ray<C>(r, S.has_spheres != 0);
     HitRefT<R> inner;
     const rt_prim* const blas_prims = S.leaf_prims + in.pad;   // the BLAS's leaf codes count from its first slot
     if (!traverse<C>(S, in.child, r, t_min, t_max, inner, stack, sp0, cnt,
@@ -1506,7 +1511,7 @@ __device__ bool trace_world(const SceneDev& S, const RayT<R>& r, HitT<R>& h, Sta
         if constexpr ((C::F & FEAT_INST) != 0)
             if (p.kind == RT_PRIM_INSTANCE) {
                 if constexpr (DeferInst<C>()) {
-                    if (pend < 0) {
+                    if (pend < 0 && p.b != 0) {   // (b: its child is a BVH, upload)
                         pend = slot;
                         return false;
                     }

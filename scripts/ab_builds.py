@@ -7,6 +7,8 @@ one after another, `--rounds` times round-robin, so clock drift spreads over all
 Prints per-build median kernel ms and whether the f64 test image equals the first build's.
 
 usage: python scripts/ab_builds.py lib/a.so lib/b.so [--scene 0 --width 1200 --height 800 --spp 500]
+       (a build given as lib/a.so@RT_X=1,RT_Y=2 runs with those environment variables: host-side
+       options such as the flattener's RT_INST_DISSOLVE)
 """
 import argparse
 import hashlib
@@ -59,7 +61,9 @@ def main():
     imgs = {}
     for _ in range(a.rounds):
         for lib in a.libs:
-            env = dict(os.environ, RT_LIB_PATH=os.path.abspath(os.path.join(REPO, lib)))
+            path, _, extra = lib.partition("@")   # lib.so@NAME=V,NAME=V: that build under those env vars
+            env = dict(os.environ, RT_LIB_PATH=os.path.abspath(os.path.join(REPO, path)))
+            env.update(kv.split("=", 1) for kv in extra.split(",") if kv)
             out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=600)
             if out.returncode != 0:
                 print(f"{lib}: child failed ({out.returncode})\n{out.stderr[-2000:]}")

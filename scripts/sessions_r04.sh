@@ -108,6 +108,16 @@ jg)
     # sessions J and G in one call (boxes are scarce): the LDS suspension A/B, then the final-build passes
     "$0" j && "$0" g
     ;;
+k)
+    # round-4 session K: the final scene's instanced cluster dissolved into the top-level tree
+    # (RT_INST_DISSOLVE=1, flatten.cpp) — nesting tests incl. bit identity with the nested walk; A/B on C4
+    # against the deferred BLAS walk; phase timers of C4 dissolved
+    scripts/gpu_session.sh \
+      "400:r04k_gpu_tests_nesting:python -u -m pytest tests/test_gpu_nesting.py -x -v --timeout 120 --timeout-method thread" \
+      "600:r04k_ab_c4:python scripts/ab_builds.py $L/librtiow_amd.so $L/librtiow_amd.so@RT_INST_DISSOLVE=1 --scene 7 --width 1920 --height 1080 --spp 100 --rounds 3" \
+      "200:r04k_phases_c4_dissolve:RT_INST_DISSOLVE=1 python scripts/phases.py --scene 7 --width 1920 --height 1080 --spp 8" \
+      "200:r04k_phases_c4:python scripts/phases.py --scene 7 --width 1920 --height 1080 --spp 8"
+    ;;
 g2h)
     # sessions G2 (C5's passes) and H (calibration with the r04 kmix replays) in one call
     "$0" g2 && "$0" h

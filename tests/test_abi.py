@@ -60,6 +60,22 @@ def test_flatten_all_scenes(rt, scene_id):
         assert soa.n_media == 2 and soa.n_instances == 2
 
 
+def test_final_scene_dissolved_cluster_flattens(rt, monkeypatch):
+    """RT_INST_DISSOLVE=1 (flatten.cpp lower_instance): the final scene's Translate(RotateY(BVH
+    of 1000 spheres)) becomes 1000 one-sphere instances in the top-level SAH tree — no BLAS left,
+    every instance reachable from the TLAS once, and rt_scene_validate accepts the tables."""
+    monkeypatch.setenv("RT_INST_DISSOLVE", "1")
+    w = rt.World(1).build_scene(7)
+    soa = rt.SceneSoA.from_buffer_copy(w.flatten())
+    prims, refs, nodes, inst = soa_tables(soa)
+    assert soa.n_instances == 1000 and soa.blas_depth == 0
+    assert np.all(inst["kind"] == 0) and np.all(inst["n_ops"] == 2)
+    kinds = np.frombuffer(prims.tobytes(), "<i4").reshape(-1, 24)[:, 0]
+    walk = reachable(soa.tlas_root, refs, nodes)
+    assert sorted(int(kinds[i]) == 6 for i in walk).count(True) == 1000 and len(set(walk)) == len(walk)
+    assert rt.validate_soa(soa)[1] == 0
+
+
 NODE_DT = np.dtype([("lo0", "<f4", 3), ("hi0", "<f4", 3), ("lo1", "<f4", 3), ("hi1", "<f4", 3),
                     ("child", "<i4", 2), ("pad", "<i4", 2)])
 

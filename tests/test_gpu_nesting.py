@@ -241,3 +241,68 @@ def test_box_world_on_final_variant_matches_oracle(rt, look_from, look_at):
     ref = tw.oracle.render(_cam24(cam), bg, W, H, spp)
     assert float(ref.max()) > 0.0
     assert_parity(imgs[0], ref, "box world")
+
+
+def _upload_render(rt, renderer, world, cam, p, dissolve):
+    """Upload (flatten) with RT_INST_DISSOLVE set or not, render, and return the image."""
+    import os
+    os.environ["RT_INST_DISSOLVE"] = "1" if dissolve else "0"
+    try:
+        renderer.upload(world)
+    finally:
+        del os.environ["RT_INST_DISSOLVE"]
+    return renderer.render(cam, p)
+
+
+@pytest.mark.parametrize("world", ["instanced", "shared", "nested"])
+def test_dissolved_instances_match_nested_walks_and_oracle(rt, renderer, world):
+    """RT_INST_DISSOLVE=1 (flatten.cpp lower_instance): an instance over a BVH of simple
+    primitives becomes one instance per primitive in the enclosing SAH tree, tested where the
+    top-level walk meets it instead of in a deferred nested walk. Closest hit does not depend on
+    the hierarchy: the image equals the nested walk's bit for bit, and the oracle's to the bar."""
+    if world == "instanced":
+        tw = ob.TwinWorld(rt)
+        white = tw.lambertian(tw.solid(0.73, 0.73, 0.73))
+        glass = tw.dielectric(1.5)
+        ids = [tw.sphere(glass if i % 4 == 0 else white, (0.5 * i - 1.0, 0.3 + 0.1 * (i % 3), 0.2 * (i % 2)), 0.25)
+               for i in range(12)]
+        tw.push(tw.translate(tw.rotate_y(tw.bvh(ids), 25.0), (0.2, 0.0, -0.5)))
+        tw.push(tw.sphere(white, (0.0, -100.0, 0.0), 100.0))
+        view = ((5.0, 2.0, 6.0), (0.0, 0.5, 0.0))
+    elif world == "shared":
+        tw = ob.TwinWorld(rt)
+        white = tw.lambertian(tw.solid(0.73, 0.73, 0.73))
+        balls = tw.bvh([tw.sphere(white, (0.3 * (i % 8) - 1.0, 0.25 + 0.3 * (i // 8), 0.1 * (i % 2)), 0.14)
+                        for i in range(40)])
+        tw.push(tw.translate(tw.rotate_y(balls, 30.0), (-0.8, 0.0, 0.0)))
+        tw.push(tw.translate(balls, (1.0, 0.0, -0.6)))
+        tw.push(tw.sphere(white, (0.0, -100.0, 0.0), 100.0))
+        view = ((3.0, 2.0, 6.0), (0.0, 0.6, 0.0))
+    else:
+        tw = _nested_world(rt)
+        view = ((7.0, 4.0, 9.0), (0.0, 0.7, 0.0))
+    W, H, spp, bg = 48, 32, 6, (0.7, 0.8, 1.0)
+    cam = rt.camera_new(view[0], view[1], (0.0, 1.0, 0.0), 40.0, W / H, 0.1, 10.0, 0.0, 1.0)
+    p = rt.Renderer.params(W, H, spp, 50, bg, 1, out_format=rt.RT_OUT_F64)
+    nested = _upload_render(rt, renderer, tw.product, cam, p, False)
+    dissolved = _upload_render(rt, renderer, tw.product, cam, p, True)
+    same = nested == dissolved
+    assert same.all(), f"{int((~same.all(axis=2)).sum())} px differ"
+    ref = tw.oracle.render(_cam24(cam), bg, W, H, spp)
+    assert_parity(dissolved, ref, f"dissolved instances ({world})")
+
+
+def test_final_scene_dissolved_cluster_is_bit_identical(rt, renderer):
+    """The final scene (C4's world) with its 1000-sphere cluster dissolved into the top level:
+    the same image bit for bit as the deferred BLAS walk, on the final-scene variant."""
+    W, H, spp = 96, 54, 4
+    cam, bg = rt.scene_camera(7, W, H)
+    p = rt.Renderer.params(W, H, spp, 50, bg, 1, out_format=rt.RT_OUT_F64)
+    world = rt.World(1).build_scene(7)
+    nested = _upload_render(rt, renderer, world, cam, p, False)
+    n_nested = renderer.stats().variant_features
+    dissolved = _upload_render(rt, renderer, world, cam, p, True)
+    assert n_nested == renderer.stats().variant_features == 287
+    same = nested == dissolved
+    assert same.all(), f"{int((~same.all(axis=2)).sum())} px differ"
+    assert float(nested.max()) > 0.0
