@@ -35,6 +35,7 @@ struct Item {
     int ref;
     double lo[3], hi[3];
     double c[3];
+    double cost = 1.0;   // SAH intersection cost relative to the others (a dissolved instance's own)
 };
 
 struct Builder {
@@ -314,8 +315,10 @@ struct Builder {
             // Dissolved: one instance per leaf of the BVH, each with the whole chain, in the
             // enclosing hierarchy under its world box — the walk then crosses the cluster's
             // boxes in the same node loop as everything else instead of in a nested walk.
-            for (int hid : simple)
+            for (int hid : simple) {
                 items.push_back(item_box(make_instance(ops, RT_CHILD_PRIM, lower_simple_in(ops, hid)), world_box(ops, hid)));
+                items.back().cost = dissolve_cost;
+            }
         } else if (!simple.empty()) {
             AABB b = box_of(simple[0]);
             for (int hid : simple) {
@@ -530,26 +533,34 @@ struct Builder {
         // full-sweep SAH over the three axes (centroid order; ties by prim index)
         double best_cost = INFINITY;
         int best_axis = -1, best_split = -1;
-        std::vector<double> right_area(n);
+        // (costs: sums of the items' own; with every item at 1 these are the counts i and n - i)
+        std::vector<double> right_area(n), right_cost(n);
+        double total_cost = 0.0;
+        for (int i = b; i < e; ++i) total_cost += items[i].cost;
         for (int axis = 0; axis < 3; ++axis) {
             std::sort(items.begin() + b, items.begin() + e, [axis](const Item& x, const Item& y) {
                 return x.c[axis] < y.c[axis] || (x.c[axis] == y.c[axis] && x.prim < y.prim);
             });
             double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+            double rcost = 0.0;
             for (int i = n - 1; i >= 1; --i) {
                 for (int a = 0; a < 3; ++a) {
                     lo[a] = std::min(lo[a], items[b + i].lo[a]);
                     hi[a] = std::max(hi[a], items[b + i].hi[a]);
                 }
+                rcost += items[b + i].cost;
                 right_area[i] = area(lo, hi);
+                right_cost[i] = rcost;
             }
             for (int a = 0; a < 3; ++a) { lo[a] = INFINITY; hi[a] = -INFINITY; }
+            double lcost = 0.0;
             for (int i = 1; i < n; ++i) {
                 for (int a = 0; a < 3; ++a) {
                     lo[a] = std::min(lo[a], items[b + i - 1].lo[a]);
                     hi[a] = std::max(hi[a], items[b + i - 1].hi[a]);
                 }
-                double cost = c_trav + c_isect * (area(lo, hi) * i + right_area[i] * (n - i)) / std::max(parea, 1e-300);
+                lcost += items[b + i - 1].cost;
+                double cost = c_trav + c_isect * (area(lo, hi) * lcost + right_area[i] * right_cost[i]) / std::max(parea, 1e-300);
                 if (cost < best_cost) {
                     best_cost = cost;
                     best_axis = axis;
@@ -557,7 +568,7 @@ struct Builder {
                 }
             }
         }
-        double leaf_cost = c_isect * n;
+        double leaf_cost = c_isect * total_cost;
         if (n <= max_leaf && leaf_cost <= best_cost) return make_leaf(items, b, e);
         if (best_axis < 0) best_axis = 0, best_split = n / 2;
         return split_at(items, b, e, best_axis, best_split, depth);
@@ -589,6 +600,7 @@ struct Builder {
     // RT_INST_DISSOLVE=1: an instance over a BVH of simple primitives becomes one instance per
     // primitive in the enclosing SAH hierarchy (lower_instance)
     bool dissolve_inst = false;
+    double dissolve_cost = 1.0;   // RT_DISSOLVE_CI: a dissolved instance's SAH cost (the others' is 1)
 
     // LINEAR / MEDIAN: the list in order. Runs of primitives become <=31-prim leaves, a
     // subtree stays a child; node k = (segment k, node k+1), both boxes unbounded, so the
@@ -676,6 +688,7 @@ int flatten(World& w, int accel, std::string& err)
     if (const char* e = std::getenv("RT_BVH_LEAFN")) bld.force_leaf = std::min(31, std::max(1, std::atoi(e)));
     if (const char* e = std::getenv("RT_BVH_ROOTLEAF")) bld.root_leaf = std::min(31, std::max(0, std::atoi(e)));
     if (const char* e = std::getenv("RT_INST_DISSOLVE")) bld.dissolve_inst = std::atoi(e) != 0;
+    if (const char* e = std::getenv("RT_DISSOLVE_CI")) bld.dissolve_cost = std::max(0.01, std::atof(e));
     std::vector<Item> top;
     for (int id : w.hittables) {  // M for the f32-slab padding (see to_f32_box)
         AABB b;

@@ -114,9 +114,20 @@ k)
     # against the deferred BLAS walk; phase timers of C4 dissolved
     scripts/gpu_session.sh \
       "400:r04k_gpu_tests_nesting:python -u -m pytest tests/test_gpu_nesting.py -x -v --timeout 120 --timeout-method thread" \
-      "600:r04k_ab_c4:python scripts/ab_builds.py $L/librtiow_amd.so $L/librtiow_amd.so@RT_INST_DISSOLVE=1 --scene 7 --width 1920 --height 1080 --spp 100 --rounds 3" \
-      "200:r04k_phases_c4_dissolve:RT_INST_DISSOLVE=1 python scripts/phases.py --scene 7 --width 1920 --height 1080 --spp 8" \
+      "600:r04k_ab_c4:python scripts/ab_builds.py $L/librtiow_amd.so $L/librtiow_amd.so@RT_INST_DISSOLVE=1 $L/librtiow_amd.so@RT_INST_DISSOLVE=1,RT_DISSOLVE_CI=0.35 $L/librtiow_amd.so@RT_INST_DISSOLVE=1,RT_DISSOLVE_CI=0.25 --scene 7 --width 1920 --height 1080 --spp 100 --rounds 3" \
+      "200:r04k_phases_c4_dissolve:RT_INST_DISSOLVE=1 RT_DISSOLVE_CI=0.35 python scripts/phases.py --scene 7 --width 1920 --height 1080 --spp 8" \
       "200:r04k_phases_c4:python scripts/phases.py --scene 7 --width 1920 --height 1080 --spp 8"
+    ;;
+k2)
+    # round-4 session K2: the single-primitive instance rays without node-slab set-up (and the BVH-only
+    # deferral) against the build before it (librtiow_exp_prev.so, commit 7d4bc81) on C3 and C4
+    scripts/gpu_session.sh \
+      "600:r04k2_ab_c3:python scripts/ab_builds.py $L/librtiow_exp_prev.so $L/librtiow_amd.so --scene 5 --width 800 --height 800 --spp 200 --rounds 3" \
+      "600:r04k2_ab_c4:python scripts/ab_builds.py $L/librtiow_exp_prev.so $L/librtiow_amd.so --scene 7 --width 1920 --height 1080 --spp 100 --rounds 2"
+    ;;
+kk)
+    # sessions K and K2 in one call
+    "$0" k && "$0" k2
     ;;
 g2h)
     # sessions G2 (C5's passes) and H (calibration with the r04 kmix replays) in one call
