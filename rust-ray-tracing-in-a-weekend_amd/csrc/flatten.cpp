@@ -598,7 +598,12 @@ struct Builder {
 
     int blas_depth = 0;   // max over instance BLASes
     // RT_INST_DISSOLVE=1: an instance over a BVH of simple primitives becomes one instance per
-    // primitive in the enclosing SAH hierarchy (lower_instance)
+    // primitive in the enclosing SAH hierarchy (lower_instance). Same image; measured slower and
+    // off: C4 1920x1080x100 107.25 -> 131.29 ms (RT_DISSOLVE_CI 0.35 / 0.25, TLAS back under the
+    // LDS node cap: 149.1 / 158.9 ms; profiles/r04k_ab_c4.log). The instanced sphere tests then
+    // run in the top-level leaf loop beside box and medium tests (leaf-loop lane occupancy 0.330
+    // -> 0.237, leaf steps per wave iteration 11.7 -> 17.7, r04k_phases_c4*.log), where the
+    // deferred walk ran them together for the lanes that need them.
     bool dissolve_inst = false;
     double dissolve_cost = 1.0;   // RT_DISSOLVE_CI: a dissolved instance's SAH cost (the others' is 1)
 

@@ -129,6 +129,19 @@ kk)
     # sessions K and K2 in one call
     "$0" k && "$0" k2
     ;;
+m)
+    # round-4 session M (final build, after K): GPU tests, smoke, rocprofv3 kernel trace + PMC passes of C1-C4
+    PREFIX=r04m_ scripts/gpu_session.sh tests smoke prof_c1 prof_c2 prof_c3 prof_c4
+    ;;
+m2)
+    # session M2: C5's passes, then the VALU calibration with the kmix replays of M's PMC (gen_kmix.py)
+    PREFIX=r04m_ scripts/gpu_session.sh prof_c5 && scripts/gpu_session.sh "600:r04m_calib:scripts/calib_r02.sh r04m_calib"
+    ;;
+n)
+    # session N: the final bench lines (roofline from M's PMC and M2's calibration), C1-C5 f64, the
+    # default line the driver runs, f32 lines of C2-C4
+    PREFIX=r04n_ scripts/gpu_session.sh bench bench_c1 bench_c2 bench_c3 bench_c4 bench_c5 f32_c2 f32_c3 f32_c4
+    ;;
 g2h)
     # sessions G2 (C5's passes) and H (calibration with the r04 kmix replays) in one call
     "$0" g2 && "$0" h
