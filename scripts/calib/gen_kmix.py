@@ -97,7 +97,7 @@ def main():
     isa_doc = json.load(open(os.path.join(REPO, "profiles", "isa_mix.json")))
     out, meta = [], {}
     for name, (tag, key) in MIXES.items():
-        entry = next(e for e in pmc["entries"] if e["tag"] == tag)
+        entry = [e for e in pmc["entries"] if e["tag"] == tag][-1]   # the latest entry of that tag
         isa = isa_doc[entry["src_hash"]][key]
         seq, count = sequence(op_shares(entry, isa))
         meta["kmix_" + name] = {"pmc_entry": tag, "isa_mix": key, "src_hash": entry["src_hash"], "ops": count}
