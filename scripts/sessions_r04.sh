@@ -142,6 +142,25 @@ n)
     # default line the driver runs, f32 lines of C2-C4
     PREFIX=r04n_ scripts/gpu_session.sh bench bench_c1 bench_c2 bench_c3 bench_c4 bench_c5 f32_c2 f32_c3 f32_c4
     ;;
+q)
+    # session Q: one-leaf top levels (Cornell scenes) walked as a wave-uniform slot loop (scalar records and
+    # kind dispatch; librtiow_exp_uleaf.so, built from a csrc copy with RT_UNIFORM_LEAF) against HEAD on C3
+    # and Cornell smoke; C3's phase timers at HEAD
+    scripts/gpu_session.sh \
+      "600:r04q_ab_c3:python scripts/ab_builds.py $L/librtiow_amd.so $L/librtiow_exp_uleaf.so --scene 5 --width 800 --height 800 --spp 200 --rounds 3" \
+      "600:r04q_ab_smoke:python scripts/ab_builds.py $L/librtiow_amd.so $L/librtiow_exp_uleaf.so --scene 6 --width 800 --height 800 --spp 200 --rounds 3" \
+      "200:r04q_phases_c3:python scripts/phases.py --scene 5 --width 800 --height 800 --spp 16"
+    ;;
+r)
+    # session R: the uniform one-leaf walk (uleaf), + wave-uniform kind / instance index (uleaf2), + one finisher
+    # for top-level and instanced primitives and for rects / box sides (uleaf3), each from a csrc copy, against
+    # HEAD on C3 and Cornell smoke; uleaf3 on C4 (its box-side finisher change)
+    E="$L/librtiow_exp_uleaf.so $L/librtiow_exp_uleaf2.so $L/librtiow_exp_uleaf3.so"
+    scripts/gpu_session.sh \
+      "600:r04r_ab_c3:python scripts/ab_builds.py $L/librtiow_amd.so $E --scene 5 --width 800 --height 800 --spp 200 --rounds 3" \
+      "600:r04r_ab_smoke:python scripts/ab_builds.py $L/librtiow_amd.so $E --scene 6 --width 800 --height 800 --spp 200 --rounds 3" \
+      "600:r04r_ab_c4:python scripts/ab_builds.py $L/librtiow_amd.so $L/librtiow_exp_uleaf3.so --scene 7 --width 1920 --height 1080 --spp 100 --rounds 2"
+    ;;
 g2h)
     # sessions G2 (C5's passes) and H (calibration with the r04 kmix replays) in one call
     "$0" g2 && "$0" h
