@@ -1488,6 +1488,19 @@ constexpr bool DeferInst() { return RT_DEFER_INST && (C::F & FEAT_INST_BLAS) != 
 template <class C>
 constexpr bool Pause() { return RT_PAUSE > 0 && C::F == FEAT_SET_SPHERES && !C::F32; }
 
+// The variants that walk a one-leaf top level (the Cornell scenes: S.tlas_root is a leaf code) as
+// a plain loop over its slots: no stack, no node loop, a loop count the same in every lane (scalar
+// control instead of exec-masked loops). Measured: C3 800x800x200 45.71 -> 41.88 ms, Cornell smoke
+// 57.80 -> 52.50, same images; making the kind and instance index wave-uniform on top (scalar
+// dispatch) was slower (42.51 / 52.80; profiles/r04q_ab_*.log, r04r_ab_*.log). Not in the variants
+// with nested BLAS walks (the final and all-features ones keep their register allocation); the
+// spheres variants take the pre-leaf path.
+#ifndef RT_UNIFORM_LEAF
+#define RT_UNIFORM_LEAF 1
+#endif
+template <class C>
+constexpr bool UniformLeaf() { return RT_UNIFORM_LEAF && (C::F & FEAT_INST_BLAS) == 0 && !PreLeaf<C>(); }
+
 // HitRecord of the closest primitive. Pause<C>(): with ws, the top-level walk may be
 // suspended (*paused: no record; the lane resumes it with resume = true next iteration).
 template <class C, class R = typename C::Real>
@@ -1575,7 +1588,24 @@ __device__ bool trace_world(const SceneDev& S, const RayT<R>& r, HitT<R>& h, Sta
         }
     } else {
         RT_STAMP(cnt.t_pre, tp);
-        hit = traverse<C, true>(S, S.tlas_root, r, t_min, (R)RT_INF, best, stack, 0, cnt, leaf);
+        if (UniformLeaf<C>() && S.tlas_root < 0 && S.tlas_root != RT_DONE) {   // (wave-uniform)
+            const int code = ~S.tlas_root;
+            R t_max = (R)RT_INF;
+            hit = false;
+            uint64_t tl = 0;
+            if (C::COUNT) tl = __builtin_amdgcn_s_memtime();
+            for (int slot = code >> 5, end = (code >> 5) + (code & 31); slot < end; ++slot) {
+                if (C::COUNT && first_active_lane()) cnt.wave_leaves++;
+                if (leaf(slot, t_max, best)) {   // traverse's do_leaf, in slot order
+                    best.prim = slot;
+                    t_max = best.t;
+                    hit = true;
+                }
+            }
+            RT_STAMP(cnt.t_leaves, tl);
+        } else {
+            hit = traverse<C, true>(S, S.tlas_root, r, t_min, (R)RT_INF, best, stack, 0, cnt, leaf);
+        }
     }
     if (C::COUNT) tp = __builtin_amdgcn_s_memtime();   // the walk stamped its own phases
     if constexpr (DeferInst<C>()) {
