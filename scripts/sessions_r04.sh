@@ -161,6 +161,18 @@ r)
       "600:r04r_ab_smoke:python scripts/ab_builds.py $L/librtiow_amd.so $E --scene 6 --width 800 --height 800 --spp 200 --rounds 3" \
       "600:r04r_ab_c4:python scripts/ab_builds.py $L/librtiow_amd.so $L/librtiow_exp_uleaf3.so --scene 7 --width 1920 --height 1080 --spp 100 --rounds 2"
     ;;
+s)
+    # round-4 session S (final build, after the one-leaf loop): GPU tests, smoke, PMC passes of C1-C4
+    PREFIX=r04s_ scripts/gpu_session.sh tests smoke prof_c1 prof_c2 prof_c3 prof_c4
+    ;;
+s2)
+    # session S2: C5's passes, then the VALU calibration with the kmix replays of S's PMC
+    PREFIX=r04s_ scripts/gpu_session.sh prof_c5 && scripts/gpu_session.sh "600:r04s_calib:scripts/calib_r02.sh r04s_calib"
+    ;;
+t)
+    # session T: the final bench lines of this build (C1-C5 f64, the default line, f32 C2-C4)
+    PREFIX=r04t_ scripts/gpu_session.sh bench bench_c1 bench_c2 bench_c3 bench_c4 bench_c5 f32_c2 f32_c3 f32_c4
+    ;;
 g2h)
     # sessions G2 (C5's passes) and H (calibration with the r04 kmix replays) in one call
     "$0" g2 && "$0" h
