@@ -173,6 +173,18 @@ t)
     # session T: the final bench lines of this build (C1-C5 f64, the default line, f32 C2-C4)
     PREFIX=r04t_ scripts/gpu_session.sh bench bench_c1 bench_c2 bench_c3 bench_c4 bench_c5 f32_c2 f32_c3 f32_c4
     ;;
+st)
+    # sessions S and T in one call (boxes are scarce): tests, smoke, PMC passes of C1-C5, their pmc.json
+    # entries written on the box (scripts/pmc_r02.py, the same step the builder runs after merging), then
+    # the bench lines, which read them
+    PREFIX=r04s_ scripts/gpu_session.sh tests smoke prof_c1 prof_c2 prof_c3 prof_c4 prof_c5 && \
+    python scripts/pmc_r02.py bench r04s_prof_c1 r04_final_c1 0,1200,800,10,8,1,1 "round-4 final build (r04s)" && \
+    python scripts/pmc_r02.py bench r04s_prof_c2 r04_final_c2 0,1200,800,500,50,1,1 "round-4 final build (r04s)" && \
+    python scripts/pmc_r02.py bench r04s_prof_c3 r04_final_c3 5,800,800,1000,50,1,1 "round-4 final build (r04s)" && \
+    python scripts/pmc_r02.py bench r04s_prof_c4 r04_final_c4 7,1920,1080,1000,50,1,1 "round-4 final build (r04s)" && \
+    python scripts/pmc_r02.py bench r04s_prof_c5 r04_final_c5 0,4096,4096,4096,50,1,2 "round-4 final build (r04s)" && \
+    "$0" t
+    ;;
 g2h)
     # sessions G2 (C5's passes) and H (calibration with the r04 kmix replays) in one call
     "$0" g2 && "$0" h
