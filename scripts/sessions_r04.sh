@@ -185,6 +185,14 @@ st)
     python scripts/pmc_r02.py bench r04s_prof_c5 r04_final_c5 0,4096,4096,4096,50,1,2 "round-4 final build (r04s)" && \
     "$0" t
     ;;
+u)
+    # session U: the VALU calibration with the kmix replays of the final build's mixes (C3's changed with the
+    # one-leaf loop), then C3's and the default bench lines priced by it
+    scripts/gpu_session.sh "600:r04u_calib:scripts/calib_r02.sh r04u_calib"
+    ;;
+u2)
+    PREFIX=r04u_ scripts/gpu_session.sh bench bench_c3
+    ;;
 g2h)
     # sessions G2 (C5's passes) and H (calibration with the r04 kmix replays) in one call
     "$0" g2 && "$0" h
