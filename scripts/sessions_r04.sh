@@ -191,7 +191,11 @@ u)
     scripts/gpu_session.sh "600:r04u_calib:scripts/calib_r02.sh r04u_calib"
     ;;
 u2)
-    PREFIX=r04u_ scripts/gpu_session.sh bench bench_c3
+    PREFIX=r04u_ scripts/gpu_session.sh bench bench_c2 bench_c3 bench_c4
+    ;;
+uu)
+    # U, its calibration block written on the box (scripts/pmc_r02.py calib), then the default, C2, C3 and C4 lines
+    "$0" u && python scripts/pmc_r02.py calib r04u_calib r04u && "$0" u2
     ;;
 g2h)
     # sessions G2 (C5's passes) and H (calibration with the r04 kmix replays) in one call
