@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
 """DESIGN.md §7's results table from bench logs (one JSON line each).
 
-usage: python scripts/results_table.py PREFIX   (reads profiles/PREFIX{bench_c1..c5,f32_c2..c4}.log)
+usage: python scripts/results_table.py PREFIX [cN=OTHER_PREFIX ...]
+       (reads profiles/PREFIX{bench_c1..c5,f32_c2..c4}.log; cN=OTHER takes config N's f64 line from
+       profiles/OTHERbench_cN.log instead)
 """
 import json
 import os
@@ -22,6 +24,7 @@ def line(path):
 
 def main():
     pre = sys.argv[1]
+    over = dict(a.split("=", 1) for a in sys.argv[2:])
     names = {"C1": "C1 random 1200×800×10, depth 8", "C2": "**C2 random 1200×800×500** (headline)",
              "C3": "C3 Cornell 800×800×1000", "C4": "C4 final 1920×1080×1000", "C5": "C5 random 4096²×4096"}
     print("| config (BASELINE) | Msamples/s | ms/frame (kernel + reduce) | schedule, batches, waves/SIMD | "
@@ -29,7 +32,7 @@ def main():
           "ref. split, 10 threads | parity L∞ |")
     print("|---|---|---|---|---|---|---|---|---|---|---|---|")
     for c in ("C1", "C2", "C3", "C4", "C5"):
-        d = line(os.path.join(REPO, "profiles", f"{pre}bench_{c.lower()}.log"))
+        d = line(os.path.join(REPO, "profiles", f"{over.get(c.lower(), pre)}bench_{c.lower()}.log"))
         if d is None:
             continue
         f = line(os.path.join(REPO, "profiles", f"{pre}f32_{c.lower()}.log"))
