@@ -197,6 +197,13 @@ uu)
     # U, its calibration block written on the box (scripts/pmc_r02.py calib), then the default, C2, C3 and C4 lines
     "$0" u && python scripts/pmc_r02.py calib r04u_calib r04u && "$0" u2
     ;;
+v)
+    # session V: the SAH build parameters re-swept at HEAD (host-side env, same library): C4 and C2
+    A=$L/librtiow_amd.so
+    scripts/gpu_session.sh \
+      "600:r04v_ab_c4:python scripts/ab_builds.py $A $A@RT_BVH_CI=0.7 $A@RT_BVH_CI=0.85 $A@RT_BVH_LEAFN=1 $A@RT_BVH_CI=0.7,RT_BVH_LEAFN=1 --scene 7 --width 1920 --height 1080 --spp 100 --rounds 2" \
+      "600:r04v_ab_c2:python scripts/ab_builds.py $A $A@RT_BVH_CI=0.7 $A@RT_BVH_CI=0.85 --scene 0 --width 1200 --height 800 --spp 100 --rounds 3"
+    ;;
 g2h)
     # sessions G2 (C5's passes) and H (calibration with the r04 kmix replays) in one call
     "$0" g2 && "$0" h
