@@ -512,6 +512,11 @@ struct Builder {
     double c_isect = 1.0;
     int max_leaf = 8;
     int force_leaf = 2;   // RT_BVH_LEAFN: a set this small is always one leaf
+    // ... unless it holds a Box (RT_BVH_BOXPAIRS=0: no exception): two Boxes' twelve rect tests in
+    // one leaf cost more than a node visit that separates them (C4 1920x1080x100: 108.51 -> 103.52
+    // ms with sets of two split by the SAH, profiles/r04v_ab_c4.log; the random scene's sphere
+    // pairs stay leaves, whose split would push its TLAS past the LDS node budget)
+    bool split_box_pairs = true;
     int root_leaf = 8;    // a whole BVH of at most this many items is one leaf
 
     int build_rec(std::vector<Item>& items, int b, int e, int depth)
@@ -521,7 +526,11 @@ struct Builder {
         double plo[3], phi[3];
         bounds(items, b, e, plo, phi);
         double parea = area(plo, phi);
-        if (n <= std::max(1, force_leaf) || (depth == 0 && n <= root_leaf)) return make_leaf(items, b, e);
+        bool has_box = false;
+        if (split_box_pairs)
+            for (int i = b; i < e && !has_box; ++i)
+                has_box = items[i].prim >= 0 && f.prims[(size_t)items[i].prim].kind == RT_PRIM_BOX;
+        if (n <= 1 || (n <= force_leaf && !has_box) || (depth == 0 && n <= root_leaf)) return make_leaf(items, b, e);
         if (depth >= 20) {  // bound the traversal stack: median split on the widest centroid axis
             double clo[3] = {INFINITY, INFINITY, INFINITY}, chi[3] = {-INFINITY, -INFINITY, -INFINITY};
             for (int i = b; i < e; ++i)
@@ -692,6 +701,7 @@ int flatten(World& w, int accel, std::string& err)
     if (const char* e = std::getenv("RT_BVH_MAXLEAF")) bld.max_leaf = std::min(31, std::max(2, std::atoi(e)));
     if (const char* e = std::getenv("RT_BVH_LEAFN")) bld.force_leaf = std::min(31, std::max(1, std::atoi(e)));
     if (const char* e = std::getenv("RT_BVH_ROOTLEAF")) bld.root_leaf = std::min(31, std::max(0, std::atoi(e)));
+    if (const char* e = std::getenv("RT_BVH_BOXPAIRS")) bld.split_box_pairs = std::atoi(e) != 0;
     if (const char* e = std::getenv("RT_INST_DISSOLVE")) bld.dissolve_inst = std::atoi(e) != 0;
     if (const char* e = std::getenv("RT_DISSOLVE_CI")) bld.dissolve_cost = std::max(0.01, std::atof(e));
     std::vector<Item> top;

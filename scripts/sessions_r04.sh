@@ -204,6 +204,17 @@ v)
       "600:r04v_ab_c4:python scripts/ab_builds.py $A $A@RT_BVH_CI=0.7 $A@RT_BVH_CI=0.85 $A@RT_BVH_LEAFN=1 $A@RT_BVH_CI=0.7,RT_BVH_LEAFN=1 --scene 7 --width 1920 --height 1080 --spp 100 --rounds 2" \
       "600:r04v_ab_c2:python scripts/ab_builds.py $A $A@RT_BVH_CI=0.7 $A@RT_BVH_CI=0.85 --scene 0 --width 1200 --height 800 --spp 100 --rounds 3"
     ;;
+w)
+    # session W: Box pairs split by the SAH (flatten.cpp split_box_pairs) against the old rule and against
+    # every pair split (RT_BVH_LEAFN=1) on C4, same library
+    A=$L/librtiow_amd.so
+    scripts/gpu_session.sh \
+      "600:r04w_ab_c4:python scripts/ab_builds.py $A $A@RT_BVH_BOXPAIRS=0 $A@RT_BVH_LEAFN=1 --scene 7 --width 1920 --height 1080 --spp 100 --rounds 2"
+    ;;
+stw)
+    # W, then the final-build passes and lines (ST) of this build
+    "$0" w && "$0" st
+    ;;
 g2h)
     # sessions G2 (C5's passes) and H (calibration with the r04 kmix replays) in one call
     "$0" g2 && "$0" h
