@@ -185,6 +185,18 @@ st)
     python scripts/pmc_r02.py bench r04s_prof_c5 r04_final_c5 0,4096,4096,4096,50,1,2 "round-4 final build (r04s)" && \
     "$0" t
     ;;
+st2)
+    # ST for the box-pairs build (prefixes r04x_ / r04y_): sessions S and T in one call (boxes are scarce): tests, smoke, PMC passes of C1-C5, their pmc.json
+    # entries written on the box (scripts/pmc_r02.py, the same step the builder runs after merging), then
+    # the bench lines, which read them
+    PREFIX=r04x_ scripts/gpu_session.sh tests smoke prof_c1 prof_c2 prof_c3 prof_c4 prof_c5 && \
+    python scripts/pmc_r02.py bench r04x_prof_c1 r04_final_c1 0,1200,800,10,8,1,1 "round-4 final build (r04x)" && \
+    python scripts/pmc_r02.py bench r04x_prof_c2 r04_final_c2 0,1200,800,500,50,1,1 "round-4 final build (r04x)" && \
+    python scripts/pmc_r02.py bench r04x_prof_c3 r04_final_c3 5,800,800,1000,50,1,1 "round-4 final build (r04x)" && \
+    python scripts/pmc_r02.py bench r04x_prof_c4 r04_final_c4 7,1920,1080,1000,50,1,1 "round-4 final build (r04x)" && \
+    python scripts/pmc_r02.py bench r04x_prof_c5 r04_final_c5 0,4096,4096,4096,50,1,2 "round-4 final build (r04x)" && \
+    PREFIX=r04y_ scripts/gpu_session.sh bench bench_c1 bench_c2 bench_c3 bench_c4 bench_c5 f32_c2 f32_c3 f32_c4
+    ;;
 u)
     # session U: the VALU calibration with the kmix replays of the final build's mixes (C3's changed with the
     # one-leaf loop), then C3's and the default bench lines priced by it
@@ -213,7 +225,7 @@ w)
     ;;
 stw)
     # W, then the final-build passes and lines (ST) of this build
-    "$0" w && "$0" st
+    "$0" w && "$0" st2
     ;;
 g2h)
     # sessions G2 (C5's passes) and H (calibration with the r04 kmix replays) in one call
