@@ -271,7 +271,9 @@ struct Builder {
         } else {
             std::vector<Item> items;
             for (int hid : leaves) items.push_back(item_of(lower_simple(hid), hid));
+            in_blas = true;
             root = build_bvh(items);
+            in_blas = false;
         }
         pad_abs = saved;
         if (rc) return 0;
@@ -517,6 +519,12 @@ struct Builder {
     // ms with sets of two split by the SAH, profiles/r04v_ab_c4.log; the random scene's sphere
     // pairs stay leaves, whose split would push its TLAS past the LDS node budget)
     bool split_box_pairs = true;
+    // ... and inside an instance's BLAS any set of two (RT_BVH_BLASPAIRS=0: no): the final scene's
+    // 1000-sphere cluster, walked by the lanes that reach it together after the top-level walk
+    // (C4 1920x1080x100 with every pair split, the top level's too: 105.84 -> 103.40 ms,
+    // profiles/r04w_ab_c4.log; the random scene's top level keeps its pairs, see above)
+    bool split_blas_pairs = true;
+    bool in_blas = false;   // make_blas is building
     int root_leaf = 8;    // a whole BVH of at most this many items is one leaf
 
     int build_rec(std::vector<Item>& items, int b, int e, int depth)
@@ -530,7 +538,8 @@ struct Builder {
         if (split_box_pairs)
             for (int i = b; i < e && !has_box; ++i)
                 has_box = items[i].prim >= 0 && f.prims[(size_t)items[i].prim].kind == RT_PRIM_BOX;
-        if (n <= 1 || (n <= force_leaf && !has_box) || (depth == 0 && n <= root_leaf)) return make_leaf(items, b, e);
+        const bool split_pair = has_box || (split_blas_pairs && in_blas);
+        if (n <= 1 || (n <= force_leaf && !split_pair) || (depth == 0 && n <= root_leaf)) return make_leaf(items, b, e);
         if (depth >= 20) {  // bound the traversal stack: median split on the widest centroid axis
             double clo[3] = {INFINITY, INFINITY, INFINITY}, chi[3] = {-INFINITY, -INFINITY, -INFINITY};
             for (int i = b; i < e; ++i)
@@ -702,6 +711,7 @@ int flatten(World& w, int accel, std::string& err)
     if (const char* e = std::getenv("RT_BVH_LEAFN")) bld.force_leaf = std::min(31, std::max(1, std::atoi(e)));
     if (const char* e = std::getenv("RT_BVH_ROOTLEAF")) bld.root_leaf = std::min(31, std::max(0, std::atoi(e)));
     if (const char* e = std::getenv("RT_BVH_BOXPAIRS")) bld.split_box_pairs = std::atoi(e) != 0;
+    if (const char* e = std::getenv("RT_BVH_BLASPAIRS")) bld.split_blas_pairs = std::atoi(e) != 0;
     if (const char* e = std::getenv("RT_INST_DISSOLVE")) bld.dissolve_inst = std::atoi(e) != 0;
     if (const char* e = std::getenv("RT_DISSOLVE_CI")) bld.dissolve_cost = std::max(0.01, std::atof(e));
     std::vector<Item> top;
