@@ -534,10 +534,14 @@ struct Builder {
         double plo[3], phi[3];
         bounds(items, b, e, plo, phi);
         double parea = area(plo, phi);
-        bool has_box = false;
+        bool has_box = false;   // a Box, a medium or an instance over a BVH: a costly test
         if (split_box_pairs)
-            for (int i = b; i < e && !has_box; ++i)
-                has_box = items[i].prim >= 0 && f.prims[(size_t)items[i].prim].kind == RT_PRIM_BOX;
+            for (int i = b; i < e && !has_box; ++i) {
+                if (items[i].prim < 0) continue;
+                const rt_prim& q = f.prims[(size_t)items[i].prim];
+                has_box = q.kind == RT_PRIM_BOX || q.kind == RT_PRIM_MEDIUM ||
+                          (q.kind == RT_PRIM_INSTANCE && f.instances[(size_t)q.a].child_kind == RT_CHILD_BVH);
+            }
         const bool split_pair = has_box || (split_blas_pairs && in_blas);
         if (n <= 1 || (n <= force_leaf && !split_pair) || (depth == 0 && n <= root_leaf)) return make_leaf(items, b, e);
         if (depth >= 20) {  // bound the traversal stack: median split on the widest centroid axis

@@ -209,6 +209,28 @@ st3)
     python scripts/pmc_r02.py bench r04z_prof_c5 r04_final_c5 0,4096,4096,4096,50,1,2 "round-4 final build (r04z)" && \
     PREFIX=r04zb_ scripts/gpu_session.sh bench bench_c1 bench_c2 bench_c3 bench_c4 bench_c5 f32_c2 f32_c3 f32_c4
     ;;
+st4)
+    # ST for the box-pairs build (prefixes r04v2_ / r04y_): sessions S and T in one call (boxes are scarce): tests, smoke, PMC passes of C1-C5, their pmc.json
+    # entries written on the box (scripts/pmc_r02.py, the same step the builder runs after merging), then
+    # the bench lines, which read them
+    PREFIX=r04v2_ scripts/gpu_session.sh tests smoke prof_c1 prof_c2 prof_c3 prof_c4 prof_c5 && \
+    python scripts/pmc_r02.py bench r04v2_prof_c1 r04_final_c1 0,1200,800,10,8,1,1 "round-4 final build (r04v2)" && \
+    python scripts/pmc_r02.py bench r04v2_prof_c2 r04_final_c2 0,1200,800,500,50,1,1 "round-4 final build (r04v2)" && \
+    python scripts/pmc_r02.py bench r04v2_prof_c3 r04_final_c3 5,800,800,1000,50,1,1 "round-4 final build (r04v2)" && \
+    python scripts/pmc_r02.py bench r04v2_prof_c4 r04_final_c4 7,1920,1080,1000,50,1,1 "round-4 final build (r04v2)" && \
+    python scripts/pmc_r02.py bench r04v2_prof_c5 r04_final_c5 0,4096,4096,4096,50,1,2 "round-4 final build (r04v2)" && \
+    PREFIX=r04vb_ scripts/gpu_session.sh bench bench_c1 bench_c2 bench_c3 bench_c4 bench_c5 f32_c2 f32_c3 f32_c4
+    ;;
+w3)
+    # session W3: pairs holding a Box, a medium or an instance over a BVH split (heavy pairs) against the
+    # BLAS-pairs build's rule (only Boxes; RT_BVH_BOXPAIRS=0 turns both off) and every pair split, on C4
+    A=$L/librtiow_amd.so
+    scripts/gpu_session.sh \
+      "600:r04w3_ab_c4:python scripts/ab_builds.py $A $A@RT_BVH_BOXPAIRS=0 $A@RT_BVH_LEAFN=1 --scene 7 --width 1920 --height 1080 --spp 100 --rounds 2"
+    ;;
+stw3)
+    "$0" w3 && "$0" st4
+    ;;
 w2)
     # session W2: pairs split inside BLASes too (split_blas_pairs) against the box-pairs build
     # (RT_BVH_BLASPAIRS=0) and every pair split (RT_BVH_LEAFN=1) on C4
