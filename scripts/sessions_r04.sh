@@ -271,6 +271,13 @@ stw)
     # W, then the final-build passes and lines (ST) of this build
     "$0" w && "$0" st2
     ;;
+ph)
+    # session PH: phase timers of HEAD's build on C4, C3 and C2 (count variants)
+    scripts/gpu_session.sh \
+      "200:r04ph_phases_c4:python scripts/phases.py --scene 7 --width 1920 --height 1080 --spp 8" \
+      "200:r04ph_phases_c3:python scripts/phases.py --scene 5 --width 800 --height 800 --spp 16" \
+      "200:r04ph_phases_c2:python scripts/phases.py --scene 0 --width 1200 --height 800 --spp 16"
+    ;;
 g2h)
     # sessions G2 (C5's passes) and H (calibration with the r04 kmix replays) in one call
     "$0" g2 && "$0" h
