@@ -50,6 +50,7 @@ CONFIGS = {
     "C4": dict(scene=7, width=1920, height=1080, spp=1000, depth=50),
     "C5": dict(scene=0, width=4096, height=4096, spp=4096, depth=50),
 }
+SCHEDULES = {"chunks": 0, "pool": 1, "items": 2, "auto": 3, "wavefront": 4}
 SCENE_NAMES = {0: "random_scene (main.rs:245-289)", 5: "cornell_box_scene (main.rs:107-136)",
                7: "final_scene (main.rs:173-243)"}
 
@@ -88,6 +89,11 @@ def parse():
                          "1-GPU box: launch as torch.distributed.run --nproc-per-node 1 ... --gpus 1 --force-dist")
     ap.add_argument("--precision", default="f64", choices=["f64", "f32"],
                     help="f64: the reference's arithmetic (the headline); f32: the fast mode (SURVEY §8 f3)")
+    ap.add_argument("--schedule", default="auto", choices=sorted(SCHEDULES),
+                    help="work schedule (rt_ctx_set_schedule); images are bit-identical under all of them")
+    ap.add_argument("--buf-mb", type=int, default=0,
+                    help="trace-output buffer bound in MB (rt_ctx_set_option RT_OPT_TRACE_BUF_BYTES; 0: default)")
+    ap.add_argument("--no-overlap", action="store_true", help="buffer batches in order in one buffer")
     args = ap.parse_args()
     for k, v in CONFIGS[args.config].items():
         if getattr(args, k) is None:
@@ -225,6 +231,11 @@ def main():
     f32 = args.precision == "f32"
     if f32:
         renderer.set_precision(rt.RT_PREC_F32)
+    renderer.set_schedule(SCHEDULES[args.schedule])
+    if args.buf_mb:
+        renderer.set_option(rt.RT_OPT_TRACE_BUF_BYTES, args.buf_mb << 20)
+    if args.no_overlap:
+        renderer.set_option(rt.RT_OPT_BATCH_OVERLAP, 0)
     t_build = time.perf_counter() - t_build
 
     # N > 1: ranks take the frame's 8x8 tiles round-robin (tile shards: every work tile stays a
@@ -341,13 +352,20 @@ def main():
     ms_per_step = elapsed / args.steps * 1e3
     k_ms = float(np.mean(kernel_ms)) if kernel_ms else float("nan")
 
-    # ---- roofline: VALU issue (the binding resource), from the PMC pass of this build
-    src_hash = ge.source_hash()
+    # ---- roofline: VALU issue (the binding resource), from the PMC pass of this build. The build
+    # is the LOADED library's (rt_build_info, compiled in from __graft_entry__.source_hash()); a
+    # library that does not match the sources next to it is a stale build, and no PMC record is
+    # quoted for it
+    src_hash = rt.build_info()
+    tree_hash = ge.source_hash()
     workload = [args.scene, W, H, spp, depth, world, last.schedule] + ([1] if f32 else [])
-    pmc, calib = pmc_entry(src_hash, workload)
+    pmc, calib = pmc_entry(src_hash, workload) if src_hash == tree_hash else (None, None)
     roofline = {"bound": "valu", "achieved": None, "peak": None, "unit": "G SIMD-cycles/s", "frac": None,
-                "traffic": None, "src_hash": src_hash}
-    if pmc is not None and calib is not None:
+                "traffic": None, "src_hash": src_hash, "src_hash_from": "rt_build_info (the loaded library)"}
+    if src_hash != tree_hash:
+        roofline["note"] = ("stale library: built from sources %s, the tree is %s; no PMC record quoted"
+                            % (src_hash, tree_hash))
+    elif pmc is not None and calib is not None:
         isa = isa_prices(src_hash, last.variant_features, last.schedule, last.slab32, int(last.lds_nodes > 0))
         additive = valu_issue_cycles(pmc["counters"], calib, isa=isa)   # SIMD-cycles of VALU issue per launch
         rp = replay_price(calib, last.variant_features)

@@ -57,6 +57,11 @@ typedef struct rt_world rt_world;
 int rt_abi_version(void);
 /* Text of the last error on this thread ("" if none). */
 const char* rt_last_error(void);
+/* Build identity of the loaded library: the source hash it was compiled from (16 hex digits
+ * of sha256 over csrc/, include/rt/ and the compile flags: __graft_entry__.source_hash()),
+ * "unknown" for a build without one. Profiles and PMC records are keyed by it, so a caller can
+ * check that the library it times is the build its counters describe. */
+const char* rt_build_info(void);
 
 /* ---- device context --------------------------------------------------------- */
 int rt_device_count(int* count);
@@ -131,6 +136,18 @@ int rt_scene_preset_get(int scene_id, rt_scene_preset* out);
 int rt_scene_camera(int scene_id, int width, int height, rt_camera* cam_out, double background_out[3]);
 
 /* ---- lowering + upload ---------------------------------------------------------------- */
+/* SAH builder options of this world's rt_world_flatten (the tree changes, the image does not):
+ * value < 0 (or 0 for the sizes and the cost) restores the default. Tuning knobs for A/B runs
+ * (scripts/ab_variants.py --bvh); the defaults are DESIGN.md §2's. */
+enum {
+    RT_BUILD_C_ISECT = 1,          /* primitive-test cost relative to a node visit (default 1) */
+    RT_BUILD_MAX_LEAF = 2,         /* largest leaf the cost model may pick (8) */
+    RT_BUILD_FORCE_LEAF = 3,       /* a set this small is always one leaf (2) */
+    RT_BUILD_ROOT_LEAF = 4,        /* a whole BVH of at most this many items is one leaf (8) */
+    RT_BUILD_SPLIT_BOX_PAIRS = 5,  /* pairs holding a Box, a medium or a BLAS instance split by cost (1) */
+    RT_BUILD_SPLIT_BLAS_PAIRS = 6  /* pairs inside instance BLASes split by cost (1) */
+};
+int rt_world_set_build_option(rt_world* w, int key, double value);
 /* Flattens the world into SoA tables owned by the world (valid until the next
  * flatten or rt_world_destroy). accel: RT_ACCEL_SAH / _LINEAR / _MEDIAN (rt_scene.h). */
 int rt_world_flatten(rt_world* w, int accel, const rt_scene_soa** soa_out);
@@ -281,15 +298,35 @@ int rt_write_ppm(const float* mean_rgb, int width, int height, const char* path)
 
 /* Kernel variant knobs of a context: slab32 (conservative f32 BVH slab tests),
  * lds_stack (traversal stack in LDS instead of scratch), lds_nodes (keep the TLAS in LDS
- * when it fits). Defaults 1/1/1, or the RT_SLAB32 / RT_LDS_STACK / RT_LDS_NODES
- * environment variables. Results do not depend on them (tests check this).
- * RT_EXTRA_FEATURES (environment, read at context creation): feature bits OR-ed into the
- * scene's, so a scene runs on a larger feature-set variant than it needs (the tests use it
- * to run the all-features variant, which no reference scene selects). */
+ * when it fits). Defaults 1/1/1. Results do not depend on them (tests check this). */
 int rt_ctx_set_variant(rt_ctx* ctx, int slab32, int lds_stack, int lds_nodes);
 
-/* Work schedule of a context (default RT_SCHED_AUTO, or the RT_SCHEDULE environment
- * variable 0/1/2/3). Images are bit-identical under all of them.
+/* Context options (rt_ctx_set_option / rt_ctx_get_option). The library reads no environment
+ * variable: every behaviour switch is one of these or a setter above. Images do not depend on
+ * any of them (the tests check this); they trade speed and memory.
+ *   RT_OPT_TRACE_BUF_BYTES  bound of the trace-output buffer (below); 0 restores the default
+ *   RT_OPT_BATCH_OVERLAP    1 (default): buffer batches overlap on two streams; 0: one buffer, in order
+ *   RT_OPT_BLOCK_SAMPLES    per-sample pool: samples per work block (0: auto, 16 down to 4 for small shards)
+ *   RT_OPT_BLOCK_CHUNKS     item pool: chunks per work block (0: auto = 2)
+ *   RT_OPT_EXTRA_FEATURES   feature bits OR-ed into the scene's, so a scene runs on a larger
+ *                           feature-set variant than it needs (tests: the all-features variant)
+ *   RT_OPT_HOIST            1 (default): the spheres variants test a huge root-child leaf before
+ *                           the walk (SceneDev.pre_leaf); takes effect at the next upload
+ *   RT_OPT_WF_PATHS         wavefront schedule: path slots (0: auto) */
+enum {
+    RT_OPT_TRACE_BUF_BYTES = 1,
+    RT_OPT_BATCH_OVERLAP = 2,
+    RT_OPT_BLOCK_SAMPLES = 3,
+    RT_OPT_BLOCK_CHUNKS = 4,
+    RT_OPT_EXTRA_FEATURES = 5,
+    RT_OPT_HOIST = 6,
+    RT_OPT_WF_PATHS = 7
+};
+int rt_ctx_set_option(rt_ctx* ctx, int key, int64_t value);
+int rt_ctx_get_option(rt_ctx* ctx, int key, int64_t* value);
+
+/* Work schedule of a context (default RT_SCHED_AUTO). Images are bit-identical under all of
+ * them.
  *   CHUNKS: a wave owns an 8x8 tile x one chunk of samples, each lane one pixel's chunk,
  *           written as one partial per (pixel, chunk); the wave waits for its slowest lane.
  *   POOL:   persistent waves take (tile, chunk) blocks from a device counter and a lane
@@ -301,18 +338,17 @@ int rt_ctx_set_variant(rt_ctx* ctx, int slab32, int lds_stack, int lds_nodes);
  *           buffer bytes); a lane whose item ended takes the next item at once.
  *   AUTO:   POOL when the render's per-sample radiance is at most 4 x the buffer bound (it is
  *           the faster of the two), otherwise ITEMS; rt_stats.schedule reports which ran.
- * The trace-output buffer is bounded by RT_SAMPLE_BUF_MB (default: sized at context creation
+ * The trace-output buffer is bounded by RT_OPT_TRACE_BUF_BYTES (default: sized at context creation
  * to 3/8 of the device's free memory, at most 128 GiB, at least 32 GiB where half the free
  * memory allows; allocated lazily, as large as a render needs). A larger render runs in buffer
  * batches whose sums are carried across, in two halves of the bound: batch k traces into half
  * k & 1 on one of two context streams while the render's stream reduces batch k - 1, so
- * consecutive traces overlap (RT_BATCH_OVERLAP=0: one buffer, in order). A 4 GB bound
- * (RT_SAMPLE_BUF_MB=4000) renders C2 as fast as one batch; long-path scenes pay per batch. */
+ * consecutive traces overlap (RT_OPT_BATCH_OVERLAP 0: one buffer, in order). A 4 GB bound renders
+ * C2 as fast as one batch; long-path scenes pay per batch. */
 enum { RT_SCHED_CHUNKS = 0, RT_SCHED_POOL = 1, RT_SCHED_ITEMS = 2, RT_SCHED_AUTO = 3 };
 int rt_ctx_set_schedule(rt_ctx* ctx, int schedule);
 
-/* Arithmetic of a context's renders (default RT_PREC_F64, or the RT_PRECISION
- * environment variable 0/1).
+/* Arithmetic of a context's renders (default RT_PREC_F64).
  *   F64: the reference's f64 everywhere (math.rs:13-17), path-identical to the oracle: the
  *        same rays, hits and draws; the per-pixel means differ only in the last ulps (the
  *        throughput product T = a0*a1*...*e associates left here, right in the recursive

@@ -48,9 +48,6 @@ size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 constexpr int kParamSlots = 16;
 
 // LDS stack entries per lane above which the scratch stack is used (48 KB per block)
-#ifndef RT_HOIST_DEFAULT
-#define RT_HOIST_DEFAULT 1
-#endif
 constexpr int kMaxLdsStack = 48;
 // TLAS nodes kept in LDS (32 KB per block): the first kMaxLdsNodes in BFS order, i.e.
 // the top levels; deeper ones are read from L1/L2
@@ -101,21 +98,21 @@ struct rt_ctx {
     rt_stats stats{};
     uint32_t features = rtk::FEAT_ALL;  // of the uploaded scene
     int n_materials = 0, n_textures = 0;
-    int block_chunks = 0;               // RT_BLOCK_CHUNKS: chunks per item-pool work block (0: auto)
-    int block_samples = 0;              // RT_BLOCK_SAMPLES: samples per per-sample-pool work block (0: auto)
+    int block_chunks = 0;               // RT_OPT_BLOCK_CHUNKS: chunks per item-pool work block (0: auto)
+    int block_samples = 0;              // RT_OPT_BLOCK_SAMPLES: samples per per-sample-pool work block (0: auto)
+    int64_t wf_paths = 0;               // RT_OPT_WF_PATHS: wavefront schedule path slots (0: auto)
     unsigned long long raw_counters[kCounters] = {};   // the last count_work render's counters (rt_last_counters)
-    uint32_t extra_features = 0;        // RT_EXTRA_FEATURES: a larger kernel variant than the scene needs (tests)
+    uint32_t extra_features = 0;        // RT_OPT_EXTRA_FEATURES: a larger kernel variant than the scene needs (tests)
     double pad_extent = 0.0;
-    int opt_slab32 = 1;                 // rt_ctx_set_variant / RT_SLAB32
-    int opt_lds = 1;                    // rt_ctx_set_variant / RT_LDS_STACK
-    int opt_lds_nodes = 1;              // RT_LDS_NODES: keep the TLAS in LDS when it fits
-    int opt_hoist = RT_HOIST_DEFAULT;   // RT_HOIST: test a huge root-child leaf before the walk (pre_leaf)
-    int opt_box_cand = 1;               // RT_BOX_CAND: boxes take the candidate-side test (0: six exact sides; A/B)
-    int opt_pool = RT_SCHED_AUTO;       // rt_ctx_set_schedule / RT_SCHEDULE: RT_SCHED_*
-    int opt_precision = RT_PREC_F64;    // rt_ctx_set_precision / RT_PRECISION: RT_PREC_*
-    size_t sample_buf_cap = (size_t)32 << 30;  // RT_SAMPLE_BUF_MB: bound of the trace-output buffer
+    int opt_slab32 = 1;                 // rt_ctx_set_variant
+    int opt_lds = 1;                    // rt_ctx_set_variant
+    int opt_lds_nodes = 1;              // rt_ctx_set_variant: keep the TLAS in LDS when it fits
+    int opt_hoist = 1;                  // RT_OPT_HOIST: test a huge root-child leaf before the walk (pre_leaf)
+    int opt_pool = RT_SCHED_AUTO;       // rt_ctx_set_schedule: RT_SCHED_*
+    int opt_precision = RT_PREC_F64;    // rt_ctx_set_precision: RT_PREC_*
+    size_t sample_buf_cap = (size_t)32 << 30;  // RT_OPT_TRACE_BUF_BYTES: bound of the trace-output buffer
     unsigned* work = nullptr;           // pool / item schedules: work-block counters (one per overlapped batch)
-    // Overlapped buffer batches (RT_BATCH_OVERLAP): batch k traces on tstream[k & 1] into half k & 1
+    // Overlapped buffer batches (RT_OPT_BATCH_OVERLAP): batch k traces on tstream[k & 1] into half k & 1
     // of the trace-output buffer while the caller's stream reduces batch k - 1
     hipStream_t tstream[2] = {nullptr, nullptr};
     hipEvent_t ev_in = nullptr, ev_tr[2] = {nullptr, nullptr}, ev_rd[2] = {nullptr, nullptr};
@@ -124,16 +121,36 @@ struct rt_ctx {
     size_t acc_tmp_cap = 0;
     int n_tlas_nodes = 0;
     int n_nodes = 0;                    // BVH nodes of the uploaded scene (TLAS + BLASes)
-    rtk::WalkSave* walk_save = nullptr; // RT_PAUSE builds: suspended walks, one slot per thread of a full grid
     int n_cus = 256;
     size_t lds_per_cu = 160 * 1024;     // the device's LDS per CU and per workgroup (read at creation)
     size_t lds_per_block = 160 * 1024;
 };
 
+// The trace-output buffer's default bound, sized for the device: 3/8 of its free HBM, at most
+// 128 GiB (an MI355X: ~107 GB, so C4's 49.8 GB of per-sample radiance is one launch), at least
+// 32 GiB where half the free memory allows it (allocated lazily, only as large as a render needs).
+// A bound of 4 GB costs C2 nothing (six overlapped batches: 74.77 vs 74.75 ms
+// per frame) but the final scene 4.4 % in the item pool and 18 % in 25 overlapped per-sample
+// batches (profiles/r04e_*, r04f_*): its paths are long and its 512-thread blocks free CUs late,
+// so every batch pays a tail. The default keeps speed.
+static size_t default_buf_cap()
+{
+    size_t fr = 0, tot = 0;
+    if (hipMemGetInfo(&fr, &tot) != hipSuccess || fr == 0) return (size_t)32 << 30;
+    size_t cap = std::min(fr / 8 * 3, (size_t)128 << 30);
+    cap = std::max(cap, std::min((size_t)32 << 30, fr / 2));
+    return std::max(cap >> 20, (size_t)1) << 20;
+}
+
+#ifndef RT_SRC_HASH
+#define RT_SRC_HASH "unknown"
+#endif
+
 extern "C" {
 
 int rt_abi_version(void) { return RT_ABI_VERSION; }
 const char* rt_last_error(void) { return g_last_error.c_str(); }
+const char* rt_build_info(void) { return RT_SRC_HASH; }
 
 int rt_device_count(int* count)
 {
@@ -159,34 +176,7 @@ int rt_ctx_create(int device, rt_ctx** out)
     rt_ctx* c = new (std::nothrow) rt_ctx();
     if (!c) return fail(RT_ERR_OOM, "rt_ctx");
     c->device = device;
-    if (const char* e = std::getenv("RT_SLAB32")) c->opt_slab32 = std::atoi(e) != 0;
-    if (const char* e = std::getenv("RT_LDS_STACK")) c->opt_lds = std::atoi(e) != 0;
-    if (const char* e = std::getenv("RT_LDS_NODES")) c->opt_lds_nodes = std::atoi(e) != 0;
-    if (const char* e = std::getenv("RT_HOIST")) c->opt_hoist = std::atoi(e) != 0;
-    if (const char* e = std::getenv("RT_BOX_CAND")) c->opt_box_cand = std::atoi(e) != 0;
-    if (const char* e = std::getenv("RT_BATCH_OVERLAP")) c->opt_overlap = std::atoi(e) != 0;
-    if (const char* e = std::getenv("RT_SCHEDULE")) c->opt_pool = std::min(3, std::max(0, std::atoi(e)));
-    if (const char* e = std::getenv("RT_PRECISION")) c->opt_precision = std::atoi(e) == RT_PREC_F32 ? RT_PREC_F32 : RT_PREC_F64;
-    if (const char* e = std::getenv("RT_BLOCK_CHUNKS")) c->block_chunks = std::min(64, std::max(1, std::atoi(e)));
-    if (const char* e = std::getenv("RT_BLOCK_SAMPLES")) c->block_samples = std::min(1024, std::max(1, std::atoi(e)));
-    if (const char* e = std::getenv("RT_EXTRA_FEATURES")) c->extra_features = (uint32_t)std::atoi(e) & rtk::FEAT_ALL;
-    if (const char* e = std::getenv("RT_SAMPLE_BUF_MB")) {
-        c->sample_buf_cap = (size_t)std::max(1L, std::atol(e)) << 20;
-    } else {
-        // sized for the device: 3/8 of its free HBM, at most 128 GiB (an MI355X: ~107 GB, so C4's
-        // 49.8 GB of per-sample radiance is one launch), at least 32 GiB where half the free
-        // memory allows it (allocated lazily, only as large as a render needs). A bound of 4 GB
-        // (RT_SAMPLE_BUF_MB=4000) costs C2 nothing (six overlapped batches:
-        // 74.77 vs 74.75 ms per frame) but the final scene 4.4 % in the item pool and 18 % in 25
-        // overlapped per-sample batches (profiles/r04e_*, r04f_*): its paths are long and its
-        // 512-thread blocks free CUs late, so every batch pays a tail. The default keeps speed.
-        size_t fr = 0, tot = 0;
-        if (hipMemGetInfo(&fr, &tot) == hipSuccess && fr > 0) {
-            size_t cap = std::min(fr / 8 * 3, (size_t)128 << 30);
-            cap = std::max(cap, std::min((size_t)32 << 30, fr / 2));
-            c->sample_buf_cap = std::max(cap >> 20, (size_t)1) << 20;
-        }
-    }
+    c->sample_buf_cap = default_buf_cap();
     {
         int v = 0;
         if (hipDeviceGetAttribute(&v, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, device) == hipSuccess && v > 0)
@@ -228,7 +218,6 @@ void rt_ctx_destroy(rt_ctx* c)
     (void)hipFree(c->params);
     (void)hipFree(c->work);
     (void)hipFree(c->acc_tmp);
-    (void)hipFree(c->walk_save);
     for (auto& e : c->ev)
         if (e) (void)hipEventDestroy(e);
     if (c->ev_done) (void)hipEventDestroy(c->ev_done);
@@ -489,6 +478,23 @@ int rt_scene_camera(int scene_id, int width, int height, rt_camera* cam, double 
 }
 
 // ---- lowering + upload ---------------------------------------------------------------
+int rt_world_set_build_option(rt_world* w, int key, double v)
+{
+    if (!w) return fail(RT_ERR_INVALID, "null world");
+    if (!std::isfinite(v)) return fail(RT_ERR_INVALID, "build option value not finite");
+    rtw::BuildOptions& b = w->w.build;
+    const int iv = v < 0 ? -1 : (int)std::min(v, 1e6);
+    switch (key) {
+    case RT_BUILD_C_ISECT: b.c_isect = v > 0 ? v : 0.0; return RT_OK;
+    case RT_BUILD_MAX_LEAF: b.max_leaf = std::max(iv, 0); return RT_OK;
+    case RT_BUILD_FORCE_LEAF: b.force_leaf = std::max(iv, 0); return RT_OK;
+    case RT_BUILD_ROOT_LEAF: b.root_leaf = iv; return RT_OK;
+    case RT_BUILD_SPLIT_BOX_PAIRS: b.split_box_pairs = iv; return RT_OK;
+    case RT_BUILD_SPLIT_BLAS_PAIRS: b.split_blas_pairs = iv; return RT_OK;
+    default: return fail(RT_ERR_INVALID, "unknown build option");
+    }
+}
+
 int rt_world_flatten(rt_world* w, int accel, const rt_scene_soa** soa_out)
 {
     if (!w || !soa_out) return fail(RT_ERR_INVALID, "null argument");
@@ -532,81 +538,6 @@ static int walk_need(const rt_scene_soa* s, int ref, std::vector<int>& need, std
         colour[i] = 2;
     }
     return need[ref];
-}
-
-constexpr int RT_DONE_HOST = std::numeric_limits<int>::min();   // an empty W4 slot's reference (never hit)
-
-// The 4-wide TLAS (RT_WIDE; SceneDev.w4) from binary node `root`. Each W4 record starts from
-// a binary node's two children and, while it has fewer than four, replaces the internal child
-// of largest box surface by that child's two children (greedy collapse; boxes come from the
-// binary records, already padded). Records in BFS order, child references as record indices.
-// Returns the stack entries the walk needs: a visit pushes all but the nearest hit child, so
-// need(w) = (children - 1) + max need(internal child); + the RT_DONE sentinel and the
-// branch-free push's spare slot. 0 if there is nothing to build (root is a leaf).
-static int build_w4(const std::vector<rt_bvh_node>& nodes, int root, std::vector<rtk::W4Node>& out)
-{
-    out.clear();
-    if (root < 0) return 0;
-    struct Slot {
-        float lo[3], hi[3];
-        int ref;
-    };
-    auto area = [](const Slot& b) {
-        const double x = (double)b.hi[0] - b.lo[0], y = (double)b.hi[1] - b.lo[1], z = (double)b.hi[2] - b.lo[2];
-        return x * y + y * z + z * x;
-    };
-    auto kids_of = [&](int ref, Slot& a, Slot& b) {
-        const rt_bvh_node& n = nodes[(size_t)ref];
-        std::memcpy(a.lo, n.lo0, 12); std::memcpy(a.hi, n.hi0, 12); a.ref = n.child[0];
-        std::memcpy(b.lo, n.lo1, 12); std::memcpy(b.hi, n.hi1, 12); b.ref = n.child[1];
-    };
-    std::vector<int> src{root};   // binary node of each record
-    std::vector<std::array<int, 4>> kids;   // record index of internal children, else -1
-    for (size_t w = 0; w < src.size(); ++w) {
-        std::vector<Slot> slots(2);
-        kids_of(src[w], slots[0], slots[1]);
-        while (slots.size() < 4) {
-            int best = -1;
-            for (int i = 0; i < (int)slots.size(); ++i)
-                if (slots[(size_t)i].ref >= 0 && (best < 0 || area(slots[(size_t)i]) > area(slots[(size_t)best]))) best = i;
-            if (best < 0) break;
-            Slot a, b;
-            kids_of(slots[(size_t)best].ref, a, b);
-            slots[(size_t)best] = a;
-            slots.push_back(b);
-        }
-        rtk::W4Node o;
-        std::array<int, 4> kid{-1, -1, -1, -1};
-        const float inf = std::numeric_limits<float>::infinity();
-        for (int c = 0; c < 4; ++c) {
-            Slot sl{{inf, inf, inf}, {-inf, -inf, -inf}, RT_DONE_HOST};   // empty: never hit
-            if (c < (int)slots.size()) sl = slots[(size_t)c];
-            for (int a = 0; a < 3; ++a) {
-                o.ax[a][c] = sl.lo[a];
-                o.ax[a][4 + c] = sl.hi[a];
-                o.ax[a][8 + c] = sl.lo[a];
-            }
-            o.child[c] = sl.ref;
-            if (c < (int)slots.size() && sl.ref >= 0) {
-                kid[(size_t)c] = (int)src.size();
-                o.child[c] = (int)src.size();
-                src.push_back(sl.ref);
-            }
-        }
-        out.push_back(o);
-        kids.push_back(kid);
-    }
-    std::vector<int> need(out.size(), 0);
-    for (size_t w = out.size(); w-- > 0;) {
-        int k = 0, deep = 0;
-        for (int c = 0; c < 4; ++c) {
-            if (out[w].ax[0][c] > out[w].ax[0][4 + c]) continue;   // empty slot
-            ++k;
-            if (kids[w][(size_t)c] >= 0) deep = std::max(deep, need[(size_t)kids[w][(size_t)c]]);
-        }
-        need[w] = std::max(0, k - 1) + deep;
-    }
-    return need[0] + 2;
 }
 
 // SceneDev.pre_leaf: a root child that is a leaf of <= 2 primitives whose box holds at least
@@ -810,28 +741,6 @@ int rt_ctx_upload_soa(rt_ctx* c, const rt_scene_soa* s)
             // b = 1: the instance's child is a BVH (the kernel defers the first such walk of a
             // cast, RT_DEFER_INST); a single child primitive is tested where the walk meets it
             p.b = s->instances[p.a].child_kind == RT_CHILD_BVH ? 1 : 0;
-        } else if (p.kind == RT_PRIM_BOX && p.b != 0 && c->opt_box_cand) {
-            // The kernel's candidate-side test (box_candidates) takes thin slabs around each face
-            // plane as wide as the padding of the box's f32 bounds on the outer side: w = twice
-            // the largest padding, stored after the bounds (p[9], b = 2). Bounds that do not
-            // contain the box (a foreign SoA) or are not finite leave b = 0: six exact sides.
-            const float* fb = reinterpret_cast<const float*>(&p.p[6]);
-            double pad = 0.0;
-            bool ok = true;
-            for (int a = 0; a < 3; ++a) {
-                const double lo = (double)fb[a], hi = (double)fb[3 + a];
-                if (!std::isfinite(lo) || !std::isfinite(hi) || lo > p.p[a] || hi < p.p[3 + a]) ok = false;
-                else pad = std::max({pad, p.p[a] - lo, hi - p.p[3 + a]});
-            }
-            float w = (float)(2.0 * pad);
-            if ((double)w < 2.0 * pad) w = std::nextafter(w, INFINITY);
-            if (!ok || !std::isfinite(w)) {
-                p.b = 0;
-            } else {
-                p.b = 2;
-                float wv[2] = {w, 0.0f};
-                std::memcpy(&p.p[9], wv, sizeof wv);
-            }
         }
     }
     std::vector<rt_prim> leaf_prims((size_t)s->n_prim_refs);
@@ -974,24 +883,15 @@ int rt_ctx_upload_soa(rt_ctx* c, const rt_scene_soa* s)
             n_blas_bfs = (int)bfs.size();
         }
     }
-    // RT_WIDE: the 4-wide TLAS from the walk's start node (hoist_root_leaf's pre_root where it
-    // applies; the TLAS prefix keeps its indices and leaf codes in nodes_dev)
-    std::vector<rtk::W4Node> w4;
-    int w4_stack = 0;
-    if (RT_WIDE && n_tlas_nodes > 0) {
-        rtk::SceneDev hs{};
-        if (c->opt_hoist) hoist_root_leaf(s, hs);
-        w4_stack = build_w4(nodes_dev, hs.pre_leaf != 0 ? hs.pre_root : s->tlas_root, w4);
-    }
-    size_t off[11], bytes[11] = {
+    size_t off[10], bytes[10] = {
         (size_t)s->n_nodes * sizeof(rt_bvh_node), (size_t)s->n_prim_refs * 4, (size_t)s->n_prims * sizeof(rt_prim),
         (size_t)s->n_instances * sizeof(rt_instance), (size_t)s->n_materials * sizeof(rt_material),
         (size_t)s->n_textures * sizeof(rt_texture), (size_t)s->n_perlin * 768 * 8, (size_t)s->n_perlin * 768 * 4,
-        (size_t)s->image_bytes, (size_t)s->n_prim_refs * sizeof(rt_prim), w4.size() * sizeof(rtk::W4Node)};
-    const void* src[11] = {nodes_dev.data(), s->prim_refs, prims.data(), inst_dev.data(), s->materials, s->textures,
-                           s->perlin_ranvec, s->perlin_perm, s->image_data, leaf_prims.data(), w4.data()};
+        (size_t)s->image_bytes, (size_t)s->n_prim_refs * sizeof(rt_prim)};
+    const void* src[10] = {nodes_dev.data(), s->prim_refs, prims.data(), inst_dev.data(), s->materials, s->textures,
+                           s->perlin_ranvec, s->perlin_perm, s->image_data, leaf_prims.data()};
     size_t total = 0;
-    for (int i = 0; i < 11; ++i) {
+    for (int i = 0; i < 10; ++i) {
         off[i] = total;
         total = align_up(total + bytes[i], 256);
     }
@@ -1007,7 +907,7 @@ int rt_ctx_upload_soa(rt_ctx* c, const rt_scene_soa* s)
         c->scene_bytes = total;
     }
     char* base = (char*)c->scene_buf;
-    for (int i = 0; i < 11; ++i)
+    for (int i = 0; i < 10; ++i)
         if (bytes[i]) HIP_TRY(hipMemcpy(base + off[i], src[i], bytes[i], hipMemcpyHostToDevice));
     c->S.nodes = (const rt_bvh_node*)(base + off[0]);
     c->S.prim_refs = (const int32_t*)(base + off[1]);
@@ -1019,9 +919,6 @@ int rt_ctx_upload_soa(rt_ctx* c, const rt_scene_soa* s)
     c->S.perlin_perm = (const int32_t*)(base + off[7]);
     c->S.image = (const uint8_t*)(base + off[8]);
     c->S.leaf_prims = (const rt_prim*)(base + off[9]);
-    c->S.w4 = (const rtk::W4Node*)(base + off[10]);
-    c->S.n_w4 = (int32_t)w4.size();
-    c->S.w4_stack = w4_stack;
     c->S.tlas_root = s->tlas_root;
     c->S.pre_leaf = 0;
     if (c->opt_hoist) hoist_root_leaf(s, c->S);
@@ -1030,7 +927,6 @@ int rt_ctx_upload_soa(rt_ctx* c, const rt_scene_soa* s)
     // relative, above) strictly above the -32768 = ~32767 sentinel: every code < 32767 (a leaf
     // at first slot 1023 holding 31 primitives would complement to the sentinel itself)
     c->S.stack16_ok = (n_tlas_nodes * (int64_t)80 <= 32767 - 80 && max_code < 32767 && s->n_nodes <= 32767) ? 1 : 0;
-    if (RT_WIDE && (w4.empty() || (int64_t)w4.size() * 160 > 32767 - 160 || w4_stack > kMaxLdsStack)) c->S.stack16_ok = 0;
     c->S.n_lds_nodes = 0;
     c->S.n_blas_bfs = n_blas_bfs;
     c->S.n_lds_blas = 0;
@@ -1368,14 +1264,6 @@ static int run_range(rt_ctx* c, const rt_camera* cam, const rt_render_params* p,
     K.tile_shard = p->tile_shard;
     K.img_tiles_x = (p->width + 7) / 8;
     K.n_rows = n_rows;
-    if (RT_PAUSE > 0) {   // suspended walks (trace_kernel.hpp RT_PAUSE): a slot per thread the grid can hold
-        if (!c->walk_save) {
-            HIP_TRY(hipStreamSynchronize(stream));
-            HIP_TRY(hipMalloc((void**)&c->walk_save,
-                              (size_t)c->n_cus * rtk::kWalkSaveThreadsPerCU * sizeof(rtk::WalkSave)));
-        }
-        K.walk_save = c->walk_save;
-    }
     K.tiles_x = (lay.w + 7) / 8;
     K.tiles_y = (n_rows + 7) / 8;
 
@@ -1408,9 +1296,6 @@ static int run_range(rt_ctx* c, const rt_camera* cam, const rt_render_params* p,
     // the TLAS in LDS (read-only, shared by the block) when it fits the per-block budget
     rtk::SceneDev S = c->S;
     S.n_lds_nodes = c->opt_lds_nodes ? std::min(c->n_tlas_nodes, kMaxLdsNodes) : 0;
-    // RT_WIDE: the spheres variant's whole-TLAS instantiation walks the 4-wide records
-    if (RT_WIDE && rtk::variant_features(o.features) == rtk::FEAT_SET_SPHERES && c->S.n_w4 > 0)
-        S.stack_entries = std::max(S.stack_entries, c->S.w4_stack);
     // small material and texture tables in LDS too (the variants with rects or media)
     const bool stage = c->opt_lds_nodes && c->n_materials <= kMaxLdsMaterials && c->n_textures <= kMaxLdsMaterials &&
                        c->n_materials > 0;
@@ -1984,6 +1869,51 @@ int rt_ctx_set_precision(rt_ctx* c, int precision)
     if (!c || (precision != RT_PREC_F64 && precision != RT_PREC_F32)) return fail(RT_ERR_INVALID, "bad precision");
     c->opt_precision = precision;
     return RT_OK;
+}
+
+int rt_ctx_set_option(rt_ctx* c, int key, int64_t v)
+{
+    if (!c) return fail(RT_ERR_INVALID, "null context");
+    switch (key) {
+    case RT_OPT_TRACE_BUF_BYTES:
+        if (v < 0) return fail(RT_ERR_INVALID, "negative buffer bound");
+        c->sample_buf_cap = v == 0 ? default_buf_cap() : std::max<size_t>((size_t)v, (size_t)1 << 20);
+        return RT_OK;
+    case RT_OPT_BATCH_OVERLAP: c->opt_overlap = v != 0; return RT_OK;
+    case RT_OPT_BLOCK_SAMPLES:
+        if (v < 0 || v > 1024) return fail(RT_ERR_INVALID, "block samples out of range (0..1024)");
+        c->block_samples = (int)v;
+        return RT_OK;
+    case RT_OPT_BLOCK_CHUNKS:
+        if (v < 0 || v > 64) return fail(RT_ERR_INVALID, "block chunks out of range (0..64)");
+        c->block_chunks = (int)v;
+        return RT_OK;
+    case RT_OPT_EXTRA_FEATURES:
+        if (v < 0 || (v & ~(int64_t)rtk::FEAT_ALL)) return fail(RT_ERR_INVALID, "unknown feature bits");
+        c->extra_features = (uint32_t)v;
+        return RT_OK;
+    case RT_OPT_HOIST: c->opt_hoist = v != 0; return RT_OK;
+    case RT_OPT_WF_PATHS:
+        if (v < 0 || v > ((int64_t)1 << 26)) return fail(RT_ERR_INVALID, "path slots out of range");
+        c->wf_paths = v;
+        return RT_OK;
+    default: return fail(RT_ERR_INVALID, "unknown option");
+    }
+}
+
+int rt_ctx_get_option(rt_ctx* c, int key, int64_t* v)
+{
+    if (!c || !v) return fail(RT_ERR_INVALID, "null argument");
+    switch (key) {
+    case RT_OPT_TRACE_BUF_BYTES: *v = (int64_t)c->sample_buf_cap; return RT_OK;
+    case RT_OPT_BATCH_OVERLAP: *v = c->opt_overlap; return RT_OK;
+    case RT_OPT_BLOCK_SAMPLES: *v = c->block_samples; return RT_OK;
+    case RT_OPT_BLOCK_CHUNKS: *v = c->block_chunks; return RT_OK;
+    case RT_OPT_EXTRA_FEATURES: *v = c->extra_features; return RT_OK;
+    case RT_OPT_HOIST: *v = c->opt_hoist; return RT_OK;
+    case RT_OPT_WF_PATHS: *v = c->wf_paths; return RT_OK;
+    default: return fail(RT_ERR_INVALID, "unknown option");
+    }
 }
 
 int rt_ctx_set_schedule(rt_ctx* c, int schedule)

@@ -35,7 +35,6 @@ struct Item {
     int ref;
     double lo[3], hi[3];
     double c[3];
-    double cost = 1.0;   // SAH intersection cost relative to the others (a dissolved instance's own)
 };
 
 struct Builder {
@@ -94,8 +93,8 @@ struct Builder {
             p.kind = RT_PRIM_BOX;
             p.p[0] = h.bmin.x; p.p[1] = h.bmin.y; p.p[2] = h.bmin.z;
             p.p[3] = h.bmax.x; p.p[4] = h.bmax.y; p.p[5] = h.bmax.z;
-            // the box's own bounds in f32, padded and rounded outward like a BVH node's, for
-            // the kernel's conservative pre-test before the 6 rect tests (rt_scene.h)
+            // the box's own bounds in f32, padded and rounded outward like a BVH node's
+            // (rt_scene.h; the kernel's per-box pre-test measured slower and is not built)
             const double lo[3] = {h.bmin.x, h.bmin.y, h.bmin.z}, hi[3] = {h.bmax.x, h.bmax.y, h.bmax.z};
             float fb[6];
             to_f32_box(lo, hi, fb, fb + 3);
@@ -181,28 +180,6 @@ struct Builder {
             b = r;
         }
         return b;
-    }
-
-    // The world box of a primitive under ops: a static sphere's centre mapped to world space
-    // (the same per-op formulas) +- r (tighter than its rotated object box); others box_through.
-    AABB world_box(const Ops& ops, int hid) const
-    {
-        const HNode& h = w.nodes[hid];
-        if (h.kind != HKind::Sphere) return box_through(ops, box_of(hid));
-        double x = h.c0.x, y = h.c0.y, z = h.c0.z;
-        for (int i = ops.n - 1; i >= 0; --i) {
-            if (ops.kind[i] == RT_OP_TRANSLATE) {
-                x += ops.op[i][0]; y += ops.op[i][1]; z += ops.op[i][2];
-                continue;
-            }
-            const double sn = ops.op[i][0], cs = ops.op[i][1];
-            const double nx = cs * x + sn * z, nz = -sn * x + cs * z;
-            x = nx;
-            z = nz;
-        }
-        // the mapped centre is off by a few ulps of the coordinates; to_f32_box pads by far more
-        const double r = std::fabs(h.radius);
-        return AABB{v3(x - r, y - r, z - r), v3(x + r, y + r, z + r)};
     }
 
     Item item_box(int prim, const AABB& b)
@@ -313,15 +290,7 @@ struct Builder {
         }
         std::vector<int> simple, complex;
         collect_split(child, simple, complex);
-        if (!simple.empty() && dissolve_inst && accel == RT_ACCEL_SAH) {
-            // Dissolved: one instance per leaf of the BVH, each with the whole chain, in the
-            // enclosing hierarchy under its world box — the walk then crosses the cluster's
-            // boxes in the same node loop as everything else instead of in a nested walk.
-            for (int hid : simple) {
-                items.push_back(item_box(make_instance(ops, RT_CHILD_PRIM, lower_simple_in(ops, hid)), world_box(ops, hid)));
-                items.back().cost = dissolve_cost;
-            }
-        } else if (!simple.empty()) {
+        if (!simple.empty()) {
             AABB b = box_of(simple[0]);
             for (int hid : simple) {
                 const AABB bi = box_of(hid);
@@ -555,34 +524,26 @@ struct Builder {
         // full-sweep SAH over the three axes (centroid order; ties by prim index)
         double best_cost = INFINITY;
         int best_axis = -1, best_split = -1;
-        // (costs: sums of the items' own; with every item at 1 these are the counts i and n - i)
-        std::vector<double> right_area(n), right_cost(n);
-        double total_cost = 0.0;
-        for (int i = b; i < e; ++i) total_cost += items[i].cost;
+        std::vector<double> right_area(n);
         for (int axis = 0; axis < 3; ++axis) {
             std::sort(items.begin() + b, items.begin() + e, [axis](const Item& x, const Item& y) {
                 return x.c[axis] < y.c[axis] || (x.c[axis] == y.c[axis] && x.prim < y.prim);
             });
             double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
-            double rcost = 0.0;
             for (int i = n - 1; i >= 1; --i) {
                 for (int a = 0; a < 3; ++a) {
                     lo[a] = std::min(lo[a], items[b + i].lo[a]);
                     hi[a] = std::max(hi[a], items[b + i].hi[a]);
                 }
-                rcost += items[b + i].cost;
                 right_area[i] = area(lo, hi);
-                right_cost[i] = rcost;
             }
             for (int a = 0; a < 3; ++a) { lo[a] = INFINITY; hi[a] = -INFINITY; }
-            double lcost = 0.0;
             for (int i = 1; i < n; ++i) {
                 for (int a = 0; a < 3; ++a) {
                     lo[a] = std::min(lo[a], items[b + i - 1].lo[a]);
                     hi[a] = std::max(hi[a], items[b + i - 1].hi[a]);
                 }
-                lcost += items[b + i - 1].cost;
-                double cost = c_trav + c_isect * (area(lo, hi) * lcost + right_area[i] * right_cost[i]) / std::max(parea, 1e-300);
+                double cost = c_trav + c_isect * (area(lo, hi) * i + right_area[i] * (n - i)) / std::max(parea, 1e-300);
                 if (cost < best_cost) {
                     best_cost = cost;
                     best_axis = axis;
@@ -590,7 +551,7 @@ struct Builder {
                 }
             }
         }
-        double leaf_cost = c_isect * total_cost;
+        double leaf_cost = c_isect * n;
         if (n <= max_leaf && leaf_cost <= best_cost) return make_leaf(items, b, e);
         if (best_axis < 0) best_axis = 0, best_split = n / 2;
         return split_at(items, b, e, best_axis, best_split, depth);
@@ -619,15 +580,6 @@ struct Builder {
     }
 
     int blas_depth = 0;   // max over instance BLASes
-    // RT_INST_DISSOLVE=1: an instance over a BVH of simple primitives becomes one instance per
-    // primitive in the enclosing SAH hierarchy (lower_instance). Same image; measured slower and
-    // off: C4 1920x1080x100 107.25 -> 131.29 ms (RT_DISSOLVE_CI 0.35 / 0.25, TLAS back under the
-    // LDS node cap: 149.1 / 158.9 ms; profiles/r04k_ab_c4.log). The instanced sphere tests then
-    // run in the top-level leaf loop beside box and medium tests (leaf-loop lane occupancy 0.330
-    // -> 0.237, leaf steps per wave iteration 11.7 -> 17.7, r04k_phases_c4*.log), where the
-    // deferred walk ran them together for the lanes that need them.
-    bool dissolve_inst = false;
-    double dissolve_cost = 1.0;   // RT_DISSOLVE_CI: a dissolved instance's SAH cost (the others' is 1)
 
     // LINEAR / MEDIAN: the list in order. Runs of primitives become <=31-prim leaves, a
     // subtree stays a child; node k = (segment k, node k+1), both boxes unbounded, so the
@@ -710,14 +662,14 @@ int flatten(World& w, int accel, std::string& err)
     FlatScene f;
     Builder bld{w, f, err};
     bld.accel = accel;
-    if (const char* e = std::getenv("RT_BVH_CI")) bld.c_isect = std::max(0.01, std::atof(e));
-    if (const char* e = std::getenv("RT_BVH_MAXLEAF")) bld.max_leaf = std::min(31, std::max(2, std::atoi(e)));
-    if (const char* e = std::getenv("RT_BVH_LEAFN")) bld.force_leaf = std::min(31, std::max(1, std::atoi(e)));
-    if (const char* e = std::getenv("RT_BVH_ROOTLEAF")) bld.root_leaf = std::min(31, std::max(0, std::atoi(e)));
-    if (const char* e = std::getenv("RT_BVH_BOXPAIRS")) bld.split_box_pairs = std::atoi(e) != 0;
-    if (const char* e = std::getenv("RT_BVH_BLASPAIRS")) bld.split_blas_pairs = std::atoi(e) != 0;
-    if (const char* e = std::getenv("RT_INST_DISSOLVE")) bld.dissolve_inst = std::atoi(e) != 0;
-    if (const char* e = std::getenv("RT_DISSOLVE_CI")) bld.dissolve_cost = std::max(0.01, std::atof(e));
+    // SAH build options (rt_world_set_build_option; defaults DESIGN.md §2 / §5.2)
+    const BuildOptions& bo = w.build;
+    if (bo.c_isect > 0.0) bld.c_isect = std::max(0.01, bo.c_isect);
+    if (bo.max_leaf > 0) bld.max_leaf = std::min(31, std::max(2, bo.max_leaf));
+    if (bo.force_leaf > 0) bld.force_leaf = std::min(31, std::max(1, bo.force_leaf));
+    if (bo.root_leaf >= 0) bld.root_leaf = std::min(31, bo.root_leaf);
+    if (bo.split_box_pairs >= 0) bld.split_box_pairs = bo.split_box_pairs != 0;
+    if (bo.split_blas_pairs >= 0) bld.split_blas_pairs = bo.split_blas_pairs != 0;
     std::vector<Item> top;
     for (int id : w.hittables) {  // M for the f32-slab padding (see to_f32_box)
         AABB b;

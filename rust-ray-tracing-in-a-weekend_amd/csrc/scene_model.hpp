@@ -91,6 +91,17 @@ struct FlatScene {
     rt_scene_soa soa{};
 };
 
+// SAH builder options of a world's flatten (rt_world_set_build_option; a value < 0, or 0 for the
+// sizes and the cost, keeps the builder's default)
+struct BuildOptions {
+    double c_isect = 0.0;       // RT_BUILD_C_ISECT: primitive-test cost relative to a node visit
+    int max_leaf = 0;           // RT_BUILD_MAX_LEAF: the largest leaf the cost model may pick
+    int force_leaf = 0;         // RT_BUILD_FORCE_LEAF: a set this small is always one leaf
+    int root_leaf = -1;         // RT_BUILD_ROOT_LEAF: a whole BVH of at most this many items is one leaf
+    int split_box_pairs = -1;   // RT_BUILD_SPLIT_BOX_PAIRS: pairs holding a Box / medium / BLAS instance split by cost
+    int split_blas_pairs = -1;  // RT_BUILD_SPLIT_BLAS_PAIRS: pairs inside instance BLASes split by cost
+};
+
 class World {
 public:
     explicit World(uint64_t scene_seed);
@@ -137,6 +148,7 @@ public:
     std::vector<HNode> nodes;
     std::vector<int> hittables;
     int n_media = 0;
+    BuildOptions build;
     FlatScene flat;
 };
 

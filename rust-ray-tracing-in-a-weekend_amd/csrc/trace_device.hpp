@@ -111,46 +111,18 @@ __device__ __forceinline__ bool first_active_lane()
 //   S32    conservative f32 slab tests (boxes padded on the host, see flatten.cpp)
 //   LDS    traversal stack in LDS (interleaved per lane) instead of scratch
 //   COUNT  diagnostic: count casts / node visits / primitive tests and time the phases
-// Traversal is while-while (Aila & Laine 2009); the if-if form and a per-lane state
-// machine with ballot-gated shading both measured slower.
+// Traversal is while-while (Aila & Laine 2009); the if-if form, speculative while-while and
+// a per-lane state machine with ballot-gated shading all measured slower (DESIGN.md §5.2;
+// the rejected experiments are kept as patches under scripts/experiments/).
 //   NALL   every TLAS node is in LDS (no per-node LDS/global choice)
 #ifndef RT_RECT_RCP
 #define RT_RECT_RCP 1   // rect / box tests divide through the ray's reciprocals (rects + instances variant only): round 3, without machine LICM, Cornell 800x800x200 45.76 vs 47.04 ms (r03d_ab_c3.log); round 2 measured it slower (58.1 vs 56.5) when its registers spilled
 #endif
-#ifndef RT_BOX_PRETEST
-#define RT_BOX_PRETEST 0   // slab pre-test of a Box before its 6 rect tests (measured slower: Cornell 58.5 vs 56.6 ms, final 83.3 vs 82.6, smoke 41.9 vs 39.9 — a culled lane saves no wave instructions unless the whole wave is culled)
-#endif
 #ifndef RT_BOX_RCP
 #define RT_BOX_RCP 1   // a Box's six sides divide through three per-box reciprocals (BoxRcp)
 #endif
-#ifndef RT_FINISH_AT_TRACE
-// pool schedules: a ray's traversal set-up (finish_ray) runs once per bounce iteration, for
-// every lane about to trace, instead of once in the camera step and once in shading (the wave
-// issued both exec-masked copies every iteration)
-#define RT_FINISH_AT_TRACE 1
-#endif
-#ifndef RT_MERGED_DRAWS
-// pool schedules: camera rays of new samples and scattered rays of the last iteration's hits
-// are generated in one step, their rejection-loop tries in one loop
-#define RT_MERGED_DRAWS 1
-#endif
-#ifndef RT_SPTR
-#define RT_SPTR 1
-#endif
-#ifndef RT_MED3
-#define RT_MED3 1
-#endif
-#ifndef RT_PK_SLAB
-#define RT_PK_SLAB 0   // packed-f32 (v_pk_fma_f32, op_sel) plane products of the two children: v_pk_fma_f32 issues in 4.1 cycles, two v_fma_f32 in 2 x 2.3 (profiles/r03b_calib.log); C2 76.34 vs 73.93 ms (r03b_ab_c2.log): rejected
-#endif
-#ifndef RT_TRACE_LOOP
-#define RT_TRACE_LOOP 1   // 0 if-if, 1 while-while, 2 while-while with speculative node visits
-#endif
-#ifndef RT_PERLIN_ROLLED
-#define RT_PERLIN_ROLLED 0   // rolled: C4 143.3 vs 136.9 ms unrolled (r03b_ab_c4.log); no spills either way without machine LICM
-#endif
 #ifndef RT_TRY_LEFT
-// pool schedules (RT_MERGED_DRAWS): the wave leaves its rejection loop (random_in_unit_disk /
+// pool schedules: the wave leaves its rejection loop (random_in_unit_disk /
 // random_in_unit_sphere tries, math.rs:51-76) once at most RT_TRY_LEFT lanes still reject, after
 // at least RT_TRY_MIN tries; those lanes keep their stream position and candidate state and go
 // on drawing in the next bounce-loop iteration instead of tracing in this one. Each lane's draws
@@ -160,24 +132,15 @@ __device__ __forceinline__ bool first_active_lane()
 // off 15.28 ms, 2 15.12, 4 15.07, 8 15.37, 4 after one try 15.22; images identical.
 #define RT_TRY_LEFT 4
 #endif
-#ifndef RT_TRY_ALL
-// the variants it applies to: the spheres ones (C2, C5) and the Cornell box's (C3 800x800x200
-// 46.00 -> 45.80 ms, profiles/r04d_ab_c3.log). The final scene's is 1-2 % slower with it (C4
-// 1920x1080x100 106.84 -> 109.04 ms, r04c_ab_c4.log; 107.83 -> 109.19, r04d_ab_c4.log): its
-// iterations are long, so a lane that sits one out loses more than the wave saves on tries
-#define RT_TRY_ALL 0
-#endif
 #ifndef RT_TRY_MIN
 #define RT_TRY_MIN 2
 #endif
+// the variants the cap applies to: the spheres ones (C2, C5) and the Cornell box's (C3 800x800x200
+// 46.00 -> 45.80 ms, profiles/r04d_ab_c3.log). The final scene's is 1-2 % slower with it (C4
+// 1920x1080x100 106.84 -> 109.04 ms, r04c_ab_c4.log; 107.83 -> 109.19, r04d_ab_c4.log): its
+// iterations are long, so a lane that sits one out loses more than the wave saves on tries
 template <class C>
-constexpr bool TryLeft() { return RT_TRY_LEFT > 0 && (RT_TRY_ALL || C::F == FEAT_SET_SPHERES || C::F == FEAT_SET_RECTINST); }
-#ifndef RT_KILL_H
-// pool schedules: the hit record carried across the loop edge (RT_MERGED_DRAWS) is marked dead
-// before the next trace (trace_world writes only the fields its primitive kind has, so the
-// compiler otherwise keeps the whole old record live through the walk)
-#define RT_KILL_H 1
-#endif
+constexpr bool TryLeft() { return RT_TRY_LEFT > 0 && (C::F == FEAT_SET_SPHERES || C::F == FEAT_SET_RECTINST); }
 //   F32    the f32 fast mode (Real = float): statistically, not bitwise, equal
 template <uint32_t F_, bool S32_, bool LDS_, bool NALL_, bool COUNT_, bool F32_ = false>
 struct Cfg {
@@ -187,7 +150,6 @@ struct Cfg {
     static constexpr bool NALL = NALL_;
     static constexpr bool COUNT = COUNT_;
     static constexpr bool F32 = F32_;
-    static constexpr int LOOP = RT_TRACE_LOOP;
     // threads per workgroup (RT_BLOCK_FINAL): a property of the launched kernel, inherited by the
     // reduced configurations of nested code (CfgDrop), which share its LDS stack
     static constexpr int BT = block_threads_of(F_, F32_);
@@ -224,9 +186,6 @@ using InstMedC = CfgDropStatic<C, FEAT_INST_MEDIUM>;   // a medium under an inst
 // (consecutive lanes hit consecutive banks) sized per scene by the host (TLAS depth +
 // BLAS depth); scratch: a private array (deep scenes).
 extern __shared__ int rt_lds[];  // [cached TLAS nodes] [stack entries x block lanes] [materials, textures]
-#ifndef RT_STACK_REMAT
-#define RT_STACK_REMAT 1
-#endif
 // The lane's index in its wave, recomputed where it is used (volatile: not CSE'd into one
 // value that stays live through the bounce loop; at 128 VGPRs the final variant spilled the
 // stack base it replaces and reloaded it from scratch at every walk)
@@ -265,30 +224,21 @@ struct Stack<false, false, BT> {
 // VGPRs, min_waves) — C2 1200x800x100 16.48 -> 15.40 ms, same bits (profiles/r02ao_*)
 #define RT_STACK16 1
 #endif
-#ifndef RT_STACK16_FINAL
-#define RT_STACK16_FINAL 0   // measured: the final variant with 16-bit entries (4 waves) 142.1 ms vs 132.7 with 32-bit (3 waves, LDS-bound); at 3 waves both ways 141.8 vs 132.4 (C4 1920x1080x100, r03f_ab_c4.log): the 16-bit stack itself costs ~7 % here
-#endif
 template <int BT>
 struct Stack16 {   // node records at LDS addresses < 32 KB, leaf codes > -32768 (SceneDev.stack16_ok)
     short* base;
     __device__ __forceinline__ short& operator[](int i) const { return base[i * BT]; }
 };
+// (the final-scene variant with 16-bit entries measured ~7 % slower: C4 1920x1080x100 142.1 vs
+// 132.7 ms, r03f_ab_c4.log; the spheres variant only)
 template <class C>
 constexpr bool Stack16Cfg()
 {
-    return RT_STACK16 && C::LDS && C::NALL && C::S32 && (C::F == FEAT_SET_SPHERES || (RT_STACK16_FINAL && C::F == FEAT_SET_FINAL)) &&
-           !C::F32;
+    return RT_STACK16 && C::LDS && C::NALL && C::S32 && C::F == FEAT_SET_SPHERES && !C::F32;
 }
-// the 4-wide TLAS walk (RT_WIDE, SceneDev.w4): the spheres variant with the whole TLAS in LDS
-template <class C>
-constexpr bool Wide() { return RT_WIDE && Stack16Cfg<C>() && C::F == FEAT_SET_SPHERES; }
-// (final-scene variant: 25 entries x 256 lanes x 2 B instead of 4 take its LDS per block from
-// 45.8 to 33.3 KB, so 4 blocks (4 waves per SIMD) share a CU instead of 3; the BLAS walk's leaf
-// codes are relative to the BLAS's first slot, rt_instance.pad on the device, abi.cpp)
 template <class C>
 using StackT = typename std::conditional<Stack16Cfg<C>(), Stack16<BlockThreads<C>()>,
-                                         Stack<C::LDS, C::LDS && RT_STACK_REMAT && (C::F & FEAT_INST_BLAS) != 0,
-                                               BlockThreads<C>()>>::type;
+                                         Stack<C::LDS, C::LDS && (C::F & FEAT_INST_BLAS) != 0, BlockThreads<C>()>>::type;
 
 // Division by a value b used many times, through its correctly rounded reciprocal
 // y = RN(1/b): q0 = RN(q*y), then one correction q1 = RN(q0 + RN-exact(q - b*q0) * y).
@@ -390,15 +340,9 @@ __device__ __forceinline__ void finish_ray(RayT<typename C::Real>& r, bool spher
         r.sz.y = -(float)r.oz * r.sz.x;
         // the LDS node (LdsNode): per axis [lo0 lo1 hi0 hi1 lo0 lo1] at bytes 0/24/48; the
         // near planes of both children at +0 (direction >= 0) or +8, the far ones 8 bytes on
-        if constexpr (Wide<C>()) {   // W4Node: per axis 48 B, the near quadruple at +0 or +16
-            r.onx = r.sx.x >= 0.0f ? 0u : 16u;
-            r.ony = r.sy.x >= 0.0f ? 48u : 64u;
-            r.onz = r.sz.x >= 0.0f ? 96u : 112u;
-        } else {
-            r.onx = r.sx.x >= 0.0f ? 0u : 8u;
-            r.ony = r.sy.x >= 0.0f ? 24u : 32u;
-            r.onz = r.sz.x >= 0.0f ? 48u : 56u;
-        }
+        r.onx = r.sx.x >= 0.0f ? 0u : 8u;
+        r.ony = r.sy.x >= 0.0f ? 24u : 32u;
+        r.onz = r.sz.x >= 0.0f ? 48u : 56u;
     } else {
         r.ix = (typename C::Real)1 / r.dx;
         r.iy = (typename C::Real)1 / r.dy;
@@ -627,96 +571,13 @@ __device__ __forceinline__ void box_side(const rt_prim& p, int side, int& axis, 
     else { axis = 2; a0 = mny; a1 = mxy; b0 = mnz; b1 = mxz; k = side == 4 ? mxx : mnx; }
 }
 
-#ifndef RT_BOX_CAND
-// Box candidate sides: a conservative f32 test per side first, the exact
-// f64 rect test only on the sides that can pass it. Measured slower and off: C4 1920x1080x100
-// 111.30 vs 107.23 ms with six sides, leaf-test share 0.338 vs 0.329 (profiles/r04b_ab_c4.log,
-// r04b_phases_c4*.log): a wave enters an axis's block when any lane has a candidate there, and
-// the lanes testing a box are mostly the ones that hit it (entry and exit sides on two or three
-// axes), so the wave still runs about three exact tests and a reciprocal per axis, plus the
-// candidate test itself.
-#define RT_BOX_CAND 0
-#endif
-// The variants that take it: the final scene's (400 boxes at the top level, f32 slab terms
-// in every ray). In the Cornell variants (f64 slabs, boxes under instances) its values cost a
-// wave per SIMD (rects + instances 122 -> 137 VGPRs, media 121 -> 141: 4 -> 3 waves).
-template <class C>
-constexpr bool BoxCand() { return RT_BOX_CAND && C::S32 && !C::F32 && C::F == FEAT_SET_FINAL; }
-// The sides of a Box whose exact rect test (hittable.rs:308-384) can pass, as a bit mask
-// (bit s = side s of box_side). The box record holds its bounds padded outward and rounded
-// to f32 (lo', hi': flatten.cpp, the padding a BVH node box gets) and w = twice the largest
-// padding (upload, rt_prim.b = 2). Side s lies on the plane k of axis A; take the thin slab
-// [k - pad, k + pad] on A (lo face: [lo', lo' + w], hi face: [hi' - w, hi']). If the exact
-// test of side s passes at t*, the point o + t* d lies on the side's rect (to f64 rounding),
-// so t* lies inside the padded slabs of the two other axes and inside the thin slab of A, the
-// padding covering the f32 rounding of the slab products exactly as it does for a BVH node
-// (|o| <= 2M); and t* is in [t_min, t_max]. So s is a candidate when the intersection of those
-// three t intervals with [t_min, t_max] (rounded outward) is non-empty: a slab test of the
-// side's padded flat box. A side that is not a candidate fails its exact test (with this
-// t_max, and with any smaller one), so testing the candidates only, in side order with the
-// same t_max updates, gives the reference's (t, side) bit for bit.
-template <bool S32, class R>
-__device__ __forceinline__ uint32_t box_candidates(const rt_prim& p, const RayT<R>& r, R t_min, R t_max)
-{
-    using T = typename std::conditional<S32, float, R>::type;
-    const float* fb = reinterpret_cast<const float*>(&p.p[6]);
-    const T w = (T)reinterpret_cast<const float*>(&p.p[9])[0];
-    // t of plane x on axis a: f32 x * (1/d) - o/d with the ray's slab terms (finish_ray), or f64
-    auto tp = [&](int a, T x) -> T {
-        if constexpr (S32) {
-            const f2v sa = a == 0 ? r.sx : a == 1 ? r.sy : r.sz;
-            return __builtin_fmaf(x, sa.x, sa.y);
-        } else {
-            return (x - (a == 0 ? r.ox : a == 1 ? r.oy : r.oz)) * (a == 0 ? r.ix : a == 1 ? r.iy : r.iz);
-        }
-    };
-    T nr[3], fr[3];   // the padded box's slab per axis
-#pragma unroll
-    for (int a = 0; a < 3; ++a) {
-        const T tl = tp(a, (T)fb[a]), th = tp(a, (T)fb[3 + a]);
-        nr[a] = fmin(tl, th);
-        fr[a] = fmax(tl, th);
-    }
-    T tmn, tmx;
-    if constexpr (S32) {
-        tmn = f32_down(t_min);
-        tmx = f32_up(t_max);
-    } else {
-        tmn = t_min;
-        tmx = t_max;
-    }
-    uint32_t m = 0;
-#pragma unroll
-    for (int a = 0; a < 3; ++a) {   // axis a = x, y, z: its hi side 4 - 2a, lo side 5 - 2a
-        const int b = a == 0 ? 1 : 0, c = a == 2 ? 1 : 2;
-        const T tn = fmax(fmax(nr[b], nr[c]), tmn), tf = fmin(fmin(fr[b], fr[c]), tmx);
-        // the face slabs [lo', lo' + w] and [hi' - w, hi'] (plane products recomputed: fewer live values)
-        const T tl = tp(a, (T)fb[a]), tli = tp(a, (T)fb[a] + w);
-        const T th = tp(a, (T)fb[3 + a]), thi = tp(a, (T)fb[3 + a] - w);
-        if (fmax(fmin(th, thi), tn) <= fmin(fmax(th, thi), tf)) m |= 1u << (4 - 2 * a);
-        if (fmax(fmin(tl, tli), tn) <= fmin(fmax(tl, tli), tf)) m |= 1u << (5 - 2 * a);
-    }
-    return m;
-}
-
 // Box::hit = hit_hittables over its sides (hittable.rs:229-231): closest, ties to the later side.
-// The reference has no bounding-box pre-test (Q8); a conservative one on the box's padded
-// f32 bounds (flatten.cpp) only skips rect tests that cannot hit, like a BVH node box does.
-template <bool RCP = false, bool S32 = true, bool LRCP = false, bool CAND = false, class R>
+// No bounding-box pre-test, like the reference (Q8): a per-box slab pre-test and per-side
+// candidate tests both measured slower (a lane that skips a test saves the wave nothing unless
+// every lane does).
+template <bool RCP = false, bool LRCP = false, class R>
 __device__ __forceinline__ bool box_t(const rt_prim& p, const RayT<R>& r, R t_min, R t_max, R& t, int& side)
 {
-    if (RT_BOX_PRETEST && p.b) {
-        const float* fb = reinterpret_cast<const float*>(&p.p[6]);
-        bool hit;
-        if constexpr (S32) {
-            float tn;
-            hit = slab32(fb, fb + 3, r, f32_down(t_min), f32_up(t_max), tn);
-        } else {
-            R tn;
-            hit = slab(fb, fb + 3, r, t_min, t_max, tn);
-        }
-        if (!hit) return false;
-    }
     bool any = false;
     // f64: the six sides divide by three directions; one correctly rounded reciprocal y per
     // direction and a Markstein step per side (RN(q / d) bit for bit when y = RN(1 / d): see
@@ -724,45 +585,6 @@ __device__ __forceinline__ bool box_t(const rt_prim& p, const RayT<R>& r, R t_mi
     // direction component outside [2^-900, 2^900], e.g. an exact 0, divides as the reference).
     constexpr bool LOCAL_RCP = LRCP && !RCP && std::is_same<R, double>::value;
     auto in_range = [](R d) { const R m = r_fabs(d); return m >= (R)0x1.0p-900 && m <= (R)0x1.0p+900; };
-    if constexpr (CAND && std::is_same<R, double>::value) {
-        // candidate sides only (box_candidates), with every direction component in [2^-60, 2^60]
-        // (finite f32 slab terms; outside, e.g. an exact 0, all six sides run below). Per axis
-        // one block, entered by the wave when any lane has a candidate on that axis: a lane
-        // tests its pair's first candidate, and the second only in the rare case that both are
-        // (a box thinner than its padding); the sides keep their order 0..5.
-        auto cand_range = [](R d) { const R m = r_fabs(d); return m >= (R)0x1.0p-60 && m <= (R)0x1.0p+60; };
-        if (p.b == 2 && cand_range(r.dx) && cand_range(r.dy) && cand_range(r.dz)) {
-            const uint32_t m = box_candidates<S32>(p, r, t_min, t_max);
-            const R mnx = (R)p.p[0], mny = (R)p.p[1], mnz = (R)p.p[2], mxx = (R)p.p[3], mxy = (R)p.p[4], mxz = (R)p.p[5];
-#pragma unroll
-            for (int ax = 0; ax < 3; ++ax) {   // rect axis: 0 XY (k on z, sides 0/1), 1 XZ (y, 2/3), 2 YZ (x, 4/5)
-                const uint32_t bits = (m >> (2 * ax)) & 3u;
-                if (bits == 0) continue;
-                const R a0 = ax == 2 ? mny : mnx, a1 = ax == 2 ? mxy : mxx;
-                const R b0 = ax == 0 ? mny : mnz, b1 = ax == 0 ? mxy : mxz;
-                const R kmax = ax == 0 ? mxz : ax == 1 ? mxy : mxx, kmin = ax == 0 ? mnz : ax == 1 ? mny : mnx;
-                const R dk = ax == 0 ? r.dz : ax == 1 ? r.dy : r.dx;
-                R y = (R)0;
-                if constexpr (RCP) y = ax == 0 ? r.yz : ax == 1 ? r.yy : r.yx;
-                else if constexpr (LOCAL_RCP) y = (R)1 / dk;
-                auto test = [&](int s, R k) {
-                    R ts;
-                    bool ok;
-                    if constexpr (RCP || LOCAL_RCP) ok = rect_t_y(ax, a0, a1, b0, b1, k, r, y, t_min, t_max, ts);
-                    else ok = rect_t<false>(ax, a0, a1, b0, b1, k, r, t_min, t_max, ts);
-                    if (ok) {
-                        t_max = ts;
-                        t = ts;
-                        side = s;
-                        any = true;
-                    }
-                };
-                test((bits & 1u) ? 2 * ax : 2 * ax + 1, (bits & 1u) ? kmax : kmin);
-                if (bits == 3u) test(2 * ax + 1, kmin);
-            }
-            return any;
-        }
-    }
     if (LOCAL_RCP && in_range(r.dx) && in_range(r.dy) && in_range(r.dz)) {
         R y = (R)0;   // of the side pair's direction (sides 2a, 2a+1 share axis a)
 #pragma unroll
@@ -835,7 +657,7 @@ __device__ __forceinline__ bool simple_t(const rt_prim& p, const RayT<R>& r, R t
         case RT_PRIM_XY_RECT: return rect_t<RectRcp<C>()>(0, q0, q1, q2, q3, q4, r, t_min, t_max, t);
         case RT_PRIM_XZ_RECT: return rect_t<RectRcp<C>()>(1, q0, q1, q2, q3, q4, r, t_min, t_max, t);
         case RT_PRIM_YZ_RECT: return rect_t<RectRcp<C>()>(2, q0, q1, q2, q3, q4, r, t_min, t_max, t);
-        case RT_PRIM_BOX: return box_t<RectRcp<C>(), C::S32, BoxRcp<C>(), BoxCand<C>()>(p, r, t_min, t_max, t, side);
+        case RT_PRIM_BOX: return box_t<RectRcp<C>(), BoxRcp<C>()>(p, r, t_min, t_max, t, side);
         default: return false;
         }
     }
@@ -890,12 +712,6 @@ __device__ __forceinline__ Node load_node(const rt_bvh_node* base, int i)
 // generic pointer that may be LDS or global would be read with flat loads)
 __device__ __forceinline__ Node load_node_lds(uint32_t addr);
 
-// The variants whose LDS node visits use packed-f32 plane products (v_pk_fma_f32 with op_sel:
-// 6 instead of 12 FMAs per visit, no extra registers; round 2's broadcast-pair form cost ~4
-// VGPRs and was rejected)
-template <class C>
-constexpr bool PkSlab() { return RT_PK_SLAB != 0; }
-
 // The TLAS node as staged in LDS by the variants whose whole TLAS is there and whose slab
 // tests are f32 (OctNodes): per axis both children's lower planes, upper planes and the lower
 // ones again, so a ray reads its near and far planes with one 16-B (2 x 8-B) read at an
@@ -919,10 +735,8 @@ __device__ __forceinline__ const __attribute__((address_space(3))) T* lds_ptr(ui
 template <class C>
 constexpr int lds_node_bytes()
 {
-    return Wide<C>() ? (int)sizeof(W4Node) : OctNodes<C>() ? (int)sizeof(LdsNode) : (int)sizeof(rt_bvh_node);
+    return OctNodes<C>() ? (int)sizeof(LdsNode) : (int)sizeof(rt_bvh_node);
 }
-template <class C>
-__device__ __forceinline__ int lds_node_count(const SceneDev& S) { return Wide<C>() ? S.n_w4 : S.n_lds_nodes; }
 __device__ __forceinline__ Node load_node_lds(uint32_t addr)
 {
     typedef unsigned u4v __attribute__((ext_vector_type(4)));
@@ -967,7 +781,7 @@ constexpr bool StageBlas() { return RT_STAGE_BLAS && (C::F & FEAT_INST_BLAS) != 
 template <class C>
 __device__ __forceinline__ LdsLayout lds_layout_of(const SceneDev& S)
 {
-    return lds_layout(lds_node_count<C>(S), lds_node_bytes<C>(), StageBlas<C>() ? S.n_lds_blas : 0, C::LDS ? S.stack_entries : 0,
+    return lds_layout(S.n_lds_nodes, lds_node_bytes<C>(), StageBlas<C>() ? S.n_lds_blas : 0, C::LDS ? S.stack_entries : 0,
                       Stack16Cfg<C>() ? 2 : 4, StageShade<C>() ? S.n_lds_materials : 0,
                       StageShade<C>() ? S.n_lds_textures : 0, BlockThreads<C>());
 }
@@ -975,57 +789,28 @@ __device__ __forceinline__ LdsLayout lds_layout_of(const SceneDev& S)
 // Closest hit in a BVH (nodes + leaf ranges of slots j, whose records are leaf_prims[j]).
 // `leaf(slot, t_max, best)` tests one primitive; on a closer hit it fills best (t and sub
 // ids) and returns true; best.prim is then the slot.
-// PAUSE (RT_PAUSE): the walk may be suspended (see RT_PAUSE) into *ws, *paused set, and
-// resumed from it (resume: root, t_max and best come from *ws instead).
-template <class C, bool NL = false, bool PAUSE = false, class LeafFn, class R = typename C::Real>
+template <class C, bool NL = false, class LeafFn, class R = typename C::Real>
 __device__ __forceinline__ bool traverse(const SceneDev& S, int root, const RayT<R>& r, R t_min, R t_max,
-                                         HitRefT<R>& best, StackT<C>& stack, int sp0, Count& cnt, LeafFn&& leaf,
-                                         WalkSave* ws = nullptr, bool resume = false, bool* paused = nullptr,
-                                         bool may_pause = false, bool pre_any = false)
+                                         HitRefT<R>& best, StackT<C>& stack, int sp0, Count& cnt, LeafFn&& leaf)
 {
     // NL: this is the TLAS, whose first S.n_lds_nodes nodes (BFS order) were copied into
     // LDS at block start; deeper nodes are read from L1/L2
     const rt_bvh_node* lds_nodes =
         reinterpret_cast<const rt_bvh_node*>(rt_lds);   // at LDS address 0: node offsets are addresses
-    bool any = PAUSE && pre_any;   // PAUSE: the caller's pre-leaf hit travels with the walk's state
+    bool any = false;
     // the walk's bottom entry is RT_DONE (the host reserves it: SceneDev.stack_entries,
     // blas_base), so a pop needs no empty-stack test: popping it ends the walk
     constexpr int DONE = Stack16Cfg<C>() ? -32768 : RT_DONE;   // the walk's bottom entry
-#if RT_SPTR
     // the stack pointer as an address, pre-scaled by the entry stride: a push or pop is one
     // add (not an add plus a shift-add of the index)
     constexpr int SSTR = C::LDS ? BlockThreads<C>() : 1;
     auto* sptr = &stack[sp0];
     using SE = typename std::remove_reference<decltype(*sptr)>::type;
-    if (!(PAUSE && resume)) {
-        *sptr = (SE)DONE;
-        sptr += SSTR;
-    }
+    *sptr = (SE)DONE;
+    sptr += SSTR;
     auto push = [&](int v) { *sptr = (SE)v; sptr += SSTR; };
     auto pop = [&]() -> int { sptr -= SSTR; return (int)*sptr; };
-#else
-    stack[sp0] = DONE;
-    int sp = sp0 + 1;
-    auto push = [&](int v) { stack[sp++] = v; };
-    auto pop = [&]() -> int { return stack[--sp]; };
-#endif
     int cur = root;
-    if constexpr (PAUSE) {
-        // ws: the block's slots; the lane's is its thread index, recovered from its stack column's
-        // address where that is an LDS column (no register held for it through the bounce loop)
-        if constexpr (Stack16Cfg<C>())
-            ws += (int)(stack.base - reinterpret_cast<short*>(rt_lds + lds_stack_offset<C>(S)));
-        else
-            ws += threadIdx.x;
-        if (resume) {   // the suspended walk: its node (already an LDS address), stack depth, t_max, hit
-            cur = ws->cur;
-            sptr += ws->sp;
-            t_max = (R)ws->t_max;
-            best.t = (R)ws->best_t;
-            best.prim = ws->best_prim;
-            any = ws->any != 0;
-        }
-    }
     float tmin_f = 0.0f, tmax_f = 0.0f;
     if constexpr (C::S32) {
         tmin_f = f32_down(t_min);
@@ -1038,65 +823,15 @@ __device__ __forceinline__ bool traverse(const SceneDev& S, int root, const RayT
     // min(far planes). One address add per axis, the child pair at a fixed offset.
     constexpr bool OCT = NL && OctNodes<C>();
     float ninf = -__builtin_inff();
-    if constexpr (OCT && RT_MED3) asm("s_mov_b32 %0, 0xff800000" : "=s"(ninf));
+    if constexpr (OCT) asm("s_mov_b32 %0, 0xff800000" : "=s"(ninf));
     const char* const lb = reinterpret_cast<const char*>(lds_nodes);
     uint32_t blas_lds_base = 0;   // LDS byte address of the staged BLAS nodes (nested walks)
     if constexpr (!NL && StageBlas<C>()) blas_lds_base = lds_addr(lb) + (uint32_t)lds_layout_of<C>(S).blas;
     (void)blas_lds_base;
-    // t_min's f32 bound in a register set once per walk (an asm result: not rematerialized as a
-    // v_mov inside the node loop, which machine LICM no longer hoists)
-    float tmin_v = tmin_f;
-    if constexpr (OCT && PkSlab<C>()) asm("v_mov_b32 %0, %1" : "=v"(tmin_v) : "v"(tmin_f));
-    constexpr bool W4 = OCT && Wide<C>();   // the 4-wide TLAS: its root record (index 0) is the walk's start
-    if (!(PAUSE && resume)) {
-        if constexpr (W4) cur = cur >= 0 ? (int)lds_addr(lb) : cur;
-        else if constexpr (OCT) cur = cur >= 0 ? (int)(lds_addr(lb) + (uint32_t)cur * (uint32_t)sizeof(LdsNode)) : cur;
-    }
+    if constexpr (OCT) cur = cur >= 0 ? (int)(lds_addr(lb) + (uint32_t)cur * (uint32_t)sizeof(LdsNode)) : cur;
     // one node visit: test both children, continue with the nearer, push the farther
     auto visit = [&](int node) -> int {
         if (C::COUNT) cnt.nodes++;
-#if RT_SPTR
-        if constexpr (W4) {
-            // four children: near / far plane quadruples per axis (two ds_read_b128 each), the
-            // same conservative f32 slab test per child as the binary visit; the nearest hit child
-            // continues, the other hits are pushed (a two-round tournament on the entry distances:
-            // the winner of the other pair last, so it pops first) with branch-free pushes
-            const uint32_t nb = (uint32_t)node;
-            typedef float f4v __attribute__((ext_vector_type(4)));
-            typedef int i4v __attribute__((ext_vector_type(4)));
-            const f4v nx = *lds_ptr<f4v>(nb + r.onx), fx = *lds_ptr<f4v>(nb + r.onx + 16u);
-            const f4v ny = *lds_ptr<f4v>(nb + r.ony), fy = *lds_ptr<f4v>(nb + r.ony + 16u);
-            const f4v nz = *lds_ptr<f4v>(nb + r.onz), fz = *lds_ptr<f4v>(nb + r.onz + 16u);
-            const i4v ch = *lds_ptr<i4v>(nb + (uint32_t)offsetof(W4Node, child));
-            const float INF = __builtin_inff();
-            float k[4];
-#pragma unroll
-            for (int c = 0; c < 4; ++c) {
-                const float ax = __builtin_fmaf(nx[c], r.sx.x, r.sx.y), bx = __builtin_fmaf(fx[c], r.sx.x, r.sx.y);
-                const float ay = __builtin_fmaf(ny[c], r.sy.x, r.sy.y), by = __builtin_fmaf(fy[c], r.sy.x, r.sy.y);
-                const float az = __builtin_fmaf(nz[c], r.sz.x, r.sz.y), bz = __builtin_fmaf(fz[c], r.sz.x, r.sz.y);
-                const float tn = fmaxf(fmaxf(ax, ay), fmaxf(az, tmin_f));
-                const float tf = fminf(fminf(bx, by), __builtin_amdgcn_fmed3f(bz, tmax_f, ninf));
-                k[c] = tn <= tf ? tn : INF;
-            }
-            const bool a01 = k[0] <= k[1], a23 = k[2] <= k[3];
-            const float kA = a01 ? k[0] : k[1], lA = a01 ? k[1] : k[0];
-            const int rA = a01 ? ch.x : ch.y, qA = a01 ? ch.y : ch.x;
-            const float kB = a23 ? k[2] : k[3], lB = a23 ? k[3] : k[2];
-            const int rB = a23 ? ch.z : ch.w, qB = a23 ? ch.w : ch.z;
-            const bool aN = kA <= kB;
-            const float kN = aN ? kA : kB, kS = aN ? kB : kA;
-            const int rN = aN ? rA : rB, rS = aN ? rB : rA;
-            if (kN == INF) return pop();
-            *sptr = (SE)qA;
-            sptr += lA < INF ? SSTR : 0;
-            *sptr = (SE)qB;
-            sptr += lB < INF ? SSTR : 0;
-            *sptr = (SE)rS;
-            sptr += kS < INF ? SSTR : 0;
-            return rN;
-        }
-#endif
         if constexpr (OCT) {
             const uint32_t nb = (uint32_t)node;   // LDS address of the node
             typedef float f2v __attribute__((ext_vector_type(2)));
@@ -1112,31 +847,6 @@ __device__ __forceinline__ bool traverse(const SceneDev& S, int root, const RayT
             pairs(r.onz, npz, fpz);
             const i2v ch = *lds_ptr<i2v>(nb + (uint32_t)offsetof(LdsNode, child));
             float tn[2], tf[2];
-            if constexpr (PkSlab<C>()) {
-            // Both children's plane of one axis in one v_pk_fma_f32, the ray's (1/d, -o/d) pair of
-            // the axis read as factor / addend for both halves (op_sel): 6 instead of 12 FMAs per
-            // visit, no broadcast copies, the same single rounding as v_fma_f32. The reductions
-            // are raw v_max3 / v_max / v_med3 / v_min3 as well: through fmaxf the compiler would
-            // first quiet each asm result (v_max x, x), which FMA results never need (the
-            // products are finite: f32_inv_dir bounds 1/d).
-            f2v nx, ny, nz, fx, fy, fz;
-#define RT_PKFMA(d, a, b) asm("v_pk_fma_f32 %0, %1, %2, %2 op_sel:[0,0,1] op_sel_hi:[1,0,1]" : "=v"(d) : "v"(a), "v"(b))
-            RT_PKFMA(nx, npx, r.sx);
-            RT_PKFMA(ny, npy, r.sy);
-            RT_PKFMA(nz, npz, r.sz);
-            RT_PKFMA(fx, fpx, r.sx);
-            RT_PKFMA(fy, fpy, r.sy);
-            RT_PKFMA(fz, fpz, r.sz);
-#undef RT_PKFMA
-#pragma unroll
-            for (int c = 0; c < 2; ++c) {
-                float a, b;
-                asm("v_max3_f32 %0, %1, %2, %3" : "=v"(a) : "v"(nx[c]), "v"(ny[c]), "v"(nz[c]));
-                asm("v_max_f32 %0, %1, %2" : "=v"(tn[c]) : "v"(a), "v"(tmin_v));
-                asm("v_med3_f32 %0, %1, %2, %3" : "=v"(b) : "v"(fz[c]), "v"(tmax_f), "s"(ninf));
-                asm("v_min3_f32 %0, %1, %2, %3" : "=v"(tf[c]) : "v"(fx[c]), "v"(fy[c]), "v"(b));
-            }
-            } else {
 #pragma unroll
             for (int c = 0; c < 2; ++c) {
                 const float nx = __builtin_fmaf(c ? npx.y : npx.x, r.sx.x, r.sx.y);
@@ -1149,9 +859,7 @@ __device__ __forceinline__ bool traverse(const SceneDev& S, int root, const RayT
                 // min(fz, t_max) as v_med3(fz, t_max, -inf): fminf would re-quiet the loop-carried
                 // t_max (a v_max_f32 t, t) at every visit; the plane products are never NaN.
                 // (-inf from an SGPR: with the constant the compiler folds med3 back to fminf.)
-                tf[c] = RT_MED3 ? fminf(fminf(fx, fy), __builtin_amdgcn_fmed3f(fz, tmax_f, ninf))
-                                : fminf(fminf(fx, fy), fminf(fz, tmax_f));
-            }
+                tf[c] = fminf(fminf(fx, fy), __builtin_amdgcn_fmed3f(fz, tmax_f, ninf));
             }
             const bool h0 = tn[0] <= tf[0], h1 = tn[1] <= tf[1], near0 = tn[0] <= tn[1];
             if (h0 && h1) {
@@ -1206,77 +914,18 @@ __device__ __forceinline__ bool traverse(const SceneDev& S, int root, const RayT
             }
         }
     };
-    if constexpr (C::LOOP == 0) {
-        while (cur != DONE) {
-            if (cur < 0) {
-                do_leaf(cur);
-                cur = pop();
-            } else {
-                cur = visit(cur);
-            }
+    uint64_t t0 = 0;
+    while (cur != DONE) {
+        if (C::COUNT && NL) t0 = __builtin_amdgcn_s_memtime();
+        while (cur >= 0) {
+            if (C::COUNT && first_active_lane()) cnt.wave_nodes++;
+            cur = visit(cur);
         }
-    } else if constexpr (C::LOOP == 1) {
-        uint64_t t0 = 0;
-        int leaves = 0;
-        (void)leaves;
-        while (cur != DONE) {
-            if constexpr (PAUSE) {
-                // every lane still walking is here (the wave's outer-loop head): few enough left?
-                // RT_PAUSE_ONCE: a resumed walk is not suspended again; while one is still walking the
-                // wave walks on anyway, so then no lane is suspended
-                const bool eligible = !(RT_PAUSE_ONCE && resume);
-                if (may_pause && ++leaves > RT_PAUSE_MIN && __popcll(__ballot(1)) <= RT_PAUSE &&
-                    __ballot(!eligible) == 0) {
-                    ws->cur = cur;
-                    ws->sp = (int32_t)(sptr - &stack[sp0]);
-                    ws->t_max = (double)t_max;
-                    ws->best_t = (double)best.t;
-                    ws->best_prim = best.prim;
-                    ws->any = any ? 1 : 0;
-                    *paused = true;
-                    break;
-                }
-            }
-            if (C::COUNT && NL) t0 = __builtin_amdgcn_s_memtime();
-            while (cur >= 0) {
-                if (C::COUNT && first_active_lane()) cnt.wave_nodes++;
-                cur = visit(cur);
-            }
-            if (NL) RT_STAMP(cnt.t_nodes, t0);   // the TLAS walk only: a nested walk is part of its leaf
-            if (cur == DONE) break;
-            do_leaf(cur);
-            cur = pop();
-            if (NL) RT_STAMP(cnt.t_leaves, t0);
-        }
-    } else {
-        // Speculative while-while (Aila & Laine 2009, §4): a lane that reaches a leaf parks
-        // it and keeps visiting nodes until every lane still in the node loop holds one,
-        // so the node loop runs with more lanes busy; then each lane tests one leaf.
-        int parked = 0;  // 0: none; else a leaf code (< 0, never RT_DONE)
-        for (;;) {
-            while (cur >= 0) {
-                if (C::COUNT && first_active_lane()) cnt.wave_nodes++;
-                cur = visit(cur);
-                if (cur < 0 && cur != DONE && parked == 0) {
-                    parked = cur;
-                    cur = pop();
-                }
-                if (__all(parked != 0)) break;
-            }
-            int lf;
-            if (parked != 0) {
-                lf = parked;
-                parked = 0;
-            } else if (cur != DONE && cur < 0) {
-                lf = cur;
-                cur = pop();
-            } else if (cur == DONE) {
-                break;
-            } else {
-                continue;
-            }
-            do_leaf(lf);
-        }
+        if (NL) RT_STAMP(cnt.t_nodes, t0);   // the TLAS walk only: a nested walk is part of its leaf
+        if (cur == DONE) break;
+        do_leaf(cur);
+        cur = pop();
+        if (NL) RT_STAMP(cnt.t_leaves, t0);
     }
     return any;
 }
@@ -1330,8 +979,8 @@ __device__ bool instance_t(const SceneDev& S, const rt_instance& in, const RayT<
                 return true;
             }
         }
-        // one primitive: no node-slab terms (the candidate-side box test reads them)
-        finish_ray<C, BoxCand<InstC<C>>()>(r, S.has_spheres != 0);
+        // one primitive: no node-slab terms
+        finish_ray<C, false>(r, S.has_spheres != 0);
         int side = 0;
         if (!simple_t<InstC<C>>(S.prims[in.child], r, t_min, t_max, ref.t, side, cnt, (C::F & FEAT_SHUTTER) != 0)) return false;
         ref.sub = in.child;
@@ -1484,10 +1133,6 @@ constexpr bool PreLeaf() { return C::F == FEAT_SET_SPHERES; }
 template <class C>
 constexpr bool DeferInst() { return RT_DEFER_INST && (C::F & FEAT_INST_BLAS) != 0; }
 
-// the variants whose top-level walk may be suspended (RT_PAUSE): the spheres ones (C2, C5)
-template <class C>
-constexpr bool Pause() { return RT_PAUSE > 0 && C::F == FEAT_SET_SPHERES && !C::F32; }
-
 // The variants that walk a one-leaf top level (the Cornell scenes: S.tlas_root is a leaf code) as
 // a plain loop over its slots: no stack, no node loop, a loop count the same in every lane (scalar
 // control instead of exec-masked loops). Measured: C3 800x800x200 45.71 -> 41.88 ms, Cornell smoke
@@ -1501,12 +1146,10 @@ constexpr bool Pause() { return RT_PAUSE > 0 && C::F == FEAT_SET_SPHERES && !C::
 template <class C>
 constexpr bool UniformLeaf() { return RT_UNIFORM_LEAF && (C::F & FEAT_INST_BLAS) == 0 && !PreLeaf<C>(); }
 
-// HitRecord of the closest primitive. Pause<C>(): with ws, the top-level walk may be
-// suspended (*paused: no record; the lane resumes it with resume = true next iteration).
+// HitRecord of the closest primitive.
 template <class C, class R = typename C::Real>
 __device__ bool trace_world(const SceneDev& S, const RayT<R>& r, HitT<R>& h, StackT<C>& stack, const Keyed& key,
-                            Count& cnt, WalkSave* ws = nullptr, bool resume = false, bool* paused = nullptr,
-                            bool may_pause = false)
+                            Count& cnt)
 {
     const R t_min = (R)0.001;
     HitRefT<R> best;
@@ -1552,7 +1195,7 @@ __device__ bool trace_world(const SceneDev& S, const RayT<R>& r, HitT<R>& h, Sta
         R t_max = (R)RT_INF;
         hit = false;
         int root = S.tlas_root;
-        if (S.pre_leaf != 0 && !(Pause<C>() && resume)) {   // wave-uniform: the huge root-child leaf first (SceneDev.pre_leaf)
+        if (S.pre_leaf != 0) {   // wave-uniform: the huge root-child leaf first (SceneDev.pre_leaf)
             root = S.pre_root;
             bool in_box;
             if constexpr (C::S32) {
@@ -1575,17 +1218,7 @@ __device__ bool trace_world(const SceneDev& S, const RayT<R>& r, HitT<R>& h, Sta
         }
         if (S.pre_leaf != 0) root = S.pre_root;
         RT_STAMP(cnt.t_pre, tp);
-        if constexpr (Pause<C>()) {   // (ws is NULL only without a walk_save buffer: no suspension then)
-            bool susp = false;
-            hit = traverse<C, true, true>(S, root, r, t_min, t_max, best, stack, 0, cnt, leaf, ws, resume, &susp,
-                                          may_pause && ws != nullptr, hit);
-            if (susp) {
-                *paused = true;
-                return false;
-            }
-        } else {
-            hit |= traverse<C, true>(S, root, r, t_min, t_max, best, stack, 0, cnt, leaf);
-        }
+        hit |= traverse<C, true>(S, root, r, t_min, t_max, best, stack, 0, cnt, leaf);
     } else {
         RT_STAMP(cnt.t_pre, tp);
         if (UniformLeaf<C>() && S.tlas_root < 0 && S.tlas_root != RT_DONE) {   // (wave-uniform)
@@ -1660,26 +1293,13 @@ __device__ R perlin_noise(const double* ranvec, const int32_t* perm, R px, R py,
     const R vv = v * v * ((R)3 - (R)2 * v);
     const R ww = w * w * ((R)3 - (R)2 * w);
     R accum = (R)0;
-    // RT_PERLIN_ROLLED: the corner and octave loops stay rolled, so the 8 corners' table loads are
-    // not all in flight (and live) at once: the Perlin texture (one sphere of the final scene)
-    // set the final-scene variant's register peak (158 VGPRs before RA with the loops unrolled)
-#if RT_PERLIN_ROLLED
-#pragma unroll 1
-#else
+    // (the corner and octave loops unrolled: rolled measured slower, C4 143.3 vs 136.9 ms,
+    // r03b_ab_c4.log)
 #pragma unroll
-#endif
     for (int di = 0; di < 2; ++di)
-#if RT_PERLIN_ROLLED
-#pragma unroll 1
-#else
 #pragma unroll
-#endif
         for (int dj = 0; dj < 2; ++dj)
-#if RT_PERLIN_ROLLED
-#pragma unroll 1
-#else
 #pragma unroll
-#endif
             for (int dk = 0; dk < 2; ++dk) {
                 const uint32_t xi = ((uint32_t)i + (uint32_t)di) & 255u;
                 const uint32_t yi = ((uint32_t)j + (uint32_t)dj) & 255u;
@@ -1698,9 +1318,6 @@ template <class R>
 __device__ R perlin_turb(const double* ranvec, const int32_t* perm, R px, R py, R pz)
 {
     R accum = (R)0, weight = (R)1;
-#if RT_PERLIN_ROLLED
-#pragma unroll 1
-#endif
     for (int i = 0; i < 7; ++i) {
         accum += weight * perlin_noise(ranvec, perm, px, py, pz);
         weight *= (R)0.5;
@@ -1960,16 +1577,7 @@ __device__ __forceinline__ void stage_lds(const SceneDev& S)
     bool any = false;
     const int off = 0;   // the TLAS nodes first (traverse)
     if (S.n_lds_nodes > 0) {
-        if constexpr (Wide<C>()) {   // the 4-wide records, child indices -> LDS byte addresses
-            W4Node* dst = reinterpret_cast<W4Node*>(rt_lds + off);
-            for (int i = threadIdx.x; i < S.n_w4; i += BlockThreads<C>()) {
-                W4Node o = S.w4[i];
-#pragma unroll
-                for (int c = 0; c < 4; ++c)
-                    if (o.child[c] >= 0) o.child[c] = (int)(lds_addr(dst) + (uint32_t)o.child[c] * (uint32_t)sizeof(W4Node));
-                dst[i] = o;
-            }
-        } else if constexpr (OctNodes<C>()) {   // one node per thread, rt_bvh_node -> LdsNode
+        if constexpr (OctNodes<C>()) {   // one node per thread, rt_bvh_node -> LdsNode
             LdsNode* dst = reinterpret_cast<LdsNode*>(rt_lds + off);
             for (int i = threadIdx.x; i < S.n_lds_nodes; i += BlockThreads<C>()) {
                 const rt_bvh_node n = S.nodes[i];
@@ -2021,7 +1629,7 @@ __device__ __forceinline__ void stage_lds(const SceneDev& S)
 // as the reference's per-sample sum. In three steps: shade_begin (emission; false if the
 // path ends there), the material's draws (random_in_unit_sphere unless Dielectric), and
 // shade_end (the scattered ray; false if Metal absorbs it). shade() runs them in a row; the
-// pool schedules run the draws in one rejection loop with the camera's (RT_MERGED_DRAWS).
+// pool schedules run the draws in one rejection loop with the camera's.
 template <class C, class R = typename C::Real>
 __device__ __forceinline__ bool shade_begin(const SceneDev& S, const HitT<R>& h, R Tr, R Tg, R Tb, double& sum_r,
                                             double& sum_g, double& sum_b)
@@ -2194,7 +1802,6 @@ __device__ __forceinline__ bool lane_work(const KParams& P, LaneWork& w)
     return true;
 }
 
-// LOOP 0/1: every lane traces its cast to the end, then every lane shades.
 #ifndef RT_MIN_WAVES_SPHERES
 #define RT_MIN_WAVES_SPHERES 1
 #endif
@@ -2325,7 +1932,7 @@ __global__ void __launch_bounds__(BlockThreads<C>(), min_waves<C>()) trace_chunk
 // ([tile][sample][pixel of the tile], tiled_record); reduce_samples then sums every pixel's samples in sample order,
 // so the image does not depend on which lane or wave computed a sample.
 // ---------------------------------------------------------------------------
-// The hit record's old contents are dead (RT_KILL_H): freeze(poison) for every field, so the
+// The hit record's old contents are dead: freeze(poison) for every field, so the
 // register allocator need not carry them through the walk that writes the next record.
 template <class R>
 __device__ __forceinline__ void forget(HitT<R>& h)
@@ -2398,19 +2005,10 @@ __global__ void __launch_bounds__(BlockThreads<C>(), min_waves<C>()) trace_pool(
     Keyed key{P.seed, 0, 0, 0};
     rt_pstream st;
     RayT<R> r;
-    HitT<R> h;             // RT_MERGED_DRAWS: a hit whose scattered ray the next iteration draws
+    HitT<R> h;             // a hit whose scattered ray the next iteration draws
     bool pending = false;
-    (void)pending;
     bool cam_wait = false;  // RT_TRY_LEFT: camera_begin ran, the disk tries go on (u, v in r.dx, r.dy)
     (void)cam_wait;
-    // RT_PAUSE: the lane's suspended top-level walk (the block's slots in KParams.walk_save)
-    bool walk_paused = false;
-    WalkSave* ws = nullptr;
-    if constexpr (Pause<C>()) {
-        if (P.walk_save) ws = P.walk_save + (size_t)blockIdx.x * BlockThreads<C>();
-    }
-    (void)walk_paused;
-    (void)ws;
     for (;;) {
         if (ITEMS && own) {
             own = false;
@@ -2486,7 +2084,6 @@ __global__ void __launch_bounds__(BlockThreads<C>(), min_waves<C>()) trace_pool(
             t_prev = tw;
             RT_STAMP(cnt.t_refill, t_prev);
         }
-#if RT_MERGED_DRAWS
         // Ray generation: the camera rays of new samples and the scattered rays of last
         // iteration's hits (pending), whose random_in_unit_disk / random_in_unit_sphere tries
         // run in one rejection loop (the wave used to run the two loops one after the other).
@@ -2496,9 +2093,7 @@ __global__ void __launch_bounds__(BlockThreads<C>(), min_waves<C>()) trace_pool(
         {
             R u = 0, v = 0;
             bool tries = false;
-            if (Pause<C>() && walk_paused) {
-                // the lane's walk resumes in the trace step (its ray kept in r)
-            } else if (new_sample) {
+            if (new_sample) {
                 if (TryLeft<C>() && cam_wait) {   // camera_begin ran: the jitter waits in r.dx / r.dy
                     u = r.dx;
                     v = r.dy;
@@ -2536,8 +2131,7 @@ __global__ void __launch_bounds__(BlockThreads<C>(), min_waves<C>()) trace_pool(
                 while (tries && !unit_try(st, (R)P.scale_m11, three, qx, qy, qz, l2)) {
                 }
             }
-            if (Pause<C>() && walk_paused) {
-            } else if (gen_wait) {   // (RT_TRY_LEFT) no trace this iteration; pending / new_sample stay set
+            if (gen_wait) {   // (RT_TRY_LEFT) no trace this iteration; pending / new_sample stay set
                 go = false;
                 if (new_sample) {
                     cam_wait = true;
@@ -2556,17 +2150,13 @@ __global__ void __launch_bounds__(BlockThreads<C>(), min_waves<C>()) trace_pool(
         RT_STAMP(t_cam, t_prev);
         if (go && depth > 0) {  // main.rs:21-23: depth 0 is black
             key.bounce = (uint32_t)(P.max_depth - depth);
-            if (C::COUNT && !walk_paused) cnt.casts++;
+            if (C::COUNT) cnt.casts++;
             finish_ray<C>(r, S.has_spheres != 0);
-            if (RT_KILL_H) forget(h);
+            forget(h);
             RT_STAMP(cnt.t_setup, t_prev);
-            bool suspended = false;
-            // no suspension once the grid's work is exhausted: no new walks would fill the lanes
-            const bool hit = trace_world<C>(S, r, h, stack, key, cnt, ws, walk_paused, &suspended, !exhausted);
-            walk_paused = suspended;
+            const bool hit = trace_world<C>(S, r, h, stack, key, cnt);
             if (C::COUNT) t_prev = __builtin_amdgcn_s_memtime();   // trace_world stamped its phases
-            if (Pause<C>() && suspended) {
-            } else if (!hit) {  // main.rs:37: background
+            if (!hit) {  // main.rs:37: background
                 cr = cr + Tr * P.bg[0];
                 cg = cg + Tg * P.bg[1];
                 cb = cb + Tb * P.bg[2];
@@ -2580,7 +2170,7 @@ __global__ void __launch_bounds__(BlockThreads<C>(), min_waves<C>()) trace_pool(
             RT_STAMP(t_shade, t_prev);
         }
         if (C::COUNT) t_prev = __builtin_amdgcn_s_memtime();   // lanes that did not trace
-        if (pending || gen_wait || walk_paused) {
+        if (pending || gen_wait) {
         } else if (ITEMS && left > 0) {  // the item's next sample: the lane takes it at the loop top
             active = false;
             own = true;
@@ -2594,63 +2184,6 @@ __global__ void __launch_bounds__(BlockThreads<C>(), min_waves<C>()) trace_pool(
             o[2] = cb;
             active = false;
         }
-#else
-        if (new_sample) {
-            if (C::COUNT) {
-                cnt.cam_lanes++;
-                if (first_active_lane()) cnt.cam_steps++;
-            }
-            new_sample = false;
-            int ix, y;
-            image_xy(P, x, k, ix, y);
-            key.pixel = (uint32_t)y * (uint32_t)P.img_width + (uint32_t)ix;
-            key.sample = (uint32_t)s;
-            ds_start(st, P.seed, key.pixel, (uint32_t)s);
-            camera_ray(P, ix, y, st, r);
-            if constexpr (!RT_FINISH_AT_TRACE) finish_ray<C>(r, S.has_spheres != 0);
-            Tr = Tg = Tb = (R)1;
-            if constexpr (!ITEMS) cr = cg = cb = 0.0;  // ITEMS: the chunk's running sum
-            depth = P.max_depth;
-        }
-        if (C::COUNT) { const uint64_t t = __builtin_amdgcn_s_memtime(); t_cam += t - t_prev; t_prev = t; }
-        bool cont = false;
-        if (depth > 0) {  // main.rs:21-23: depth 0 is black
-            key.bounce = (uint32_t)(P.max_depth - depth);
-            if (C::COUNT) cnt.casts++;
-            if constexpr (RT_FINISH_AT_TRACE) finish_ray<C>(r, S.has_spheres != 0);
-            HitT<R> h;
-            const bool hit = trace_world<C>(S, r, h, stack, key, cnt);
-            if (C::COUNT) { const uint64_t t = __builtin_amdgcn_s_memtime(); t_trace += t - t_prev; t_prev = t; }
-            if (!hit) {  // main.rs:37: background
-                cr = cr + Tr * P.bg[0];
-                cg = cg + Tg * P.bg[1];
-                cb = cb + Tb * P.bg[2];
-            } else {
-                if (C::COUNT) {
-                    cnt.shade_lanes++;
-                    if (first_active_lane()) cnt.shade_steps++;
-                }
-                cont = shade<C, !RT_FINISH_AT_TRACE>(S, P, h, r, st, Tr, Tg, Tb, cr, cg, cb);
-            }
-        }
-        if (C::COUNT) { const uint64_t t = __builtin_amdgcn_s_memtime(); t_shade += t - t_prev; t_prev = t; }
-        if (cont) {
-            depth -= 1;
-        } else if (ITEMS && left > 0) {  // the item's next sample: the lane takes it at the loop top
-            active = false;
-            own = true;
-        } else {
-            // per-sample pool: this sample's radiance (tiled_record order); items: the chunk's
-            // partial (the chunk of its last sample), [chunk][pixel]
-            double* o = ITEMS ? samples + ((size_t)((unsigned)(s - P.sample_begin) / (unsigned)P.spp_chunk) * n_px +
-                                           (size_t)k * P.width + x) * 3
-                              : samples + tiled_record(P.tiles_x, P.spp - P.sample_begin, x, k, s - P.sample_begin) * 3;
-            o[0] = cr;
-            o[1] = cg;
-            o[2] = cb;
-            active = false;
-        }
-#endif
     }
     if (C::COUNT) {
         atomicAdd(&counters[0], (unsigned long long)cnt.casts);
@@ -2723,14 +2256,12 @@ template <uint32_t F, bool S32, bool LDS, bool COUNT, bool F32>
 static void launch_one(const Launch& L, hipStream_t stream, bool nall)
 {
     const SceneDev& S = *L.S;
-    const bool s16 = RT_STACK16 && LDS && nall && S32 && (F == FEAT_SET_SPHERES || (RT_STACK16_FINAL && F == FEAT_SET_FINAL)) &&
-                     !F32;   // Stack16Cfg
-    const bool wide = RT_WIDE && s16 && F == FEAT_SET_SPHERES;   // Wide
-    const int node_bytes = wide ? (int)sizeof(W4Node) : nall && S32 ? (int)sizeof(LdsNode) : (int)sizeof(rt_bvh_node);   // lds_node_bytes
+    const bool s16 = RT_STACK16 && LDS && nall && S32 && F == FEAT_SET_SPHERES && !F32;   // Stack16Cfg
+    const int node_bytes = nall && S32 ? (int)sizeof(LdsNode) : (int)sizeof(rt_bvh_node);   // lds_node_bytes
     const bool stage = F != FEAT_SET_SPHERES;                   // StageShade
     const bool blas = RT_STAGE_BLAS && (F & FEAT_INST_BLAS) != 0 && !F32;   // StageBlas
     constexpr int bt = block_threads_of(F, F32), wpb = bt / 64;   // BlockThreads
-    const size_t lds = lds_layout(wide ? S.n_w4 : S.n_lds_nodes, node_bytes, blas ? S.n_lds_blas : 0, LDS ? S.stack_entries : 0,
+    const size_t lds = lds_layout(S.n_lds_nodes, node_bytes, blas ? S.n_lds_blas : 0, LDS ? S.stack_entries : 0,
                                   s16 ? 2 : 4, stage ? S.n_lds_materials : 0, stage ? S.n_lds_textures : 0, bt).total;
     if (L.pool) {
         auto go = [&](auto kernel) {
@@ -2764,7 +2295,7 @@ static void launch_f(const Launch& L, int slab32, int lds, hipStream_t stream)
     bool nall = S.n_lds_nodes > 0 && S.n_lds_nodes == S.n_tlas_nodes;
     // the whole-TLAS spheres instantiation keeps 16-bit stack entries (Stack16Cfg): a scene
     // whose node addresses or leaf codes do not fit takes the partial-TLAS instantiation
-    constexpr bool S16F = F == FEAT_SET_SPHERES || (RT_STACK16_FINAL && F == FEAT_SET_FINAL);   // Stack16Cfg's feature sets
+    constexpr bool S16F = F == FEAT_SET_SPHERES;   // Stack16Cfg's feature set
     if (RT_STACK16 && S16F && slab32 && lds && !S.stack16_ok) nall = false;
     // stack16_ok (abi.cpp) assumes the node records start at LDS address 0, i.e. that rt_lds is
     // the kernels' only __shared__ object: a static __shared__ variable would move the dynamic

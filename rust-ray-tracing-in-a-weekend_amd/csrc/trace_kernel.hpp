@@ -13,12 +13,6 @@
 #define RT_DEFER_INST 1
 #endif
 
-// 4-wide TLAS in the spheres variant (A/B experiment): the binary SAH tree
-// collapsed two levels per node (W4Node), walked with one 4-child visit per step
-#ifndef RT_WIDE
-#define RT_WIDE 0
-#endif
-
 // Threads per workgroup of the final-scene variant's kernels (the others: 256). 512 (8 waves)
 // shares one LDS copy of the TLAS and materials among twice the waves, which leaves room for
 // the instanced BLAS in LDS (SceneDev.n_lds_blas; the host sizes that budget with it): the
@@ -35,17 +29,6 @@ __host__ __device__ constexpr int block_threads_of(uint32_t variant_features, bo
 {
     return variant_features == 287u /* FEAT_SET_FINAL */ && !f32 ? RT_BLOCK_FINAL : 256;
 }
-
-// A 4-wide TLAS node (RT_WIDE): binary node n with each internal child replaced by that child's
-// two children. Per axis the four children's lower planes, upper planes and lower planes again,
-// so a ray reads its four near planes and four far planes as two 16-B reads at +0 (direction
-// >= 0) or +16; children as W4 indices (LDS byte addresses once staged), leaf codes, or an
-// empty slot (box +inf..-inf, never hit).
-struct W4Node {
-    float ax[3][12];
-    int32_t child[4];
-};
-static_assert(sizeof(W4Node) == 160, "W4Node layout");
 
 // Device view of the uploaded rt_scene_soa tables.
 struct SceneDev {
@@ -87,38 +70,7 @@ struct SceneDev {
     // nodes[n_tlas_nodes, n_tlas_nodes + n_blas_bfs) (abi.cpp), and a launch stages the first
     // n_lds_blas of them (its LDS budget): the nested walk's top levels then read LDS
     int32_t n_blas_bfs, n_lds_blas;
-    // RT_WIDE: the 4-wide TLAS from the walk's start node (pre_root with a hoisted leaf, else
-    // tlas_root), its record count and the stack entries its walk needs (+ sentinel, + the
-    // branch-free push's spare slot)
-    const W4Node* w4;
-    int32_t n_w4, w4_stack;
 };
-
-#ifndef RT_PAUSE
-// Walk suspension (regrouping live rays across bounce iterations): in the
-// spheres variant's top-level walk, once at most RT_PAUSE lanes of the wave are still walking
-// (checked at each leaf, after RT_PAUSE_MIN of them), those lanes store their walk state (node,
-// stack pointer, t_max, closest hit so far) to a per-thread slot in global memory and leave
-// the walk; the wave goes on to shade and generate rays for its other lanes, and the suspended
-// lanes resume their walk in the next iteration's trace step beside the new walks, so the
-// wave no longer idles behind its longest walks. The stack stays in the lane's LDS column; the
-// ray stays in its registers (it is live across the loop edge anyway). Closest hit does not
-// depend on when the steps run, so the bits do not change. 0: off.
-#define RT_PAUSE 0
-#endif
-#ifndef RT_PAUSE_MIN
-#define RT_PAUSE_MIN 2
-#endif
-#ifndef RT_PAUSE_ONCE
-#define RT_PAUSE_ONCE 0
-#endif
-// A suspended top-level walk (RT_PAUSE, trace_device.hpp): 32 B per thread of the persistent
-// grid (KParams.walk_save, allocated by the context: walk_save_threads() slots)
-struct WalkSave {
-    double t_max, best_t;
-    int32_t cur, sp, best_prim, any;
-};
-constexpr int kWalkSaveThreadsPerCU = 2048;   // the most threads a CU holds at once
 
 struct KParams {
     rt_camera cam;
@@ -141,7 +93,6 @@ struct KParams {
     int32_t img_width;          // the image's width (pixel keys)
     int32_t tile_shard;         // rt_render_params.tile_shard: grid tile m = the frame's tile row_begin + m*row_stride
     int32_t img_tiles_x;        // tiles per tile row of the image
-    WalkSave* walk_save;        // RT_PAUSE builds: one slot per thread of the persistent grid (NULL: no suspension)
 };
 
 // Scene features (which code a kernel variant must contain).

@@ -41,6 +41,21 @@ RT_PREC_F32 = 1
 RT_ACCEL_SAH = 0
 RT_ACCEL_LINEAR = 1     # hit_hittables linear scan (hittable.rs:31-41)
 RT_ACCEL_MEDIAN = 2     # the reference BvhNode hierarchy (hittable.rs:77-130)
+# context options (rt_ctx_set_option)
+RT_OPT_TRACE_BUF_BYTES = 1
+RT_OPT_BATCH_OVERLAP = 2
+RT_OPT_BLOCK_SAMPLES = 3
+RT_OPT_BLOCK_CHUNKS = 4
+RT_OPT_EXTRA_FEATURES = 5
+RT_OPT_HOIST = 6
+RT_OPT_WF_PATHS = 7
+# SAH builder options (rt_world_set_build_option)
+RT_BUILD_C_ISECT = 1
+RT_BUILD_MAX_LEAF = 2
+RT_BUILD_FORCE_LEAF = 3
+RT_BUILD_ROOT_LEAF = 4
+RT_BUILD_SPLIT_BOX_PAIRS = 5
+RT_BUILD_SPLIT_BLAS_PAIRS = 6
 
 # every symbol include/rt/rt_abi.h declares
 EXPORTED = [
@@ -56,7 +71,7 @@ EXPORTED = [
     "rt_write_ppm_f64", "rt_write_color",
     "rt_ctx_set_variant", "rt_device_eval", "rt_accum_create", "rt_accum_destroy", "rt_accum_add",
     "rt_accum_get", "rt_accum_set", "rt_accum_resolve", "rt_render_progressive", "rt_ctx_set_schedule", "rt_ctx_set_precision",
-    "rt_scene_validate",
+    "rt_scene_validate", "rt_build_info", "rt_ctx_set_option", "rt_ctx_get_option", "rt_world_set_build_option",
 ]
 
 # int (*rt_progress_fn)(void* user, int64_t samples_done, int64_t samples_total)
@@ -147,7 +162,10 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     PI = ctypes.POINTER(ctypes.c_int)
     PD = ctypes.POINTER(ctypes.c_double)
     sigs = {
-        "rt_abi_version": ([], I), "rt_last_error": ([], ctypes.c_char_p),
+        "rt_abi_version": ([], I), "rt_last_error": ([], ctypes.c_char_p), "rt_build_info": ([], ctypes.c_char_p),
+        "rt_ctx_set_option": ([P, I, ctypes.c_int64], I),
+        "rt_ctx_get_option": ([P, I, ctypes.POINTER(ctypes.c_int64)], I),
+        "rt_world_set_build_option": ([P, I, D], I),
         "rt_device_count": ([PI], I), "rt_ctx_create": ([I, ctypes.POINTER(P)], I),
         "rt_ctx_destroy": ([P], None), "rt_world_create": ([U64, ctypes.POINTER(P)], I),
         "rt_world_destroy": ([P], None), "rt_world_texture_solid": ([P, D, D, D, PI], I),
@@ -189,11 +207,18 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
                                    P], I),
     }
     for name, (args, res) in sigs.items():
-        fn = getattr(lib, name)
+        fn = getattr(lib, name, None)
+        if fn is None:   # an older build (A/B runs); build() and tests/test_abi.py check every export
+            continue
         fn.argtypes = args
         fn.restype = res
     _lib = lib
     return lib
+
+
+def build_info() -> str:
+    """rt_build_info: the source hash the loaded library was compiled from."""
+    return load_library().rt_build_info().decode()
 
 
 def _check(rc: int, what: str) -> None:
@@ -276,6 +301,11 @@ class World:
 
     def push(self, hid):
         _check(self.lib.rt_world_push(self.h, hid), "rt_world_push")
+
+    def set_build_option(self, key: int, value: float):
+        """rt_world_set_build_option: an SAH builder option of this world's flatten (RT_BUILD_*)."""
+        _check(self.lib.rt_world_set_build_option(self.h, key, float(value)), "rt_world_set_build_option")
+        return self
 
     def build_scene(self, scene_id: int, image: Optional[np.ndarray] = None):
         """The reference's scene builders (main.rs:52-289)."""
@@ -517,6 +547,15 @@ class Renderer:
         """RT_PREC_F64 (default: path-identical to the oracle, last-ulp summation differences) or
         RT_PREC_F32 (fast mode, statistical parity)."""
         _check(self.lib.rt_ctx_set_precision(self.h, precision), "rt_ctx_set_precision")
+
+    def set_option(self, key: int, value: int):
+        """rt_ctx_set_option (RT_OPT_*): buffer bound, batch overlap, block sizes, extra features, ..."""
+        _check(self.lib.rt_ctx_set_option(self.h, key, int(value)), "rt_ctx_set_option")
+
+    def get_option(self, key: int) -> int:
+        v = ctypes.c_int64()
+        _check(self.lib.rt_ctx_get_option(self.h, key, ctypes.byref(v)), "rt_ctx_get_option")
+        return v.value
 
     def set_variant(self, slab32: int = 1, lds_stack: int = 1, lds_nodes: int = 1):
         _check(self.lib.rt_ctx_set_variant(self.h, slab32, lds_stack, lds_nodes), "rt_ctx_set_variant")

@@ -40,7 +40,8 @@ for _ in range(a["reps"]):
     r.render(cam, p, out)
     ms.append(r.stats().kernel_ms)
 import hashlib
-print("RESULT", json.dumps({{"ms": ms, "img": hashlib.sha1(img.tobytes()).hexdigest()}}))
+print("RESULT", json.dumps({{"ms": ms, "img": hashlib.sha1(img.tobytes()).hexdigest(),
+                            "frame": hashlib.sha1(out.tobytes()).hexdigest()}}))
 """
 
 
@@ -71,14 +72,15 @@ def main():
             line = [x for x in out.stdout.splitlines() if x.startswith("RESULT ")][-1]
             d = json.loads(line[7:])
             res[lib] += d["ms"]
-            imgs[lib] = d["img"]
+            imgs[lib] = (d["img"], d.get("frame"))
             print(f"  {lib}: {['%.2f' % m for m in d['ms']]}", flush=True)
     base = imgs[a.libs[0]]
     n = a.width * a.height * a.spp
     for lib in a.libs:
         ms = sorted(res[lib])[len(res[lib]) // 2]
         print(f"{lib}: median {ms:.2f} ms  min {min(res[lib]):.2f}  -> {n / ms / 1e3:.1f} Msamples/s  "
-              f"image == {a.libs[0]}: {imgs[lib] == base}")
+              f"image == {a.libs[0]}: {imgs[lib][0] == base[0]}  whole timed frame == {a.libs[0]}: "
+              f"{imgs[lib][1] == base[1]}")
 
 
 if __name__ == "__main__":

@@ -12,6 +12,13 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 
 
+def bvh_options(rt, world, b):
+    """(c_isect, max_leaf, force_leaf) as rt_world_set_build_option values (0: the default)."""
+    world.set_build_option(rt.RT_BUILD_C_ISECT, float(b[0]))
+    world.set_build_option(rt.RT_BUILD_MAX_LEAF, float(b[1]))
+    world.set_build_option(rt.RT_BUILD_FORCE_LEAF, float(b[2]))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--scene", type=int, default=0)
@@ -123,17 +130,17 @@ def main():
         r.set_variant(*variants[0])
         for rnd in range(args.rounds + 1):
             for b in builds:
-                os.environ["RT_BVH_CI"], os.environ["RT_BVH_MAXLEAF"], os.environ["RT_BVH_LEAFN"] = b
+                bvh_options(rt, world, b)
                 r.upload(world)
                 r.render(cam, p, out)
                 if rnd > 0:
                     bt[b].append(r.stats().kernel_ms)
         for b in builds:
-            os.environ["RT_BVH_CI"], os.environ["RT_BVH_MAXLEAF"], os.environ["RT_BVH_LEAFN"] = b
+            bvh_options(rt, world, b)
             soa = world.flatten()
             print(f"bvh ci={b[0]} maxleaf={b[1]} leafn={b[2]} nodes={soa.n_nodes} depth={soa.tlas_depth}/{soa.blas_depth}: "
                   f"median {float(np.median(bt[b])):.2f} ms")
-        os.environ.pop("RT_BVH_CI"); os.environ.pop("RT_BVH_MAXLEAF")
+        bvh_options(rt, world, ("0", "0", "0"))   # the defaults
         r.upload(world)
     # phase shares from the diagnostic count_work variant (first variant's knobs), at the
     # timed run's chunk size so the lane-occupancy figures describe the same waves

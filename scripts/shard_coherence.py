@@ -38,11 +38,10 @@ def main():
         cases += [(n, "tiles", None) for n in (2, 4, 8)]
     renderers = {}
     for n, block, bs in cases:
-        if bs not in renderers:   # RT_BLOCK_SAMPLES is read at context creation
-            if bs:
-                os.environ["RT_BLOCK_SAMPLES"] = str(bs)
+        if bs not in renderers:
             renderers[bs] = rt.Renderer(0)
-            os.environ.pop("RT_BLOCK_SAMPLES", None)
+            if bs:
+                renderers[bs].set_option(rt.RT_OPT_BLOCK_SAMPLES, bs)
             renderers[bs].upload(world)
         r = renderers[bs]
         if block == "tiles":

@@ -60,20 +60,32 @@ def test_flatten_all_scenes(rt, scene_id):
         assert soa.n_media == 2 and soa.n_instances == 2
 
 
-def test_final_scene_dissolved_cluster_flattens(rt, monkeypatch):
-    """RT_INST_DISSOLVE=1 (flatten.cpp lower_instance): the final scene's Translate(RotateY(BVH
-    of 1000 spheres)) becomes 1000 one-sphere instances in the top-level SAH tree — no BLAS left,
-    every instance reachable from the TLAS once, and rt_scene_validate accepts the tables."""
-    monkeypatch.setenv("RT_INST_DISSOLVE", "1")
+def test_build_options_change_the_tree_not_the_scene(rt):
+    """rt_world_set_build_option (the SAH knobs, no environment variable): forcing every set of
+    two into one leaf and disabling the Box-pair rule builds a different final-scene tree from
+    the same primitives; the tables stay valid; an unknown key or a NaN is refused."""
+    a = rt.SceneSoA.from_buffer_copy(rt.World(1).build_scene(7).flatten())
     w = rt.World(1).build_scene(7)
-    soa = rt.SceneSoA.from_buffer_copy(w.flatten())
-    prims, refs, nodes, inst = soa_tables(soa)
-    assert soa.n_instances == 1000 and soa.blas_depth == 0
-    assert np.all(inst["kind"] == 0) and np.all(inst["n_ops"] == 2)
-    kinds = np.frombuffer(prims.tobytes(), "<i4").reshape(-1, 24)[:, 0]
-    walk = reachable(soa.tlas_root, refs, nodes)
-    assert sorted(int(kinds[i]) == 6 for i in walk).count(True) == 1000 and len(set(walk)) == len(walk)
-    assert rt.validate_soa(soa)[1] == 0
+    w.set_build_option(rt.RT_BUILD_SPLIT_BOX_PAIRS, 0).set_build_option(rt.RT_BUILD_SPLIT_BLAS_PAIRS, 0)
+    b = rt.SceneSoA.from_buffer_copy(w.flatten())
+    assert a.n_prims == b.n_prims and a.n_prim_refs == b.n_prim_refs
+    assert a.n_nodes != b.n_nodes
+    rt.validate_soa(b)
+    w.set_build_option(rt.RT_BUILD_SPLIT_BOX_PAIRS, -1).set_build_option(rt.RT_BUILD_SPLIT_BLAS_PAIRS, -1)
+    c = rt.SceneSoA.from_buffer_copy(w.flatten())
+    assert c.n_nodes == a.n_nodes   # defaults restored
+    with pytest.raises(rt.RTError):
+        w.set_build_option(99, 1.0)
+    with pytest.raises(rt.RTError):
+        w.set_build_option(rt.RT_BUILD_C_ISECT, float("nan"))
+
+
+def test_library_build_identity_matches_sources(rt):
+    """the loaded library carries the source hash it was compiled from
+    (rt_build_info); it must be the hash of the tree it sits in, or profiles keyed by that hash
+    would describe another build."""
+    import __graft_entry__ as ge
+    assert rt.build_info() == ge.source_hash(), (rt.build_info(), ge.source_hash())
 
 
 NODE_DT = np.dtype([("lo0", "<f4", 3), ("hi0", "<f4", 3), ("lo1", "<f4", 3), ("hi1", "<f4", 3),

@@ -123,14 +123,10 @@ def test_c5_full_spp_row_against_oracle(rt, sched):
     samples; pixel keys ~8.6 M), under a 16 MB trace-output bound: the per-sample pool runs
     in ~26 batches whose chunk sums are carried across batches (samples up to 4095), the item
     pool in 2."""
-    import os
     W = H = 4096
     spp, rows = 4096, dict(row_begin=2100, row_stride=4096)
-    os.environ["RT_SAMPLE_BUF_MB"] = "16"
-    try:
-        r = rt.Renderer(0)
-    finally:
-        os.environ.pop("RT_SAMPLE_BUF_MB")
+    r = rt.Renderer(0)
+    r.set_option(rt.RT_OPT_TRACE_BUF_BYTES, 16 << 20)
     try:
         r.set_schedule(getattr(rt, "RT_SCHED_" + sched))
         world = rt.World(1).build_scene(0)
@@ -153,14 +149,10 @@ def test_c5_geometry_many_buffer_batches(rt, sched):
     the top one, 40 spp (chunks of 3), with a 1 MB trace-output bound so the render runs
     in many buffer batches: per-sample pool 1 sample per batch, chunks straddling batches
     (reduce_samples_carry); item pool 1 chunk per batch (accumulate_chunks)."""
-    import os
     W = H = 4096
     spp, rows = 40, dict(row_begin=511, row_stride=512)
-    os.environ["RT_SAMPLE_BUF_MB"] = "1"
-    try:
-        r = rt.Renderer(0)
-    finally:
-        os.environ.pop("RT_SAMPLE_BUF_MB")
+    r = rt.Renderer(0)
+    r.set_option(rt.RT_OPT_TRACE_BUF_BYTES, 1 << 20)
     r.set_schedule(getattr(rt, "RT_SCHED_" + sched))
     world = rt.World(1).build_scene(0)
     cam, bg = rt.scene_camera(0, W, H)
@@ -288,8 +280,7 @@ def test_overlapped_buffer_batches_at_c2_size(rt, renderer, sched):
     render's stream reduces the previous batch. The whole C2 frame at 48 spp under a 256 MB bound
     (per-sample pool: 5 samples per half, 10 batches; item pool: chunks of 3, 5 chunks per half,
     4 batches) equals the one-batch render bit for bit, and so does the same bound without
-    overlap (RT_BATCH_OVERLAP=0: 11 samples or chunks per batch, 5 and 2 batches)."""
-    import os
+    overlap (RT_OPT_BATCH_OVERLAP 0: 11 samples or chunks per batch, 5 and 2 batches)."""
     W, H, spp = 1200, 800, 48
     world = rt.World(1).build_scene(0)
     cam, bg = rt.scene_camera(0, W, H)
@@ -302,13 +293,9 @@ def test_overlapped_buffer_batches_at_c2_size(rt, renderer, sched):
     finally:
         renderer.set_schedule(rt.RT_SCHED_AUTO)
     for overlap in ("1", "0"):
-        os.environ["RT_SAMPLE_BUF_MB"] = "256"
-        os.environ["RT_BATCH_OVERLAP"] = overlap
-        try:
-            r = rt.Renderer(0)
-        finally:
-            os.environ.pop("RT_SAMPLE_BUF_MB")
-            os.environ.pop("RT_BATCH_OVERLAP")
+        r = rt.Renderer(0)
+        r.set_option(rt.RT_OPT_TRACE_BUF_BYTES, 256 << 20)
+        r.set_option(rt.RT_OPT_BATCH_OVERLAP, int(overlap))
         try:
             r.set_schedule(getattr(rt, "RT_SCHED_" + sched))
             r.upload(world)

@@ -64,6 +64,14 @@ def test_device_numerics_bit_equal_host(rt, renderer):
         assert same.all(), f"fn {fn}: {int((~same).sum())} mismatches, e.g. {args[0][~same][:3]}"
 
 
+
+def test_loaded_library_is_the_build_of_this_tree(built_from_tree):
+    """The .so the GPU tier loads carries the source hash it was compiled from; it must be this
+    tree's (a stale library would make every GPU result here evidence for another build)."""
+    lib_hash, tree_hash = built_from_tree
+    assert lib_hash == tree_hash, f"stale library: built from {lib_hash}, sources are {tree_hash}"
+
+
 @pytest.mark.parametrize("scene_id,W,H,spp", [
     (0, 64, 48, 8),      # random spheres (C1/C2/C5 scene)
     (1, 48, 27, 4),      # two checker spheres
@@ -224,18 +232,15 @@ def test_kernel_variants_identical(rt, renderer, scene_id, W, H):
 def test_feature_set_variants_identical(rt, renderer, scene_id, W, H, feat):
     """Each scene runs on the smallest feature-set variant covering it (final scene: instances
     over spheres only, media bounded by spheres); the all-features variant, which no reference
-    scene selects, renders the same bits (RT_EXTRA_FEATURES forces it)."""
+    scene selects, renders the same bits (RT_OPT_EXTRA_FEATURES forces it)."""
     world = rt.World(1).build_scene(scene_id)
     cam, bg = rt.scene_camera(scene_id, W, H)
     p = rt.Renderer.params(W, H, 4, 50, bg, 1, out_format=rt.RT_OUT_F64)
     renderer.upload(world)
     img = renderer.render(cam, p)
     assert renderer.stats().variant_features == feat
-    os.environ["RT_EXTRA_FEATURES"] = "4095"   # incl. FEAT_NEST_MOVING: nested spheres as moving
-    try:
-        big = rt.Renderer(0)
-    finally:
-        del os.environ["RT_EXTRA_FEATURES"]
+    big = rt.Renderer(0)
+    big.set_option(rt.RT_OPT_EXTRA_FEATURES, 4095)   # incl. FEAT_NEST_MOVING: nested spheres as moving
     try:
         big.upload(world)
         img_all = big.render(cam, p)
@@ -387,30 +392,18 @@ def test_schedules_render_identically(rt, scene_id, W, H, spp):
     """The three schedules give the same bits: chunks; the per-sample pool (persistent
     waves, per-lane refill, [sample][pixel] buffer); the item pool (persistent waves, a lane
     takes a whole (pixel, chunk) item). So do the pools split into many buffer batches
-    (RT_SAMPLE_BUF_MB), at ragged sizes and with row shards."""
-    import os
+    (RT_OPT_TRACE_BUF_BYTES), at ragged sizes and with row shards."""
     world = rt.World(1).build_scene(scene_id)
     cam, bg = rt.scene_camera(scene_id, W, H)
     imgs = []
-    os.environ["RT_SAMPLE_BUF_MB"] = "1"
-    try:
-        small = rt.Renderer(0)                       # reads the buffer bound at creation
-    finally:
-        os.environ.pop("RT_SAMPLE_BUF_MB")
-    os.environ["RT_BLOCK_CHUNKS"] = "3"
-    os.environ["RT_BLOCK_SAMPLES"] = "5"
-    try:
-        grouped = rt.Renderer(0)                     # item-pool blocks of 3 chunks, pool blocks of 5 samples
-    finally:
-        os.environ.pop("RT_BLOCK_CHUNKS")
-        os.environ.pop("RT_BLOCK_SAMPLES")
-    os.environ["RT_SAMPLE_BUF_MB"] = "1"
-    os.environ["RT_BATCH_OVERLAP"] = "0"
-    try:
-        serial = rt.Renderer(0)                      # buffer batches one after another in one buffer
-    finally:
-        os.environ.pop("RT_SAMPLE_BUF_MB")
-        os.environ.pop("RT_BATCH_OVERLAP")
+    small = rt.Renderer(0)
+    small.set_option(rt.RT_OPT_TRACE_BUF_BYTES, 1 << 20)
+    grouped = rt.Renderer(0)                         # item-pool blocks of 3 chunks, pool blocks of 5 samples
+    grouped.set_option(rt.RT_OPT_BLOCK_CHUNKS, 3)
+    grouped.set_option(rt.RT_OPT_BLOCK_SAMPLES, 5)
+    serial = rt.Renderer(0)                          # buffer batches one after another in one buffer
+    serial.set_option(rt.RT_OPT_TRACE_BUF_BYTES, 1 << 20)
+    serial.set_option(rt.RT_OPT_BATCH_OVERLAP, 0)
     r = rt.Renderer(0)
     runs = [(r, rt.RT_SCHED_CHUNKS), (r, rt.RT_SCHED_POOL), (r, rt.RT_SCHED_ITEMS), (small, rt.RT_SCHED_POOL),
             (small, rt.RT_SCHED_ITEMS), (grouped, rt.RT_SCHED_ITEMS), (r, rt.RT_SCHED_AUTO),
