@@ -236,7 +236,7 @@ typedef struct rt_stats {
     int32_t waves_per_simd;      /* resident waves per SIMD of the last trace kernel (occupancy) */
     int64_t trace_buf_bytes;     /* the trace-output buffer the last render used (both halves when overlapped) */
     int32_t overlapped;          /* 1 if its buffer batches ran overlapped (two trace streams) */
-    int32_t pad0;
+    int32_t wf_iterations;       /* RT_SCHED_WAVEFRONT: wf_logic / wf_trace iterations of the last render */
 } rt_stats;
 int rt_last_stats(rt_ctx* ctx, rt_stats* out);
 /* Diagnostic: the raw count_work counters of the last render (n entries; returns how many
@@ -338,6 +338,12 @@ int rt_ctx_get_option(rt_ctx* ctx, int key, int64_t* value);
  *           buffer bytes); a lane whose item ended takes the next item at once.
  *   AUTO:   POOL when the render's per-sample radiance is at most 4 x the buffer bound (it is
  *           the faster of the two), otherwise ITEMS; rt_stats.schedule reports which ran.
+ *   WAVEFRONT: the final-scene feature set (f64, f32 slabs, one instanced BLAS, every node fits
+ *           LDS): a pool of path slots in HBM (RT_OPT_WF_PATHS) and per iteration two kernels —
+ *           wf_logic (hit records, materials, camera rays of new units; live slots compacted into
+ *           a ray queue) and wf_trace (persistent; a lane whose walk ends takes the next queued ray
+ *           at once; the top-level and instanced-BLAS walks in one step loop). Per-sample output as
+ *           POOL. A scene outside that set runs AUTO's choice (rt_stats.schedule says which ran).
  * The trace-output buffer is bounded by RT_OPT_TRACE_BUF_BYTES (default: sized at context creation
  * to 3/8 of the device's free memory, at most 128 GiB, at least 32 GiB where half the free
  * memory allows; allocated lazily, as large as a render needs). A larger render runs in buffer
@@ -345,7 +351,7 @@ int rt_ctx_get_option(rt_ctx* ctx, int key, int64_t* value);
  * k & 1 on one of two context streams while the render's stream reduces batch k - 1, so
  * consecutive traces overlap (RT_OPT_BATCH_OVERLAP 0: one buffer, in order). A 4 GB bound renders
  * C2 as fast as one batch; long-path scenes pay per batch. */
-enum { RT_SCHED_CHUNKS = 0, RT_SCHED_POOL = 1, RT_SCHED_ITEMS = 2, RT_SCHED_AUTO = 3 };
+enum { RT_SCHED_CHUNKS = 0, RT_SCHED_POOL = 1, RT_SCHED_ITEMS = 2, RT_SCHED_AUTO = 3, RT_SCHED_WAVEFRONT = 4 };
 int rt_ctx_set_schedule(rt_ctx* ctx, int schedule);
 
 /* Arithmetic of a context's renders (default RT_PREC_F64).

@@ -122,6 +122,14 @@ struct rt_ctx {
     int n_tlas_nodes = 0;
     int n_nodes = 0;                    // BVH nodes of the uploaded scene (TLAS + BLASes)
     int n_cus = 256;
+    // RT_SCHED_WAVEFRONT: the path pool (one allocation, WfPaths views into it), the host's poll of
+    // the live flag (pinned) and the scene's fitness for the schedule (upload)
+    rtk::WfPaths wf{};
+    void* wf_buf = nullptr;
+    size_t wf_cap = 0;
+    int32_t* wf_flag_host = nullptr;
+    hipEvent_t wf_ev[2] = {nullptr, nullptr};
+    bool wf_scene_ok = false;
     size_t lds_per_cu = 160 * 1024;     // the device's LDS per CU and per workgroup (read at creation)
     size_t lds_per_block = 160 * 1024;
 };
@@ -197,6 +205,8 @@ int rt_ctx_create(int device, rt_ctx** out)
     for (int i = 0; i < 2 && e == hipSuccess; ++i) e = hipEventCreateWithFlags(&c->ev_tr[i], hipEventDisableTiming);
     for (int i = 0; i < 2 && e == hipSuccess; ++i) e = hipEventCreateWithFlags(&c->ev_rd[i], hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_in, hipEventDisableTiming);
+    for (int i = 0; i < 2 && e == hipSuccess; ++i) e = hipEventCreateWithFlags(&c->wf_ev[i], hipEventDisableTiming);
+    if (e == hipSuccess) e = hipHostMalloc((void**)&c->wf_flag_host, 2 * sizeof(int32_t), hipHostMallocDefault);
     if (e != hipSuccess) {
         rt_ctx_destroy(c);
         return hip_fail(e, "rt_ctx_create");
@@ -218,6 +228,10 @@ void rt_ctx_destroy(rt_ctx* c)
     (void)hipFree(c->params);
     (void)hipFree(c->work);
     (void)hipFree(c->acc_tmp);
+    (void)hipFree(c->wf_buf);
+    if (c->wf_flag_host) (void)hipHostFree(c->wf_flag_host);
+    for (auto& e : c->wf_ev)
+        if (e) (void)hipEventDestroy(e);
     for (auto& e : c->ev)
         if (e) (void)hipEventDestroy(e);
     if (c->ev_done) (void)hipEventDestroy(c->ev_done);
@@ -965,7 +979,14 @@ int rt_ctx_upload_soa(rt_ctx* c, const rt_scene_soa* s)
             }
         }
         if (n_inst <= 1 && !inst_boundary) c->S.stack_entries = std::max(tlas_depth + 1, blas_depth + 1);
+        // the wavefront schedule walks the top level and the deferred BLAS in one region of one
+        // stack, every node staged in LDS: at most one instance over a BVH, that BVH the BFS-
+        // ordered one right after the TLAS, nothing else (wf_trace)
+        c->wf_scene_ok = n_inst <= 1 && !inst_boundary && n_tlas_nodes + n_blas_bfs == s->n_nodes;
+    } else {
+        c->wf_scene_ok = blas_depth == 0 && n_tlas_nodes == s->n_nodes;
     }
+    if (s->tlas_root < 0 && s->n_nodes == 0) c->wf_scene_ok = false;   // (no node: the Cornell scenes)
     c->n_tlas_nodes = n_tlas_nodes;
     c->n_nodes = s->n_nodes;
     c->n_materials = s->n_materials;
@@ -1201,6 +1222,57 @@ static int grow(rt_ctx* c, hipStream_t stream, double*& buf, size_t& cap, size_t
     return RT_OK;
 }
 
+// The wavefront schedule's path pool for a batch of `units` (pixel, sample) units: RT_OPT_WF_PATHS
+// slots (default kWfDefaultPaths), at most the units rounded up, a multiple of 2048 (whole logic
+// blocks of 256 per shard). One allocation carved into the WfPaths arrays, grown on demand.
+constexpr long long kWfDefaultPaths = 2LL << 20;
+static int wf_pool(rt_ctx* c, hipStream_t stream, long long units)
+{
+    long long n = c->wf_paths > 0 ? c->wf_paths : kWfDefaultPaths;
+    n = std::max<long long>(2048, std::min(n, (units + 2047) / 2048 * 2048));
+    n = (n + 2047) / 2048 * 2048;
+    const size_t seg = (size_t)n / 64;
+    const size_t a = 256;
+    const size_t bytes[] = {3 * 8 * (size_t)n, 3 * 8 * (size_t)n, 8 * (size_t)n, 3 * 8 * (size_t)n, 16 * (size_t)n,
+                            8 * (size_t)n, 4 * (size_t)n, 4 * (size_t)n, 4 * (size_t)n, 4 * (size_t)n, 8 * (size_t)n,
+                            8 * (size_t)n, 4 * (size_t)n, 4 * seg, 16 * seg, 4 * rtk::kWfShards, 4 * rtk::kWfFlags};
+    constexpr int N = (int)(sizeof(bytes) / sizeof(bytes[0]));
+    size_t off[N], total = 0;
+    for (int i = 0; i < N; ++i) {
+        off[i] = total;
+        total = align_up(total + bytes[i], a);
+    }
+    if (total > c->wf_cap) {
+        HIP_TRY(hipStreamSynchronize(stream));
+        (void)hipFree(c->wf_buf);
+        c->wf_buf = nullptr;
+        c->wf_cap = 0;
+        HIP_TRY(hipMalloc(&c->wf_buf, total));
+        c->wf_cap = total;
+    }
+    char* b = (char*)c->wf_buf;
+    rtk::WfPaths& W = c->wf;
+    W.n = (int32_t)n;
+    W.o = (double*)(b + off[0]);
+    W.d = (double*)(b + off[1]);
+    W.time = (double*)(b + off[2]);
+    W.T = (double*)(b + off[3]);
+    W.rng = (uint4*)(b + off[4]);
+    W.xk = (int2*)(b + off[5]);
+    W.smp = (uint32_t*)(b + off[6]);
+    W.pix = (uint32_t*)(b + off[7]);
+    W.st = (int32_t*)(b + off[8]);
+    W.bnc = (uint32_t*)(b + off[9]);
+    W.ht = (double*)(b + off[10]);
+    W.hp = (int2*)(b + off[11]);
+    W.q = (uint32_t*)(b + off[12]);
+    W.qn = (uint32_t*)(b + off[13]);
+    W.wblk = (int4*)(b + off[14]);
+    W.tctr = (unsigned*)(b + off[15]);
+    W.flag = (int32_t*)(b + off[16]);
+    return RT_OK;
+}
+
 // Where a sample range's per-pixel sums go: added to acc (n_px x 3 f64), or (acc null)
 // written as sum * scale to out (f32 / f64).
 struct Sink {
@@ -1329,6 +1401,11 @@ static int run_range(rt_ctx* c, const rt_camera* cam, const rt_render_params* p,
     // two (C2 kernel ms, pool 1/2/4 chunks: 99.8/100.2/103.2; items 1/2/4: 106.8/104.1/105.0;
     // profiles/r02f_*, r02g_*)
     K.block_chunks = c->block_chunks > 0 ? c->block_chunks : 2;
+    // RT_SCHED_WAVEFRONT: the final-scene feature set (wf_logic / wf_trace are its kernels), f64,
+    // f32 slabs, the stack and every node in LDS; otherwise AUTO's choice runs
+    const bool wavefront = c->opt_pool == RT_SCHED_WAVEFRONT && c->wf_scene_ok && !o.f32 && o.slab32 && o.lds_stack &&
+                           rtk::variant_features(o.features) == rtk::FEAT_SET_FINAL &&
+                           S.n_lds_nodes == c->n_tlas_nodes && rtk::wavefront_fits(c->S, c->lds_per_block);
 
     // Schedule and buffer batches, from the context's trace-output bound (sample_buf_cap). The
     // bound is sized from the free HBM when the context is created; if the device has less by
@@ -1350,19 +1427,22 @@ static int run_range(rt_ctx* c, const rt_camera* cam, const rt_render_params* p,
         // Round 2, pool vs items: C2 101.6 vs 106.7 ms per frame, C4 1492 vs 1571 (r02d_*, r02e_*);
         // round 4: C2 74.75 vs 76.06, C4 1018.5 vs 1074.7; C5 in 25 overlapped pool batches of
         // 64 GB halves 10,578 ms vs the item pool 10,649 in 64 batches at a 4 GB bound (r04f_*)
-        o.pool = c->opt_pool != RT_SCHED_AUTO ? c->opt_pool
-                 : ((size_t)total * sample_bytes <= 4 * buf_cap ? RT_SCHED_POOL : RT_SCHED_ITEMS);
+        o.pool = wavefront ? RT_SCHED_WAVEFRONT
+                 : c->opt_pool != RT_SCHED_AUTO && c->opt_pool != RT_SCHED_WAVEFRONT
+                     ? c->opt_pool
+                     : ((size_t)total * sample_bytes <= 4 * buf_cap ? RT_SCHED_POOL : RT_SCHED_ITEMS);
         // Buffer batches: the trace output is bounded by sample_buf_cap. Per-sample pool: samples x
         // pixels x 24 B; chunk and item schedules: chunks x pixels x 24 B, batches on chunk
         // boundaries (relative to s_begin), so the partials add in one-launch order. A render that
         // does not fit in one batch takes two buffers of half the bound: batch k traces into half
         // k & 1 on stream tstream[k & 1] while the caller's stream reduces batch k - 1, so the
         // next trace fills the CUs its predecessor's last waves leave (no tail per batch).
-        per_sample = o.pool == RT_SCHED_POOL;
+        per_sample = o.pool == RT_SCHED_POOL || o.pool == RT_SCHED_WAVEFRONT;
         const size_t unit = per_sample ? sample_bytes : px_bytes;
         long long fit = (long long)std::max<size_t>(1, buf_cap / unit);
         batch = std::min<long long>(total, per_sample ? fit : fit * chunk);
-        overlap = c->opt_overlap && batch < total && o.pool != RT_SCHED_CHUNKS;
+        // (the wavefront schedule's host loop enqueues one batch after the other)
+        overlap = c->opt_overlap && batch < total && o.pool != RT_SCHED_CHUNKS && o.pool != RT_SCHED_WAVEFRONT;
         if (overlap) {
             fit = (long long)std::max<size_t>(1, buf_cap / 2 / unit);
             batch = std::min<long long>(total, per_sample ? fit : fit * chunk);
@@ -1411,6 +1491,11 @@ static int run_range(rt_ctx* c, const rt_camera* cam, const rt_render_params* p,
         K.block_samples = bs;
     }
     if (count) HIP_TRY(hipMemsetAsync(c->counters, 0, kCounters * sizeof(unsigned long long), stream));
+    if (wavefront) {
+        const int rc = wf_pool(c, stream, (long long)K.tiles_x * K.tiles_y * 64 * std::min<long long>(total, batch));
+        if (rc) return rc;
+    }
+    int wf_iterations = 0;
     int waves_per_simd = 0;
     o.waves_per_simd = &waves_per_simd;
     HIP_TRY(hipEventRecord(c->ev[0], stream));
@@ -1429,7 +1514,7 @@ static int run_range(rt_ctx* c, const rt_camera* cam, const rt_render_params* p,
         K.spp = b1;
         K.n_chunks = (b1 - b0 + chunk - 1) / chunk;
         {
-            const unsigned g = o.pool == RT_SCHED_ITEMS ? (unsigned)K.block_chunks : (unsigned)K.block_samples;
+            const unsigned g = o.pool == RT_SCHED_ITEMS ? (unsigned)K.block_chunks : (unsigned)K.block_samples;   // (POOL, WAVEFRONT: samples)
             const unsigned n = o.pool == RT_SCHED_ITEMS ? (unsigned)K.n_chunks : (unsigned)(K.spp - K.sample_begin);
             K.n_work_blocks = (unsigned)K.tiles_x * (unsigned)K.tiles_y * ((n + g - 1) / std::max(g, 1u));
         }
@@ -1441,7 +1526,14 @@ static int run_range(rt_ctx* c, const rt_camera* cam, const rt_render_params* p,
         rtk::KParams* dK = c->params + c->param_slot;
         c->param_slot = (c->param_slot + 1) % kParamSlots;
         HIP_TRY(hipMemcpyAsync(dK, &K, sizeof K, hipMemcpyHostToDevice, ts));
-        HIP_TRY(rtk::launch_trace(S, K, dK, buf, c->counters, c->work + h, o, ts));
+        if (o.pool == RT_SCHED_WAVEFRONT) {
+            rtk::WfHost host{c->wf_flag_host, {c->wf_ev[0], c->wf_ev[1]}, 0, 0};
+            HIP_TRY(rtk::launch_wavefront(S, K, dK, buf, c->work + h, c->wf, c->counters, count, host, ts));
+            wf_iterations += host.iterations;
+            waves_per_simd = host.waves_per_simd;
+        } else {
+            HIP_TRY(rtk::launch_trace(S, K, dK, buf, c->counters, c->work + h, o, ts));
+        }
         if (bi == n_batches - 1) HIP_TRY(hipEventRecord(c->ev[1], ts));
         if (overlap) {   // reduce in batch order on `stream`, after this batch's trace
             HIP_TRY(hipEventRecord(c->ev_tr[h], ts));
@@ -1475,6 +1567,7 @@ static int run_range(rt_ctx* c, const rt_camera* cam, const rt_render_params* p,
                                                  : (per_sample ? (size_t)batch * sample_bytes
                                                                : (size_t)((batch + chunk - 1) / chunk) * px_bytes));
     c->stats.overlapped = overlap ? 1 : 0;
+    c->stats.wf_iterations = wf_iterations;
     c->stats.samples = (uint64_t)n_px * (uint64_t)total;
     c->stats.n_chunks = (int32_t)((total + chunk - 1) / chunk);
     c->stats.n_items = (uint64_t)n_px * (uint64_t)c->stats.n_chunks;
@@ -1918,7 +2011,7 @@ int rt_ctx_get_option(rt_ctx* c, int key, int64_t* v)
 
 int rt_ctx_set_schedule(rt_ctx* c, int schedule)
 {
-    if (!c || schedule < RT_SCHED_CHUNKS || schedule > RT_SCHED_AUTO) return fail(RT_ERR_INVALID, "bad schedule");
+    if (!c || schedule < RT_SCHED_CHUNKS || schedule > RT_SCHED_WAVEFRONT) return fail(RT_ERR_INVALID, "bad schedule");
     c->opt_pool = schedule;
     return RT_OK;
 }

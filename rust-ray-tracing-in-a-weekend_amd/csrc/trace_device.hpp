@@ -1123,6 +1123,30 @@ __device__ __forceinline__ void medium_finish(const rt_prim& m, const RayT<R>& r
     h.uvkind = 0;
 }
 
+// The HitRecord of the closest hit (t, leaf slot, sub-primitive, box side) of a world-space ray:
+// the arithmetic of the winning primitive's hit (hittable.rs:254-384, 417-473) and of the
+// instance chain back to world space (hittable.rs:232-244, 386-415). Traversal keeps only the
+// reference; the record is built once per cast (trace_world; the wavefront schedule's logic step).
+template <class C, class R = typename C::Real>
+__device__ __forceinline__ void finish_hit(const SceneDev& S, const RayT<R>& r, const HitRefT<R>& best, HitT<R>& h)
+{
+    const rt_prim& p = S.leaf_prims[best.prim];
+    bool done = false;
+    if constexpr ((C::F & FEAT_INST) != 0) {
+        if (p.kind == RT_PRIM_INSTANCE) {
+            instance_finish<C>(S, S.instances[p.a], r, best, h);
+            done = true;
+        }
+    }
+    if constexpr ((C::F & FEAT_MEDIUM) != 0) {
+        if (!done && p.kind == RT_PRIM_MEDIUM) {
+            medium_finish(p, r, best.t, h);
+            done = true;
+        }
+    }
+    if (!done) simple_finish<C>(p, r, best.t, best.side, h, (C::F & FEAT_SHUTTER) != 0);
+}
+
 // hit_hittables(world, ray, 0.001, inf) (hittable.rs:43-55) over the TLAS, then the
 // The variants that test SceneDev.pre_leaf before the walk: the spheres ones (random scene:
 // C2 19.17 -> 17.70 ms); the final scene gains nothing (its fog medium's test inlined twice
@@ -1258,21 +1282,7 @@ __device__ bool trace_world(const SceneDev& S, const RayT<R>& r, HitT<R>& h, Sta
         if (C::COUNT) tp = __builtin_amdgcn_s_memtime();   // lanes without one
     }
     if (!hit) return false;
-    const rt_prim& p = S.leaf_prims[best.prim];
-    bool done = false;
-    if constexpr ((C::F & FEAT_INST) != 0) {
-        if (p.kind == RT_PRIM_INSTANCE) {
-            instance_finish<C>(S, S.instances[p.a], r, best, h);
-            done = true;
-        }
-    }
-    if constexpr ((C::F & FEAT_MEDIUM) != 0) {
-        if (!done && p.kind == RT_PRIM_MEDIUM) {
-            medium_finish(p, r, best.t, h);
-            done = true;
-        }
-    }
-    if (!done) simple_finish<C>(p, r, best.t, best.side, h, (C::F & FEAT_SHUTTER) != 0);
+    finish_hit<C>(S, r, best, h);
     RT_STAMP(cnt.t_rec, tp);
     return true;
 }

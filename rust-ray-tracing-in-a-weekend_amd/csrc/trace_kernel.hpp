@@ -150,12 +150,61 @@ __host__ __device__ inline size_t tiled_pixels(int width, int n_rows)   // recor
     return (size_t)((width + 7) / 8) * (size_t)((n_rows + 7) / 8) * 64;
 }
 
+// ---- the wavefront schedule (RT_SCHED_WAVEFRONT, trace_wavefront.hip) ------------------------
+// A pool of P path slots in HBM, structure of arrays (component-major: x[0..P) y[..] z[..]), and
+// per iteration two launches: wf_logic (one thread per slot: the hit record of the slot's last
+// cast, emission / background, the material's draws and scattered ray, or a new (pixel, sample)
+// unit's camera ray; each wave appends its live slots to its 64-entry segment of the ray queue)
+// and wf_trace (a persistent grid whose lanes take rays from the queue segments and, when their
+// walk ends, the next ray at once: closest hit over the TLAS and the deferred instance BLAS in
+// one step loop). The per-(pixel, sample) arithmetic is the megakernel's, in the same order.
+constexpr int kWfShards = 8;         // trace-side segment counters (one per XCD of round-robin placement)
+constexpr int kWfFlags = 64;         // ring of per-iteration "any path live" flags the host polls
+struct WfPaths {
+    int32_t n;              // slots (a multiple of 2048: whole logic blocks per shard)
+    double* o;              // [3][n] ray origin (world)
+    double* d;              // [3][n] ray direction
+    double* time;           // [n] the path's shutter time (Ray::time, set by the camera)
+    double* T;              // [3][n] path throughput
+    uint4* rng;             // [n] the path stream (rt_pstream)
+    int2* xk;               // [n] the unit's pixel on the shard grid
+    uint32_t* smp;          // [n] its sample
+    uint32_t* pix;          // [n] its image pixel key (medium draws, camera)
+    int32_t* st;            // [n] -1: no path; else the remaining depth (the slot's ray is queued)
+    uint32_t* bnc;          // [n] the queued cast's bounce (medium draws)
+    double* ht;             // [n] closest hit t of the last cast
+    int2* hp;               // [n] (leaf slot, sub << 3 | box side) of it; x = -1: a miss
+    uint32_t* q;            // [n] ray queue: wave w's live slots at q[64 w ..]
+    uint32_t* qn;           // [n / 64] live slots per segment
+    int4* wblk;             // [n / 64] per logic wave: current work block (b, next, units, exhausted)
+    unsigned* tctr;         // [kWfShards] trace segment counters (reset by every wf_logic)
+    int32_t* flag;          // [kWfFlags] iteration i: any slot live after its wf_logic
+};
+// bytes of one slot's arrays
+constexpr size_t kWfSlotBytes = 3 * 8 + 3 * 8 + 8 + 3 * 8 + 16 + 8 + 4 + 4 + 4 + 4 + 8 + 8 + 4;
+
 uint32_t variant_features(uint32_t scene_features);
 // Ph: host copy of the params (grid size); P: the same params in device memory
 // chunk schedule: out = chunk partials [n_chunks][n_px][3]; pool schedule: out = per-sample
 // radiance, tiled_record order over spp - sample_begin samples; work = one device counter
 hipError_t launch_trace(const SceneDev& S, const KParams& Ph, const KParams* P, double* out,
                         unsigned long long* counters, unsigned* work, const LaunchOpts& o, hipStream_t stream);
+// The wavefront schedule of one batch (samples [Ph.sample_begin, Ph.spp) of the shard) into the
+// per-sample buffer `out` (tiled_record order, as the per-sample pool): wf_logic / wf_trace
+// iterations enqueued on `stream` in chunks until an iteration leaves no path live (polled through
+// `flag_host`, pinned memory, and `ev`). S: the scene as uploaded; the launcher builds the two
+// kernels' LDS views. Returns hipErrorNotSupported if the scene does not fit the schedule.
+struct WfHost {
+    volatile int32_t* flag_host;   // pinned, 2 entries
+    hipEvent_t ev[2];
+    int iterations;                // out: iterations enqueued
+    int waves_per_simd;            // out: of the trace kernel
+};
+bool wavefront_fits(const SceneDev& S, size_t lds_per_block);
+hipError_t launch_wavefront(const SceneDev& S, const KParams& Ph, const KParams* P, double* out, unsigned* work,
+                            const WfPaths& W, unsigned long long* counters, bool count, WfHost& host,
+                            hipStream_t stream);
+
 // pool schedule: per pixel, chunk sums of its samples (sample order) added to 0.0, scaled to out
 // (out and the carried sums are in pixel order k * width + x)
 hipError_t launch_reduce_samples(const double* samples, void* out, bool f64, SampleTiles g, int n_samples,

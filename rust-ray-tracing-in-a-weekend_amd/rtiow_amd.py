@@ -36,6 +36,7 @@ RT_SCHED_CHUNKS = 0
 RT_SCHED_POOL = 1
 RT_SCHED_ITEMS = 2
 RT_SCHED_AUTO = 3
+RT_SCHED_WAVEFRONT = 4
 RT_PREC_F64 = 0
 RT_PREC_F32 = 1
 RT_ACCEL_SAH = 0
@@ -141,7 +142,7 @@ class Stats(ctypes.Structure):
                 ("wave_leaf_steps", ctypes.c_uint64), ("camera_lanes", ctypes.c_uint64),
                 ("camera_steps", ctypes.c_uint64), ("shade_lanes", ctypes.c_uint64),
                 ("shade_steps", ctypes.c_uint64), ("precision", ctypes.c_int32), ("waves_per_simd", ctypes.c_int32),
-                ("trace_buf_bytes", ctypes.c_int64), ("overlapped", ctypes.c_int32), ("pad0", ctypes.c_int32)]
+                ("trace_buf_bytes", ctypes.c_int64), ("overlapped", ctypes.c_int32), ("wf_iterations", ctypes.c_int32)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
