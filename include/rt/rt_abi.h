@@ -312,7 +312,9 @@ int rt_ctx_set_variant(rt_ctx* ctx, int slab32, int lds_stack, int lds_nodes);
  *                           feature-set variant than it needs (tests: the all-features variant)
  *   RT_OPT_HOIST            1 (default): the spheres variants test a huge root-child leaf before
  *                           the walk (SceneDev.pre_leaf); takes effect at the next upload
- *   RT_OPT_WF_PATHS         wavefront schedule: path slots (0: auto) */
+ *   RT_OPT_WF_PATHS         wavefront schedule: path slots (0: auto)
+ *   RT_OPT_WF_REFILL        wavefront schedule: a wf_trace wave takes queued rays once this many of
+ *                           its 64 lanes are idle (0: auto) */
 enum {
     RT_OPT_TRACE_BUF_BYTES = 1,
     RT_OPT_BATCH_OVERLAP = 2,
@@ -320,7 +322,8 @@ enum {
     RT_OPT_BLOCK_CHUNKS = 4,
     RT_OPT_EXTRA_FEATURES = 5,
     RT_OPT_HOIST = 6,
-    RT_OPT_WF_PATHS = 7
+    RT_OPT_WF_PATHS = 7,
+    RT_OPT_WF_REFILL = 8
 };
 int rt_ctx_set_option(rt_ctx* ctx, int key, int64_t value);
 int rt_ctx_get_option(rt_ctx* ctx, int key, int64_t* value);

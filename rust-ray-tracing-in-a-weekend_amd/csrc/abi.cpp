@@ -101,6 +101,7 @@ struct rt_ctx {
     int block_chunks = 0;               // RT_OPT_BLOCK_CHUNKS: chunks per item-pool work block (0: auto)
     int block_samples = 0;              // RT_OPT_BLOCK_SAMPLES: samples per per-sample-pool work block (0: auto)
     int64_t wf_paths = 0;               // RT_OPT_WF_PATHS: wavefront schedule path slots (0: auto)
+    int wf_refill = 0;                  // RT_OPT_WF_REFILL: idle lanes before a wf_trace wave refills (0: auto)
     unsigned long long raw_counters[kCounters] = {};   // the last count_work render's counters (rt_last_counters)
     uint32_t extra_features = 0;        // RT_OPT_EXTRA_FEATURES: a larger kernel variant than the scene needs (tests)
     double pad_extent = 0.0;
@@ -955,6 +956,7 @@ int rt_ctx_upload_soa(rt_ctx* c, const rt_scene_soa* s)
     // level holds one instance over a BVH and none of the others (the final scene) needs the
     // larger of the two walks, not their sum: 13 entries instead of 25 per lane, 12 KB less LDS
     // per block.
+    c->S.defer_inst = -1;
     if (RT_DEFER_INST && blas_depth > 0) {
         int n_inst = 0;
         bool inst_boundary = false;
@@ -972,7 +974,10 @@ int rt_ctx_upload_soa(rt_ctx* c, const rt_scene_soa* s)
                 const rt_prim& p = s->prims[s->prim_refs[j]];
                 if (p.kind == RT_PRIM_INSTANCE) {   // an instance that may walk a BLAS
                     const rt_instance& in = s->instances[p.a];
-                    if (in.child_kind == RT_CHILD_BVH) ++n_inst;
+                    if (in.child_kind == RT_CHILD_BVH) {
+                        ++n_inst;
+                        c->S.defer_inst = p.a;
+                    }
                     else if (s->prims[in.child].kind == RT_PRIM_MEDIUM) inst_boundary = true;   // never deferred
                 }
                 if (p.kind == RT_PRIM_MEDIUM && s->prims[p.a].kind == RT_PRIM_INSTANCE) inst_boundary = true;
@@ -983,6 +988,7 @@ int rt_ctx_upload_soa(rt_ctx* c, const rt_scene_soa* s)
         // stack, every node staged in LDS: at most one instance over a BVH, that BVH the BFS-
         // ordered one right after the TLAS, nothing else (wf_trace)
         c->wf_scene_ok = n_inst <= 1 && !inst_boundary && n_tlas_nodes + n_blas_bfs == s->n_nodes;
+        if (n_inst != 1) c->S.defer_inst = -1;
     } else {
         c->wf_scene_ok = blas_depth == 0 && n_tlas_nodes == s->n_nodes;
     }
@@ -1226,6 +1232,7 @@ static int grow(rt_ctx* c, hipStream_t stream, double*& buf, size_t& cap, size_t
 // slots (default kWfDefaultPaths), at most the units rounded up, a multiple of 2048 (whole logic
 // blocks of 256 per shard). One allocation carved into the WfPaths arrays, grown on demand.
 constexpr long long kWfDefaultPaths = 2LL << 20;
+constexpr int kWfDefaultRefill = 16;
 static int wf_pool(rt_ctx* c, hipStream_t stream, long long units)
 {
     long long n = c->wf_paths > 0 ? c->wf_paths : kWfDefaultPaths;
@@ -1233,9 +1240,11 @@ static int wf_pool(rt_ctx* c, hipStream_t stream, long long units)
     n = (n + 2047) / 2048 * 2048;
     const size_t seg = (size_t)n / 64;
     const size_t a = 256;
-    const size_t bytes[] = {3 * 8 * (size_t)n, 3 * 8 * (size_t)n, 8 * (size_t)n, 3 * 8 * (size_t)n, 16 * (size_t)n,
-                            8 * (size_t)n, 4 * (size_t)n, 4 * (size_t)n, 4 * (size_t)n, 4 * (size_t)n, 8 * (size_t)n,
-                            8 * (size_t)n, 4 * (size_t)n, 4 * seg, 16 * seg, 4 * rtk::kWfShards, 4 * rtk::kWfFlags};
+    const size_t N1 = (size_t)n;
+    const size_t bytes[] = {3 * 8 * N1, 16 * N1, 8 * N1, 4 * N1, 4 * N1,                  // T rng xk st qpos
+                            2 * 3 * 8 * N1, 2 * 3 * 8 * N1, 2 * 8 * N1, 2 * 16 * N1,     // qo qd qtime qkey
+                            2 * 8 * N1, 2 * 8 * N1,                                      // ht hp
+                            4 * seg, 16 * seg, 4 * rtk::kWfShards, 4 * rtk::kWfFlags};
     constexpr int N = (int)(sizeof(bytes) / sizeof(bytes[0]));
     size_t off[N], total = 0;
     for (int i = 0; i < N; ++i) {
@@ -1253,23 +1262,21 @@ static int wf_pool(rt_ctx* c, hipStream_t stream, long long units)
     char* b = (char*)c->wf_buf;
     rtk::WfPaths& W = c->wf;
     W.n = (int32_t)n;
-    W.o = (double*)(b + off[0]);
-    W.d = (double*)(b + off[1]);
-    W.time = (double*)(b + off[2]);
-    W.T = (double*)(b + off[3]);
-    W.rng = (uint4*)(b + off[4]);
-    W.xk = (int2*)(b + off[5]);
-    W.smp = (uint32_t*)(b + off[6]);
-    W.pix = (uint32_t*)(b + off[7]);
-    W.st = (int32_t*)(b + off[8]);
-    W.bnc = (uint32_t*)(b + off[9]);
-    W.ht = (double*)(b + off[10]);
-    W.hp = (int2*)(b + off[11]);
-    W.q = (uint32_t*)(b + off[12]);
-    W.qn = (uint32_t*)(b + off[13]);
-    W.wblk = (int4*)(b + off[14]);
-    W.tctr = (unsigned*)(b + off[15]);
-    W.flag = (int32_t*)(b + off[16]);
+    W.T = (double*)(b + off[0]);
+    W.rng = (uint4*)(b + off[1]);
+    W.xk = (int2*)(b + off[2]);
+    W.st = (int32_t*)(b + off[3]);
+    W.qpos = (uint32_t*)(b + off[4]);
+    W.qo = (double*)(b + off[5]);
+    W.qd = (double*)(b + off[6]);
+    W.qtime = (double*)(b + off[7]);
+    W.qkey = (uint4*)(b + off[8]);
+    W.ht = (double*)(b + off[9]);
+    W.hp = (int2*)(b + off[10]);
+    W.qn = (uint32_t*)(b + off[11]);
+    W.wblk = (int4*)(b + off[12]);
+    W.tctr = (unsigned*)(b + off[13]);
+    W.flag = (int32_t*)(b + off[14]);
     return RT_OK;
 }
 
@@ -1335,6 +1342,7 @@ static int run_range(rt_ctx* c, const rt_camera* cam, const rt_render_params* p,
     while ((1 << K.row_block_shift) < row_block_of(p)) K.row_block_shift++;
     K.tile_shard = p->tile_shard;
     K.img_tiles_x = (p->width + 7) / 8;
+    K.wf_refill = c->wf_refill > 0 ? c->wf_refill : kWfDefaultRefill;
     K.n_rows = n_rows;
     K.tiles_x = (lay.w + 7) / 8;
     K.tiles_y = (n_rows + 7) / 8;
@@ -1990,6 +1998,10 @@ int rt_ctx_set_option(rt_ctx* c, int key, int64_t v)
         if (v < 0 || v > ((int64_t)1 << 26)) return fail(RT_ERR_INVALID, "path slots out of range");
         c->wf_paths = v;
         return RT_OK;
+    case RT_OPT_WF_REFILL:
+        if (v < 0 || v > 64) return fail(RT_ERR_INVALID, "refill lanes out of range (0..64)");
+        c->wf_refill = (int)v;
+        return RT_OK;
     default: return fail(RT_ERR_INVALID, "unknown option");
     }
 }
@@ -2005,6 +2017,7 @@ int rt_ctx_get_option(rt_ctx* c, int key, int64_t* v)
     case RT_OPT_EXTRA_FEATURES: *v = c->extra_features; return RT_OK;
     case RT_OPT_HOIST: *v = c->opt_hoist; return RT_OK;
     case RT_OPT_WF_PATHS: *v = c->wf_paths; return RT_OK;
+    case RT_OPT_WF_REFILL: *v = c->wf_refill; return RT_OK;
     default: return fail(RT_ERR_INVALID, "unknown option");
     }
 }

@@ -70,6 +70,9 @@ struct SceneDev {
     // nodes[n_tlas_nodes, n_tlas_nodes + n_blas_bfs) (abi.cpp), and a launch stages the first
     // n_lds_blas of them (its LDS budget): the nested walk's top levels then read LDS
     int32_t n_blas_bfs, n_lds_blas;
+    // the wavefront schedule's scenes (abi.cpp wf_scene_ok): the one instance over a BVH that a
+    // top-level walk can defer (its record is staged in LDS by wf_trace), or -1
+    int32_t defer_inst;
 };
 
 struct KParams {
@@ -93,6 +96,7 @@ struct KParams {
     int32_t img_width;          // the image's width (pixel keys)
     int32_t tile_shard;         // rt_render_params.tile_shard: grid tile m = the frame's tile row_begin + m*row_stride
     int32_t img_tiles_x;        // tiles per tile row of the image
+    int32_t wf_refill;          // wavefront schedule: a wf_trace wave refills once this many lanes are idle
 };
 
 // Scene features (which code a kernel variant must contain).
@@ -162,26 +166,28 @@ constexpr int kWfShards = 8;         // trace-side segment counters (one per XCD
 constexpr int kWfFlags = 64;         // ring of per-iteration "any path live" flags the host polls
 struct WfPaths {
     int32_t n;              // slots (a multiple of 2048: whole logic blocks per shard)
-    double* o;              // [3][n] ray origin (world)
-    double* d;              // [3][n] ray direction
-    double* time;           // [n] the path's shutter time (Ray::time, set by the camera)
+    // per slot: the path's state between its casts
     double* T;              // [3][n] path throughput
     uint4* rng;             // [n] the path stream (rt_pstream)
     int2* xk;               // [n] the unit's pixel on the shard grid
-    uint32_t* smp;          // [n] its sample
-    uint32_t* pix;          // [n] its image pixel key (medium draws, camera)
     int32_t* st;            // [n] -1: no path; else the remaining depth (the slot's ray is queued)
-    uint32_t* bnc;          // [n] the queued cast's bounce (medium draws)
-    double* ht;             // [n] closest hit t of the last cast
-    int2* hp;               // [n] (leaf slot, sub << 3 | box side) of it; x = -1: a miss
-    uint32_t* q;            // [n] ray queue: wave w's live slots at q[64 w ..]
-    uint32_t* qn;           // [n / 64] live slots per segment
+    uint32_t* qpos;         // [n] the slot's entry in the last iteration's queue
+    // the ray queue, two buffers (iteration parity): wave w of wf_logic writes its live rays to
+    // entries [64 w, 64 w + qn[w]) of this iteration's buffer, wf_trace reads them there and writes
+    // the hits beside them, and the next wf_logic reads both back (one dependent load per slot)
+    double* qo;             // [2][3][n] ray origin (world)
+    double* qd;             // [2][3][n] ray direction
+    double* qtime;          // [2][n] the path's shutter time (Ray::time, set by the camera)
+    uint4* qkey;            // [2][n] image pixel key, sample, bounce (the medium draws' key), -
+    double* ht;             // [2][n] closest hit t
+    int2* hp;               // [2][n] (leaf slot, sub << 3 | box side); x = -1: a miss
+    uint32_t* qn;           // [n / 64] live entries per segment
     int4* wblk;             // [n / 64] per logic wave: current work block (b, next, units, exhausted)
     unsigned* tctr;         // [kWfShards] trace segment counters (reset by every wf_logic)
     int32_t* flag;          // [kWfFlags] iteration i: any slot live after its wf_logic
 };
 // bytes of one slot's arrays
-constexpr size_t kWfSlotBytes = 3 * 8 + 3 * 8 + 8 + 3 * 8 + 16 + 8 + 4 + 4 + 4 + 4 + 8 + 8 + 4;
+constexpr size_t kWfSlotBytes = 3 * 8 + 16 + 8 + 4 + 4 + 2 * (3 * 8 + 3 * 8 + 8 + 16 + 8 + 8);
 
 uint32_t variant_features(uint32_t scene_features);
 // Ph: host copy of the params (grid size); P: the same params in device memory

@@ -39,10 +39,6 @@ struct WfCfg : Cfg<F_, S32_, LDS_, NALL_, COUNT_, false> {
 };
 constexpr int kWfTraceThreads = 1024;   // one block per CU: the LDS holds one copy of every node
 constexpr int kWfLogicThreads = 256;
-#ifndef RT_WF_REFILL
-// a wave refills its idle lanes from the queue once at least this many are idle (or none is busy)
-#define RT_WF_REFILL 8
-#endif
 #ifndef RT_WF_CHUNK
 #define RT_WF_CHUNK 16   // iterations enqueued between two polls of the live flag
 #endif
@@ -57,7 +53,7 @@ __device__ __forceinline__ __attribute__((address_space(3))) int* lds_int(uint32
 // ---------------------------------------------------------------------------------------------
 template <class C>
 __global__ void __launch_bounds__(kWfTraceThreads, 1) wf_trace(SceneDev S, const KParams* __restrict__ Pp, WfPaths W,
-                                                              unsigned long long* __restrict__ counters)
+                                                              unsigned long long* __restrict__ counters, int parity)
 {
     using R = double;
     const KParams& P = *Pp;
@@ -80,9 +76,16 @@ __global__ void __launch_bounds__(kWfTraceThreads, 1) wf_trace(SceneDev S, const
             o.child[c] = n.child[c] >= 0 ? (int)(nb0 + (uint32_t)n.child[c] * (uint32_t)sizeof(LdsNode)) : n.child[c];
         nodes[i] = o;
     }
+    // the deferred instance's record after the nodes (S.defer_inst: the scene's one instance over a
+    // BVH, abi.cpp), then the stacks
+    char* const lds_inst = reinterpret_cast<char*>(nodes + n_nodes);
+    if (threadIdx.x < sizeof(rt_instance) / 8 && S.defer_inst >= 0)
+        reinterpret_cast<uint64_t*>(lds_inst)[threadIdx.x] =
+            reinterpret_cast<const uint64_t*>(S.instances + S.defer_inst)[threadIdx.x];
     __syncthreads();
     // the lane's stack column: entry e at stack0 + e * (block threads * 4)
-    const uint32_t stack0 = nb0 + (uint32_t)n_nodes * (uint32_t)sizeof(LdsNode) + (uint32_t)threadIdx.x * 4u;
+    const uint32_t stack0 = nb0 + (uint32_t)n_nodes * (uint32_t)sizeof(LdsNode) + (uint32_t)sizeof(rt_instance) +
+                            (uint32_t)threadIdx.x * 4u;
     constexpr uint32_t SSTR = kWfTraceThreads * 4u;
     StackT<C> nostack;   // (medium boundaries and single-primitive instances walk no BVH here)
     nostack.init(0);
@@ -97,13 +100,26 @@ __global__ void __launch_bounds__(kWfTraceThreads, 1) wf_trace(SceneDev S, const
     const uint32_t n_seg = n >> 6, seg_per_shard = n_seg / kWfShards;
     const int lane = threadIdx.x & 63;
 
-    // wave state: the queue segment being drained (segments of the shard's logic blocks first)
-    int shard = (int)(blockIdx.x % kWfShards), shards_tried = 0;
-    uint32_t seg_base = 0, seg_cnt = 0, seg_next = 0;
+    // wave state: a window of two queue segments (128 entries) being drained
+    // this iteration's queue buffer: entry e of component c at [c * n + e]
+    const double* const qo = W.qo + (size_t)parity * 3 * n;
+    const double* const qd = W.qd + (size_t)parity * 3 * n;
+    const double* const qtime = W.qtime + (size_t)parity * n;
+    const uint4* const qkey = W.qkey + (size_t)parity * n;
+    double* const ht = W.ht + (size_t)parity * n;
+    int2* const hp = W.hp + (size_t)parity * n;
+    const uint32_t refill_min = (uint32_t)max(1, P.wf_refill);
+    // static windows: wave g drains windows g, g + n_waves, ... (the queue is dense: every logic
+    // wave fills its segment with its live slots), each window's counts loaded one window ahead
+    const uint32_t n_win = n_seg / 2, n_waves = gridDim.x * (kWfTraceThreads / 64);
+    uint32_t nxt = blockIdx.x * (kWfTraceThreads / 64) + (threadIdx.x >> 6);
+    uint2 pre = make_uint2(0u, 0u);
+    if (nxt < n_win) pre = *reinterpret_cast<const uint2*>(W.qn + 2 * nxt);
+    uint32_t win_a = 0, cnt_a = 0, win_b = 0, cnt_b = 0, win_next = 0;
     bool exhausted = false;
     // lane state
     bool busy = false, blas = false, any = false;
-    uint32_t slot = 0, sp = 0;
+    uint32_t pos = 0, sp = 0;
     int cur = RT_DONE, pend = -1, base = 0;
     RayT<R> r;
     R t_max = (R)RT_INF;
@@ -157,41 +173,44 @@ __global__ void __launch_bounds__(kWfTraceThreads, 1) wf_trace(SceneDev S, const
         // ---- refill: idle lanes take the next queued rays (ballot + mbcnt over the segment)
         if (C::COUNT) tp = __builtin_amdgcn_s_memtime();
         uint64_t idle = __ballot(!busy);
-        if (idle != 0 && !exhausted && (__popcll(idle) >= RT_WF_REFILL || idle == ~0ull)) {
+        if (idle != 0 && !exhausted && ((uint32_t)__popcll(idle) >= refill_min || idle == ~0ull)) {
             while (idle != 0) {
-                if (seg_next == seg_cnt) {
-                    // next segment: the shard's counter, then the other shards'
-                    uint32_t seg = 0xffffffffu;
-                    while (shards_tried < kWfShards) {
-                        unsigned j = 0;
-                        if (lane == 0) j = atomicAdd(&W.tctr[shard], 1u);
-                        j = __builtin_amdgcn_readfirstlane(j);
-                        if (j < seg_per_shard) {   // the j-th segment of the shard's logic blocks
-                            seg = ((uint32_t)shard + (uint32_t)kWfShards * (j >> 2)) * 4u + (j & 3u);
-                            break;
-                        }
-                        shard = (shard + 1) % kWfShards;
-                        ++shards_tried;
-                    }
-                    if (seg == 0xffffffffu) {
+                uint64_t tf = 0;
+                if (C::COUNT) tf = __builtin_amdgcn_s_memtime();
+                if (win_next == cnt_a + cnt_b) {
+                    // the next window: the prefetched one, whose successor's counts are loaded now
+                    if (nxt >= n_win) {
                         exhausted = true;
                         break;
                     }
-                    seg_base = seg << 6;
-                    seg_cnt = __builtin_amdgcn_readfirstlane(W.qn[seg]);
-                    seg_next = 0;
+                    win_a = nxt << 7;
+                    win_b = win_a + 64;
+                    cnt_a = __builtin_amdgcn_readfirstlane(pre.x);
+                    cnt_b = __builtin_amdgcn_readfirstlane(pre.y);
+                    win_next = 0;
+                    nxt += n_waves;
+                    if (nxt < n_win) pre = *reinterpret_cast<const uint2*>(W.qn + 2 * nxt);
+                    RT_STAMP(cnt.t_pre, tf);   // window changes
                     continue;
                 }
                 const unsigned rank = lanes_below(idle);
-                const unsigned take = min((unsigned)__popcll(idle), seg_cnt - seg_next);
+                const unsigned take = min((unsigned)__popcll(idle), cnt_a + cnt_b - win_next);
                 if (!busy && rank < take) {
-                    slot = W.q[seg_base + seg_next + rank];
-                    r.ox = W.o[slot]; r.oy = W.o[n + slot]; r.oz = W.o[2 * n + slot];
-                    r.dx = W.d[slot]; r.dy = W.d[n + slot]; r.dz = W.d[2 * n + slot];
-                    r.time = W.time[slot];
-                    key.pixel = W.pix[slot];
-                    key.sample = W.smp[slot];
-                    key.bounce = W.bnc[slot];
+                    const uint32_t e = win_next + rank;
+                    pos = e < cnt_a ? win_a + e : win_b + (e - cnt_a);
+                    // non-temporal: the queue streams through once and must not evict the scene
+                    r.ox = __builtin_nontemporal_load(&qo[pos]);
+                    r.oy = __builtin_nontemporal_load(&qo[n + pos]);
+                    r.oz = __builtin_nontemporal_load(&qo[2 * n + pos]);
+                    r.dx = __builtin_nontemporal_load(&qd[pos]);
+                    r.dy = __builtin_nontemporal_load(&qd[n + pos]);
+                    r.dz = __builtin_nontemporal_load(&qd[2 * n + pos]);
+                    r.time = __builtin_nontemporal_load(&qtime[pos]);
+                    typedef unsigned u4v __attribute__((ext_vector_type(4)));
+                    const u4v kq = __builtin_nontemporal_load(reinterpret_cast<const u4v*>(&qkey[pos]));
+                    key.pixel = kq.x;
+                    key.sample = kq.y;
+                    key.bounce = kq.z;
                     finish_ray<C>(r, S.has_spheres != 0);
                     t_max = (R)RT_INF;
                     tmax_f = f32_up(t_max);
@@ -205,7 +224,8 @@ __global__ void __launch_bounds__(kWfTraceThreads, 1) wf_trace(SceneDev S, const
                     busy = true;
                     if (C::COUNT) cnt.casts++;
                 }
-                seg_next += take;
+                RT_STAMP(cnt.t_setup, tf);   // lanes' ray loads and set-up
+                win_next += take;
                 idle = __ballot(!busy);
             }
         }
@@ -273,8 +293,9 @@ __global__ void __launch_bounds__(kWfTraceThreads, 1) wf_trace(SceneDev S, const
             cur = pop();
             RT_STAMP(cnt.t_leaves, tp);
         } else if (!blas && pend >= 0) {
-            // the deferred instance: its BLAS walked in object space with the walk's t_max
-            const rt_instance& in = S.instances[S.leaf_prims[pend].a];
+            // the deferred instance (the scene's one instance over a BVH, staged in LDS): its BLAS
+            // walked in object space with the walk's t_max
+            const rt_instance& in = *reinterpret_cast<const rt_instance*>(lds_inst);
             instance_ray(in, r);
             finish_ray<C>(r, S.has_spheres != 0);
             t_max = any ? best.t : (R)RT_INF;
@@ -286,8 +307,10 @@ __global__ void __launch_bounds__(kWfTraceThreads, 1) wf_trace(SceneDev S, const
             cur = root_ref(in.child);
             RT_STAMP(cnt.t_defer, tp);
         } else {
-            W.ht[slot] = best.t;
-            W.hp[slot] = make_int2(any ? best.prim : -1, (best.sub << 3) | (best.side & 7));
+            __builtin_nontemporal_store(best.t, &ht[pos]);
+            typedef int i2w __attribute__((ext_vector_type(2)));
+            const i2w hv = {any ? best.prim : -1, (best.sub << 3) | (best.side & 7)};
+            __builtin_nontemporal_store(hv, reinterpret_cast<i2w*>(&hp[pos]));
             busy = false;
             RT_STAMP(cnt.t_rec, tp);
         }
@@ -305,6 +328,8 @@ __global__ void __launch_bounds__(kWfTraceThreads, 1) wf_trace(SceneDev S, const
         atomicAdd(&counters[17], (unsigned long long)cnt.t_rec);
         atomicAdd(&counters[20], (unsigned long long)cnt.t_refill);
         atomicAdd(&counters[22], (unsigned long long)cnt.t_defer);
+        atomicAdd(&counters[15], (unsigned long long)cnt.t_setup);
+        atomicAdd(&counters[16], (unsigned long long)cnt.t_pre);
         if (lane == 0) atomicAdd(&counters[21], (unsigned long long)(__builtin_amdgcn_s_memtime() - t_start));
     }
 }
@@ -326,6 +351,8 @@ __global__ void __launch_bounds__(kWfLogicThreads) wf_logic(SceneDev S, const KP
     const uint32_t slot = blockIdx.x * kWfLogicThreads + threadIdx.x;   // the grid covers n exactly
     const uint32_t w = slot >> 6;
     const int lane = threadIdx.x & 63;
+    // the last iteration's queue (parity ^ 1: its rays and hits) and this one's (parity)
+    const size_t lo = (size_t)((iter & 1) ^ 1) * n, cu = (size_t)(iter & 1) * n;
     const int32_t st = W.st[slot];
     const bool traced = st >= 0;   // the slot's ray was queued and traced in the last iteration
     int depth = st;
@@ -336,23 +363,33 @@ __global__ void __launch_bounds__(kWfLogicThreads) wf_logic(SceneDev S, const KP
     HitT<R> h;
     bool pending = false, ended = false;
     int x = 0, k = 0, s = 0;
+    uint32_t pixel = 0;
+    // the slot's state in one round of loads (whether or not it holds a path: no load waits on st)
+    const uint32_t qp = W.qpos[slot];
+    const double T0 = W.T[slot], T1 = W.T[n + slot], T2 = W.T[2 * n + slot];
+    const uint4 q = W.rng[slot];
     if (traced) {
-        Tr = W.T[slot]; Tg = W.T[n + slot]; Tb = W.T[2 * n + slot];
-        const uint4 q = W.rng[slot];
+        Tr = T0; Tg = T1; Tb = T2;
         rs.s0 = q.x; rs.s1 = q.y; rs.s2 = q.z; rs.s3 = q.w;
-        const int2 hp = W.hp[slot];
+        // the slot's queue entry: its ray, key and hit (one dependent round of loads)
+        const size_t e = lo + qp;
+        const int2 hp = W.hp[e];
+        const uint4 kq = W.qkey[e];
+        pixel = kq.x;
+        s = (int)kq.y;
+        r.ox = W.qo[3 * lo + qp]; r.oy = W.qo[3 * lo + n + qp]; r.oz = W.qo[3 * lo + 2 * n + qp];
+        r.dx = W.qd[3 * lo + qp]; r.dy = W.qd[3 * lo + n + qp]; r.dz = W.qd[3 * lo + 2 * n + qp];
+        r.time = W.qtime[e];
+        const double t_hit = W.ht[e];
         if (hp.x < 0) {   // main.rs:37: the background
             cr = cr + Tr * P.bg[0];
             cg = cg + Tg * P.bg[1];
             cb = cb + Tb * P.bg[2];
             ended = true;
         } else {
-            r.ox = W.o[slot]; r.oy = W.o[n + slot]; r.oz = W.o[2 * n + slot];
-            r.dx = W.d[slot]; r.dy = W.d[n + slot]; r.dz = W.d[2 * n + slot];
-            r.time = W.time[slot];
             r.a = r.dx * r.dx + r.dy * r.dy + r.dz * r.dz;   // finish_ray's |d|^2 (shade_end's 1/sqrt)
             HitRefT<R> best;
-            best.t = W.ht[slot];
+            best.t = t_hit;
             best.prim = hp.x;
             best.sub = hp.y >> 3;
             best.side = hp.y & 7;
@@ -367,11 +404,10 @@ __global__ void __launch_bounds__(kWfLogicThreads) wf_logic(SceneDev S, const KP
         o[1] = vg;
         o[2] = vb;
     };
-    auto load_unit = [&]() {
+    auto load_unit = [&]() {   // (s and pixel came with the queue entry)
         const int2 xk = W.xk[slot];
         x = xk.x;
         k = xk.y;
-        s = (int)W.smp[slot];
     };
     if (ended) {
         load_unit();
@@ -441,7 +477,6 @@ __global__ void __launch_bounds__(kWfLogicThreads) wf_logic(SceneDev S, const KP
 
     // ---- ray generation: camera rays of new samples and scattered rays of pending hits, their
     // random_in_unit_disk / random_in_unit_sphere tries in one rejection loop (trace_pool)
-    uint32_t pixel = 0;
     R u = (R)0, v = (R)0;
     if (new_sample) {
         int ix, y;
@@ -471,22 +506,19 @@ __global__ void __launch_bounds__(kWfLogicThreads) wf_logic(SceneDev S, const KP
         if (!new_sample) load_unit();
         record(0.0, 0.0, 0.0);
     }
-    if (live) {
-        W.o[slot] = r.ox; W.o[n + slot] = r.oy; W.o[2 * n + slot] = r.oz;
-        W.d[slot] = r.dx; W.d[n + slot] = r.dy; W.d[2 * n + slot] = r.dz;
+    const uint64_t lm = __ballot(live);
+    if (live) {   // the ray goes to this wave's segment of this iteration's queue
+        const uint32_t qp = (w << 6) + lanes_below(lm);
+        W.qo[3 * cu + qp] = r.ox; W.qo[3 * cu + n + qp] = r.oy; W.qo[3 * cu + 2 * n + qp] = r.oz;
+        W.qd[3 * cu + qp] = r.dx; W.qd[3 * cu + n + qp] = r.dy; W.qd[3 * cu + 2 * n + qp] = r.dz;
+        W.qtime[cu + qp] = r.time;
+        W.qkey[cu + qp] = make_uint4(pixel, (uint32_t)s, (uint32_t)(P.max_depth - depth), slot);
+        W.qpos[slot] = qp;
         W.T[slot] = Tr; W.T[n + slot] = Tg; W.T[2 * n + slot] = Tb;
         W.rng[slot] = make_uint4(rs.s0, rs.s1, rs.s2, rs.s3);
-        W.bnc[slot] = (uint32_t)(P.max_depth - depth);
-        if (new_sample) {
-            W.time[slot] = r.time;
-            W.xk[slot] = make_int2(x, k);
-            W.smp[slot] = (uint32_t)s;
-            W.pix[slot] = pixel;
-        }
+        if (new_sample) W.xk[slot] = make_int2(x, k);
     }
     if (live || traced) W.st[slot] = live ? depth : -1;
-    const uint64_t lm = __ballot(live);
-    if (live) W.q[(w << 6) + lanes_below(lm)] = slot;
     if (lane == 0) {
         W.qn[w] = (uint32_t)__popcll(lm);
         if (lm != 0) W.flag[iter % kWfFlags] = 1;
@@ -502,7 +534,7 @@ using WfLogicC = WfCfg<FEAT_SET_FINAL, true, false, false, false, kWfLogicThread
 
 static size_t wf_trace_lds(const SceneDev& S)
 {
-    return (size_t)(S.n_tlas_nodes + S.n_blas_bfs) * sizeof(LdsNode) +
+    return (size_t)(S.n_tlas_nodes + S.n_blas_bfs) * sizeof(LdsNode) + sizeof(rt_instance) +
            (size_t)S.stack_entries * kWfTraceThreads * sizeof(int);
 }
 
@@ -539,7 +571,8 @@ hipError_t launch_wavefront(const SceneDev& S, const KParams& Ph, const KParams*
         per_cu <= 0)
         return hipErrorNotSupported;
     host.waves_per_simd = per_cu * kWfTraceThreads / 256;
-    const unsigned trace_blocks = (unsigned)(cus * per_cu);
+    // a multiple of the shard count: every shard's segments have their own waves
+    const unsigned trace_blocks = (unsigned)std::max(kWfShards, cus * per_cu / kWfShards * kWfShards);
     const unsigned logic_blocks = (unsigned)(W.n / kWfLogicThreads);
     // an upper bound on the iterations (a path casts at most max_depth rays; a slot waits at most
     // one iteration between two paths), so a fault in the loop cannot spin forever
@@ -550,7 +583,8 @@ hipError_t launch_wavefront(const SceneDev& S, const KParams& Ph, const KParams*
         for (int j = 0; j < RT_WF_CHUNK; ++j, ++it) {
             hipLaunchKernelGGL(wf_logic<WfLogicC>, dim3(logic_blocks), dim3(kWfLogicThreads), lds_logic, stream, SL, P,
                                W, out, work, it);
-            hipLaunchKernelGGL(trace, dim3(trace_blocks), dim3(kWfTraceThreads), lds_trace, stream, S, P, W, counters);
+            hipLaunchKernelGGL(trace, dim3(trace_blocks), dim3(kWfTraceThreads), lds_trace, stream, S, P, W, counters,
+                               it & 1);
         }
         if ((e = hipGetLastError()) != hipSuccess) return e;
         // the flag of this chunk's last iteration, read by the host one chunk later (pipelined)

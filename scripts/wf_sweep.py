@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--spp", type=int, default=100)
     ap.add_argument("--paths", default="0")
+    ap.add_argument("--refill", default="0", help="RT_OPT_WF_REFILL values (0: the default)")
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--rounds", type=int, default=1)
     ap.add_argument("--count", action="store_true", help="also a count_work render per schedule (work and occupancy)")
@@ -38,15 +39,17 @@ def main():
     r.upload(world)
     p = rt.Renderer.params(W, H, spp, 50, bg, 1, out_format=rt.RT_OUT_F64)
     out = np.empty((H, W, 3), np.float64)
-    runs = [("pool", rt.RT_SCHED_POOL, 0)] + [("wavefront", rt.RT_SCHED_WAVEFRONT, int(x)) for x in a.paths.split(",")]
+    runs = [("pool", rt.RT_SCHED_POOL, 0, 0)] + [("wavefront", rt.RT_SCHED_WAVEFRONT, int(x), int(f))
+                                                 for x in a.paths.split(",") for f in a.refill.split(",")]
     res = {k: [] for k in runs}
     frames = {}
     stats = {}
     for _ in range(a.rounds):
         for run in runs:
-            name, sched, paths = run
+            name, sched, paths, refill = run
             r.set_schedule(sched)
             r.set_option(rt.RT_OPT_WF_PATHS, paths)
+            r.set_option(rt.RT_OPT_WF_REFILL, refill)
             r.render(cam, p, out)   # warm-up
             for _ in range(a.reps):
                 r.render(cam, p, out)
@@ -54,19 +57,20 @@ def main():
             st = r.stats()
             stats[run] = (st.schedule, st.wf_iterations, st.waves_per_simd)
             frames[run] = hashlib.sha1(out.tobytes()).hexdigest()
-            print(f"  {name} paths={paths}: {['%.2f' % m for m in res[run][-a.reps:]]}", flush=True)
+            print(f"  {name} paths={paths} refill={refill}: {['%.2f' % m for m in res[run][-a.reps:]]}", flush=True)
     base = frames[runs[0]]
     n = W * H * spp
     for run in runs:
         ms = sorted(res[run])[len(res[run]) // 2]
         sch, its, wps = stats[run]
-        print(f"{run[0]} paths={run[2]}: median {ms:.2f} ms -> {n / ms / 1e3:.1f} Msamples/s  schedule {sch} "
+        print(f"{run[0]} paths={run[2]} refill={run[3]}: median {ms:.2f} ms -> {n / ms / 1e3:.1f} Msamples/s  schedule {sch} "
               f"iterations {its} waves/SIMD {wps}  frame == pool: {frames[run] == base}", flush=True)
     if a.count:
         cp = rt.Renderer.params(W, H, min(spp, 16), 50, bg, 1, out_format=rt.RT_OUT_F32, count_work=1)
         for run in runs[:2]:
             r.set_schedule(run[1])
             r.set_option(rt.RT_OPT_WF_PATHS, run[2])
+            r.set_option(rt.RT_OPT_WF_REFILL, run[3])
             r.render(cam, cp)
             s = r.stats()
             c = r.counters(24)
@@ -78,7 +82,8 @@ def main():
                 d["busy_lane_occupancy"] = int(c[13]) / max(64 * int(c[6]), 1)
                 tot = max(int(c[21]), 1)   # wave-cycles summed over waves
                 d["phase_shares"] = {k: round(int(c[i]) / tot, 4) for k, i in
-                                     (("refill", 20), ("nodes", 8), ("leaves", 9), ("blas_start", 22), ("hit_write", 17))}
+                                     (("refill", 20), ("fetch", 16), ("ray_load_setup", 15), ("nodes", 8), ("leaves", 9),
+                                                    ("blas_start", 22), ("hit_write", 17))}
             print("count", run[0], json.dumps(d), flush=True)
 
 
