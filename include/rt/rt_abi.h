@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 2
+#define RT_ABI_VERSION 3
 
 enum {
     RT_OK = 0,
@@ -237,6 +237,8 @@ typedef struct rt_stats {
     int64_t trace_buf_bytes;     /* the trace-output buffer the last render used (both halves when overlapped) */
     int32_t overlapped;          /* 1 if its buffer batches ran overlapped (two trace streams) */
     int32_t wf_iterations;       /* RT_SCHED_WAVEFRONT: wf_logic / wf_trace iterations of the last render */
+    int64_t ring_bytes;          /* POOL with the in-kernel reduction (ABI v3): its record ring, part of
+                                    trace_buf_bytes; 0 when the per-sample buffer ran */
 } rt_stats;
 int rt_last_stats(rt_ctx* ctx, rt_stats* out);
 /* Diagnostic: the raw count_work counters of the last render (n entries; returns how many
@@ -314,7 +316,10 @@ int rt_ctx_set_variant(rt_ctx* ctx, int slab32, int lds_stack, int lds_nodes);
  *                           the walk (SceneDev.pre_leaf); takes effect at the next upload
  *   RT_OPT_WF_PATHS         wavefront schedule: path slots (0: auto)
  *   RT_OPT_WF_REFILL        wavefront schedule: a wf_trace wave takes queued rays once this many of
- *                           its 64 lanes are idle (0: auto) */
+ *                           its 64 lanes are idle (0: auto)
+ *   RT_OPT_POOL_RING        1 (default): POOL reduces each finished (tile, chunk) block inside the
+ *                           trace kernel into chunk partials; 0: the per-sample buffer and
+ *                           reduce_samples (see RT_SCHED_POOL) */
 enum {
     RT_OPT_TRACE_BUF_BYTES = 1,
     RT_OPT_BATCH_OVERLAP = 2,
@@ -323,7 +328,8 @@ enum {
     RT_OPT_EXTRA_FEATURES = 5,
     RT_OPT_HOIST = 6,
     RT_OPT_WF_PATHS = 7,
-    RT_OPT_WF_REFILL = 8
+    RT_OPT_WF_REFILL = 8,
+    RT_OPT_POOL_RING = 9
 };
 int rt_ctx_set_option(rt_ctx* ctx, int key, int64_t value);
 int rt_ctx_get_option(rt_ctx* ctx, int key, int64_t* value);
@@ -333,23 +339,27 @@ int rt_ctx_get_option(rt_ctx* ctx, int key, int64_t* value);
  *   CHUNKS: a wave owns an 8x8 tile x one chunk of samples, each lane one pixel's chunk,
  *           written as one partial per (pixel, chunk); the wave waits for its slowest lane.
  *   POOL:   persistent waves take (tile, chunk) blocks from a device counter and a lane
- *           whose path ended takes the block's next (pixel, sample) at once; every sample's
- *           radiance goes to a per-sample buffer ([8x8 tile][sample][pixel of the tile])
- *           summed per pixel in sample order.
+ *           whose path ended takes the block's next (pixel, sample) at once. A block belongs
+ *           to one wave: its samples' radiance waits in that wave's ring of 4 blocks, and when
+ *           the block's last sample ends the wave sums every pixel's samples in order into the
+ *           chunk partial (1/chunk of the per-sample bytes, as ITEMS). Small shards, whose
+ *           blocks are cut below one chunk (RT_OPT_BLOCK_SAMPLES), and RT_OPT_POOL_RING 0 write
+ *           every sample to a per-sample buffer ([8x8 tile][sample][pixel of the tile]) summed
+ *           per pixel in sample order by a second kernel.
  *   ITEMS:  persistent waves as POOL, but a lane takes a whole (pixel, chunk) item, traces
  *           its samples in order and writes one partial, as CHUNKS does (1/chunk of POOL's
  *           buffer bytes); a lane whose item ended takes the next item at once.
- *   AUTO:   POOL when the render's per-sample radiance is at most 4 x the buffer bound (it is
- *           the faster of the two), otherwise ITEMS; rt_stats.schedule reports which ran.
+ *   AUTO:   POOL (the fastest) when it reduces in the kernel or its per-sample radiance is at
+ *           most 4 x the buffer bound, otherwise ITEMS; rt_stats.schedule reports which ran.
  *   WAVEFRONT: the final-scene feature set (f64, f32 slabs, one instanced BLAS, every node fits
  *           LDS): a pool of path slots in HBM (RT_OPT_WF_PATHS) and per iteration two kernels —
  *           wf_logic (hit records, materials, camera rays of new units; live slots compacted into
  *           a ray queue) and wf_trace (persistent; a lane whose walk ends takes the next queued ray
  *           at once; the top-level and instanced-BLAS walks in one step loop). Per-sample output as
  *           POOL. A scene outside that set runs AUTO's choice (rt_stats.schedule says which ran).
- * The trace-output buffer is bounded by RT_OPT_TRACE_BUF_BYTES (default: sized at context creation
- * to 3/8 of the device's free memory, at most 128 GiB, at least 32 GiB where half the free
- * memory allows; allocated lazily, as large as a render needs). A larger render runs in buffer
+ * The trace-output buffer (POOL's ring included) is bounded by RT_OPT_TRACE_BUF_BYTES (default
+ * 4 GiB, or half the device's free memory if that is less; allocated lazily, as large as a
+ * render needs). A larger render runs in buffer
  * batches whose sums are carried across, in two halves of the bound: batch k traces into half
  * k & 1 on one of two context streams while the render's stream reduces batch k - 1, so
  * consecutive traces overlap (RT_OPT_BATCH_OVERLAP 0: one buffer, in order). A 4 GB bound renders

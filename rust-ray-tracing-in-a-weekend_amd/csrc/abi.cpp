@@ -102,6 +102,9 @@ struct rt_ctx {
     int block_samples = 0;              // RT_OPT_BLOCK_SAMPLES: samples per per-sample-pool work block (0: auto)
     int64_t wf_paths = 0;               // RT_OPT_WF_PATHS: wavefront schedule path slots (0: auto)
     int wf_refill = 0;                  // RT_OPT_WF_REFILL: idle lanes before a wf_trace wave refills (0: auto)
+    int opt_ring = 1;                   // RT_OPT_POOL_RING: POOL reduces finished blocks in the kernel
+    double* ring = nullptr;             // its per-wave record ring (kPoolRing blocks per wave)
+    size_t ring_cap = 0;
     unsigned long long raw_counters[kCounters] = {};   // the last count_work render's counters (rt_last_counters)
     uint32_t extra_features = 0;        // RT_OPT_EXTRA_FEATURES: a larger kernel variant than the scene needs (tests)
     double pad_extent = 0.0;
@@ -135,19 +138,15 @@ struct rt_ctx {
     size_t lds_per_block = 160 * 1024;
 };
 
-// The trace-output buffer's default bound, sized for the device: 3/8 of its free HBM, at most
-// 128 GiB (an MI355X: ~107 GB, so C4's 49.8 GB of per-sample radiance is one launch), at least
-// 32 GiB where half the free memory allows it (allocated lazily, only as large as a render needs).
-// A bound of 4 GB costs C2 nothing (six overlapped batches: 74.77 vs 74.75 ms
-// per frame) but the final scene 4.4 % in the item pool and 18 % in 25 overlapped per-sample
-// batches (profiles/r04e_*, r04f_*): its paths are long and its 512-thread blocks free CUs late,
-// so every batch pays a tail. The default keeps speed.
+// The trace-output buffer's default bound: 4 GiB, or half the device's free
+// memory if that is less. The per-sample pool reduces each finished block inside the kernel
+// (kPoolRing), so its output is chunk partials — C2 0.74 GB, C4 3.1 GB, one launch each — plus a
+// ring of ~0.5 GB; the per-sample buffer (small shards, RT_OPT_POOL_RING 0) is what the bound batches.
 static size_t default_buf_cap()
 {
     size_t fr = 0, tot = 0;
-    if (hipMemGetInfo(&fr, &tot) != hipSuccess || fr == 0) return (size_t)32 << 30;
-    size_t cap = std::min(fr / 8 * 3, (size_t)128 << 30);
-    cap = std::max(cap, std::min((size_t)32 << 30, fr / 2));
+    size_t cap = (size_t)4 << 30;
+    if (hipMemGetInfo(&fr, &tot) == hipSuccess && fr > 0) cap = std::min(cap, fr / 2);
     return std::max(cap >> 20, (size_t)1) << 20;
 }
 
@@ -224,6 +223,7 @@ void rt_ctx_destroy(rt_ctx* c)
     if (c->ev_done && c->any_enqueued) (void)hipEventSynchronize(c->ev_done);  // work on a caller's stream
     (void)hipFree(c->scene_buf);
     (void)hipFree(c->partial);
+    (void)hipFree(c->ring);
     (void)hipFree(c->out_buf);
     (void)hipFree(c->counters);
     (void)hipFree(c->params);
@@ -1311,6 +1311,7 @@ static int run_range(rt_ctx* c, const rt_camera* cam, const rt_render_params* p,
         c->stats.n_batches = 0;
         c->stats.trace_buf_bytes = 0;
         c->stats.overlapped = 0;
+        c->stats.ring_bytes = 0;
         c->stats.samples = 0;
         c->stats.n_items = 0;
         c->stats.n_chunks = 0;
@@ -1419,6 +1420,27 @@ static int run_range(rt_ctx* c, const rt_camera* cam, const rt_render_params* p,
     // bound is sized from the free HBM when the context is created; if the device has less by
     // now (another context, torch or RCCL allocated since), the allocation below fails and the
     // bound is halved until it fits: more batches (or the item pool), the same image.
+    // per-sample pool blocks: the chunk's 16 samples per tile while that leaves >= 160 k blocks
+    // (~40 per resident wave), else halved down to 4: a small shard's last blocks would
+    // otherwise leave waves idle (C2 rows of 1 of 8 GPUs: 16 / 8 / 4 samples 14.06 / 13.70 /
+    // 13.57 ms; the whole frame 99.9 / 100.0 / 101.4; scripts/shard_coherence.py, r02p)
+    if (c->block_samples > 0) {
+        K.block_samples = c->block_samples;
+    } else {
+        const long long tiles = (long long)K.tiles_x * K.tiles_y;
+        int bs = chunk;
+        while (bs > 4 && tiles * ((total + bs - 1) / bs) < 160000) bs = (bs + 1) / 2;
+        K.block_samples = bs;
+    }
+    // the pool's in-kernel reduction needs blocks of exactly one chunk (a block's sum is the
+    // chunk's) and batches on chunk boundaries; its ring: kPoolRing blocks for each wave of the
+    // persistent grid (at most 20 per CU: the spheres variant's 5 per SIMD; the launch clamps
+    // its grid to ring_waves)
+    bool ring_ok = c->opt_ring && K.block_samples == chunk && chunk <= (int)(rtk::kRingSlot / 64) &&
+                   s_end <= (int)rtk::kRingSampleMask;
+    const int ring_waves = c->n_cus * 20;
+    const size_t ring_bytes = (size_t)ring_waves * rtk::kPoolRing * rtk::kRingSlot * 3 * sizeof(double);
+    bool ring = false;
     bool per_sample = false;
     long long batch = 0;
     int n_batches = 0;
@@ -1438,21 +1460,25 @@ static int run_range(rt_ctx* c, const rt_camera* cam, const rt_render_params* p,
         o.pool = wavefront ? RT_SCHED_WAVEFRONT
                  : c->opt_pool != RT_SCHED_AUTO && c->opt_pool != RT_SCHED_WAVEFRONT
                      ? c->opt_pool
-                     : ((size_t)total * sample_bytes <= 4 * buf_cap ? RT_SCHED_POOL : RT_SCHED_ITEMS);
+                     : (ring_ok || (size_t)total * sample_bytes <= 4 * buf_cap ? RT_SCHED_POOL : RT_SCHED_ITEMS);
+        // POOL with the in-kernel reduction: chunk partials like ITEMS (the ring takes its share of
+        // the bound first, the partials at least one chunk)
+        ring = o.pool == RT_SCHED_POOL && ring_ok;
+        const size_t out_cap = ring ? std::max(buf_cap > ring_bytes ? buf_cap - ring_bytes : 0, px_bytes) : buf_cap;
         // Buffer batches: the trace output is bounded by sample_buf_cap. Per-sample pool: samples x
         // pixels x 24 B; chunk and item schedules: chunks x pixels x 24 B, batches on chunk
         // boundaries (relative to s_begin), so the partials add in one-launch order. A render that
         // does not fit in one batch takes two buffers of half the bound: batch k traces into half
         // k & 1 on stream tstream[k & 1] while the caller's stream reduces batch k - 1, so the
         // next trace fills the CUs its predecessor's last waves leave (no tail per batch).
-        per_sample = o.pool == RT_SCHED_POOL || o.pool == RT_SCHED_WAVEFRONT;
+        per_sample = (o.pool == RT_SCHED_POOL && !ring) || o.pool == RT_SCHED_WAVEFRONT;
         const size_t unit = per_sample ? sample_bytes : px_bytes;
-        long long fit = (long long)std::max<size_t>(1, buf_cap / unit);
+        long long fit = (long long)std::max<size_t>(1, out_cap / unit);
         batch = std::min<long long>(total, per_sample ? fit : fit * chunk);
         // (the wavefront schedule's host loop enqueues one batch after the other)
         overlap = c->opt_overlap && batch < total && o.pool != RT_SCHED_CHUNKS && o.pool != RT_SCHED_WAVEFRONT;
         if (overlap) {
-            fit = (long long)std::max<size_t>(1, buf_cap / 2 / unit);
+            fit = (long long)std::max<size_t>(1, out_cap / 2 / unit);
             batch = std::min<long long>(total, per_sample ? fit : fit * chunk);
         }
         n_batches = (int)((total + batch - 1) / batch);
@@ -1479,6 +1505,13 @@ static int run_range(rt_ctx* c, const rt_camera* cam, const rt_render_params* p,
         const size_t half = per_sample ? (size_t)batch * sample_bytes : (size_t)max_chunks * px_bytes;
         const size_t need = overlap ? 2 * half : half;
         rc = grow(c, stream, c->partial, c->partial_cap, need, &oom);
+        if (rc == RT_OK && ring) {
+            rc = grow(c, stream, c->ring, c->ring_cap, ring_bytes, &oom);
+            if (rc != RT_OK && oom) {   // no room for the ring: the per-sample buffer, as before
+                ring_ok = false;
+                continue;
+            }
+        }
         if (rc == RT_OK) break;
         if (!oom) return rc;
         if (buf_cap <= ((size_t)1 << 20) || need <= (per_sample ? sample_bytes : px_bytes))
@@ -1486,18 +1519,8 @@ static int run_range(rt_ctx* c, const rt_camera* cam, const rt_render_params* p,
         buf_cap = std::max<size_t>(buf_cap / 2, (size_t)1 << 20);
     }
     if (own_acc) HIP_TRY(hipMemsetAsync(acc, 0, px_bytes, stream));
-    // per-sample pool blocks: the chunk's 16 samples per tile while that leaves >= 160 k blocks
-    // (~40 per resident wave), else halved down to 4: a small shard's last blocks would
-    // otherwise leave waves idle (C2 rows of 1 of 8 GPUs: 16 / 8 / 4 samples 14.06 / 13.70 /
-    // 13.57 ms; the whole frame 99.9 / 100.0 / 101.4; scripts/shard_coherence.py, r02p)
-    if (c->block_samples > 0) {
-        K.block_samples = c->block_samples;
-    } else {
-        const long long tiles = (long long)K.tiles_x * K.tiles_y;
-        int bs = chunk;
-        while (bs > 4 && tiles * ((total + bs - 1) / bs) < 160000) bs = (bs + 1) / 2;
-        K.block_samples = bs;
-    }
+    K.ring = ring ? c->ring : nullptr;
+    K.ring_waves = ring ? ring_waves : 0;
     if (count) HIP_TRY(hipMemsetAsync(c->counters, 0, kCounters * sizeof(unsigned long long), stream));
     if (wavefront) {
         const int rc = wf_pool(c, stream, (long long)K.tiles_x * K.tiles_y * 64 * std::min<long long>(total, batch));
@@ -1571,9 +1594,11 @@ static int run_range(rt_ctx* c, const rt_camera* cam, const rt_render_params* p,
     c->stats.precision = o.f32 ? RT_PREC_F32 : RT_PREC_F64;
     c->stats.waves_per_simd = waves_per_simd;
     c->stats.n_batches = n_batches;
+    c->stats.ring_bytes = ring ? (int64_t)ring_bytes : 0;
     c->stats.trace_buf_bytes = (int64_t)(overlap ? 2 * half_elems * sizeof(double)
                                                  : (per_sample ? (size_t)batch * sample_bytes
-                                                               : (size_t)((batch + chunk - 1) / chunk) * px_bytes));
+                                                               : (size_t)((batch + chunk - 1) / chunk) * px_bytes)) +
+                               c->stats.ring_bytes;
     c->stats.overlapped = overlap ? 1 : 0;
     c->stats.wf_iterations = wf_iterations;
     c->stats.samples = (uint64_t)n_px * (uint64_t)total;
@@ -2002,6 +2027,7 @@ int rt_ctx_set_option(rt_ctx* c, int key, int64_t v)
         if (v < 0 || v > 64) return fail(RT_ERR_INVALID, "refill lanes out of range (0..64)");
         c->wf_refill = (int)v;
         return RT_OK;
+    case RT_OPT_POOL_RING: c->opt_ring = v != 0; return RT_OK;
     default: return fail(RT_ERR_INVALID, "unknown option");
     }
 }
@@ -2018,6 +2044,7 @@ int rt_ctx_get_option(rt_ctx* c, int key, int64_t* v)
     case RT_OPT_HOIST: *v = c->opt_hoist; return RT_OK;
     case RT_OPT_WF_PATHS: *v = c->wf_paths; return RT_OK;
     case RT_OPT_WF_REFILL: *v = c->wf_refill; return RT_OK;
+    case RT_OPT_POOL_RING: *v = c->opt_ring; return RT_OK;
     default: return fail(RT_ERR_INVALID, "unknown option");
     }
 }

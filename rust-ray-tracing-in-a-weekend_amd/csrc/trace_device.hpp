@@ -374,21 +374,67 @@ __device__ __forceinline__ bool sphere_t(double cx, double cy, double cz, double
     const double c = (ocx * ocx + ocy * ocy + ocz * ocz) - radius * radius;
     const double disc = half_b * half_b - r.a * c;
     if (disc < 0.0) return false;
-#ifdef RT_PROBE_FAST_SPHERE  // timing probe (inexact sqrt / division): NOT the product
-    const double sqrtd = __builtin_amdgcn_sqrt(disc);
-    const double ia = __builtin_amdgcn_rcp(r.a);
-    double root = (-half_b - sqrtd) * ia;
-    if (root < t_min || t_max < root) {
-        root = (-half_b + sqrtd) * ia;
-#else
     const double sqrtd = __builtin_sqrt(disc);
     double root = div_rcp(-half_b - sqrtd, r.a, r.ya);
     if (root < t_min || t_max < root) {
         root = div_rcp(-half_b + sqrtd, r.a, r.ya);
-#endif
         if (root < t_min || t_max < root) return false;
     }
     t = root;
+    return true;
+}
+
+// A sphere-bounded ConstantMedium's two boundary queries (hittable.rs:430-434: hit over
+// (-inf, inf), then over (t1 + 0.0001, inf)) from one quadratic: both calls of sphere_t above
+// compute the same discriminant and roots, and differ only in the range the roots are checked
+// against, so the pair (t1, t2) is theirs bit for bit; the second discriminant, sqrt and
+// division are not computed again (round 5, VERDICT r04 item 6: the final scene's r = 5000
+// fog sphere is queried by nearly every cast).
+__device__ __forceinline__ bool sphere_t2(double cx, double cy, double cz, double radius, const RayT<double>& r,
+                                          double& t1, double& t2)
+{
+    const double ocx = r.ox - cx, ocy = r.oy - cy, ocz = r.oz - cz;
+    const double half_b = ocx * r.dx + ocy * r.dy + ocz * r.dz;
+    const double c = (ocx * ocx + ocy * ocy + ocz * ocz) - radius * radius;
+    const double disc = half_b * half_b - r.a * c;
+    if (disc < 0.0) return false;   // both queries miss
+    const double sqrtd = __builtin_sqrt(disc);
+    const double near = div_rcp(-half_b - sqrtd, r.a, r.ya);
+    // first query, (-inf, inf): the near root (no double lies outside it; a NaN root passes
+    // sphere_t's range test too)
+    t1 = near;
+    const double lo = t1 + 0.0001;
+    if (near < lo || RT_INF < near) {
+        const double far = div_rcp(-half_b + sqrtd, r.a, r.ya);
+        if (far < lo || RT_INF < far) return false;
+        t2 = far;
+    } else {
+        t2 = near;
+    }
+    return true;
+}
+
+// f32 mode: sphere_t's f32 roots, the same selection (its second query starts at
+// t1 + max(1e-4, |t1| 2^-19), medium_t)
+__device__ __forceinline__ bool sphere_t2(double cx, double cy, double cz, double radius, const RayT<float>& r,
+                                          float& t1, float& t2)
+{
+    const double ocx = (double)r.ox - cx, ocy = (double)r.oy - cy, ocz = (double)r.oz - cz;
+    const float c = (float)((ocx * ocx + ocy * ocy + ocz * ocz) - radius * radius);
+    const float half_b = (float)ocx * r.dx + (float)ocy * r.dy + (float)ocz * r.dz;
+    const float disc = half_b * half_b - r.a * c;
+    if (disc < 0.0f) return false;
+    const float q = -(half_b + __builtin_copysignf(__builtin_sqrtf(disc), half_b));
+    const float r0 = c / q, r1 = q / r.a;
+    const float tn = fminf(r0, r1), tf = fmaxf(r0, r1);
+    t1 = tn;
+    const float lo = t1 + fmaxf(0.0001f, __builtin_fabsf(t1) * 0x1.0p-19f);
+    float root = tn;
+    if (root < lo || (float)RT_INF < root) {
+        root = tf;
+        if (root < lo || (float)RT_INF < root) return false;
+    }
+    t2 = root;
     return true;
 }
 
@@ -1087,12 +1133,21 @@ __device__ bool medium_t(const SceneDev& S, const rt_prim& m, const RayT<R>& r, 
                          StackT<C>& stack, int sp0, const Keyed& key, Count& cnt)
 {
     R t1, t2;
-    if (!boundary_t<C>(S, m.a, r, (R)-RT_INF, (R)RT_INF, t1, stack, sp0, key, cnt)) return false;
-    // the second boundary hit after t1 + 0.0001 (hittable.rs:433); in f32 the step must
-    // also clear t1's own rounding (a fog sphere of r = 5000 has ulp(t1) = 4.9e-4 > 1e-4)
-    R t1_next = t1 + (R)0.0001;
-    if constexpr (C::F32) t1_next = t1 + fmaxf(0.0001f, __builtin_fabsf(t1) * 0x1.0p-19f);
-    if (!boundary_t<C>(S, m.a, r, t1_next, (R)RT_INF, t2, stack, sp0, key, cnt)) return false;
+    if constexpr ((BoundC<C>::F & (FEAT_INST | FEAT_RECT)) == 0) {
+        // every medium boundary of this variant is a sphere: both queries from one quadratic
+        const rt_prim& p = S.prims[m.a];
+        if (C::COUNT) cnt.prims += 2;
+        double cx, cy, cz;
+        sphere_center(p, r, (C::F & FEAT_SHUTTER) != 0, cx, cy, cz, (BoundC<C>::F & FEAT_STATIC) != 0);
+        if (!sphere_t2(cx, cy, cz, p.p[3], r, t1, t2)) return false;
+    } else {
+        if (!boundary_t<C>(S, m.a, r, (R)-RT_INF, (R)RT_INF, t1, stack, sp0, key, cnt)) return false;
+        // the second boundary hit after t1 + 0.0001 (hittable.rs:433); in f32 the step must
+        // also clear t1's own rounding (a fog sphere of r = 5000 has ulp(t1) = 4.9e-4 > 1e-4)
+        R t1_next = t1 + (R)0.0001;
+        if constexpr (C::F32) t1_next = t1 + fmaxf(0.0001f, __builtin_fabsf(t1) * 0x1.0p-19f);
+        if (!boundary_t<C>(S, m.a, r, t1_next, (R)RT_INF, t2, stack, sp0, key, cnt)) return false;
+    }
     if (t1 < t_min) t1 = t_min;
     if (t2 > t_max) t2 = t_max;
     if (t1 >= t2) return false;
@@ -1968,13 +2023,65 @@ __device__ __forceinline__ unsigned lanes_below(uint64_t mask)
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
 }
 
+// Per-sample pool, in-kernel reduction (kPoolRing): the whole wave sums one finished block —
+// lane p the tile's pixel p — over its samples in order from 0.0, reduce_samples' chunk sum,
+// and writes the chunk partial ([chunk][pixel], reduce_chunks' input). The block is one chunk
+// of samples (block_samples == spp_chunk, chunk-aligned batches), so the chunk is its group.
+#ifndef RING_LOADS
+#define RING_LOADS 4
+#endif
+// lane q of v set to val (the ring state's writes; readlane reads it back as a scalar)
+__device__ __forceinline__ int ring_set(int val, int q, int v) { return (int)__lane_id() == q ? val : v; }
+
+template <class C>
+__device__ __forceinline__ double* ring_of_wave(const KParams& P)
+{
+    const unsigned wave = __builtin_amdgcn_readfirstlane(blockIdx.x * (unsigned)(BlockThreads<C>() / 64) + threadIdx.x / 64u);
+    return P.ring + (size_t)wave * kPoolRing * kRingSlot * 3;
+}
+
+__device__ __forceinline__ void ring_reduce(const KParams& P, const double* __restrict__ rec,
+                                            double* __restrict__ partial, unsigned blk, unsigned n_tiles, unsigned group,
+                                            size_t n_px, int lane)
+{
+    const unsigned grp = blk / n_tiles, tile = blk - grp * n_tiles;
+    const int s0 = P.sample_begin + (int)(grp * group);
+    const int x = (int)(tile % (unsigned)P.tiles_x) * 8 + (lane & 7);
+    const int k = (int)(tile / (unsigned)P.tiles_x) * 8 + (lane >> 3);
+    const int ns = min(P.spp, s0 + (int)group) - s0;
+    // the records were stored by lanes of this wave: order their stores before these loads
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    // one channel at a time, RING_LOADS samples' loads in flight (the wave's path state stays live
+    // beside them; one load per round trip left the wave waiting on L2 ~48 times per block)
+    constexpr int NB = RING_LOADS;
+    const bool own = x < P.width && k < P.n_rows;
+    double* o = partial + ((size_t)grp * n_px + (size_t)k * P.width + x) * 3;
+#pragma unroll 1
+    for (int c = 0; c < 3; ++c) {
+        const double* p = rec + (size_t)lane * 3 + c;
+        double a = 0.0;
+#pragma unroll 1
+        for (int j0 = 0; j0 < ns; j0 += NB) {
+            double v[NB];
+#pragma unroll
+            for (int j = 0; j < NB; ++j) v[j] = j0 + j < ns ? p[(size_t)j * 64 * 3] : 0.0;
+#pragma unroll
+            for (int j = 0; j < NB; ++j)
+                if (j0 + j < ns) a = a + v[j];
+            p += (size_t)NB * 64 * 3;
+        }
+        if (own) o[c] = a;
+    }
+}
+
 // ITEMS (the item pool, default): a unit is a (pixel, chunk) item instead of one sample.
 // The lane that takes it traces the chunk's samples in order, summing their radiance in
 // registers exactly as trace_chunks does, and writes one partial per (pixel, chunk) when
 // the last one ends; a lane whose item ended takes the next item at once, as in the
 // per-sample pool, so lanes still do not idle. Output: chunk partials for
 // reduce_chunks, 1/chunk of the per-sample buffer's bytes.
-template <class C, bool ITEMS>
+template <class C, bool ITEMS, bool RING = false>
 __global__ void __launch_bounds__(BlockThreads<C>(), min_waves<C>()) trace_pool(SceneDev S, const KParams* __restrict__ Pp,
                                                                   double* __restrict__ samples,
                                                                   unsigned long long* __restrict__ counters,
@@ -2019,7 +2126,32 @@ __global__ void __launch_bounds__(BlockThreads<C>(), min_waves<C>()) trace_pool(
     bool pending = false;
     bool cam_wait = false;  // RT_TRY_LEFT: camera_begin ran, the disk tries go on (u, v in r.dx, r.dy)
     (void)cam_wait;
+    // In-kernel reduction (RING, the per-sample pool with P.ring; kPoolRing): the wave's blocks
+    // in flight live in the lanes of one VGPR (wave-uniform values; as SGPRs they pushed the
+    // variants into spills): lane q the block of ring slot q, lane kRingCur the slot units are
+    // taken from, lane kRingOcc the occupied slots (bit q). A lane's record index in the wave's
+    // ring (slot x kRingSlot + sample of the block x 64 + pixel of the tile) rides in the bits
+    // of `s` above kRingSampleBits, so a block is finished when it is not the one units are taken
+    // from and no active lane holds one of its units.
+    constexpr bool ring = RING && !ITEMS;
+    int ringv = 0;
     for (;;) {
+        if (ring) {   // blocks whose last sample ended: every pixel's samples summed in order
+            unsigned occ = (unsigned)__builtin_amdgcn_readlane(ringv, kRingOcc);
+            if (occ != 0) {
+                const unsigned open = blk_next < blk_units ? (unsigned)__builtin_amdgcn_readlane(ringv, kRingCur) : 99u;
+#pragma unroll
+                for (int q = 0; q < kPoolRing; ++q) {
+                    if ((occ >> q & 1u) && (unsigned)q != open &&
+                        __ballot(active && ((unsigned)s >> kRingSampleBits) / kRingSlot == (unsigned)q) == 0) {
+                        ring_reduce(P, ring_of_wave<C>(P) + (size_t)q * kRingSlot * 3, samples,
+                                    (unsigned)__builtin_amdgcn_readlane(ringv, q), n_tiles, group, n_px, lane);
+                        occ &= ~(1u << q);
+                        ringv = ring_set((int)occ, kRingOcc, ringv);
+                    }
+                }
+            }
+        }
         if (ITEMS && own) {
             own = false;
             active = true;
@@ -2030,6 +2162,12 @@ __global__ void __launch_bounds__(BlockThreads<C>(), min_waves<C>()) trace_pool(
         uint64_t need = __ballot(!active);
         while (need != 0 && !exhausted) {
             if (blk_next == blk_units) {
+                int free_slot = -1;
+                if (ring) {   // a free ring slot first: every one holds an unfinished block -> wait
+                    const unsigned occ = (unsigned)__builtin_amdgcn_readlane(ringv, kRingOcc);
+                    if (occ == (1u << kPoolRing) - 1) break;
+                    free_slot = __builtin_ctz(~occ);
+                }
                 unsigned b = 0;
                 if (lane == 0) b = atomicAdd(work, 1u);
                 b = __builtin_amdgcn_readfirstlane(b);
@@ -2049,6 +2187,11 @@ __global__ void __launch_bounds__(BlockThreads<C>(), min_waves<C>()) trace_pool(
                 } else {
                     s0 = P.sample_begin + (int)(grp * group);
                     blk_units = nvalid * (unsigned)(min(P.spp, s0 + (int)group) - s0);
+                    if (ring) {
+                        ringv = ring_set((int)b, free_slot, ringv);
+                        ringv = ring_set(free_slot, kRingCur, ringv);
+                        ringv = ring_set(__builtin_amdgcn_readlane(ringv, kRingOcc) | (1 << free_slot), kRingOcc, ringv);
+                    }
                 }
                 blk_next = 0;
             }
@@ -2073,6 +2216,10 @@ __global__ void __launch_bounds__(BlockThreads<C>(), min_waves<C>()) trace_pool(
                     cr = cg = cb = 0.0;
                 } else {
                     s = s0 + (int)si;
+                    if (ring) {
+                        const unsigned cur_slot = (unsigned)__builtin_amdgcn_readlane(ringv, kRingCur);
+                        s |= (int)((cur_slot * kRingSlot + si * 64u + (unsigned)((k & 7) * 8 + (x & 7))) << kRingSampleBits);
+                    }
                 }
                 active = true;
                 new_sample = true;
@@ -2116,8 +2263,9 @@ __global__ void __launch_bounds__(BlockThreads<C>(), min_waves<C>()) trace_pool(
                     int ix, y;
                     image_xy(P, x, k, ix, y);
                     key.pixel = (uint32_t)y * (uint32_t)P.img_width + (uint32_t)ix;
-                    key.sample = (uint32_t)s;
-                    ds_start(st, P.seed, key.pixel, (uint32_t)s);
+                    const uint32_t sample = ring ? (uint32_t)s & kRingSampleMask : (uint32_t)s;
+                    key.sample = sample;
+                    ds_start(st, P.seed, key.pixel, sample);
                     camera_begin(P, ix, y, st, u, v);
                     Tr = Tg = Tb = (R)1;
                     if constexpr (!ITEMS) cr = cg = cb = 0.0;  // ITEMS: the chunk's running sum
@@ -2185,10 +2333,17 @@ __global__ void __launch_bounds__(BlockThreads<C>(), min_waves<C>()) trace_pool(
             active = false;
             own = true;
         } else {
-            // items: the chunk's partial, [chunk][pixel]; per-sample pool: tiled_record order
-            double* o = ITEMS ? samples + ((size_t)((unsigned)(s - P.sample_begin) / (unsigned)P.spp_chunk) * n_px +
-                                           (size_t)k * P.width + x) * 3
-                              : samples + tiled_record(P.tiles_x, P.spp - P.sample_begin, x, k, s - P.sample_begin) * 3;
+            // items: the chunk's partial, [chunk][pixel]; per-sample pool: tiled_record order,
+            // or (ring) the record index taken with the unit (in the high bits of s)
+            double* o;
+            if (ITEMS) {
+                o = samples + ((size_t)((unsigned)(s - P.sample_begin) / (unsigned)P.spp_chunk) * n_px +
+                               (size_t)k * P.width + x) * 3;
+            } else if (ring) {
+                o = ring_of_wave<C>(P) + (size_t)((unsigned)s >> kRingSampleBits) * 3;
+            } else {
+                o = samples + tiled_record(P.tiles_x, P.spp - P.sample_begin, x, k, s - P.sample_begin) * 3;
+            }
             o[0] = cr;
             o[1] = cg;
             o[2] = cb;
@@ -2237,6 +2392,7 @@ struct Launch {
     int pool;                      // 0 chunks, 1 per-sample pool, 2 item pool
     unsigned long long n_blocks;   // 8x8 tiles x chunks
     int* waves_per_simd;           // out (optional): resident blocks per CU = waves per SIMD (4-wave blocks)
+    unsigned max_waves = 0;        // per-sample pool with the in-kernel reduction: waves its ring holds
 };
 
 // Resident blocks per CU of a kernel (registers, LDS); waves per SIMD reported to the caller.
@@ -2275,12 +2431,16 @@ static void launch_one(const Launch& L, hipStream_t stream, bool nall)
                                   s16 ? 2 : 4, stage ? S.n_lds_materials : 0, stage ? S.n_lds_textures : 0, bt).total;
     if (L.pool) {
         auto go = [&](auto kernel) {
-            const unsigned nb = std::min<unsigned long long>(resident_blocks(L, kernel, lds, bt), (L.n_blocks + wpb - 1) / wpb);
+            unsigned nb = std::min<unsigned long long>(resident_blocks(L, kernel, lds, bt), (L.n_blocks + wpb - 1) / wpb);
+            if (L.max_waves) nb = std::max(1u, std::min(nb, L.max_waves / (unsigned)wpb));
             hipLaunchKernelGGL(kernel, dim3(nb), dim3(bt), lds, stream, S, L.P, L.out, L.counters, L.work);
         };
         if (L.pool == 2) {
             if (nall) go(trace_pool<Cfg<F, S32, LDS, true, COUNT, F32>, true>);
             else go(trace_pool<Cfg<F, S32, LDS, false, COUNT, F32>, true>);
+        } else if (L.max_waves) {   // the per-sample pool reducing in the kernel (KParams.ring)
+            if (nall) go(trace_pool<Cfg<F, S32, LDS, true, COUNT, F32>, false, true>);
+            else go(trace_pool<Cfg<F, S32, LDS, false, COUNT, F32>, false, true>);
         } else {
             if (nall) go(trace_pool<Cfg<F, S32, LDS, true, COUNT, F32>, false>);
             else go(trace_pool<Cfg<F, S32, LDS, false, COUNT, F32>, false>);
@@ -2316,8 +2476,9 @@ static void launch_f(const Launch& L, int slab32, int lds, hipStream_t stream)
         if (static_lds < 0) {
             static_lds = 0;
             hipFuncAttributes a;
-            const void* ks[3] = {(const void*)trace_pool<Cfg<F, true, true, true, COUNT, false>, false>,
+            const void* ks[4] = {(const void*)trace_pool<Cfg<F, true, true, true, COUNT, false>, false>,
                                  (const void*)trace_pool<Cfg<F, true, true, true, COUNT, false>, true>,
+                                 (const void*)trace_pool<Cfg<F, true, true, true, COUNT, false>, false, true>,
                                  (const void*)trace_chunks<Cfg<F, true, true, true, COUNT, false>>};
             for (const void* k : ks)
                 if (hipFuncGetAttributes(&a, k) != hipSuccess || a.sharedSizeBytes != 0) static_lds = 1;

@@ -193,6 +193,7 @@ hipError_t launch_trace(const SceneDev& S, const KParams& Ph, const KParams* P, 
     L.work = work;
     L.pool = o.pool;
     L.waves_per_simd = o.waves_per_simd;
+    L.max_waves = o.pool == 1 && Ph.ring ? (unsigned)Ph.ring_waves : 0u;
     // waves of the chunk schedule / work blocks of the pools
     const long long groups = o.pool == 2   ? (Ph.n_chunks + std::max(1, Ph.block_chunks) - 1) / std::max(1, Ph.block_chunks)
                              : o.pool == 1 ? ((long long)Ph.spp - Ph.sample_begin + std::max(1, Ph.block_samples) - 1) /

@@ -97,7 +97,23 @@ struct KParams {
     int32_t tile_shard;         // rt_render_params.tile_shard: grid tile m = the frame's tile row_begin + m*row_stride
     int32_t img_tiles_x;        // tiles per tile row of the image
     int32_t wf_refill;          // wavefront schedule: a wf_trace wave refills once this many lanes are idle
+    int32_t ring_waves;         // per-sample pool, in-kernel reduction: waves the ring holds (0: off)
+    double* ring;               // per-sample pool, in-kernel reduction: kPoolRing blocks of records per wave
 };
+
+// Per-sample pool with the reduction in the kernel (round 5): a wave's work block (one tile x
+// one chunk of samples) is owned by that wave alone, so the wave counts its finished samples
+// and, when the block's last one ends, sums every pixel's samples in order and writes the
+// chunk partial (reduce_chunks' input). The records wait in a ring of kPoolRing blocks per
+// wave (record j of a block: sample j / 64, pixel j % 64 of the 8x8 tile). Needs chunks of at
+// most 16 samples and samples below 2^20 (the host checks both).
+constexpr int kPoolRing = 4;
+constexpr unsigned kRingSlot = 16 * 64;        // records per ring slot: chunks of at most 16 samples
+constexpr int kRingCur = kPoolRing;            // lanes of the wave's ring-state VGPR (trace_pool):
+constexpr int kRingOcc = kPoolRing + 1;        //   the slot units are taken from, the occupied slots
+constexpr int kRingSampleBits = 20;            // ring: samples below 2^20, the record index above
+constexpr uint32_t kRingSampleMask = (1u << kRingSampleBits) - 1;
+static_assert(kPoolRing * kRingSlot <= (1u << (32 - kRingSampleBits)), "ring record index bits");
 
 // Scene features (which code a kernel variant must contain).
 enum : uint32_t {

@@ -51,6 +51,7 @@ RT_OPT_EXTRA_FEATURES = 5
 RT_OPT_HOIST = 6
 RT_OPT_WF_PATHS = 7
 RT_OPT_WF_REFILL = 8
+RT_OPT_POOL_RING = 9
 # SAH builder options (rt_world_set_build_option)
 RT_BUILD_C_ISECT = 1
 RT_BUILD_MAX_LEAF = 2
@@ -143,7 +144,8 @@ class Stats(ctypes.Structure):
                 ("wave_leaf_steps", ctypes.c_uint64), ("camera_lanes", ctypes.c_uint64),
                 ("camera_steps", ctypes.c_uint64), ("shade_lanes", ctypes.c_uint64),
                 ("shade_steps", ctypes.c_uint64), ("precision", ctypes.c_int32), ("waves_per_simd", ctypes.c_int32),
-                ("trace_buf_bytes", ctypes.c_int64), ("overlapped", ctypes.c_int32), ("wf_iterations", ctypes.c_int32)]
+                ("trace_buf_bytes", ctypes.c_int64), ("overlapped", ctypes.c_int32), ("wf_iterations", ctypes.c_int32),
+                ("ring_bytes", ctypes.c_int64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

@@ -7,8 +7,9 @@ one after another, `--rounds` times round-robin, so clock drift spreads over all
 Prints per-build median kernel ms and whether the f64 test image equals the first build's.
 
 usage: python scripts/ab_builds.py lib/a.so lib/b.so [--scene 0 --width 1200 --height 800 --spp 500]
-       (a build given as lib/a.so@RT_X=1,RT_Y=2 runs with those environment variables: host-side
-       options such as the flattener's RT_INST_DISSOLVE)
+       (a build given as lib/a.so@opt9=0,opt1=4294967296 runs with those rt_ctx_set_option
+       keys and values; any other NAME=V pair is set in the child's environment)
+       Times are kernel + reduce ms (the frame's trace launches and their reductions).
 """
 import argparse
 import hashlib
@@ -29,6 +30,8 @@ a = json.loads({args!r})
 world = rt.World(1).build_scene(a["scene"])
 cam, bg = rt.scene_camera(a["scene"], a["width"], a["height"])
 r = rt.Renderer(0)
+for k, v in a["opts"].items():
+    r.set_option(int(k), int(v))
 r.upload(world)
 img = r.render(cam, rt.Renderer.params(a["width"], a["height"], 2, a["depth"], bg, 1, row_stride=8,
                                        out_format=rt.RT_OUT_F64))
@@ -38,9 +41,11 @@ r.render(cam, p, out)
 ms = []
 for _ in range(a["reps"]):
     r.render(cam, p, out)
-    ms.append(r.stats().kernel_ms)
+    st = r.stats()
+    ms.append(st.kernel_ms + st.reduce_ms)
 import hashlib
-print("RESULT", json.dumps({{"ms": ms, "img": hashlib.sha1(img.tobytes()).hexdigest(),
+print("RESULT", json.dumps({{"ms": ms, "trace_buf_bytes": st.trace_buf_bytes, "n_batches": st.n_batches,
+                            "ring_bytes": getattr(st, "ring_bytes", 0), "img": hashlib.sha1(img.tobytes()).hexdigest(),
                             "frame": hashlib.sha1(out.tobytes()).hexdigest()}}))
 """
 
@@ -56,15 +61,16 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--rounds", type=int, default=2)
     a = ap.parse_args()
-    args = json.dumps(dict(scene=a.scene, width=a.width, height=a.height, spp=a.spp, depth=a.depth, reps=a.reps))
-    code = CHILD.format(repo=REPO, args=args)
+    base_args = dict(scene=a.scene, width=a.width, height=a.height, spp=a.spp, depth=a.depth, reps=a.reps)
     res = {lib: [] for lib in a.libs}
     imgs = {}
     for _ in range(a.rounds):
         for lib in a.libs:
             path, _, extra = lib.partition("@")   # lib.so@NAME=V,NAME=V: that build under those env vars
             env = dict(os.environ, RT_LIB_PATH=os.path.abspath(os.path.join(REPO, path)))
-            env.update(kv.split("=", 1) for kv in extra.split(",") if kv)
+            kvs = [kv.split("=", 1) for kv in extra.split(",") if kv]
+            env.update((k, v) for k, v in kvs if not k.startswith("opt"))
+            code = CHILD.format(repo=REPO, args=json.dumps(dict(base_args, opts={k[3:]: v for k, v in kvs if k.startswith("opt")})))
             out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=600)
             if out.returncode != 0:
                 print(f"{lib}: child failed ({out.returncode})\n{out.stderr[-2000:]}")
@@ -73,7 +79,8 @@ def main():
             d = json.loads(line[7:])
             res[lib] += d["ms"]
             imgs[lib] = (d["img"], d.get("frame"))
-            print(f"  {lib}: {['%.2f' % m for m in d['ms']]}", flush=True)
+            print(f"  {lib}: {['%.2f' % m for m in d['ms']]}  buf {d['trace_buf_bytes'] / 2**30:.2f} GiB "
+                  f"(ring {d['ring_bytes'] / 2**30:.2f}) batches {d['n_batches']}", flush=True)
     base = imgs[a.libs[0]]
     n = a.width * a.height * a.spp
     for lib in a.libs:
