@@ -323,9 +323,12 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(device)
     t0 = time.perf_counter()
+    step_ends = []
     for i in range(args.steps):
         step(timed=True)
         kernel_ms.append(renderer.stats().kernel_ms)   # HIP events around the trace kernel on `stream`
+        torch.cuda.synchronize(device)
+        step_ends.append(time.perf_counter())
         progress(f"step {i + 1}/{args.steps}: kernel {kernel_ms[-1]:.1f} ms")
     torch.cuda.synchronize(device)
     if dist_on:
@@ -351,6 +354,7 @@ def main():
     value = samples_per_step * args.steps / elapsed / 1e6
     ms_per_step = elapsed / args.steps * 1e3
     k_ms = float(np.mean(kernel_ms)) if kernel_ms else float("nan")
+    step_ms = [(b - a) * 1e3 for a, b in zip([t0] + step_ends[:-1], step_ends)]
 
     # ---- roofline: VALU issue (the binding resource), from the PMC pass of this build. The build
     # is the LOADED library's (rt_build_info, compiled in from __graft_entry__.source_hash()); a
@@ -517,7 +521,12 @@ def main():
             "roofline": roofline,
             "cpu_baseline": cpu,
             "parity": parity,
-            "detail": {"kernel_ms_mean": round(k_ms, 3), "reduce_ms": round(last.reduce_ms, 3),
+            "detail": {"kernel_ms_mean": round(k_ms, 3), "kernel_ms_median": round(float(np.median(kernel_ms)), 3),
+                       "kernel_ms_steps": [round(x, 3) for x in kernel_ms],
+                       "step_ms_median": round(float(np.median(step_ms)), 3) if step_ms else None,
+                       "value_at_median_step": (round(samples_per_step / (float(np.median(step_ms)) * 1e-3) / 1e6, 3)
+                                                if step_ms else None),
+                       "reduce_ms": round(last.reduce_ms, 3), "ring_bytes": int(getattr(last, "ring_bytes", 0)),
                        "schedule": last.schedule, "n_batches": last.n_batches, "waves_per_simd": last.waves_per_simd, "spp_chunk": last.spp_chunk,
                        "trace_buf_bytes": int(last.trace_buf_bytes), "batches_overlapped": bool(last.overlapped),
                        "scene_bytes": int(last.scene_bytes), "scene_build_upload_s": round(t_build, 3),

@@ -69,7 +69,7 @@ struct rt_world {
     rtw::World w;
 };
 
-constexpr int kCounters = 24;  // count_work counters (trace_device.hpp: the trace kernels' epilogues; rt_last_counters)
+constexpr int kCounters = 32;  // count_work counters (trace_device.hpp: the trace kernels' epilogues; rt_last_counters)
 
 struct rt_ctx {
     int device = 0;
@@ -1439,7 +1439,7 @@ static int run_range(rt_ctx* c, const rt_camera* cam, const rt_render_params* p,
     bool ring_ok = c->opt_ring && K.block_samples == chunk && chunk <= (int)(rtk::kRingSlot / 64) &&
                    s_end <= (int)rtk::kRingSampleMask;
     const int ring_waves = c->n_cus * 20;
-    const size_t ring_bytes = (size_t)ring_waves * rtk::kPoolRing * rtk::kRingSlot * 3 * sizeof(double);
+    const size_t ring_bytes = (size_t)ring_waves * rtk::kRingWaveDoubles * sizeof(double);
     bool ring = false;
     bool per_sample = false;
     long long batch = 0;
@@ -1464,7 +1464,14 @@ static int run_range(rt_ctx* c, const rt_camera* cam, const rt_render_params* p,
         // POOL with the in-kernel reduction: chunk partials like ITEMS (the ring takes its share of
         // the bound first, the partials at least one chunk)
         ring = o.pool == RT_SCHED_POOL && ring_ok;
-        const size_t out_cap = ring ? std::max(buf_cap > ring_bytes ? buf_cap - ring_bytes : 0, px_bytes) : buf_cap;
+        // overlapped batches trace two launches at once, a ring each: a render that does not fit
+        // one batch beside one ring budgets two
+        size_t out_cap = buf_cap;
+        if (ring) {
+            const size_t all = (size_t)((total + chunk - 1) / chunk) * px_bytes;
+            const int rings = c->opt_overlap && all + ring_bytes > buf_cap ? 2 : 1;
+            out_cap = std::max(buf_cap > rings * ring_bytes ? buf_cap - rings * ring_bytes : 0, px_bytes);
+        }
         // Buffer batches: the trace output is bounded by sample_buf_cap. Per-sample pool: samples x
         // pixels x 24 B; chunk and item schedules: chunks x pixels x 24 B, batches on chunk
         // boundaries (relative to s_begin), so the partials add in one-launch order. A render that
@@ -1506,7 +1513,7 @@ static int run_range(rt_ctx* c, const rt_camera* cam, const rt_render_params* p,
         const size_t need = overlap ? 2 * half : half;
         rc = grow(c, stream, c->partial, c->partial_cap, need, &oom);
         if (rc == RT_OK && ring) {
-            rc = grow(c, stream, c->ring, c->ring_cap, ring_bytes, &oom);
+            rc = grow(c, stream, c->ring, c->ring_cap, (overlap ? 2 : 1) * ring_bytes, &oom);
             if (rc != RT_OK && oom) {   // no room for the ring: the per-sample buffer, as before
                 ring_ok = false;
                 continue;
@@ -1519,7 +1526,6 @@ static int run_range(rt_ctx* c, const rt_camera* cam, const rt_render_params* p,
         buf_cap = std::max<size_t>(buf_cap / 2, (size_t)1 << 20);
     }
     if (own_acc) HIP_TRY(hipMemsetAsync(acc, 0, px_bytes, stream));
-    K.ring = ring ? c->ring : nullptr;
     K.ring_waves = ring ? ring_waves : 0;
     if (count) HIP_TRY(hipMemsetAsync(c->counters, 0, kCounters * sizeof(unsigned long long), stream));
     if (wavefront) {
@@ -1553,6 +1559,7 @@ static int run_range(rt_ctx* c, const rt_camera* cam, const rt_render_params* p,
         const int h = overlap ? (bi & 1) : 0;
         double* buf = c->partial + (size_t)h * half_elems;
         hipStream_t ts = overlap ? c->tstream[h] : stream;
+        K.ring = ring ? c->ring + (size_t)h * (ring_bytes / sizeof(double)) : nullptr;   // one ring per trace stream
         if (overlap && bi >= 2) HIP_TRY(hipStreamWaitEvent(ts, c->ev_rd[h], 0));   // batch bi - 2 reduced: half free
         rtk::KParams* dK = c->params + c->param_slot;
         c->param_slot = (c->param_slot + 1) % kParamSlots;
@@ -1594,7 +1601,7 @@ static int run_range(rt_ctx* c, const rt_camera* cam, const rt_render_params* p,
     c->stats.precision = o.f32 ? RT_PREC_F32 : RT_PREC_F64;
     c->stats.waves_per_simd = waves_per_simd;
     c->stats.n_batches = n_batches;
-    c->stats.ring_bytes = ring ? (int64_t)ring_bytes : 0;
+    c->stats.ring_bytes = ring ? (int64_t)((overlap ? 2 : 1) * ring_bytes) : 0;
     c->stats.trace_buf_bytes = (int64_t)(overlap ? 2 * half_elems * sizeof(double)
                                                  : (per_sample ? (size_t)batch * sample_bytes
                                                                : (size_t)((batch + chunk - 1) / chunk) * px_bytes)) +

@@ -89,6 +89,8 @@ struct Count {
     // it times, so summed over lanes they are wave totals): ray set-up, the walk's prologue
     // (pre-leaf test, bounds), the hit record, and inside the leaf tests the media and instances
     uint64_t t_setup, t_pre, t_rec, t_med, t_inst, t_refill, t_defer;
+    // ray generation split (pool kernels): path seeding + camera jitter, the rejection loop
+    uint64_t t_seed, t_tries;
 };
 // COUNT phase stamps: tp is the lane's last stamp; the first active lane adds the interval
 #define RT_STAMP(acc, tp)                                                   \
@@ -1432,9 +1434,6 @@ __device__ __forceinline__ bool checker_odd(const HitT<float>& h)   // f32 mode:
 }
 __device__ __forceinline__ bool checker_odd(const HitT<double>& h)
 {
-#ifdef RT_PROBE_NO_CHECKER  // timing probe: NOT the product
-    return h.px * h.pz < 0.0;
-#endif
     const double ax = 10.0 * h.px, ay = 10.0 * h.py, az = 10.0 * h.pz;
     const int sx = rt_sin_sign(ax), sy = rt_sin_sign(ay), sz = rt_sin_sign(az);
     if (sx == 2 || sy == 2 || sz == 2) return rt_sin(ax) * rt_sin(ay) * rt_sin(az) < 0.0;
@@ -1496,10 +1495,6 @@ __device__ void tex_value(const SceneDev& S, int ti, const HitT<R>& h, R& cr, R&
 // a xoshiro128++ state, from which the path draws in the reference's order.
 __device__ __forceinline__ void ds_start(rt_pstream& st, uint64_t seed, uint32_t pixel, uint32_t sample)
 {
-#ifdef RT_EXPERIMENT_CHEAP_RNG  // timing probe of the seeding's share: NOT the product's stream
-    st.s0 = pixel * 0x9E3779B1u ^ sample; st.s1 = sample * 0x85EBCA77u ^ pixel; st.s2 = ~pixel; st.s3 = (uint32_t)seed;
-    return;
-#endif
     rt_pstream_init(&st, seed, pixel, sample);
 }
 __device__ __forceinline__ uint64_t ds_u64(rt_pstream& st) { return rt_pstream_u64(&st); }
@@ -1545,13 +1540,8 @@ __device__ __forceinline__ void camera_begin(const KParams& P, int x, int y, rt_
 }
 __device__ __forceinline__ void camera_begin(const KParams& P, int x, int y, rt_pstream& st, double& u, double& v)
 {
-#ifdef RT_PROBE_FAST_CAMERA  // timing probe: NOT the product
-    u = ((double)x + rt_unit53(ds_u64(st))) * __builtin_amdgcn_rcp((double)P.img_width - 1.0);
-    v = ((double)y + rt_unit53(ds_u64(st))) * __builtin_amdgcn_rcp((double)P.height - 1.0);
-#else
     u = div_rcp((double)x + rt_unit53(ds_u64(st)), P.wm1, P.inv_wm1);
     v = div_rcp((double)y + rt_unit53(ds_u64(st)), P.hm1, P.inv_hm1);
-#endif
 }
 // one try of random_in_unit_disk (3 = false) or random_in_unit_sphere (3 = true): the
 // length test of a disk candidate is x*x + y*y + 0*0, the same value as x*x + y*y
@@ -1728,11 +1718,7 @@ __device__ __forceinline__ bool shade_end(const SceneDev& S, const HitT<R>& h, R
     // each once: one unit-sphere loop (Lambertian, Metal, Isotropic), one 1/sqrt (of the
     // candidate for Lambertian, of the ray direction for Metal and Dielectric), one texture
     // lookup (Lambertian, Isotropic).
-#ifdef RT_PROBE_FAST_SHADE  // timing probe: NOT the product
-    const R inv = __builtin_amdgcn_rsq(kind == RT_MAT_LAMBERTIAN ? l2 : r.a);
-#else
     const R inv = (R)1 / r_sqrt(kind == RT_MAT_LAMBERTIAN ? l2 : r.a);
-#endif
     R sdx, sdy, sdz, ar = (R)1, ag = (R)1, ab = (R)1;
     bool scattered = true;
     if (kind == RT_MAT_LAMBERTIAN) {  // material.rs:36-48
@@ -1980,7 +1966,9 @@ __global__ void __launch_bounds__(BlockThreads<C>(), min_waves<C>()) trace_chunk
         atomicAdd(&counters[14], (unsigned long long)cnt.shade_steps);
         // phase times are per wave (every active lane sees the same clock): one lane adds
         if ((int)(threadIdx.x & 63) == __ffsll((long long)__ballot(1)) - 1) {
-            atomicAdd(&counters[3], (unsigned long long)t_cam);
+            atomicAdd(&counters[3], (unsigned long long)(t_cam + cnt.t_seed + cnt.t_tries));   // ray generation, all of it
+        atomicAdd(&counters[23], (unsigned long long)cnt.t_seed);
+        atomicAdd(&counters[24], (unsigned long long)cnt.t_tries);
             atomicAdd(&counters[4], (unsigned long long)t_trace);
             atomicAdd(&counters[5], (unsigned long long)t_shade);
             atomicAdd(&counters[8], (unsigned long long)cnt.t_nodes);
@@ -2037,8 +2025,20 @@ template <class C>
 __device__ __forceinline__ double* ring_of_wave(const KParams& P)
 {
     const unsigned wave = __builtin_amdgcn_readfirstlane(blockIdx.x * (unsigned)(BlockThreads<C>() / 64) + threadIdx.x / 64u);
-    return P.ring + (size_t)wave * kPoolRing * kRingSlot * 3;
+    return P.ring + (size_t)wave * kRingWaveDoubles;
 }
+// the ring's header after the records: the block id of each slot (RingSgpr variants)
+__device__ __forceinline__ unsigned* ring_block_id(double* ring_wave)
+{
+    return reinterpret_cast<unsigned*>(ring_wave + (size_t)kPoolRing * kRingSlot * 3);
+}
+// Where a wave tracks its blocks in flight. The spheres variant: the occupied slots and the
+// current slot in SGPRs, the block ids in the ring's header (C2 1200x800x500 73.92 ms against
+// 74.45 with the VGPR below; round 4's per-sample buffer 74.52). The others (the final variant's
+// SGPRs are at the limit; there the SGPR form took C4 1920x1080x256 to 269.2 ms against 266.9):
+// the lanes of one VGPR (profiles/r05o_ab_c{2,4}.log).
+template <class C>
+constexpr bool RingSgpr() { return C::F == FEAT_SET_SPHERES; }
 
 __device__ __forceinline__ void ring_reduce(const KParams& P, const double* __restrict__ rec,
                                             double* __restrict__ partial, unsigned blk, unsigned n_tiles, unsigned group,
@@ -2127,27 +2127,41 @@ __global__ void __launch_bounds__(BlockThreads<C>(), min_waves<C>()) trace_pool(
     bool cam_wait = false;  // RT_TRY_LEFT: camera_begin ran, the disk tries go on (u, v in r.dx, r.dy)
     (void)cam_wait;
     // In-kernel reduction (RING, the per-sample pool with P.ring; kPoolRing): the wave's blocks
-    // in flight live in the lanes of one VGPR (wave-uniform values; as SGPRs they pushed the
-    // variants into spills): lane q the block of ring slot q, lane kRingCur the slot units are
-    // taken from, lane kRingOcc the occupied slots (bit q). A lane's record index in the wave's
-    // ring (slot x kRingSlot + sample of the block x 64 + pixel of the tile) rides in the bits
-    // of `s` above kRingSampleBits, so a block is finished when it is not the one units are taken
-    // from and no active lane holds one of its units.
+    // in flight (RingSgpr: where), wave-uniform — the occupied slots (bit q), the slot units are
+    // taken from, each slot's block. A lane's record index in the wave's ring (slot x kRingSlot +
+    // sample of the block x 64 + pixel of the tile) rides in the bits of `s` above
+    // kRingSampleBits, so a block is finished when it is not the one units are taken from and no
+    // active lane holds one of its units.
     constexpr bool ring = RING && !ITEMS;
-    int ringv = 0;
+    int ringv = 0;                       // !RingSgpr: lane q slot q's block, kRingCur, kRingOcc
+    unsigned occ = 0, cur_slot = 0;      // RingSgpr
     for (;;) {
-        if (ring) {   // blocks whose last sample ended: every pixel's samples summed in order
-            unsigned occ = (unsigned)__builtin_amdgcn_readlane(ringv, kRingOcc);
+        if constexpr (ring && RingSgpr<C>()) {   // blocks whose last sample ended: every pixel's samples summed in order
             if (occ != 0) {
-                const unsigned open = blk_next < blk_units ? (unsigned)__builtin_amdgcn_readlane(ringv, kRingCur) : 99u;
+                const unsigned open = blk_next < blk_units ? cur_slot : 99u;
 #pragma unroll
                 for (int q = 0; q < kPoolRing; ++q) {
                     if ((occ >> q & 1u) && (unsigned)q != open &&
                         __ballot(active && ((unsigned)s >> kRingSampleBits) / kRingSlot == (unsigned)q) == 0) {
+                        double* rw = ring_of_wave<C>(P);
+                        ring_reduce(P, rw + (size_t)q * kRingSlot * 3, samples,
+                                    (unsigned)__builtin_amdgcn_readfirstlane(ring_block_id(rw)[q]), n_tiles, group, n_px, lane);
+                        occ &= ~(1u << q);
+                    }
+                }
+            }
+        } else if constexpr (ring) {   // the same, the state in ringv's lanes
+            unsigned occv = (unsigned)__builtin_amdgcn_readlane(ringv, kRingOcc);
+            if (occv != 0) {
+                const unsigned open = blk_next < blk_units ? (unsigned)__builtin_amdgcn_readlane(ringv, kRingCur) : 99u;
+#pragma unroll
+                for (int q = 0; q < kPoolRing; ++q) {
+                    if ((occv >> q & 1u) && (unsigned)q != open &&
+                        __ballot(active && ((unsigned)s >> kRingSampleBits) / kRingSlot == (unsigned)q) == 0) {
                         ring_reduce(P, ring_of_wave<C>(P) + (size_t)q * kRingSlot * 3, samples,
                                     (unsigned)__builtin_amdgcn_readlane(ringv, q), n_tiles, group, n_px, lane);
-                        occ &= ~(1u << q);
-                        ringv = ring_set((int)occ, kRingOcc, ringv);
+                        occv &= ~(1u << q);
+                        ringv = ring_set((int)occv, kRingOcc, ringv);
                     }
                 }
             }
@@ -2164,9 +2178,9 @@ __global__ void __launch_bounds__(BlockThreads<C>(), min_waves<C>()) trace_pool(
             if (blk_next == blk_units) {
                 int free_slot = -1;
                 if (ring) {   // a free ring slot first: every one holds an unfinished block -> wait
-                    const unsigned occ = (unsigned)__builtin_amdgcn_readlane(ringv, kRingOcc);
-                    if (occ == (1u << kPoolRing) - 1) break;
-                    free_slot = __builtin_ctz(~occ);
+                    const unsigned o = RingSgpr<C>() ? occ : (unsigned)__builtin_amdgcn_readlane(ringv, kRingOcc);
+                    if (o == (1u << kPoolRing) - 1) break;
+                    free_slot = __builtin_ctz(~o);
                 }
                 unsigned b = 0;
                 if (lane == 0) b = atomicAdd(work, 1u);
@@ -2188,9 +2202,15 @@ __global__ void __launch_bounds__(BlockThreads<C>(), min_waves<C>()) trace_pool(
                     s0 = P.sample_begin + (int)(grp * group);
                     blk_units = nvalid * (unsigned)(min(P.spp, s0 + (int)group) - s0);
                     if (ring) {
-                        ringv = ring_set((int)b, free_slot, ringv);
-                        ringv = ring_set(free_slot, kRingCur, ringv);
-                        ringv = ring_set(__builtin_amdgcn_readlane(ringv, kRingOcc) | (1 << free_slot), kRingOcc, ringv);
+                        if constexpr (RingSgpr<C>()) {   // the block id waits in the ring's header
+                            if (lane == 0) ring_block_id(ring_of_wave<C>(P))[free_slot] = b;
+                            cur_slot = (unsigned)free_slot;
+                            occ |= 1u << free_slot;
+                        } else {
+                            ringv = ring_set((int)b, free_slot, ringv);
+                            ringv = ring_set(free_slot, kRingCur, ringv);
+                            ringv = ring_set(__builtin_amdgcn_readlane(ringv, kRingOcc) | (1 << free_slot), kRingOcc, ringv);
+                        }
                     }
                 }
                 blk_next = 0;
@@ -2217,8 +2237,8 @@ __global__ void __launch_bounds__(BlockThreads<C>(), min_waves<C>()) trace_pool(
                 } else {
                     s = s0 + (int)si;
                     if (ring) {
-                        const unsigned cur_slot = (unsigned)__builtin_amdgcn_readlane(ringv, kRingCur);
-                        s |= (int)((cur_slot * kRingSlot + si * 64u + (unsigned)((k & 7) * 8 + (x & 7))) << kRingSampleBits);
+                        const unsigned cs = RingSgpr<C>() ? cur_slot : (unsigned)__builtin_amdgcn_readlane(ringv, kRingCur);
+                        s |= (int)((cs * kRingSlot + si * 64u + (unsigned)((k & 7) * 8 + (x & 7))) << kRingSampleBits);
                     }
                 }
                 active = true;
@@ -2275,6 +2295,7 @@ __global__ void __launch_bounds__(BlockThreads<C>(), min_waves<C>()) trace_pool(
             } else if (pending) {
                 tries = shade_draws<C>(S, h.mat);
             }
+            RT_STAMP(cnt.t_seed, t_prev);
             R qx = (R)0, qy = (R)0, qz = (R)0, l2 = (R)1;
             const bool three = !new_sample;
             if constexpr (TryLeft<C>()) {
@@ -2289,6 +2310,7 @@ __global__ void __launch_bounds__(BlockThreads<C>(), min_waves<C>()) trace_pool(
                 while (tries && !unit_try(st, (R)P.scale_m11, three, qx, qy, qz, l2)) {
                 }
             }
+            RT_STAMP(cnt.t_tries, t_prev);
             if (gen_wait) {   // (RT_TRY_LEFT) no trace this iteration; pending / new_sample stay set
                 go = false;
                 if (new_sample) {
@@ -2364,7 +2386,9 @@ __global__ void __launch_bounds__(BlockThreads<C>(), min_waves<C>()) trace_pool(
         // phase times: each region's first active lane added its intervals, so every lane's
         // share goes in (trace = everything from the ray set-up to the hit record)
         const uint64_t trace = cnt.t_setup + cnt.t_pre + cnt.t_nodes + cnt.t_leaves + cnt.t_defer + cnt.t_rec;
-        atomicAdd(&counters[3], (unsigned long long)t_cam);
+        atomicAdd(&counters[3], (unsigned long long)(t_cam + cnt.t_seed + cnt.t_tries));   // ray generation, all of it
+        atomicAdd(&counters[23], (unsigned long long)cnt.t_seed);
+        atomicAdd(&counters[24], (unsigned long long)cnt.t_tries);
         atomicAdd(&counters[4], (unsigned long long)trace);
         atomicAdd(&counters[5], (unsigned long long)t_shade);
         atomicAdd(&counters[8], (unsigned long long)cnt.t_nodes);

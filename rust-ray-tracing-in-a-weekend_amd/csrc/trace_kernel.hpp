@@ -111,6 +111,7 @@ constexpr int kPoolRing = 4;
 constexpr unsigned kRingSlot = 16 * 64;        // records per ring slot: chunks of at most 16 samples
 constexpr int kRingCur = kPoolRing;            // lanes of the wave's ring-state VGPR (trace_pool):
 constexpr int kRingOcc = kPoolRing + 1;        //   the slot units are taken from, the occupied slots
+constexpr size_t kRingWaveDoubles = (size_t)kPoolRing * kRingSlot * 3 + 8;   // a wave's records + header
 constexpr int kRingSampleBits = 20;            // ring: samples below 2^20, the record index above
 constexpr uint32_t kRingSampleMask = (1u << kRingSampleBits) - 1;
 static_assert(kPoolRing * kRingSlot <= (1u << (32 - kRingSampleBits)), "ring record index bits");

@@ -564,7 +564,7 @@ class Renderer:
     def set_variant(self, slab32: int = 1, lds_stack: int = 1, lds_nodes: int = 1):
         _check(self.lib.rt_ctx_set_variant(self.h, slab32, lds_stack, lds_nodes), "rt_ctx_set_variant")
 
-    def counters(self, n: int = 24) -> np.ndarray:
+    def counters(self, n: int = 32) -> np.ndarray:
         """The last count_work render's raw counters (rt_last_counters: phase wave-cycles etc.)."""
         out = np.zeros(n, dtype=np.uint64)
         rc = self.lib.rt_last_counters(self.h, out.ctypes.data, n)

@@ -25,8 +25,8 @@ for s in "$@"; do
     bench_c1) specs+=("300:${P}bench_c1:python bench.py --config C1 --steps 20 --warmup 3") ;;
     bench_c2) specs+=("300:${P}bench_c2:python bench.py --steps 10 --warmup 2") ;;
     bench_c3) specs+=("300:${P}bench_c3:python bench.py --config C3 --steps 5 --warmup 1") ;;
-    bench_c4) specs+=("400:${P}bench_c4:python bench.py --config C4 --steps 2 --warmup 1") ;;
-    bench_c5) specs+=("400:${P}bench_c5:python bench.py --config C5 --steps 1 --warmup 0") ;;
+    bench_c4) specs+=("400:${P}bench_c4:python bench.py --config C4 --steps 3 --warmup 1") ;;
+    bench_c5) specs+=("600:${P}bench_c5:python bench.py --config C5 --steps 3 --warmup 1") ;;
     f32_c2) specs+=("300:${P}f32_c2:python bench.py --steps 10 --warmup 2 --precision f32 $NB") ;;
     f32_c3) specs+=("300:${P}f32_c3:python bench.py --config C3 --steps 5 --warmup 1 --precision f32 $NB") ;;
     f32_c4) specs+=("300:${P}f32_c4:python bench.py --config C4 --steps 2 --warmup 1 --precision f32 $NB") ;;

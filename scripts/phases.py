@@ -49,6 +49,9 @@ def main():
         extra = ""
         if i == 9:
             extra = f"  (media {c[18] / tot:.3f}, instances {c[19] / tot:.3f})"
+        if i == 3 and len(c) > 24:
+            extra = (f"  (seeding + jitter {c[23] / tot:.3f}, rejection loop {c[24] / tot:.3f}, "
+                     f"camera_end / scatter {(c[3] - c[23] - c[24]) / tot:.3f})")
         print(f"  {name:42s} {c[i] / tot:6.3f}{extra}")
     print(f"  {'unattributed':42s} {(tot - acc) / tot:6.3f}")
     print(f"lane occupancy: bounce loop {st.casts / max(64 * st.wave_steps, 1):.3f}  node loop "

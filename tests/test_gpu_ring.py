@@ -80,21 +80,21 @@ def test_ring_chunk_sizes(rt, renderer, chunk):
 def test_ring_shards_and_batches(rt):
     """Row shards, tile shards and a render in many (overlapped) buffer batches under the ring:
     every piece equals the one-launch render."""
-    W, H, spp = 400, 240, 48
+    W, H, spp = 400, 240, 48   # chunks of 16 (spp_chunk below): blocks of one chunk, the ring's unit
     r = rt.Renderer(0)
     try:
         world = rt.World(1).build_scene(7)
-        full, st = _render(rt, r, 7, W, H, spp, 1, world=world, block=16)
-        ref, _ = _render(rt, r, 7, W, H, spp, 0, world=world, block=16)
+        full, st = _render(rt, r, 7, W, H, spp, 1, world=world, block=16, spp_chunk=16)
+        ref, _ = _render(rt, r, 7, W, H, spp, 0, world=world, block=16, spp_chunk=16)
         _same(full, ref, "whole")
         for rb in range(3):
-            part, _ = _render(rt, r, 7, W, H, spp, 1, world=world, block=16, row_begin=rb, row_stride=3)
+            part, _ = _render(rt, r, 7, W, H, spp, 1, world=world, block=16, spp_chunk=16, row_begin=rb, row_stride=3)
             _same(part, full[rb::3], f"rows {rb}")
-        slabs = [_render(rt, r, 7, W, H, spp, 1, world=world, block=16, row_begin=t, row_stride=4, tile_shard=1)[0]
+        slabs = [_render(rt, r, 7, W, H, spp, 1, world=world, block=16, spp_chunk=16, row_begin=t, row_stride=4, tile_shard=1)[0]
                  for t in range(4)]
         _same(rt.assemble_tiles(slabs, W, H, 4), full, "tiles")
-        r.set_option(rt.RT_OPT_TRACE_BUF_BYTES, st.ring_bytes + (8 << 20))   # the ring + ~3 chunks of partials
-        batched, sb = _render(rt, r, 7, W, H, spp, 1, world=world, block=16)
+        r.set_option(rt.RT_OPT_TRACE_BUF_BYTES, st.ring_bytes + (4 << 20))   # the ring + 1 chunk of partials (2.3 MB)
+        batched, sb = _render(rt, r, 7, W, H, spp, 1, world=world, block=16, spp_chunk=16)
         assert sb.ring_bytes > 0 and sb.n_batches > 1
         _same(batched, full, "batches")
     finally:
