@@ -2133,24 +2133,12 @@ __global__ void __launch_bounds__(BlockThreads<C>(), min_waves<C>()) trace_pool(
     // kRingSampleBits, so a block is finished when it is not the one units are taken from and no
     // active lane holds one of its units.
     constexpr bool ring = RING && !ITEMS;
+    // (the two forms are separate `if constexpr` blocks, not else-branches of one another: written
+    // as else-branches the spheres variant's kernel compiled to other code, 1.4 % slower on C2)
     int ringv = 0;                       // !RingSgpr: lane q slot q's block, kRingCur, kRingOcc
-    unsigned occ = 0, cur_slot = 0;      // RingSgpr
+    unsigned occ = 0, cur_slot = 0;      // RingSgpr (the other form: read from ringv where used)
     for (;;) {
-        if constexpr (ring && RingSgpr<C>()) {   // blocks whose last sample ended: every pixel's samples summed in order
-            if (occ != 0) {
-                const unsigned open = blk_next < blk_units ? cur_slot : 99u;
-#pragma unroll
-                for (int q = 0; q < kPoolRing; ++q) {
-                    if ((occ >> q & 1u) && (unsigned)q != open &&
-                        __ballot(active && ((unsigned)s >> kRingSampleBits) / kRingSlot == (unsigned)q) == 0) {
-                        double* rw = ring_of_wave<C>(P);
-                        ring_reduce(P, rw + (size_t)q * kRingSlot * 3, samples,
-                                    (unsigned)__builtin_amdgcn_readfirstlane(ring_block_id(rw)[q]), n_tiles, group, n_px, lane);
-                        occ &= ~(1u << q);
-                    }
-                }
-            }
-        } else if constexpr (ring) {   // the same, the state in ringv's lanes
+        if constexpr (ring && !RingSgpr<C>()) {   // (final variant) the same, the state in ringv's lanes
             unsigned occv = (unsigned)__builtin_amdgcn_readlane(ringv, kRingOcc);
             if (occv != 0) {
                 const unsigned open = blk_next < blk_units ? (unsigned)__builtin_amdgcn_readlane(ringv, kRingCur) : 99u;
@@ -2162,6 +2150,21 @@ __global__ void __launch_bounds__(BlockThreads<C>(), min_waves<C>()) trace_pool(
                                     (unsigned)__builtin_amdgcn_readlane(ringv, q), n_tiles, group, n_px, lane);
                         occv &= ~(1u << q);
                         ringv = ring_set((int)occv, kRingOcc, ringv);
+                    }
+                }
+            }
+        }
+        if (ring && RingSgpr<C>()) {   // blocks whose last sample ended: every pixel's samples summed in order
+            if (occ != 0) {
+                const unsigned open = blk_next < blk_units ? cur_slot : 99u;
+#pragma unroll
+                for (int q = 0; q < kPoolRing; ++q) {
+                    if ((occ >> q & 1u) && (unsigned)q != open &&
+                        __ballot(active && ((unsigned)s >> kRingSampleBits) / kRingSlot == (unsigned)q) == 0) {
+                        double* rw = ring_of_wave<C>(P);
+                        ring_reduce(P, rw + (size_t)q * kRingSlot * 3, samples,
+                                    (unsigned)__builtin_amdgcn_readfirstlane(ring_block_id(rw)[q]), n_tiles, group, n_px, lane);
+                        occ &= ~(1u << q);
                     }
                 }
             }
@@ -2178,9 +2181,9 @@ __global__ void __launch_bounds__(BlockThreads<C>(), min_waves<C>()) trace_pool(
             if (blk_next == blk_units) {
                 int free_slot = -1;
                 if (ring) {   // a free ring slot first: every one holds an unfinished block -> wait
-                    const unsigned o = RingSgpr<C>() ? occ : (unsigned)__builtin_amdgcn_readlane(ringv, kRingOcc);
-                    if (o == (1u << kPoolRing) - 1) break;
-                    free_slot = __builtin_ctz(~o);
+                    if constexpr (!RingSgpr<C>()) occ = (unsigned)__builtin_amdgcn_readlane(ringv, kRingOcc);
+                    if (occ == (1u << kPoolRing) - 1) break;
+                    free_slot = __builtin_ctz(~occ);
                 }
                 unsigned b = 0;
                 if (lane == 0) b = atomicAdd(work, 1u);
@@ -2206,10 +2209,11 @@ __global__ void __launch_bounds__(BlockThreads<C>(), min_waves<C>()) trace_pool(
                             if (lane == 0) ring_block_id(ring_of_wave<C>(P))[free_slot] = b;
                             cur_slot = (unsigned)free_slot;
                             occ |= 1u << free_slot;
-                        } else {
+                        }
+                        if constexpr (!RingSgpr<C>()) {
                             ringv = ring_set((int)b, free_slot, ringv);
                             ringv = ring_set(free_slot, kRingCur, ringv);
-                            ringv = ring_set(__builtin_amdgcn_readlane(ringv, kRingOcc) | (1 << free_slot), kRingOcc, ringv);
+                            ringv = ring_set((int)(occ | 1u << free_slot), kRingOcc, ringv);
                         }
                     }
                 }
@@ -2237,8 +2241,8 @@ __global__ void __launch_bounds__(BlockThreads<C>(), min_waves<C>()) trace_pool(
                 } else {
                     s = s0 + (int)si;
                     if (ring) {
-                        const unsigned cs = RingSgpr<C>() ? cur_slot : (unsigned)__builtin_amdgcn_readlane(ringv, kRingCur);
-                        s |= (int)((cs * kRingSlot + si * 64u + (unsigned)((k & 7) * 8 + (x & 7))) << kRingSampleBits);
+                        if constexpr (!RingSgpr<C>()) cur_slot = (unsigned)__builtin_amdgcn_readlane(ringv, kRingCur);
+                        s |= (int)((cur_slot * kRingSlot + si * 64u + (unsigned)((k & 7) * 8 + (x & 7))) << kRingSampleBits);
                     }
                 }
                 active = true;

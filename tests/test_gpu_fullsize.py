@@ -143,23 +143,26 @@ def test_c5_full_spp_row_against_oracle(rt, sched):
     _parity(img, _C5_REF["ref"], f"C5 full spp ({sched})")
 
 
-@pytest.mark.parametrize("sched", ["POOL", "ITEMS"])
+@pytest.mark.parametrize("sched", ["POOL", "ITEMS", "RING"])
 def test_c5_geometry_many_buffer_batches(rt, sched):
     """C5's 4096x4096 frame (pixel keys y*4096 + x up to 16.7 M) on 8 full-width rows incl.
     the top one, 40 spp (chunks of 3), with a 1 MB trace-output bound so the render runs
     in many buffer batches: per-sample pool 1 sample per batch, chunks straddling batches
-    (reduce_samples_carry); item pool 1 chunk per batch (accumulate_chunks)."""
+    (reduce_samples_carry); item pool 1 chunk per batch (accumulate_chunks); RING, the per-sample
+    pool reducing in the kernel, 1 chunk of partials per batch beside its two rings."""
     W = H = 4096
     spp, rows = 40, dict(row_begin=511, row_stride=512)
     r = rt.Renderer(0)
     r.set_option(rt.RT_OPT_TRACE_BUF_BYTES, 1 << 20)
-    r.set_schedule(getattr(rt, "RT_SCHED_" + sched))
+    r.set_option(rt.RT_OPT_POOL_RING, int(sched == "RING"))
+    r.set_schedule(rt.RT_SCHED_ITEMS if sched == "ITEMS" else rt.RT_SCHED_POOL)
     world = rt.World(1).build_scene(0)
     cam, bg = rt.scene_camera(0, W, H)
     r.upload(world)
     img = r.render(cam, rt.Renderer.params(W, H, spp, 50, bg, 1, out_format=rt.RT_OUT_F64, **rows))
     st = r.stats()
     assert st.n_batches == (40 if sched == "POOL" else 14), st.n_batches
+    assert (st.ring_bytes > 0) == (sched == "RING")
     r.close()
     ref = ob.render(0, W, H, spp, 50, threads=16, **rows)
     assert img.shape == (8, W, 3)
@@ -273,7 +276,7 @@ def test_device_output_on_a_torch_stream_matches_host_render(rt, renderer):
     assert np.array_equal(frame.cpu().numpy(), host)
 
 
-@pytest.mark.parametrize("sched", ["POOL", "ITEMS"])
+@pytest.mark.parametrize("sched", ["POOL", "ITEMS", "RING"])
 def test_overlapped_buffer_batches_at_c2_size(rt, renderer, sched):
     """the trace-output buffer is bounded (default 4 GB); a render larger than
     the bound runs in batches traced on two streams into the bound's two halves while the
@@ -286,7 +289,7 @@ def test_overlapped_buffer_batches_at_c2_size(rt, renderer, sched):
     cam, bg = rt.scene_camera(0, W, H)
     p = rt.Renderer.params(W, H, spp, 50, bg, 1, out_format=rt.RT_OUT_F64)
     renderer.upload(world)
-    renderer.set_schedule(getattr(rt, "RT_SCHED_" + sched))
+    renderer.set_schedule(rt.RT_SCHED_ITEMS)   # the reference image: one launch
     try:
         one = renderer.render(cam, p)
         assert renderer.stats().n_batches == 1
@@ -296,14 +299,18 @@ def test_overlapped_buffer_batches_at_c2_size(rt, renderer, sched):
         r = rt.Renderer(0)
         r.set_option(rt.RT_OPT_TRACE_BUF_BYTES, 256 << 20)
         r.set_option(rt.RT_OPT_BATCH_OVERLAP, int(overlap))
+        r.set_option(rt.RT_OPT_POOL_RING, int(sched == "RING"))
         try:
-            r.set_schedule(getattr(rt, "RT_SCHED_" + sched))
+            r.set_schedule(rt.RT_SCHED_ITEMS if sched == "ITEMS" else rt.RT_SCHED_POOL)
             r.upload(world)
             img = r.render(cam, p)
             st = r.stats()
         finally:
             r.close()
-        expect = {("POOL", "1"): 10, ("POOL", "0"): 5, ("ITEMS", "1"): 4, ("ITEMS", "0"): 2}[(sched, overlap)]
+        # RING: the ring (two when overlapped) leaves the 256 MB bound less than one 23 MB chunk of
+        # partials per batch, so batches of one chunk (the bound's floor)
+        expect = {("POOL", "1"): 10, ("POOL", "0"): 5, ("ITEMS", "1"): 4, ("ITEMS", "0"): 2,
+                  ("RING", "1"): 16, ("RING", "0"): 16}[(sched, overlap)]
         assert st.n_batches == expect, (overlap, st.n_batches)
         same = img == one
         assert same.all(), f"overlap {overlap}: {int((~same.all(axis=2)).sum())} px differ"

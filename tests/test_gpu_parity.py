@@ -398,12 +398,14 @@ def test_schedules_render_identically(rt, scene_id, W, H, spp):
     imgs = []
     small = rt.Renderer(0)
     small.set_option(rt.RT_OPT_TRACE_BUF_BYTES, 1 << 20)
+    small.set_option(rt.RT_OPT_POOL_RING, 0)          # the per-sample buffer's batches (ring: test_gpu_ring.py)
     grouped = rt.Renderer(0)                         # item-pool blocks of 3 chunks, pool blocks of 5 samples
     grouped.set_option(rt.RT_OPT_BLOCK_CHUNKS, 3)
     grouped.set_option(rt.RT_OPT_BLOCK_SAMPLES, 5)
     serial = rt.Renderer(0)                          # buffer batches one after another in one buffer
     serial.set_option(rt.RT_OPT_TRACE_BUF_BYTES, 1 << 20)
     serial.set_option(rt.RT_OPT_BATCH_OVERLAP, 0)
+    serial.set_option(rt.RT_OPT_POOL_RING, 0)
     r = rt.Renderer(0)
     runs = [(r, rt.RT_SCHED_CHUNKS), (r, rt.RT_SCHED_POOL), (r, rt.RT_SCHED_ITEMS), (small, rt.RT_SCHED_POOL),
             (small, rt.RT_SCHED_ITEMS), (grouped, rt.RT_SCHED_ITEMS), (r, rt.RT_SCHED_AUTO),

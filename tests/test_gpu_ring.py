@@ -108,7 +108,7 @@ def test_ring_progressive_accumulation(rt, renderer):
     world = rt.World(1).build_scene(0)
     cam, bg = rt.scene_camera(0, W, H)
     one, st = _render(rt, renderer, 0, W, H, spp, 0, world=world)   # per-sample buffer, one launch
-    renderer.set_option(rt.RT_OPT_BLOCK_SAMPLES, 16)
+    renderer.set_option(rt.RT_OPT_BLOCK_SAMPLES, 4)   # spp 64: chunks of 4 (blocks of one chunk: the ring)
     acc = None
     try:
         p = rt.Renderer.params(W, H, spp, 50, bg, 1, out_format=rt.RT_OUT_F64)
@@ -127,8 +127,8 @@ def test_ring_progressive_accumulation(rt, renderer):
 
 def test_ring_counts_the_same_work(rt, renderer):
     W, H, spp = 256, 128, 16
-    a, sa = _render(rt, renderer, 7, W, H, spp, 1, block=16, count_work=1)
-    b, sb = _render(rt, renderer, 7, W, H, spp, 0, block=16, count_work=1)
+    a, sa = _render(rt, renderer, 7, W, H, spp, 1, block=16, spp_chunk=16, count_work=1)
+    b, sb = _render(rt, renderer, 7, W, H, spp, 0, block=16, spp_chunk=16, count_work=1)
     assert sa.ring_bytes > 0
     assert (sa.casts, sa.node_visits, sa.prim_tests) == (sb.casts, sb.node_visits, sb.prim_tests)
     _same(a, b, "count_work")
