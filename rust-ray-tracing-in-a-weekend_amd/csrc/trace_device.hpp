@@ -2404,7 +2404,12 @@ __global__ void __launch_bounds__(BlockThreads<C>(), min_waves<C>()) trace_pool(
         atomicAdd(&counters[19], (unsigned long long)cnt.t_inst);
         atomicAdd(&counters[20], (unsigned long long)cnt.t_refill);
         atomicAdd(&counters[22], (unsigned long long)cnt.t_defer);
-        if (lane == 0) atomicAdd(&counters[21], (unsigned long long)(__builtin_amdgcn_s_memtime() - t_start));
+        if (lane == 0) {   // the wave's lifetime; the longest, and the wave count (the launch's tail: 25, 26)
+            const unsigned long long life = __builtin_amdgcn_s_memtime() - t_start;
+            atomicAdd(&counters[21], life);
+            atomicMax(&counters[25], life);
+            atomicAdd(&counters[26], 1ull);
+        }
     }
 }
 
