@@ -319,10 +319,7 @@ int rt_ctx_set_variant(rt_ctx* ctx, int slab32, int lds_stack, int lds_nodes);
  *                           its 64 lanes are idle (0: auto)
  *   RT_OPT_POOL_RING        1 (default): POOL reduces each finished (tile, chunk) block inside the
  *                           trace kernel into chunk partials; 0: the per-sample buffer and
- *                           reduce_samples (see RT_SCHED_POOL)
- *   RT_OPT_TAIL_SPLIT       1 (default): POOL deals its last work blocks (about one per resident
- *                           wave each) as 4-row halves and 2-row quarters of a tile, so the launch
- *                           does not end waiting on whole blocks; 0: whole tiles to the end */
+ *                           reduce_samples (see RT_SCHED_POOL) */
 enum {
     RT_OPT_TRACE_BUF_BYTES = 1,
     RT_OPT_BATCH_OVERLAP = 2,
@@ -332,8 +329,7 @@ enum {
     RT_OPT_HOIST = 6,
     RT_OPT_WF_PATHS = 7,
     RT_OPT_WF_REFILL = 8,
-    RT_OPT_POOL_RING = 9,
-    RT_OPT_TAIL_SPLIT = 10
+    RT_OPT_POOL_RING = 9
 };
 int rt_ctx_set_option(rt_ctx* ctx, int key, int64_t value);
 int rt_ctx_get_option(rt_ctx* ctx, int key, int64_t* value);

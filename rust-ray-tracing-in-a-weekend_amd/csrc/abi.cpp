@@ -103,7 +103,6 @@ struct rt_ctx {
     int64_t wf_paths = 0;               // RT_OPT_WF_PATHS: wavefront schedule path slots (0: auto)
     int wf_refill = 0;                  // RT_OPT_WF_REFILL: idle lanes before a wf_trace wave refills (0: auto)
     int opt_ring = 1;                   // RT_OPT_POOL_RING: POOL reduces finished blocks in the kernel
-    int opt_tail_split = 1;             // RT_OPT_TAIL_SPLIT: POOL deals its last blocks as halves / quarters
     double* ring = nullptr;             // its per-wave record ring (kPoolRing blocks per wave)
     size_t ring_cap = 0;
     unsigned long long raw_counters[kCounters] = {};   // the last count_work render's counters (rt_last_counters)
@@ -1555,16 +1554,6 @@ static int run_range(rt_ctx* c, const rt_camera* cam, const rt_render_params* p,
             const unsigned g = o.pool == RT_SCHED_ITEMS ? (unsigned)K.block_chunks : (unsigned)K.block_samples;   // (POOL, WAVEFRONT: samples)
             const unsigned n = o.pool == RT_SCHED_ITEMS ? (unsigned)K.n_chunks : (unsigned)(K.spp - K.sample_begin);
             K.n_work_blocks = (unsigned)K.tiles_x * (unsigned)K.tiles_y * ((n + g - 1) / std::max(g, 1u));
-            // the per-sample pool's tail: the last blocks dealt as quarters, the ones before them as
-            // halves, about one of each per resident wave (trace_device.hpp tail_block), so the
-            // launch does not end waiting on whole 1,024-sample blocks
-            K.split_half = K.split_quarter = 0;
-            if (o.pool == RT_SCHED_POOL && c->opt_tail_split) {
-                const unsigned waves = (unsigned)c->n_cus * 16u, nb = K.n_work_blocks;
-                K.split_quarter = std::min(nb, waves);
-                K.split_half = std::min(nb - K.split_quarter, waves);
-                K.n_work_blocks = nb + K.split_half + 3u * K.split_quarter;
-            }
         }
         // batch bi's buffer half, trace stream and work counter (one of each per overlapped batch)
         const int h = overlap ? (bi & 1) : 0;
@@ -2046,7 +2035,6 @@ int rt_ctx_set_option(rt_ctx* c, int key, int64_t v)
         c->wf_refill = (int)v;
         return RT_OK;
     case RT_OPT_POOL_RING: c->opt_ring = v != 0; return RT_OK;
-    case RT_OPT_TAIL_SPLIT: c->opt_tail_split = v != 0; return RT_OK;
     default: return fail(RT_ERR_INVALID, "unknown option");
     }
 }
@@ -2064,7 +2052,6 @@ int rt_ctx_get_option(rt_ctx* c, int key, int64_t* v)
     case RT_OPT_WF_PATHS: *v = c->wf_paths; return RT_OK;
     case RT_OPT_WF_REFILL: *v = c->wf_refill; return RT_OK;
     case RT_OPT_POOL_RING: *v = c->opt_ring; return RT_OK;
-    case RT_OPT_TAIL_SPLIT: *v = c->opt_tail_split; return RT_OK;
     default: return fail(RT_ERR_INVALID, "unknown option");
     }
 }

@@ -2015,24 +2015,6 @@ __device__ __forceinline__ unsigned lanes_below(uint64_t mask)
 // lane p the tile's pixel p — over its samples in order from 0.0, reduce_samples' chunk sum,
 // and writes the chunk partial ([chunk][pixel], reduce_chunks' input). The block is one chunk
 // of samples (block_samples == spp_chunk, chunk-aligned batches), so the chunk is its group.
-// Per-sample pool: work item w -> (block b = group x tiles + tile, first tile row r0, rows nr).
-// The n_blocks - split_half - split_quarter first blocks are whole tiles; then split_half blocks
-// as two 4-row halves, then the last split_quarter as four 2-row quarters (wave-uniform)
-__device__ __forceinline__ void tail_block(const KParams& P, unsigned n_blocks, unsigned w, unsigned& b, int& r0,
-                                           int& nr)
-{
-    const unsigned full = n_blocks - P.split_half - P.split_quarter;
-    if (w < full) {
-        b = w; r0 = 0; nr = 8;
-    } else if (w - full < 2u * P.split_half) {
-        const unsigned v = w - full;
-        b = full + (v >> 1); r0 = (int)(v & 1u) * 4; nr = 4;
-    } else {
-        const unsigned v = w - full - 2u * P.split_half;
-        b = full + P.split_half + (v >> 2); r0 = (int)(v & 3u) * 2; nr = 2;
-    }
-}
-
 #ifndef RING_LOADS
 #define RING_LOADS 4
 #endif
@@ -2059,12 +2041,9 @@ template <class C>
 constexpr bool RingSgpr() { return C::F == FEAT_SET_SPHERES; }
 
 __device__ __forceinline__ void ring_reduce(const KParams& P, const double* __restrict__ rec,
-                                            double* __restrict__ partial, unsigned w, unsigned n_tiles, unsigned group,
-                                            size_t n_px, int lane, unsigned n_blocks)
+                                            double* __restrict__ partial, unsigned blk, unsigned n_tiles, unsigned group,
+                                            size_t n_px, int lane)
 {
-    unsigned blk;
-    int r0, nr;
-    tail_block(P, n_blocks, w, blk, r0, nr);   // the work item's block and tile rows
     const unsigned grp = blk / n_tiles, tile = blk - grp * n_tiles;
     const int s0 = P.sample_begin + (int)(grp * group);
     const int x = (int)(tile % (unsigned)P.tiles_x) * 8 + (lane & 7);
@@ -2076,7 +2055,7 @@ __device__ __forceinline__ void ring_reduce(const KParams& P, const double* __re
     // one channel at a time, RING_LOADS samples' loads in flight (the wave's path state stays live
     // beside them; one load per round trip left the wave waiting on L2 ~48 times per block)
     constexpr int NB = RING_LOADS;
-    const bool own = x < P.width && k < P.n_rows && (lane >> 3) - r0 < nr && (lane >> 3) >= r0;
+    const bool own = x < P.width && k < P.n_rows;
     double* o = partial + ((size_t)grp * n_px + (size_t)k * P.width + x) * 3;
 #pragma unroll 1
     for (int c = 0; c < 3; ++c) {
@@ -2126,8 +2105,7 @@ __global__ void __launch_bounds__(BlockThreads<C>(), min_waves<C>()) trace_pool(
     // per-sample pool: a block = one tile x block_samples consecutive samples (any count: the
     // per-sample output does not depend on it)
     const unsigned group = ITEMS ? (unsigned)P.block_chunks : (unsigned)P.block_samples;
-    const unsigned n_blocks = P.n_work_blocks;   // work items: n_tiles x ceil(samples or chunks / group)
-                                                 // (+ the per-sample pool's split tail, tail_block)
+    const unsigned n_blocks = P.n_work_blocks;   // n_tiles x ceil(samples or chunks / group)
     const size_t n_px = (size_t)P.n_rows * (size_t)P.width;
     // current work block (wave-uniform)
     unsigned blk_units = 0, blk_next = 0, nvalid = 1;
@@ -2169,8 +2147,7 @@ __global__ void __launch_bounds__(BlockThreads<C>(), min_waves<C>()) trace_pool(
                     if ((occv >> q & 1u) && (unsigned)q != open &&
                         __ballot(active && ((unsigned)s >> kRingSampleBits) / kRingSlot == (unsigned)q) == 0) {
                         ring_reduce(P, ring_of_wave<C>(P) + (size_t)q * kRingSlot * 3, samples,
-                                    (unsigned)__builtin_amdgcn_readlane(ringv, q), n_tiles, group, n_px, lane,
-                                    n_blocks - P.split_half - 3u * P.split_quarter);
+                                    (unsigned)__builtin_amdgcn_readlane(ringv, q), n_tiles, group, n_px, lane);
                         occv &= ~(1u << q);
                         ringv = ring_set((int)occv, kRingOcc, ringv);
                     }
@@ -2186,8 +2163,7 @@ __global__ void __launch_bounds__(BlockThreads<C>(), min_waves<C>()) trace_pool(
                         __ballot(active && ((unsigned)s >> kRingSampleBits) / kRingSlot == (unsigned)q) == 0) {
                         double* rw = ring_of_wave<C>(P);
                         ring_reduce(P, rw + (size_t)q * kRingSlot * 3, samples,
-                                    (unsigned)__builtin_amdgcn_readfirstlane(ring_block_id(rw)[q]), n_tiles, group, n_px, lane,
-                                    n_blocks - P.split_half - 3u * P.split_quarter);
+                                    (unsigned)__builtin_amdgcn_readfirstlane(ring_block_id(rw)[q]), n_tiles, group, n_px, lane);
                         occ &= ~(1u << q);
                     }
                 }
@@ -2216,16 +2192,11 @@ __global__ void __launch_bounds__(BlockThreads<C>(), min_waves<C>()) trace_pool(
                     exhausted = true;
                     break;
                 }
-                // the per-sample pool's work item b: a whole tile's block, or near the end a half or
-                // a quarter of one (tail_block; the ring keeps b and decodes it again)
-                unsigned blk = b;
-                int r0 = 0, nr = 8;
-                if constexpr (!ITEMS) tail_block(P, n_blocks - P.split_half - 3u * P.split_quarter, b, blk, r0, nr);
-                const unsigned grp = blk / n_tiles, tile = blk - grp * n_tiles;
+                const unsigned grp = b / n_tiles, tile = b - grp * n_tiles;
                 tx0 = (int)(tile % (unsigned)P.tiles_x) * 8;
-                tk0 = (int)(tile / (unsigned)P.tiles_x) * 8 + r0;
+                tk0 = (int)(tile / (unsigned)P.tiles_x) * 8;
                 vw = min(8, P.width - tx0);
-                nvalid = (unsigned)(vw * max(0, min(nr, P.n_rows - tk0)));
+                nvalid = (unsigned)(vw * min(8, P.n_rows - tk0));
                 if constexpr (ITEMS) {
                     const unsigned chunk = grp * group;
                     s0 = P.sample_begin + (int)chunk * P.spp_chunk;
@@ -2253,11 +2224,10 @@ __global__ void __launch_bounds__(BlockThreads<C>(), min_waves<C>()) trace_pool(
             if (!active && rank < take) {
                 const unsigned u = blk_next + rank;
                 unsigned si;
-                if (vw == 8 && (nvalid & (nvalid - 1u)) == 0) {  // whole 8-wide rows, 1/2/4/8 of them
-                    // (wave-uniform): shifts, not divisions
-                    si = u >> __builtin_ctz(nvalid | 0x80000000u);
+                if (nvalid == 64u) {  // a full 8x8 tile (wave-uniform): shifts, not divisions
+                    si = u >> 6;
                     x = tx0 + (int)(u & 7u);
-                    k = tk0 + (int)((u >> 3) & ((nvalid >> 3) - 1u));
+                    k = tk0 + (int)((u >> 3) & 7u);
                 } else {
                     si = u / nvalid;
                     const unsigned p = u - si * nvalid;

@@ -97,10 +97,6 @@ struct KParams {
     int32_t tile_shard;         // rt_render_params.tile_shard: grid tile m = the frame's tile row_begin + m*row_stride
     int32_t img_tiles_x;        // tiles per tile row of the image
     int32_t wf_refill;          // wavefront schedule: a wf_trace wave refills once this many lanes are idle
-    // per-sample pool, the launch's tail (tail_block): the last split_quarter work blocks are
-    // dealt as four 2-row quarters each and the split_half before them as two 4-row halves, so
-    // the waves' last blocks are short; work items = blocks + split_half + 3 split_quarter
-    uint32_t split_half, split_quarter;
     int32_t ring_waves;         // per-sample pool, in-kernel reduction: waves the ring holds (0: off)
     double* ring;               // per-sample pool, in-kernel reduction: kPoolRing blocks of records per wave
 };

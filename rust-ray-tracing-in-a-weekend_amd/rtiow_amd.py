@@ -52,7 +52,6 @@ RT_OPT_HOIST = 6
 RT_OPT_WF_PATHS = 7
 RT_OPT_WF_REFILL = 8
 RT_OPT_POOL_RING = 9
-RT_OPT_TAIL_SPLIT = 10
 # SAH builder options (rt_world_set_build_option)
 RT_BUILD_C_ISECT = 1
 RT_BUILD_MAX_LEAF = 2

@@ -163,25 +163,3 @@ def test_default_trace_buffer_is_bounded(rt, scene, W, H, spp):
             _same(img, ref, "C2 full")
     finally:
         r.close()
-
-
-@pytest.mark.parametrize("scene,W,H,spp,ring,shard", [(0, 1200, 800, 48, 1, 0), (0, 1000, 612, 33, 1, 3), (7, 960, 540, 16, 1, 0),
-                                                      (0, 777, 301, 21, 0, 0), (7, 1920, 1080, 8, 1, 8),
-                                                      (5, 250, 250, 40, 1, 0)])
-def test_tail_split_is_bit_identical(rt, scene, W, H, spp, ring, shard):
-    """RT_OPT_TAIL_SPLIT: the per-sample pool's last blocks dealt as 4-row halves and 2-row quarters
-    (edge tiles: quarters past the last row hold no units) — the same image as whole tiles to the
-    end, with the ring and with the per-sample buffer, whole frames and tile shards."""
-    r = rt.Renderer(0)
-    try:
-        world = rt.World(1).build_scene(scene)
-        kw = dict(row_begin=1, row_stride=shard, tile_shard=1) if shard else {}
-        r.set_option(rt.RT_OPT_TAIL_SPLIT, 1)
-        a, sa = _render(rt, r, scene, W, H, spp, ring, world=world, sched=rt.RT_SCHED_POOL, **kw)
-        r.set_option(rt.RT_OPT_TAIL_SPLIT, 0)
-        b, sb = _render(rt, r, scene, W, H, spp, ring, world=world, sched=rt.RT_SCHED_POOL, **kw)
-        assert sa.schedule == sb.schedule == rt.RT_SCHED_POOL
-        assert (sa.ring_bytes > 0) == (sb.ring_bytes > 0)
-        _same(a, b, f"tail split, scene {scene}")
-    finally:
-        r.close()
