@@ -140,13 +140,15 @@ ISA_JSON = os.path.join(REPO, "profiles", "isa_mix.json")
 VARIANT_NAMES = {0: "spheres", 35: "rectinst", 103: "media", 287: "final", 4095: "all"}
 
 
-def isa_prices(src_hash, variant_features, schedule, slab32=1, nall=1):
+def isa_prices(src_hash, variant_features, schedule, slab32=1, nall=1, ring=False):
     """Per-class issue prices from the trace kernel's own instruction mix (scripts/isa_mix.py,
-    profiles/isa_mix.json) for this build and kernel: {counter or 'other': (price, lo, hi)}."""
+    profiles/isa_mix.json) for this build and kernel: {counter or 'other': (price, lo, hi)}.
+    ring: the per-sample pool's in-kernel-reduction kernel (rt_stats.ring_bytes > 0)."""
     if not os.path.exists(ISA_JSON):
         return None
+    kind = "items" if schedule == 2 else "ring" if ring else "pool"
     e = json.load(open(ISA_JSON)).get(src_hash, {}).get(
-        "%s/%s/s%dn%d" % (VARIANT_NAMES.get(variant_features, "?"), "items" if schedule == 2 else "pool", slab32, nall))
+        "%s/%s/s%dn%d" % (VARIANT_NAMES.get(variant_features, "?"), kind, slab32, nall))
     if not e:
         return None
     return {c: (v["price"], v["range"][0], v["range"][1]) for c, v in e["classes"].items()}
@@ -370,7 +372,8 @@ def main():
         roofline["note"] = ("stale library: built from sources %s, the tree is %s; no PMC record quoted"
                             % (src_hash, tree_hash))
     elif pmc is not None and calib is not None:
-        isa = isa_prices(src_hash, last.variant_features, last.schedule, last.slab32, int(last.lds_nodes > 0))
+        isa = isa_prices(src_hash, last.variant_features, last.schedule, last.slab32, int(last.lds_nodes > 0),
+                         ring=getattr(last, "ring_bytes", 0) > 0)
         additive = valu_issue_cycles(pmc["counters"], calib, isa=isa)   # SIMD-cycles of VALU issue per launch
         rp = replay_price(calib, last.variant_features)
         # the kernel's mix replayed at saturation issues below the sum of its classes' costs

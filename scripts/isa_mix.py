@@ -93,7 +93,7 @@ def calib_op(mnemonic):
     return None
 
 
-def kernel_asm(variant, items, slab32=1, nall=1):
+def kernel_asm(variant, items, slab32=1, nall=1, ring=False):
     import __graft_entry__ as ge
     src = os.path.join(ge.CSRC, f"trace_v_{variant}.hip")
     out = f"/tmp/isa_mix_{variant}.s"
@@ -102,8 +102,8 @@ def kernel_asm(variant, items, slab32=1, nall=1):
                    capture_output=True)
     lines = open(out).read().splitlines()
     f = FEAT[variant]
-    name = re.compile(r"^(_ZN3rtk10trace_poolINS_3CfgILj%dELb%dELb1ELb%dELb0ELb0EEELb%dEEE\S*):"
-                      % (f, slab32, nall, int(items)))
+    name = re.compile(r"^(_ZN3rtk10trace_poolINS_3CfgILj%dELb%dELb1ELb%dELb0ELb0EEELb%dELb%dEEE\S*):"
+                      % (f, slab32, nall, int(items), int(ring)))
     start = next(i for i, l in enumerate(lines) if name.match(l))
     end = next(i for i in range(start + 1, len(lines)) if lines[i].strip().startswith(".size"))
     return name.match(lines[start]).group(1), lines[start:end]
@@ -129,13 +129,14 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--variant", default="spheres", choices=sorted(FEAT))
     ap.add_argument("--items", action="store_true", help="the item-pool kernel (default: the per-sample pool)")
+    ap.add_argument("--ring", action="store_true", help="the per-sample pool reducing in the kernel (RT_OPT_POOL_RING)")
     ap.add_argument("--slab32", type=int, default=1, help="0: the f64-slab instantiation (scenes without BVH nodes)")
     ap.add_argument("--nall", type=int, default=1, help="0: the partial-TLAS instantiation (no TLAS in LDS)")
     a = ap.parse_args()
     import __graft_entry__ as ge
     cal = json.load(open(PMC_JSON))["calibration"]
     raw, hits = cal["raw"], cal.get("hits", {})
-    kname, lines = kernel_asm(a.variant, a.items, a.slab32, a.nall)
+    kname, lines = kernel_asm(a.variant, a.items, a.slab32, a.nall, a.ring)
     by_depth = mix(lines)
     unknown = collections.Counter()
 
@@ -180,7 +181,7 @@ def main():
     n1, n2 = (o["depth1"] or (0, 0))[1], (o["depth2"] or (0, 0))[1]
     doc = json.load(open(OUT)) if os.path.exists(OUT) else {}
     h = ge.source_hash()
-    doc.setdefault(h, {})[f"{a.variant}/{'items' if a.items else 'pool'}/s{a.slab32}n{a.nall}"] = est
+    doc.setdefault(h, {})[f"{a.variant}/{'items' if a.items else 'ring' if a.ring else 'pool'}/s{a.slab32}n{a.nall}"] = est
     json.dump(doc, open(OUT, "w"), indent=1)
     print(f"{kname}: other priced {p1:.3f} (bounce loop, {int(n1)} static instructions) .. {p2:.3f} "
           f"(inner loops, {int(n2)}); estimate {est['other_price']:.3f}")

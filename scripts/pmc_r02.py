@@ -221,9 +221,10 @@ def bench(d, tag, workload, note=""):
         lines.append(f"VALU issue cycles the mix needs (calibration `{cal['tag']}` class means) = {need:.4g} SIMD-cycles; "
                      f"launch = {N_SIMDS} x {cycles:.4g} = {N_SIMDS * cycles:.4g} -> VALU issue roofline "
                      f"fraction {need / (N_SIMDS * cycles):.3f}")
-        m = re.search(r"Cfg<(\d+)u, (\w+), (\w+), (\w+), (\w+), (\w+)>, (true|false)>", knames[kern])
+        m = re.search(r"Cfg<(\d+)u, (\w+), (\w+), (\w+), (\w+), (\w+)>, (true|false)(?:, (true|false))?>", knames[kern])
         isa = (bn.isa_prices(entry["src_hash"], int(m.group(1)), 2 if m.group(7) == "true" else 1,
-                             int(m.group(2) == "true"), int(m.group(4) == "true")) if m else None)
+                             int(m.group(2) == "true"), int(m.group(4) == "true"), ring=m.group(8) == "true")
+               if m else None)
         if isa:
             fr = [bn.valu_issue_cycles(c, cal, isa=isa, bound=b) / (N_SIMDS * cycles) for b in (0, -1, 1)]
             lines.append(f"priced from the kernel's own instruction mix (profiles/isa_mix.json): fraction {fr[0]:.3f} "
