@@ -318,8 +318,9 @@ int rt_ctx_set_variant(rt_ctx* ctx, int slab32, int lds_stack, int lds_nodes);
  *   RT_OPT_WF_REFILL        wavefront schedule: a wf_trace wave takes queued rays once this many of
  *                           its 64 lanes are idle (0: auto)
  *   RT_OPT_POOL_RING        1 (default): POOL reduces each finished (tile, chunk) block inside the
- *                           trace kernel into chunk partials; 0: the per-sample buffer and
- *                           reduce_samples (see RT_SCHED_POOL) */
+ *                           trace kernel into chunk partials when its per-sample buffer would not
+ *                           fit the bound in one batch; 2: whenever its blocks allow; 0: never (the
+ *                           per-sample buffer and reduce_samples; see RT_SCHED_POOL) */
 enum {
     RT_OPT_TRACE_BUF_BYTES = 1,
     RT_OPT_BATCH_OVERLAP = 2,
@@ -349,8 +350,10 @@ int rt_ctx_get_option(rt_ctx* ctx, int key, int64_t* value);
  *   ITEMS:  persistent waves as POOL, but a lane takes a whole (pixel, chunk) item, traces
  *           its samples in order and writes one partial, as CHUNKS does (1/chunk of POOL's
  *           buffer bytes); a lane whose item ended takes the next item at once.
- *   AUTO:   POOL (the fastest) when it reduces in the kernel or its per-sample radiance is at
- *           most 4 x the buffer bound, otherwise ITEMS; rt_stats.schedule reports which ran.
+ *   AUTO:   ITEMS for the Cornell-box variant (rects, boxes and instances without media: measured
+ *           fastest there); otherwise POOL when it can reduce in the kernel or its
+ *           per-sample radiance is at most 4 x the buffer bound, else ITEMS; rt_stats.schedule
+ *           reports which ran.
  *   WAVEFRONT: the final-scene feature set (f64, f32 slabs, one instanced BLAS, every node fits
  *           LDS): a pool of path slots in HBM (RT_OPT_WF_PATHS) and per iteration two kernels —
  *           wf_logic (hit records, materials, camera rays of new units; live slots compacted into

@@ -102,7 +102,8 @@ struct rt_ctx {
     int block_samples = 0;              // RT_OPT_BLOCK_SAMPLES: samples per per-sample-pool work block (0: auto)
     int64_t wf_paths = 0;               // RT_OPT_WF_PATHS: wavefront schedule path slots (0: auto)
     int wf_refill = 0;                  // RT_OPT_WF_REFILL: idle lanes before a wf_trace wave refills (0: auto)
-    int opt_ring = 1;                   // RT_OPT_POOL_RING: POOL reduces finished blocks in the kernel
+    int opt_ring = 1;                   // RT_OPT_POOL_RING: POOL reduces finished blocks in the kernel (0 never,
+                                        // 1 when its per-sample buffer would not fit the bound, 2 always)
     double* ring = nullptr;             // its per-wave record ring (kPoolRing blocks per wave)
     size_t ring_cap = 0;
     unsigned long long raw_counters[kCounters] = {};   // the last count_work render's counters (rt_last_counters)
@@ -1457,13 +1458,23 @@ static int run_range(rt_ctx* c, const rt_camera* cam, const rt_render_params* p,
         // Round 2, pool vs items: C2 101.6 vs 106.7 ms per frame, C4 1492 vs 1571 (r02d_*, r02e_*);
         // round 4: C2 74.75 vs 76.06, C4 1018.5 vs 1074.7; C5 in 25 overlapped pool batches of
         // 64 GB halves 10,578 ms vs the item pool 10,649 in 64 batches at a 4 GB bound (r04f_*)
+        // AUTO, measured per variant (round 5, profiles/r05x_*, r05w_*, r05y_*): the Cornell box takes
+        // the item pool (C3 800x800x1000: items 204.5 ms, per-sample buffer 209.9, ring 215.0); the
+        // others the per-sample pool — its buffer while that fits the bound in one batch (C1: 2.03 ms,
+        // ring 2.06), else the ring (C2: 74.0 vs 74.7 unbounded; C4 x256: 267.3, items 291.8) — and
+        // the item pool only when neither fits
+        const uint32_t variant = rtk::variant_features(o.features);
+        // (the media variant, Cornell smoke 600x600x200: items 31.72 ms, per-sample buffer 30.28: pool)
+        const bool cornell = variant == rtk::FEAT_SET_RECTINST;
+        const bool fits_one = (size_t)total * sample_bytes <= buf_cap;
         o.pool = wavefront ? RT_SCHED_WAVEFRONT
                  : c->opt_pool != RT_SCHED_AUTO && c->opt_pool != RT_SCHED_WAVEFRONT
                      ? c->opt_pool
+                     : cornell && !o.f32 ? RT_SCHED_ITEMS
                      : (ring_ok || (size_t)total * sample_bytes <= 4 * buf_cap ? RT_SCHED_POOL : RT_SCHED_ITEMS);
         // POOL with the in-kernel reduction: chunk partials like ITEMS (the ring takes its share of
         // the bound first, the partials at least one chunk)
-        ring = o.pool == RT_SCHED_POOL && ring_ok;
+        ring = o.pool == RT_SCHED_POOL && ring_ok && (c->opt_ring == 2 || !fits_one);
         // overlapped batches trace two launches at once, a ring each: a render that does not fit
         // one batch beside one ring budgets two
         size_t out_cap = buf_cap;
@@ -2034,7 +2045,10 @@ int rt_ctx_set_option(rt_ctx* c, int key, int64_t v)
         if (v < 0 || v > 64) return fail(RT_ERR_INVALID, "refill lanes out of range (0..64)");
         c->wf_refill = (int)v;
         return RT_OK;
-    case RT_OPT_POOL_RING: c->opt_ring = v != 0; return RT_OK;
+    case RT_OPT_POOL_RING:
+        if (v < 0 || v > 2) return fail(RT_ERR_INVALID, "pool ring mode out of range (0 never, 1 when needed, 2 always)");
+        c->opt_ring = (int)v;
+        return RT_OK;
     default: return fail(RT_ERR_INVALID, "unknown option");
     }
 }

@@ -8,7 +8,8 @@ Prints per-build median kernel ms and whether the f64 test image equals the firs
 
 usage: python scripts/ab_builds.py lib/a.so lib/b.so [--scene 0 --width 1200 --height 800 --spp 500]
        (a build given as lib/a.so@opt9=0,opt1=4294967296 runs with those rt_ctx_set_option
-       keys and values; any other NAME=V pair is set in the child's environment)
+       keys and values, @optsched=2 with that rt_ctx_set_schedule; any other NAME=V pair is set
+       in the child's environment)
        Times are kernel + reduce ms (the frame's trace launches and their reductions).
 """
 import argparse
@@ -31,7 +32,10 @@ world = rt.World(1).build_scene(a["scene"])
 cam, bg = rt.scene_camera(a["scene"], a["width"], a["height"])
 r = rt.Renderer(0)
 for k, v in a["opts"].items():
-    r.set_option(int(k), int(v))
+    if k == "sched":
+        r.set_schedule(int(v))
+    else:
+        r.set_option(int(k), int(v))
 r.upload(world)
 img = r.render(cam, rt.Renderer.params(a["width"], a["height"], 2, a["depth"], bg, 1, row_stride=8,
                                        out_format=rt.RT_OUT_F64))

@@ -154,7 +154,7 @@ def test_c5_geometry_many_buffer_batches(rt, sched):
     spp, rows = 40, dict(row_begin=511, row_stride=512)
     r = rt.Renderer(0)
     r.set_option(rt.RT_OPT_TRACE_BUF_BYTES, 1 << 20)
-    r.set_option(rt.RT_OPT_POOL_RING, int(sched == "RING"))
+    r.set_option(rt.RT_OPT_POOL_RING, 2 if sched == "RING" else 0)
     r.set_schedule(rt.RT_SCHED_ITEMS if sched == "ITEMS" else rt.RT_SCHED_POOL)
     world = rt.World(1).build_scene(0)
     cam, bg = rt.scene_camera(0, W, H)
@@ -299,7 +299,7 @@ def test_overlapped_buffer_batches_at_c2_size(rt, renderer, sched):
         r = rt.Renderer(0)
         r.set_option(rt.RT_OPT_TRACE_BUF_BYTES, 256 << 20)
         r.set_option(rt.RT_OPT_BATCH_OVERLAP, int(overlap))
-        r.set_option(rt.RT_OPT_POOL_RING, int(sched == "RING"))
+        r.set_option(rt.RT_OPT_POOL_RING, 2 if sched == "RING" else 0)
         try:
             r.set_schedule(rt.RT_SCHED_ITEMS if sched == "ITEMS" else rt.RT_SCHED_POOL)
             r.upload(world)

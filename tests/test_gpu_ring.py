@@ -23,7 +23,7 @@ def _render(rt, r, scene, W, H, spp, ring, world=None, sched=None, block=0, **kw
     blocks are otherwise cut to 4..8 samples, so the tests pass the chunk)."""
     world = world or rt.World(1).build_scene(scene)
     cam, bg = rt.scene_camera(scene, W, H)
-    r.set_option(rt.RT_OPT_POOL_RING, ring)
+    r.set_option(rt.RT_OPT_POOL_RING, 2 if ring else 0)   # 2: whenever blocks allow (1, the default: when needed)
     r.set_option(rt.RT_OPT_BLOCK_SAMPLES, block)
     if sched is not None:
         r.set_schedule(sched)
@@ -109,6 +109,7 @@ def test_ring_progressive_accumulation(rt, renderer):
     cam, bg = rt.scene_camera(0, W, H)
     one, st = _render(rt, renderer, 0, W, H, spp, 0, world=world)   # per-sample buffer, one launch
     renderer.set_option(rt.RT_OPT_BLOCK_SAMPLES, 4)   # spp 64: chunks of 4 (blocks of one chunk: the ring)
+    renderer.set_option(rt.RT_OPT_POOL_RING, 2)
     acc = None
     try:
         p = rt.Renderer.params(W, H, spp, 50, bg, 1, out_format=rt.RT_OUT_F64)
@@ -121,6 +122,7 @@ def test_ring_progressive_accumulation(rt, renderer):
         _same(acc.resolve(out_format=rt.RT_OUT_F64), one, "accumulator")
     finally:
         renderer.set_option(rt.RT_OPT_BLOCK_SAMPLES, 0)
+        renderer.set_option(rt.RT_OPT_POOL_RING, 1)
         if acc is not None:
             acc.close()
 
