@@ -13,7 +13,7 @@ pmc)
     N="round-5 final build (r05f)"
     python scripts/pmc_r02.py bench r05f_prof_c1 r05_final_c1 0,1200,800,10,8,1,1 "$N" && \
     python scripts/pmc_r02.py bench r05f_prof_c2 r05_final_c2 0,1200,800,500,50,1,1 "$N" && \
-    python scripts/pmc_r02.py bench r05f_prof_c3 r05_final_c3 5,800,800,1000,50,1,1 "$N" && \
+    python scripts/pmc_r02.py bench r05f_prof_c3 r05_final_c3 5,800,800,1000,50,1,2 "$N" && \
     python scripts/pmc_r02.py bench r05f_prof_c4 r05_final_c4 7,1920,1080,1000,50,1,1 "$N" && \
     python scripts/pmc_r02.py bench r05f_prof_c5 r05_final_c5 0,4096,4096,4096,50,1,1 "$N"
     ;;
