@@ -378,15 +378,19 @@ def main():
         rp = replay_price(calib, last.variant_features)
         # the kernel's mix replayed at saturation issues below the sum of its classes' costs
         # (calibration 'kmix'): price the launch at the replay's measured rate when there is one
-        need = pmc["counters"]["SQ_INSTS_VALU"] * rp if rp else additive
+        # the PMC record is per trace dispatch; a render in n equal buffer batches (C5: 256 chunks in
+        # batches of 4) dispatches n of them inside the frame's kernel time
+        nb = max(1, int(last.n_batches))
+        additive *= nb
+        need = pmc["counters"]["SQ_INSTS_VALU"] * nb * rp if rp else additive
         clk = pmc["clock_ghz"]                                   # the clock the chip held in that pass
         achieved = need / (k_ms * 1e-3) / 1e9                    # per live-timed launch
         peak = N_SIMDS * clk
-        dram = pmc["dram_bytes"]
+        dram = pmc["dram_bytes"] * nb
         if isa:   # each class at the low / high end of its static-mix price
-            ests = [valu_issue_cycles(pmc["counters"], calib, isa=isa, bound=b) for b in (-1, 0, 1)]
+            ests = [nb * valu_issue_cycles(pmc["counters"], calib, isa=isa, bound=b) for b in (-1, 0, 1)]
         else:
-            ests = [valu_issue_cycles(pmc["counters"], calib, o)
+            ests = [nb * valu_issue_cycles(pmc["counters"], calib, o)
                     for o in calib.get("other_range", [calib["cycles_per_inst"]["other"]] * 2)]
         lo, hi = (x / (k_ms * 1e-3) / 1e9 / peak for x in (min(ests + [need]), max(ests + [need])))
         roofline.update({
@@ -407,7 +411,8 @@ def main():
             "additive_frac": round(additive / (k_ms * 1e-3) / 1e9 / peak, 4),
             "model_check": {"mix": calib.get("mix"),
                             **{k: round(v["ratio"], 4) for k, v in (calib.get("kmix") or {}).items()}},
-            "pmc_tag": pmc.get("tag"), "pmc_kernel_ms": pmc.get("kernel_ms"), "clock_ghz": clk})
+            "pmc_tag": pmc.get("tag"), "pmc_kernel_ms": pmc.get("kernel_ms"), "clock_ghz": clk,
+            "pmc_dispatches_per_frame": nb})
     else:
         roofline["note"] = "no PMC pass of this build (source hash) and workload in profiles/pmc.json"
 
