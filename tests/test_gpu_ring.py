@@ -165,3 +165,26 @@ def test_default_trace_buffer_is_bounded(rt, scene, W, H, spp):
             _same(img, ref, "C2 full")
     finally:
         r.close()
+
+
+def test_context_options_round_trip_and_reject_bad_values(rt):
+    """rt_ctx_set_option / rt_ctx_get_option: every key round-trips, out-of-range values and
+    unknown keys fail with RT_ERR_INVALID (no silent clamping)."""
+    r = rt.Renderer(0)
+    try:
+        assert r.get_option(rt.RT_OPT_POOL_RING) == 1          # default: the ring when needed
+        assert r.get_option(rt.RT_OPT_TRACE_BUF_BYTES) <= 4 * GIB
+        for key, val in ((rt.RT_OPT_POOL_RING, 2), (rt.RT_OPT_POOL_RING, 0), (rt.RT_OPT_BLOCK_SAMPLES, 8),
+                         (rt.RT_OPT_BLOCK_CHUNKS, 3), (rt.RT_OPT_BATCH_OVERLAP, 0), (rt.RT_OPT_WF_REFILL, 48),
+                         (rt.RT_OPT_WF_PATHS, 1 << 20), (rt.RT_OPT_TRACE_BUF_BYTES, 64 << 20)):
+            r.set_option(key, val)
+            assert r.get_option(key) == val, key
+        for key, val in ((rt.RT_OPT_POOL_RING, 3), (rt.RT_OPT_POOL_RING, -1), (rt.RT_OPT_WF_REFILL, 65), (999, 1)):
+            with pytest.raises(rt.RTError):
+                r.set_option(key, val)
+        with pytest.raises(rt.RTError):
+            r.get_option(999)
+        r.set_option(rt.RT_OPT_TRACE_BUF_BYTES, 0)               # 0 restores the default
+        assert 0 < r.get_option(rt.RT_OPT_TRACE_BUF_BYTES) <= 4 * GIB
+    finally:
+        r.close()
