@@ -129,23 +129,23 @@ def test_row_shards_reassemble_bit_exactly(rt, renderer):
 def test_tile_shards_reassemble_bit_exactly(rt, renderer):
     """Tile shards (rt_render_params.tile_shard: the frame's 8x8 tiles round-robin, bench.py's
     multi-GPU partition) reassemble into the full frame bit for bit, edge tiles included, under
-    every schedule."""
-    W, H, spp = 40, 30, 4
+    every schedule, on a wide and a tall frame."""
     world = rt.World(1).build_scene(7)
-    cam, bg = rt.scene_camera(7, W, H)
     renderer.upload(world)
-    full = renderer.render(cam, rt.Renderer.params(W, H, spp, 50, bg, 1, out_format=rt.RT_OUT_F64))
-    for sched in (rt.RT_SCHED_POOL, rt.RT_SCHED_ITEMS, rt.RT_SCHED_CHUNKS):
-        renderer.set_schedule(sched)
-        for G in (1, 2, 3, 5):
-            slabs = []
-            for r in range(G):
-                p = rt.Renderer.params(W, H, spp, 50, bg, 1, row_begin=r, row_stride=G, tile_shard=1,
-                                       out_format=rt.RT_OUT_F64)
-                slab = renderer.render(cam, p)
-                assert slab.shape == (8, 8 * rt.tiles_in_shard(W, H, r, G), 3)
-                slabs.append(slab)
-            assert np.array_equal(rt.assemble_tiles(slabs, W, H, G), full), (sched, G)
+    for (W, H, spp) in ((40, 30, 4), (17, 44, 2)):
+        cam, bg = rt.scene_camera(7, W, H)
+        full = renderer.render(cam, rt.Renderer.params(W, H, spp, 50, bg, 1, out_format=rt.RT_OUT_F64))
+        for sched in (rt.RT_SCHED_POOL, rt.RT_SCHED_ITEMS, rt.RT_SCHED_CHUNKS):
+            renderer.set_schedule(sched)
+            for G in (1, 2, 3, 5):
+                slabs = []
+                for r in range(G):
+                    p = rt.Renderer.params(W, H, spp, 50, bg, 1, row_begin=r, row_stride=G, tile_shard=1,
+                                           out_format=rt.RT_OUT_F64)
+                    slab = renderer.render(cam, p)
+                    assert slab.shape == (8, 8 * rt.tiles_in_shard(W, H, r, G), 3)
+                    slabs.append(slab)
+                assert np.array_equal(rt.assemble_tiles(slabs, W, H, G), full), (W, H, sched, G)
     renderer.set_schedule(rt.RT_SCHED_AUTO)
 
 
