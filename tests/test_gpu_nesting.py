@@ -180,8 +180,8 @@ def test_sphere_fields_both_stack_widths_match_oracle(rt, renderer, n):
 
 
 def _box_world(rt):
-    """Top-level boxes that stress the candidate-side test (trace_device.hpp box_candidates):
-    a grid of unit boxes on integer coordinates (shared edge planes, exact ties at edges), boxes
+    """Top-level boxes that stress the box test's edge cases (box_t's six sides under f32 slab
+    padding): a grid of unit boxes on integer coordinates (shared edge planes, exact ties at edges), boxes
     of thickness 0, 1e-12, 1e-7 and 1e-3 (thinner than their padding: both sides of an axis are
     candidates), boxes near the scene extent, a box the camera's rays start inside (exit sides
     win), metal and glass boxes (rays leave from and re-enter box faces) and a light."""
