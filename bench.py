@@ -78,6 +78,11 @@ def parse():
     ap.add_argument("--shard", default="tiles", choices=["tiles", "rows"],
                     help="N > 1 partition: the frame's 8x8 tiles round-robin (rt_render_params.tile_shard) or "
                          "single rows round-robin")
+    ap.add_argument("--tile-order", default="raster", choices=["raster", "cost"],
+                    help="N > 1 tile shards: raster order, or cost (rank 0 times a count_work pass of "
+                         "--cost-spp samples per pixel, untimed, and broadcasts the tiles sorted by cost; "
+                         "rt_ctx_set_tile_order)")
+    ap.add_argument("--cost-spp", type=int, default=8, help="spp of the --tile-order cost pass")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="N > 1: nccl (RCCL over xGMI, the product) or gloo (host-staged slabs; lets several "
                          "ranks share one GPU, for tests of this N > 1 path on a 1-GPU box)")
@@ -254,6 +259,22 @@ def main():
         rows = rt.rows_in_shard(H, rank, world, ROW_BLOCK)
         rows_max = max(rt.rows_in_shard(H, r, world, ROW_BLOCK) for r in range(world))
         px_mine, slab_shape = rows * W, (rows_max, W, 3)
+    # --tile-order cost: the tiles sorted by the lane-cycles of a count_work pass, most expensive
+    # first, dealt round-robin. Rank 0 measures (lane-cycles differ from run to
+    # run, so one rank decides) and broadcasts the order before the timed steps, like the upload.
+    tile_order, t_order = None, 0.0
+    if tiles and args.tile_order == "cost":
+        t0 = time.perf_counter()
+        n_img_tiles = ((W + 7) // 8) * ((H + 7) // 8)
+        obuf = torch.zeros(n_img_tiles, dtype=torch.int64, device="cpu" if gloo else device)
+        if rank == 0:
+            renderer.render(cam, rt.Renderer.params(W, H, args.cost_spp, depth, bg, args.seed, out_format=rt.RT_OUT_F32,
+                                                    count_work=1))
+            obuf.copy_(torch.from_numpy(rt.cost_tile_order(renderer.tile_costs()).astype(np.int64)))
+        dist.broadcast(obuf, src=0)
+        tile_order = obuf.cpu().numpy()
+        renderer.set_tile_order(tile_order)
+        t_order = time.perf_counter() - t0
     # the render writes its shard contiguously at the start of the slab (a tile shard's 8 x 8n
     # layout is then a prefix of the padded 8 x 8n_max buffer, read back with the same view)
     # f64 output (sum * (1/spp), the reference's `self.x * scale`, math.rs:120-125): the frame the
@@ -277,7 +298,7 @@ def main():
         if tiles:
             views = [g.reshape(-1)[: 3 * 64 * rt.tiles_in_shard(W, H, r, world)].view(8, -1, 3)
                      for r, g in enumerate(slabs)]
-            rt.assemble_tiles(views, W, H, world, out=frame)
+            rt.assemble_tiles(views, W, H, world, out=frame, order=tile_order)
         else:
             rt.assemble_rows(slabs, H, world, out=frame, row_block=ROW_BLOCK)
     kernel_ms = []
@@ -523,8 +544,9 @@ def main():
                                    % (args.config, SCENE_NAMES.get(args.scene, "scene %d" % args.scene), W, H, spp,
                                       depth, "tile" if tiles else "row", world),
                        "scene": args.scene, "width": W, "height": H, "spp": spp, "max_depth": depth,
+                       "tile_order": args.tile_order if tiles else None,
                        "parallelism": "%s interleaved over %d rank(s), %s gather"
-                                      % ("8x8 tiles" if tiles else "rows", world,
+                                      % (("8x8 tiles (%s order)" % args.tile_order) if tiles else "rows", world,
                                          "gloo (host-staged)" if gloo else "RCCL" if dist_on else "no")},
             "roofline": roofline,
             "cpu_baseline": cpu,
@@ -538,6 +560,7 @@ def main():
                        "schedule": last.schedule, "n_batches": last.n_batches, "waves_per_simd": last.waves_per_simd, "spp_chunk": last.spp_chunk,
                        "trace_buf_bytes": int(last.trace_buf_bytes), "batches_overlapped": bool(last.overlapped),
                        "scene_bytes": int(last.scene_bytes), "scene_build_upload_s": round(t_build, 3),
+                       "tile_order_pass_s": round(t_order, 3) if tile_order is not None else None,
                        "algorithmic_bytes_survey_8d": alg},
         }
         if per_rank is not None:

@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 3
+#define RT_ABI_VERSION 4
 
 enum {
     RT_OK = 0,
@@ -184,7 +184,10 @@ typedef struct rt_render_params {
                                     tiles, tile m in columns 8m .. 8m+7 (rt_tiles_in_shard tiles; the
                                     pixels of an edge tile past the image are rendered and meaningless).
                                     Every shard is whole 8x8 tiles, so a multi-GPU shard keeps the
-                                    kernel's work tiles compact in the image at any GPU count. */
+                                    kernel's work tiles compact in the image at any GPU count. With a
+                                    tile order set on the context (rt_ctx_set_tile_order), t is a
+                                    position in that order: the shard's tile m is order[row_begin +
+                                    m*row_stride]. */
 } rt_render_params;
 
 /* Renders the selected rows (or tiles) into out (rows_local x width x 3, row k = the k-th
@@ -248,6 +251,22 @@ int rt_last_stats(rt_ctx* ctx, rt_stats* out);
  * (inside the leaf tests), 20 refill, 21 kernel total (summed over waves), 22 deferred instance
  * walks (after the top-level walk). */
 int rt_last_counters(rt_ctx* ctx, uint64_t* out, int n);
+
+/* ---- tile order: balancing tile shards (ABI v4; main.rs:497-551's partition, rebalanced) ------ */
+/* Per 8x8 tile of the image (raster order, ceil(width/8) per tile row), the lane-cycles
+ * (s_memtime) its samples took in the last render, if that render had count_work set and ran
+ * a pool schedule (POOL, ITEMS; any shard mode). Copies min(n, tiles) entries; returns the
+ * tile count, or 0 when the last render counted none. A cost estimate for
+ * rt_ctx_set_tile_order: e.g. a few samples per pixel of the frame with count_work. */
+int rt_last_tile_costs(rt_ctx* ctx, uint64_t* out, int64_t n);
+/* The order in which tile shards (rt_render_params.tile_shard = 1) take the frame's tiles:
+ * order[t] is the raster tile at position t, a permutation of the frame's n tiles (checked:
+ * RT_ERR_INVALID otherwise). Shards then take positions row_begin + m*row_stride; a frame of
+ * another tile count fails with RT_ERR_INVALID. The tiles sorted by cost, most expensive
+ * first, give round-robin shards of nearly equal cost, each rendering its expensive tiles
+ * first. Only which pixels a shard renders changes, not their bits. n = 0: raster order
+ * again (the default). Waits for the device. */
+int rt_ctx_set_tile_order(rt_ctx* ctx, const uint32_t* order, int64_t n);
 
 /* ---- progressive / resumable accumulation ------------------------------------ */
 /* A device f64 running sum per pixel of one row shard. Batches render consecutive sample
@@ -365,8 +384,8 @@ int rt_ctx_get_option(rt_ctx* ctx, int key, int64_t* value);
  * render needs). A larger render runs in buffer
  * batches whose sums are carried across, in two halves of the bound: batch k traces into half
  * k & 1 on one of two context streams while the render's stream reduces batch k - 1, so
- * consecutive traces overlap (RT_OPT_BATCH_OVERLAP 0: one buffer, in order). A 4 GB bound renders
- * C2 as fast as one batch; long-path scenes pay per batch. */
+ * consecutive traces overlap (RT_OPT_BATCH_OVERLAP 0: one buffer, in order). Under the default
+ * bound C2 (1.2 GB with the ring) and C4 (3.4 GB) render in one batch, C5 in 64. */
 enum { RT_SCHED_CHUNKS = 0, RT_SCHED_POOL = 1, RT_SCHED_ITEMS = 2, RT_SCHED_AUTO = 3, RT_SCHED_WAVEFRONT = 4 };
 int rt_ctx_set_schedule(rt_ctx* ctx, int schedule);
 

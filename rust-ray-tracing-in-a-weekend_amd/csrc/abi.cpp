@@ -107,6 +107,11 @@ struct rt_ctx {
     double* ring = nullptr;             // its per-wave record ring (kPoolRing blocks per wave)
     size_t ring_cap = 0;
     unsigned long long raw_counters[kCounters] = {};   // the last count_work render's counters (rt_last_counters)
+    uint32_t* tile_order = nullptr;     // rt_ctx_set_tile_order: tile shards' position -> raster tile (device)
+    int64_t tile_order_n = 0;           //   its length (0: raster order)
+    unsigned long long* tile_cost = nullptr;   // count_work pool renders: lane-cycles per raster tile
+    int64_t tile_cost_cap = 0;          //   tiles allocated
+    int64_t tile_cost_n = 0;            //   tiles of the last count_work render (rt_last_tile_costs)
     uint32_t extra_features = 0;        // RT_OPT_EXTRA_FEATURES: a larger kernel variant than the scene needs (tests)
     double pad_extent = 0.0;
     int opt_slab32 = 1;                 // rt_ctx_set_variant
@@ -227,6 +232,8 @@ void rt_ctx_destroy(rt_ctx* c)
     (void)hipFree(c->ring);
     (void)hipFree(c->out_buf);
     (void)hipFree(c->counters);
+    (void)hipFree(c->tile_order);
+    (void)hipFree(c->tile_cost);
     (void)hipFree(c->params);
     (void)hipFree(c->work);
     (void)hipFree(c->acc_tmp);
@@ -1344,6 +1351,13 @@ static int run_range(rt_ctx* c, const rt_camera* cam, const rt_render_params* p,
     while ((1 << K.row_block_shift) < row_block_of(p)) K.row_block_shift++;
     K.tile_shard = p->tile_shard;
     K.img_tiles_x = (p->width + 7) / 8;
+    const int64_t img_tiles = (int64_t)K.img_tiles_x * ((p->height + 7) / 8);
+    if (p->tile_shard && c->tile_order_n > 0) {   // the context's tile order: every tile shard takes it
+        if (c->tile_order_n != img_tiles)
+            return fail(RT_ERR_INVALID, "the tile order has " + std::to_string(c->tile_order_n) + " tiles, the frame " +
+                                            std::to_string(img_tiles));
+        K.tile_order = c->tile_order;
+    }
     K.wf_refill = c->wf_refill > 0 ? c->wf_refill : kWfDefaultRefill;
     K.n_rows = n_rows;
     K.tiles_x = (lay.w + 7) / 8;
@@ -1538,7 +1552,21 @@ static int run_range(rt_ctx* c, const rt_camera* cam, const rt_render_params* p,
     }
     if (own_acc) HIP_TRY(hipMemsetAsync(acc, 0, px_bytes, stream));
     K.ring_waves = ring ? ring_waves : 0;
-    if (count) HIP_TRY(hipMemsetAsync(c->counters, 0, kCounters * sizeof(unsigned long long), stream));
+    if (count) {
+        HIP_TRY(hipMemsetAsync(c->counters, 0, kCounters * sizeof(unsigned long long), stream));
+        if (img_tiles > c->tile_cost_cap) {   // (a render's first use: no work on the context's streams reads it)
+            HIP_TRY(hipStreamSynchronize(stream));
+            (void)hipFree(c->tile_cost);
+            c->tile_cost = nullptr;
+            c->tile_cost_cap = 0;
+            HIP_TRY(hipMalloc((void**)&c->tile_cost, (size_t)img_tiles * sizeof(unsigned long long)));
+            c->tile_cost_cap = img_tiles;
+        }
+        HIP_TRY(hipMemsetAsync(c->tile_cost, 0, (size_t)img_tiles * sizeof(unsigned long long), stream));
+        K.tile_cost = c->tile_cost;
+        // (the pool kernels count them; the chunk and wavefront schedules do not)
+        c->tile_cost_n = o.pool == RT_SCHED_POOL || o.pool == RT_SCHED_ITEMS ? img_tiles : 0;
+    }
     if (wavefront) {
         const int rc = wf_pool(c, stream, (long long)K.tiles_x * K.tiles_y * 64 * std::min<long long>(total, batch));
         if (rc) return rc;
@@ -1924,6 +1952,39 @@ int rt_last_stats(rt_ctx* c, rt_stats* out)
         c->pending_stats = false;
     }
     *out = c->stats;
+    return RT_OK;
+}
+
+int rt_last_tile_costs(rt_ctx* c, uint64_t* out, int64_t n)
+{
+    if (!c || (!out && n > 0) || n < 0) return fail(RT_ERR_INVALID, "bad argument");
+    rt_stats st;
+    const int rc = rt_last_stats(c, &st);   // the last render done
+    if (rc) return rc;
+    if (!c->pending_counts || c->tile_cost_n == 0) return 0;   // the last render counted no tile costs
+    const int64_t m = std::min<int64_t>(n, c->tile_cost_n);
+    if (m > 0) HIP_TRY(hipMemcpy(out, c->tile_cost, (size_t)m * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    return (int)c->tile_cost_n;
+}
+
+int rt_ctx_set_tile_order(rt_ctx* c, const uint32_t* order, int64_t n)
+{
+    if (!c || n < 0 || (n > 0 && !order)) return fail(RT_ERR_INVALID, "bad argument");
+    if (n > ((int64_t)1 << 30)) return fail(RT_ERR_INVALID, "tile order too long");
+    std::vector<uint8_t> seen((size_t)n, 0);
+    for (int64_t i = 0; i < n; ++i) {
+        if ((int64_t)order[i] >= n || seen[order[i]]) return fail(RT_ERR_INVALID, "the tile order is not a permutation of 0..n-1");
+        seen[order[i]] = 1;
+    }
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipDeviceSynchronize());   // no render still reads the old order
+    (void)hipFree(c->tile_order);
+    c->tile_order = nullptr;
+    c->tile_order_n = 0;
+    if (n == 0) return RT_OK;
+    HIP_TRY(hipMalloc((void**)&c->tile_order, (size_t)n * sizeof(uint32_t)));
+    HIP_TRY(hipMemcpy(c->tile_order, order, (size_t)n * sizeof(uint32_t), hipMemcpyHostToDevice));
+    c->tile_order_n = n;
     return RT_OK;
 }
 

@@ -1813,11 +1813,13 @@ __device__ __forceinline__ int image_row(const KParams& P, int k)
     return ((P.row_begin + (k >> s) * P.row_stride) << s) + (k & ((1 << s) - 1));
 }
 // image pixel (X, Y) of the shard's grid pixel (x, k): a row shard's x and image_row(k); a tile
-// shard's grid is its tiles side by side (tile m = the frame's tile row_begin + m*row_stride)
+// shard's grid is its tiles side by side (tile m = the frame's tile at position row_begin +
+// m*row_stride of the context's tile order, or of raster order)
 __device__ __forceinline__ void image_xy(const KParams& P, int x, int k, int& X, int& Y)
 {
     if (P.tile_shard) {   // wave-uniform
-        const unsigned t = (unsigned)P.row_begin + (unsigned)(x >> 3) * (unsigned)P.row_stride;
+        unsigned t = (unsigned)P.row_begin + (unsigned)(x >> 3) * (unsigned)P.row_stride;
+        if (__builtin_expect(P.tile_order != nullptr, 0)) t = P.tile_order[t];
         const unsigned ty = t / (unsigned)P.img_tiles_x;
         X = (int)(t - ty * (unsigned)P.img_tiles_x) * 8 + (x & 7);
         Y = (int)ty * 8 + k;
@@ -2093,10 +2095,11 @@ __global__ void __launch_bounds__(BlockThreads<C>(), min_waves<C>()) trace_pool(
     if constexpr (Stack16Cfg<C>()) stack.base = reinterpret_cast<short*>(rt_lds + lds_stack_offset<C>(S)) + threadIdx.x;
     else if constexpr (C::LDS) stack.init((int)lds_stack_offset<C>(S));
     Count cnt{};
-    uint64_t t_cam = 0, t_trace = 0, t_shade = 0, t_prev = 0, t_start = 0;
+    uint64_t t_cam = 0, t_trace = 0, t_shade = 0, t_prev = 0, t_start = 0, t_sample = 0;
     if (C::COUNT) t_prev = t_start = __builtin_amdgcn_s_memtime();
     (void)t_trace;
     (void)t_start;
+    (void)t_sample;
     const int lane = threadIdx.x & 63;
     const unsigned n_tiles = (unsigned)P.tiles_x * (unsigned)P.tiles_y;
     // a work block = one tile x block_chunks consecutive chunks (items chunk-major; the
@@ -2286,6 +2289,7 @@ __global__ void __launch_bounds__(BlockThreads<C>(), min_waves<C>()) trace_pool(
                     }
                     int ix, y;
                     image_xy(P, x, k, ix, y);
+                    if (C::COUNT) t_sample = __builtin_amdgcn_s_memtime();
                     key.pixel = (uint32_t)y * (uint32_t)P.img_width + (uint32_t)ix;
                     const uint32_t sample = ring ? (uint32_t)s & kRingSampleMask : (uint32_t)s;
                     key.sample = sample;
@@ -2354,6 +2358,12 @@ __global__ void __launch_bounds__(BlockThreads<C>(), min_waves<C>()) trace_pool(
             RT_STAMP(t_shade, t_prev);
         }
         if (C::COUNT) t_prev = __builtin_amdgcn_s_memtime();   // lanes that did not trace
+        if (C::COUNT && P.tile_cost && !(pending || gen_wait)) {   // the sample ended: its lane-cycles to its tile
+            int ix, y;
+            image_xy(P, x, k, ix, y);
+            atomicAdd(&P.tile_cost[(unsigned)(y >> 3) * (unsigned)P.img_tiles_x + (unsigned)(ix >> 3)],
+                      (unsigned long long)(t_prev - t_sample));
+        }
         if (pending || gen_wait) {
         } else if (ITEMS && left > 0) {  // the item's next sample: the lane takes it at the loop top
             active = false;

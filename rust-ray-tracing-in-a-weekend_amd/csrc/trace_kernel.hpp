@@ -94,11 +94,16 @@ struct KParams {
     uint32_t n_work_blocks;     // pool schedules: tiles x sample groups of this launch (host-computed: in
                                 // the kernel the division's VGPR result stayed live through the loop)
     int32_t img_width;          // the image's width (pixel keys)
-    int32_t tile_shard;         // rt_render_params.tile_shard: grid tile m = the frame's tile row_begin + m*row_stride
+    int32_t tile_shard;         // rt_render_params.tile_shard: grid tile m = the frame's tile at position
+                                // row_begin + m*row_stride of tile_order (raster order if null)
     int32_t img_tiles_x;        // tiles per tile row of the image
     int32_t wf_refill;          // wavefront schedule: a wf_trace wave refills once this many lanes are idle
     int32_t ring_waves;         // per-sample pool, in-kernel reduction: waves the ring holds (0: off)
     double* ring;               // per-sample pool, in-kernel reduction: kPoolRing blocks of records per wave
+    // tile shards: the frame's tile order (rt_ctx_set_tile_order), position -> raster tile; null: raster
+    const uint32_t* tile_order;
+    // count_work renders (COUNT kernels): per raster tile of the image, the lane-cycles its samples took
+    unsigned long long* tile_cost;
 };
 
 // Per-sample pool with the reduction in the kernel (round 5): a wave's work block (one tile x

@@ -75,6 +75,7 @@ EXPORTED = [
     "rt_ctx_set_variant", "rt_device_eval", "rt_accum_create", "rt_accum_destroy", "rt_accum_add",
     "rt_accum_get", "rt_accum_set", "rt_accum_resolve", "rt_render_progressive", "rt_ctx_set_schedule", "rt_ctx_set_precision",
     "rt_scene_validate", "rt_build_info", "rt_ctx_set_option", "rt_ctx_get_option", "rt_world_set_build_option",
+    "rt_last_tile_costs", "rt_ctx_set_tile_order",
 ]
 
 # int (*rt_progress_fn)(void* user, int64_t samples_done, int64_t samples_total)
@@ -195,6 +196,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "rt_rows_in_shard": ([I, I, I], I), "rt_rows_in_band_shard": ([I, I, I, I], I),
         "rt_tiles_in_shard": ([I, I, I, I], I), "rt_last_stats": ([P, ctypes.POINTER(Stats)], I),
         "rt_last_counters": ([P, P, I], I),
+        "rt_last_tile_costs": ([P, P, ctypes.c_int64], I), "rt_ctx_set_tile_order": ([P, P, ctypes.c_int64], I),
         "rt_write_ppm": ([P, I, I, ctypes.c_char_p], I),
         "rt_write_ppm_f64": ([P, I, I, I, ctypes.c_char_p], I),
         "rt_write_color": ([P, I, ctypes.c_int64, P], I),
@@ -400,21 +402,39 @@ def _perm(a, axes):
     return a.permute(*axes) if hasattr(a, "permute") else a.transpose(axes)
 
 
-def assemble_tiles(slabs, width: int, height: int, world: int, out=None):
-    """Inverse of the tile partition: slabs[r] is rank r's 8 x (8 * n_r) x 3 tile slab (tiles
-    t = r + m*world of the frame's tile grid side by side; wider padding is ignored). Works on
-    numpy arrays and torch tensors alike; returns the height x width x 3 frame."""
+def cost_tile_order(costs) -> np.ndarray:
+    """rt_ctx_set_tile_order's order from per-tile costs (rt_last_tile_costs): the raster tiles
+    by cost, most expensive first (ties in raster order). Dealt round-robin, every shard gets
+    every N-th tile of the sorted list, so the shards' costs differ by at most about one
+    tile's, and each shard renders its expensive tiles first."""
+    c = np.asarray(costs, dtype=np.float64)
+    return np.argsort(-c, kind="stable").astype(np.uint32)
+
+
+def assemble_tiles(slabs, width: int, height: int, world: int, out=None, order=None):
+    """Inverse of the tile partition: slabs[r] is rank r's 8 x (8 * n_r) x 3 tile slab (the
+    tiles at positions t = r + m*world side by side: raster tiles, or order[t] with a tile order
+    set on the renderers, rt_ctx_set_tile_order; wider padding is ignored). Works on numpy
+    arrays and torch tensors alike; returns the height x width x 3 frame."""
     tx, ty = (width + 7) // 8, (height + 7) // 8
     like = slabs[0]
     if hasattr(like, "new_empty"):
         tiles = like.new_empty((ty * tx, 8, 8, like.shape[-1]))
+        if order is not None:
+            import torch as _torch
+            order = _torch.as_tensor(np.ascontiguousarray(order, dtype=np.int64), device=like.device)
     else:
         import numpy as _np
         tiles = _np.empty((ty * tx, 8, 8, like.shape[-1]), dtype=like.dtype)
+        if order is not None:
+            order = _np.asarray(order, dtype=_np.int64)
+    if order is not None and len(order) != tx * ty:
+        raise ValueError(f"tile order of {len(order)} tiles for a frame of {tx * ty}")
     for r in range(world):
         n = len(range(r, ty * tx, world))
         if n:
-            tiles[r::world] = _perm(slabs[r][:, :8 * n].reshape(8, n, 8, like.shape[-1]), (1, 0, 2, 3))
+            dst = slice(r, None, world) if order is None else order[r::world]
+            tiles[dst] = _perm(slabs[r][:, :8 * n].reshape(8, n, 8, like.shape[-1]), (1, 0, 2, 3))
     frame = _perm(tiles.reshape(ty, tx, 8, 8, like.shape[-1]), (0, 2, 1, 3, 4)).reshape(ty * 8, tx * 8, like.shape[-1])
     if out is None:
         return frame[:height, :width]
@@ -571,6 +591,26 @@ class Renderer:
         if rc < 0:
             _check(rc, "rt_last_counters")
         return out[:rc]
+
+    def tile_costs(self) -> np.ndarray:
+        """Lane-cycles per raster 8x8 tile of the last count_work render on a pool schedule
+        (rt_last_tile_costs); empty if it counted none."""
+        n = self.lib.rt_last_tile_costs(self.h, None, 0)
+        if n < 0:
+            _check(n, "rt_last_tile_costs")
+        out = np.zeros(n, dtype=np.uint64)
+        if n:
+            _check(min(0, self.lib.rt_last_tile_costs(self.h, out.ctypes.data, n)), "rt_last_tile_costs")
+        return out
+
+    def set_tile_order(self, order=None):
+        """rt_ctx_set_tile_order: tile shards take the frame's tiles in this order (a permutation
+        of its raster tiles, e.g. cost_tile_order(tile_costs())); None: raster order."""
+        if order is None:
+            _check(self.lib.rt_ctx_set_tile_order(self.h, None, 0), "rt_ctx_set_tile_order")
+            return
+        o = np.ascontiguousarray(np.asarray(order), dtype=np.uint32)
+        _check(self.lib.rt_ctx_set_tile_order(self.h, o.ctypes.data, len(o)), "rt_ctx_set_tile_order")
 
     def stats(self) -> Stats:
         s = Stats()

@@ -29,6 +29,10 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--c5-spp", type=int, default=256)
     ap.add_argument("--ns", type=int, nargs="*", default=[2, 4, 8])
+    ap.add_argument("--order", nargs="*", default=["raster"], choices=["raster", "cost"],
+                    help="tile orders to time: raster, or cost (rt_ctx_set_tile_order from a count_work pass "
+                         "of --cost-spp samples per pixel, most expensive tiles first)")
+    ap.add_argument("--cost-spp", type=int, default=8)
     a = ap.parse_args()
     import numpy as np
     import __graft_entry__ as ge
@@ -55,20 +59,31 @@ def main():
         r.upload(world)
         t1, _ = timed(cam, rt.Renderer.params(W, H, spp, 50, bg, 1, out_format=rt.RT_OUT_F32))
         print(json.dumps({"config": name, "spp": spp, "n": 1, "frame_ms": round(t1, 3)}), flush=True)
-        for n in a.ns:
-            per = []
-            for rank in range(n):
-                p = rt.Renderer.params(W, H, spp, 50, bg, 1, row_begin=rank, row_stride=n, tile_shard=1,
-                                       out_format=rt.RT_OUT_F32)
-                ms, px = timed(cam, p)
-                per.append({"rank": rank, "ms": round(ms, 3), "pixels": px, "slab_bytes_f64": px * 24})
-            mx = max(q["ms"] for q in per)
-            mean = sum(q["ms"] for q in per) / n
-            print(json.dumps({"config": name, "spp": spp, "n": n, "max_ms": round(mx, 3), "mean_ms": round(mean, 3),
-                              "max_over_mean": round(mx / mean, 4), "implied_eff": round(t1 / (n * mx), 4),
-                              "sum_over_t1": round(sum(q["ms"] for q in per) / t1, 4),
-                              "gather_bytes_to_rank0": sum(q["slab_bytes_f64"] for q in per[1:]),
-                              "per_rank": per}), flush=True)
+        for order_kind in a.order:
+            r.set_tile_order(None)
+            if order_kind == "cost":
+                import time
+                t0 = time.perf_counter()
+                r.render(cam, rt.Renderer.params(W, H, a.cost_spp, 50, bg, 1, out_format=rt.RT_OUT_F32, count_work=1))
+                order = rt.cost_tile_order(r.tile_costs())
+                r.set_tile_order(order)
+                print(json.dumps({"config": name, "order": "cost", "cost_pass_spp": a.cost_spp,
+                                    "cost_pass_wall_ms": round((time.perf_counter() - t0) * 1e3, 2)}), flush=True)
+            for n in a.ns:
+                per = []
+                for rank in range(n):
+                    p = rt.Renderer.params(W, H, spp, 50, bg, 1, row_begin=rank, row_stride=n, tile_shard=1,
+                                           out_format=rt.RT_OUT_F32)
+                    ms, px = timed(cam, p)
+                    per.append({"rank": rank, "ms": round(ms, 3), "pixels": px, "slab_bytes_f64": px * 24})
+                mx = max(q["ms"] for q in per)
+                mean = sum(q["ms"] for q in per) / n
+                print(json.dumps({"config": name, "order": order_kind, "spp": spp, "n": n, "max_ms": round(mx, 3), "mean_ms": round(mean, 3),
+                                  "max_over_mean": round(mx / mean, 4), "implied_eff": round(t1 / (n * mx), 4),
+                                  "sum_over_t1": round(sum(q["ms"] for q in per) / t1, 4),
+                                  "gather_bytes_to_rank0": sum(q["slab_bytes_f64"] for q in per[1:]),
+                                  "per_rank": per}), flush=True)
+        r.set_tile_order(None)
     r.close()
 
 

@@ -98,11 +98,13 @@ def test_bench_py_rccl_branch_at_world_size_1(tmp_path):
     init_process_group("nccl"), the render into the tile-shard slab, the device dist.gather of
     the slab, assemble_tiles on the gathered device slab, the barriers and the MAX all-reduce.
     Its frame and PPM equal the plain N = 1 run bit for bit; the JSON line says n_gpus 1, an
-    RCCL gather and the per-rank kernel / gather times."""
-    jd, fd, pd = _bench(tmp_path, 1, "rccl1", rccl=True)
+    RCCL gather and the per-rank kernel / gather times. It runs with --tile-order cost: rank 0's
+    count_work pass, the RCCL broadcast of the order, the shard in that order and its reassembly."""
+    jd, fd, pd = _bench(tmp_path, 1, "rccl1", extra=("--tile-order", "cost"), rccl=True)
     j1, f1, p1 = _bench(tmp_path, 1, "plain1")
     assert jd["n_gpus"] == 1 and "RCCL" in jd["config"]["parallelism"]
-    assert "8x8 tiles" in jd["config"]["parallelism"]
+    assert "8x8 tiles (cost order)" in jd["config"]["parallelism"] and jd["config"]["tile_order"] == "cost"
+    assert jd["detail"]["tile_order_pass_s"] > 0
     assert jd["distributed"] == {"backend": "nccl (RCCL)", "world_size": 1, "forced_at_world_1": True}
     pr = jd["per_rank"]
     assert len(pr) == 1 and pr[0]["kernel_ms"] > 0 and pr[0]["gather_ms"] >= 0 and pr[0]["samples"] >= 160 * 90 * 8

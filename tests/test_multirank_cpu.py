@@ -46,14 +46,17 @@ def _rank_main(rank, world, port, out_path):
     dist.destroy_process_group()
 
 
-def tile_slab(frame, rank, world):
+def tile_slab(frame, rank, world, order=None):
     """Rank `rank`'s tile shard of a frame in the layout rt_render writes (rt_abi.h tile_shard):
-    tiles t = rank + m*world of the 8x8 tile grid side by side in one 8-row slab."""
+    the tiles at positions t = rank + m*world (raster tile t, or order[t] with a tile order) of
+    the 8x8 tile grid side by side in one 8-row slab."""
     H, W = frame.shape[:2]
     tx, ty = (W + 7) // 8, (H + 7) // 8
     pad = np.zeros((ty * 8, tx * 8) + frame.shape[2:], frame.dtype)
     pad[:H, :W] = frame
     ts = list(range(rank, tx * ty, world))
+    if order is not None:
+        ts = [int(order[t]) for t in ts]
     slab = np.zeros((8, 8 * len(ts)) + frame.shape[2:], frame.dtype)
     for m, t in enumerate(ts):
         y0, x0 = (t // tx) * 8, (t % tx) * 8
@@ -104,6 +107,34 @@ def test_tile_shards_partition_and_assemble():
             padded = [torch.from_numpy(np.pad(s, ((0, 0), (0, wide - s.shape[1]), (0, 0)))) for s in slabs]
             assert np.array_equal(rt.assemble_tiles(padded, w, h, world).numpy(), img)
     assert rt.tiles_in_shard(24, 19, 8, 4) == 1 and rt.tiles_in_shard(24, 19, 9, 4) == 0   # 9 tiles
+
+
+def test_tile_order_assemble_and_cost_order():
+    """assemble_tiles with a tile order (rt_ctx_set_tile_order) inverts the shards that order
+    deals, numpy and torch; cost_tile_order sorts most expensive first, ties in raster order,
+    and deals shards whose costs differ by at most one tile's."""
+    import __graft_entry__ as ge
+    rt = ge.import_binding()
+    rng = np.random.default_rng(5)
+    for (h, w) in ((19, 24), (80, 16), (64, 96)):
+        img = np.arange(h * w * 3, dtype=np.float64).reshape(h, w, 3)
+        tiles = ((w + 7) // 8) * ((h + 7) // 8)
+        for order in (rng.permutation(tiles), np.arange(tiles)[::-1]):
+            for world in (1, 3, 8):
+                slabs = [tile_slab(img, r, world, order) for r in range(world)]
+                assert np.array_equal(rt.assemble_tiles(slabs, w, h, world, order=order), img)
+                wide = max(s.shape[1] for s in slabs)
+                padded = [torch.from_numpy(np.pad(s, ((0, 0), (0, wide - s.shape[1]), (0, 0)))) for s in slabs]
+                assert np.array_equal(rt.assemble_tiles(padded, w, h, world, order=order).numpy(), img)
+    with pytest.raises(ValueError):
+        rt.assemble_tiles([np.zeros((8, 8, 3))], 16, 16, 1, order=np.arange(3))
+    costs = np.array([5, 9, 9, 1, 7, 3, 0, 9], dtype=np.uint64)
+    order = rt.cost_tile_order(costs)
+    assert order.tolist() == [1, 2, 7, 4, 0, 5, 3, 6] and order.dtype == np.uint32
+    heavy = rng.pareto(1.5, 4050 * 8) + 1.0
+    o = rt.cost_tile_order(heavy)
+    sums = [heavy[o[r::8]].sum() for r in range(8)]
+    assert max(sums) - min(sums) <= heavy.max()
 
 
 @pytest.mark.parametrize("world", [2, 3])
