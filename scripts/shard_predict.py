@@ -33,11 +33,17 @@ def main():
                     help="tile orders to time: raster, or cost (rt_ctx_set_tile_order from a count_work pass "
                          "of --cost-spp samples per pixel, most expensive tiles first)")
     ap.add_argument("--cost-spp", type=int, default=8)
+    ap.add_argument("--ring", type=int, default=None, help="RT_OPT_POOL_RING for every render (default: the library's)")
+    ap.add_argument("--block", type=int, default=None, help="RT_OPT_BLOCK_SAMPLES for every render (default: automatic)")
     a = ap.parse_args()
     import numpy as np
     import __graft_entry__ as ge
     rt = ge.import_binding()
     r = rt.Renderer(0)
+    if a.ring is not None:
+        r.set_option(rt.RT_OPT_POOL_RING, a.ring)
+    if a.block is not None:
+        r.set_option(rt.RT_OPT_BLOCK_SAMPLES, a.block)
 
     def timed(cam, p):
         rows, width = rt.shard_shape(p)
@@ -75,7 +81,9 @@ def main():
                     p = rt.Renderer.params(W, H, spp, 50, bg, 1, row_begin=rank, row_stride=n, tile_shard=1,
                                            out_format=rt.RT_OUT_F32)
                     ms, px = timed(cam, p)
-                    per.append({"rank": rank, "ms": round(ms, 3), "pixels": px, "slab_bytes_f64": px * 24})
+                    st = r.stats()
+                    per.append({"rank": rank, "ms": round(ms, 3), "pixels": px, "slab_bytes_f64": px * 24,
+                                "ring": st.ring_bytes > 0, "reduce_ms": round(st.reduce_ms, 3)})
                 mx = max(q["ms"] for q in per)
                 mean = sum(q["ms"] for q in per) / n
                 print(json.dumps({"config": name, "order": order_kind, "spp": spp, "n": n, "max_ms": round(mx, 3), "mean_ms": round(mean, 3),
