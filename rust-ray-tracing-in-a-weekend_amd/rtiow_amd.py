@@ -411,6 +411,32 @@ def cost_tile_order(costs) -> np.ndarray:
     return np.argsort(-c, kind="stable").astype(np.uint32)
 
 
+def scattered_tile_order(n_tiles: int, stride: int) -> np.ndarray:
+    """Every stride-th raster tile first (0, s, 2s, ...), then 1, 1 + s, ...: one GPU's frame
+    spread over the image as an s-way round-robin shard is (scripts/tile_locality.py)."""
+    return np.concatenate([np.arange(k, n_tiles, stride) for k in range(stride)]).astype(np.uint32)
+
+
+def grouped_tile_order(n_tiles: int, world: int, group: int) -> np.ndarray:
+    """A tile order that deals runs of `group` consecutive raster tiles round-robin over `world`
+    tile shards (run j to shard j mod world), instead of single tiles: each shard's waves then work
+    on neighbouring tiles. Shard r holds positions r, r + world, ... (rt_tiles_in_shard tiles);
+    a run that does not fit its shard's remaining count continues on the next shard with room."""
+    cap = [len(range(r, n_tiles, world)) for r in range(world)]
+    lists = [[] for _ in range(world)]
+    for j, t0 in enumerate(range(0, n_tiles, group)):
+        k = j % world
+        for t in range(t0, min(t0 + group, n_tiles)):
+            while cap[k] == 0:
+                k = (k + 1) % world
+            lists[k].append(t)
+            cap[k] -= 1
+    order = np.empty(n_tiles, dtype=np.uint32)
+    for r in range(world):
+        order[r::world] = lists[r]
+    return order
+
+
 def assemble_tiles(slabs, width: int, height: int, world: int, out=None, order=None):
     """Inverse of the tile partition: slabs[r] is rank r's 8 x (8 * n_r) x 3 tile slab (the
     tiles at positions t = r + m*world side by side: raster tiles, or order[t] with a tile order

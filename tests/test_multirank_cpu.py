@@ -109,6 +109,21 @@ def test_tile_shards_partition_and_assemble():
     assert rt.tiles_in_shard(24, 19, 8, 4) == 1 and rt.tiles_in_shard(24, 19, 9, 4) == 0   # 9 tiles
 
 
+def test_grouped_and_scattered_tile_orders():
+    """grouped_tile_order deals runs of consecutive raster tiles round-robin and keeps every
+    shard's tile count (rt_tiles_in_shard); scattered_tile_order is a stride permutation."""
+    import __graft_entry__ as ge
+    rt = ge.import_binding()
+    for (n, world, g) in ((32400, 8, 30), (15000, 8, 8), (9, 4, 2), (100, 3, 7), (7, 8, 4), (5, 1, 3)):
+        o = rt.grouped_tile_order(n, world, g)
+        assert sorted(o.tolist()) == list(range(n))
+        for r in range(world):
+            assert len(o[r::world]) == len(range(r, n, world))
+    o = rt.grouped_tile_order(32400, 8, 30)
+    assert o[0::8][:32].tolist() == list(range(30)) + [240, 241]   # runs 0, 8, ...: tiles 0-29, 240-269
+    assert rt.scattered_tile_order(10, 3).tolist() == [0, 3, 6, 9, 1, 4, 7, 2, 5, 8]
+
+
 def test_tile_order_assemble_and_cost_order():
     """assemble_tiles with a tile order (rt_ctx_set_tile_order) inverts the shards that order
     deals, numpy and torch; cost_tile_order sorts most expensive first, ties in raster order,
