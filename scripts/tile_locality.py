@@ -63,9 +63,21 @@ def main():
         t_raster = timed(cam, params())
         r.set_tile_order(rt.scattered_tile_order(n_tiles, a.stride))
         t_scatter = timed(cam, params())
+        # Z-order (Morton) of the tile grid: the waves in flight work on a compact square of tiles
+        tx, ty = (W + 7) // 8, (H + 7) // 8
+
+        def morton(x, y):
+            z = 0
+            for b in range(16):
+                z |= ((x >> b) & 1) << (2 * b) | ((y >> b) & 1) << (2 * b + 1)
+            return z
+        keys = [morton(t % tx, t // tx) for t in range(n_tiles)]
+        r.set_tile_order(np.argsort(np.array(keys), kind="stable").astype(np.uint32))
+        t_morton = timed(cam, params())
         print(json.dumps({"config": name, "spp": spp, "n": 1, "frame_rows_ms": round(t_rows, 3),
                           "tile_shard_raster_ms": round(t_raster, 3),
-                          "tile_shard_scattered_ms": round(t_scatter, 3), "stride": a.stride}), flush=True)
+                          "tile_shard_scattered_ms": round(t_scatter, 3), "stride": a.stride,
+                          "tile_shard_morton_ms": round(t_morton, 3)}), flush=True)
         for g in [1] + a.groups:
             r.set_tile_order(None if g == 1 else rt.grouped_tile_order(n_tiles, a.n, g))
             per = [timed(cam, params(k, a.n)) for k in range(a.n)]
