@@ -59,9 +59,33 @@ def main():
                      "nodes": int(st.node_visits), "prims": int(st.prim_tests), "lane_cycles": lane_cycles,
                      "wave_steps": int(st.wave_steps), "wave_node_steps": int(st.wave_node_steps),
                      "wave_leaf_steps": int(st.wave_leaf_steps), "wave_life": int(c[21]),
+                     "max_life_cycles": int(c[25]), "waves": int(c[26]),
+                     "slot_use": int(c[21]) / max(1, int(c[26]) * int(c[25])),
                      "occupancy": st.casts / max(1, 64 * st.wave_steps)})
+    # the whole frame (rows, one launch) with the same counters: the ranks' sums against it
+    pf = rt.Renderer.params(W, H, a.spp, 50, bg, 1, out_format=rt.RT_OUT_F32)
+    fo = np.empty(rt.shard_shape(pf) + (3,), np.float32)
+    r.set_tile_order(None)
+    r.render(cam, pf, fo)
+    fms = []
+    for _ in range(a.reps):
+        r.render(cam, pf, fo)
+        st = r.stats()
+        fms.append(st.kernel_ms + st.reduce_ms)
+    r.render(cam, rt.Renderer.params(W, H, a.spp, 50, bg, 1, out_format=rt.RT_OUT_F32, count_work=1), fo)
+    st = r.stats()
+    c = r.counters(32)
+    whole = {"ms": float(np.median(fms)), "count_ms": st.kernel_ms, "casts": int(st.casts), "nodes": int(st.node_visits),
+             "prims": int(st.prim_tests), "lane_cycles": int(r.tile_costs().sum()), "wave_steps": int(st.wave_steps),
+             "wave_node_steps": int(st.wave_node_steps), "wave_leaf_steps": int(st.wave_leaf_steps),
+             "wave_life": int(c[21]), "max_life_cycles": int(c[25]), "waves": int(c[26]),
+             "slot_use": int(c[21]) / max(1, int(c[26]) * int(c[25])),
+             "occupancy": st.casts / max(1, 64 * st.wave_steps)}
+    print(json.dumps({"whole_frame": whole}), flush=True)
     keys = ["ms", "count_ms", "casts", "nodes", "prims", "lane_cycles", "wave_steps", "wave_node_steps",
-            "wave_leaf_steps", "wave_life", "occupancy"]
+            "wave_leaf_steps", "wave_life", "max_life_cycles", "slot_use", "occupancy"]
+    print("sum over ranks / whole frame: " + json.dumps(
+        {k: round(sum(q[k] for q in rows) / whole[k], 4) for k in keys if k not in ("occupancy", "slot_use", "max_life_cycles")}), flush=True)
     for q in rows:
         print(json.dumps(q), flush=True)
     mean = {k: sum(q[k] for q in rows) / len(rows) for k in keys}
