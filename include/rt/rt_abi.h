@@ -262,10 +262,13 @@ int rt_last_tile_costs(rt_ctx* ctx, uint64_t* out, int64_t n);
 /* The order in which tile shards (rt_render_params.tile_shard = 1) take the frame's tiles:
  * order[t] is the raster tile at position t, a permutation of the frame's n tiles (checked:
  * RT_ERR_INVALID otherwise). Shards then take positions row_begin + m*row_stride; a frame of
- * another tile count fails with RT_ERR_INVALID. The tiles sorted by cost, most expensive
- * first, give round-robin shards of nearly equal cost, each rendering its expensive tiles
- * first. Only which pixels a shard renders changes, not their bits. n = 0: raster order
- * again (the default). Waits for the device. */
+ * another tile count fails with RT_ERR_INVALID. Under a tile order the pool schedules also deal
+ * their work blocks tile-major (all of a tile's sample groups before the next tile's) instead
+ * of sample-group-major. The tiles sorted by cost, most expensive first, then give round-robin
+ * shards of nearly equal cost, each finishing its expensive tiles first and ending on its
+ * cheapest ones (a shard's launch otherwise ends on the last sample group of its most
+ * expensive tiles). Only which pixels a shard renders, and when, changes, not their bits.
+ * n = 0: raster order again (the default). Waits for the device. */
 int rt_ctx_set_tile_order(rt_ctx* ctx, const uint32_t* order, int64_t n);
 
 /* ---- progressive / resumable accumulation ------------------------------------ */

@@ -1357,6 +1357,7 @@ static int run_range(rt_ctx* c, const rt_camera* cam, const rt_render_params* p,
             return fail(RT_ERR_INVALID, "the tile order has " + std::to_string(c->tile_order_n) + " tiles, the frame " +
                                             std::to_string(img_tiles));
         K.tile_order = c->tile_order;
+        K.tile_major = 1;   // the order's first tiles done first and entirely (rt_abi.h rt_ctx_set_tile_order)
     }
     K.wf_refill = c->wf_refill > 0 ? c->wf_refill : kWfDefaultRefill;
     K.n_rows = n_rows;
@@ -1592,7 +1593,9 @@ static int run_range(rt_ctx* c, const rt_camera* cam, const rt_render_params* p,
         {
             const unsigned g = o.pool == RT_SCHED_ITEMS ? (unsigned)K.block_chunks : (unsigned)K.block_samples;   // (POOL, WAVEFRONT: samples)
             const unsigned n = o.pool == RT_SCHED_ITEMS ? (unsigned)K.n_chunks : (unsigned)(K.spp - K.sample_begin);
-            K.n_work_blocks = (unsigned)K.tiles_x * (unsigned)K.tiles_y * ((n + g - 1) / std::max(g, 1u));
+            const unsigned n_groups = (n + g - 1) / std::max(g, 1u);
+            K.n_work_blocks = (unsigned)K.tiles_x * (unsigned)K.tiles_y * n_groups;
+            K.deal_div = K.tile_major ? n_groups : (unsigned)K.tiles_x * (unsigned)K.tiles_y;
         }
         // batch bi's buffer half, trace stream and work counter (one of each per overlapped batch)
         const int h = overlap ? (bi & 1) : 0;

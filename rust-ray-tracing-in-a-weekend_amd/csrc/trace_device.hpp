@@ -2046,7 +2046,9 @@ __device__ __forceinline__ void ring_reduce(const KParams& P, const double* __re
                                             double* __restrict__ partial, unsigned blk, unsigned n_tiles, unsigned group,
                                             size_t n_px, int lane)
 {
-    const unsigned grp = blk / n_tiles, tile = blk - grp * n_tiles;
+    // the block's (sample group, tile), as trace_pool dealt it (KParams.deal_div)
+    const unsigned outer = blk / P.deal_div, inner = blk - outer * P.deal_div;
+    const unsigned grp = P.tile_major ? inner : outer, tile = P.tile_major ? outer : inner;
     const int s0 = P.sample_begin + (int)(grp * group);
     const int x = (int)(tile % (unsigned)P.tiles_x) * 8 + (lane & 7);
     const int k = (int)(tile / (unsigned)P.tiles_x) * 8 + (lane >> 3);
@@ -2195,7 +2197,26 @@ __global__ void __launch_bounds__(BlockThreads<C>(), min_waves<C>()) trace_pool(
                     exhausted = true;
                     break;
                 }
-                const unsigned grp = b / n_tiles, tile = b - grp * n_tiles;
+                // group-major (b = grp * n_tiles + tile) or, under a tile order, tile-major
+                // (b = tile * n_groups + grp): one division by KParams.deal_div either way
+                // group-major (b = grp * n_tiles + tile) or, under a tile order, tile-major
+                // (b = tile * n_groups + grp; KParams.deal_div). Two forms of the same mapping: the
+                // branch kept the spheres variant's code as it was (a select moved it, C2 +1.1 %),
+                // the select the final variant's (the branch added 8 B of spill to its ring kernel)
+                unsigned grp, tile;
+                if constexpr (C::F == FEAT_SET_SPHERES) {
+                    if (__builtin_expect(P.tile_major != 0, 0)) {   // (wave-uniform)
+                        tile = b / P.deal_div;
+                        grp = b - tile * P.deal_div;
+                    } else {
+                        grp = b / n_tiles;
+                        tile = b - grp * n_tiles;
+                    }
+                } else {
+                    const unsigned outer = b / P.deal_div, inner = b - outer * P.deal_div;
+                    grp = P.tile_major ? inner : outer;
+                    tile = P.tile_major ? outer : inner;
+                }
                 tx0 = (int)(tile % (unsigned)P.tiles_x) * 8;
                 tk0 = (int)(tile / (unsigned)P.tiles_x) * 8;
                 vw = min(8, P.width - tx0);

@@ -102,6 +102,12 @@ struct KParams {
     double* ring;               // per-sample pool, in-kernel reduction: kPoolRing blocks of records per wave
     // tile shards: the frame's tile order (rt_ctx_set_tile_order), position -> raster tile; null: raster
     const uint32_t* tile_order;
+    // pool schedules: work blocks dealt tile-major (all of a tile's sample groups, then the next
+    // tile: set with a tile order, so the most expensive tiles are done first and entirely) rather
+    // than group-major; deal_div = the block index's inner extent: tiles (group-major) or sample
+    // (chunk) groups per tile (tile-major)
+    int32_t tile_major;
+    uint32_t deal_div;
     // count_work renders (COUNT kernels): per raster tile of the image, the lane-cycles its samples took
     unsigned long long* tile_cost;
 };
