@@ -78,10 +78,11 @@ def parse():
     ap.add_argument("--shard", default="tiles", choices=["tiles", "rows"],
                     help="N > 1 partition: the frame's 8x8 tiles round-robin (rt_render_params.tile_shard) or "
                          "single rows round-robin")
-    ap.add_argument("--tile-order", default="raster", choices=["raster", "cost"],
-                    help="N > 1 tile shards: raster order, or cost (rank 0 times a count_work pass of "
-                         "--cost-spp samples per pixel, untimed, and broadcasts the tiles sorted by cost; "
-                         "rt_ctx_set_tile_order)")
+    ap.add_argument("--tile-order", default="cost", choices=["raster", "cost"],
+                    help="N > 1 tile shards: cost (default: rank 0 times a count_work pass of --cost-spp "
+                         "samples per pixel before the timed steps, like the scene upload, and broadcasts "
+                         "the tiles sorted by cost; rt_ctx_set_tile_order, whose shards then deal their "
+                         "blocks tile-major: expensive tiles first and entirely) or raster")
     ap.add_argument("--cost-spp", type=int, default=8, help="spp of the --tile-order cost pass")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="N > 1: nccl (RCCL over xGMI, the product) or gloo (host-staged slabs; lets several "
