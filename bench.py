@@ -50,7 +50,7 @@ CONFIGS = {
     "C4": dict(scene=7, width=1920, height=1080, spp=1000, depth=50),
     "C5": dict(scene=0, width=4096, height=4096, spp=4096, depth=50),
 }
-SCHEDULES = {"chunks": 0, "pool": 1, "items": 2, "auto": 3, "wavefront": 4}
+SCHEDULES = {"chunks": 0, "pool": 1, "items": 2, "auto": 3}
 SCENE_NAMES = {0: "random_scene (main.rs:245-289)", 5: "cornell_box_scene (main.rs:107-136)",
                7: "final_scene (main.rs:173-243)"}
 

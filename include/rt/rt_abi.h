@@ -239,7 +239,7 @@ typedef struct rt_stats {
     int32_t waves_per_simd;      /* resident waves per SIMD of the last trace kernel (occupancy) */
     int64_t trace_buf_bytes;     /* the trace-output buffer the last render used (both halves when overlapped) */
     int32_t overlapped;          /* 1 if its buffer batches ran overlapped (two trace streams) */
-    int32_t wf_iterations;       /* RT_SCHED_WAVEFRONT: wf_logic / wf_trace iterations of the last render */
+    int32_t reserved0;           /* always 0 (ABI v4's wavefront-schedule iteration count; that schedule is gone) */
     int64_t ring_bytes;          /* POOL with the in-kernel reduction (ABI v3): its record ring, part of
                                     trace_buf_bytes; 0 when the per-sample buffer ran */
 } rt_stats;
@@ -336,9 +336,6 @@ int rt_ctx_set_variant(rt_ctx* ctx, int slab32, int lds_stack, int lds_nodes);
  *                           feature-set variant than it needs (tests: the all-features variant)
  *   RT_OPT_HOIST            1 (default): the spheres variants test a huge root-child leaf before
  *                           the walk (SceneDev.pre_leaf); takes effect at the next upload
- *   RT_OPT_WF_PATHS         wavefront schedule: path slots (0: auto)
- *   RT_OPT_WF_REFILL        wavefront schedule: a wf_trace wave takes queued rays once this many of
- *                           its 64 lanes are idle (0: auto)
  *   RT_OPT_POOL_RING        1 (default): POOL reduces each finished (tile, chunk) block inside the
  *                           trace kernel into chunk partials when its per-sample buffer would not
  *                           fit the bound in one batch; 2: whenever its blocks allow; 0: never (the
@@ -350,8 +347,7 @@ enum {
     RT_OPT_BLOCK_CHUNKS = 4,
     RT_OPT_EXTRA_FEATURES = 5,
     RT_OPT_HOIST = 6,
-    RT_OPT_WF_PATHS = 7,
-    RT_OPT_WF_REFILL = 8,
+    /* 7, 8: ABI v4's wavefront-schedule options, removed with it (RT_ERR_INVALID) */
     RT_OPT_POOL_RING = 9
 };
 int rt_ctx_set_option(rt_ctx* ctx, int key, int64_t value);
@@ -376,12 +372,9 @@ int rt_ctx_get_option(rt_ctx* ctx, int key, int64_t* value);
  *           fastest there); otherwise POOL when it can reduce in the kernel or its
  *           per-sample radiance is at most 4 x the buffer bound, else ITEMS; rt_stats.schedule
  *           reports which ran.
- *   WAVEFRONT: the final-scene feature set (f64, f32 slabs, one instanced BLAS, every node fits
- *           LDS): a pool of path slots in HBM (RT_OPT_WF_PATHS) and per iteration two kernels —
- *           wf_logic (hit records, materials, camera rays of new units; live slots compacted into
- *           a ray queue) and wf_trace (persistent; a lane whose walk ends takes the next queued ray
- *           at once; the top-level and instanced-BLAS walks in one step loop). Per-sample output as
- *           POOL. A scene outside that set runs AUTO's choice (rt_stats.schedule says which ran).
+ * Schedule 4 (ABI v4's wavefront split: wf_logic / wf_trace kernels over a path pool in HBM) was
+ * measured 2.3x slower than POOL on the final scene and removed; rt_ctx_set_schedule(4) returns
+ * RT_ERR_UNSUPPORTED (the code: scripts/experiments/r05_wavefront.patch).
  * The trace-output buffer (POOL's ring included) is bounded by RT_OPT_TRACE_BUF_BYTES (default
  * 4 GiB, or half the device's free memory if that is less; allocated lazily, as large as a
  * render needs). A larger render runs in buffer
@@ -389,7 +382,7 @@ int rt_ctx_get_option(rt_ctx* ctx, int key, int64_t* value);
  * k & 1 on one of two context streams while the render's stream reduces batch k - 1, so
  * consecutive traces overlap (RT_OPT_BATCH_OVERLAP 0: one buffer, in order). Under the default
  * bound C2 (1.2 GB with the ring) and C4 (3.4 GB) render in one batch, C5 in 64. */
-enum { RT_SCHED_CHUNKS = 0, RT_SCHED_POOL = 1, RT_SCHED_ITEMS = 2, RT_SCHED_AUTO = 3, RT_SCHED_WAVEFRONT = 4 };
+enum { RT_SCHED_CHUNKS = 0, RT_SCHED_POOL = 1, RT_SCHED_ITEMS = 2, RT_SCHED_AUTO = 3 };
 int rt_ctx_set_schedule(rt_ctx* ctx, int schedule);
 
 /* Arithmetic of a context's renders (default RT_PREC_F64).

@@ -100,8 +100,6 @@ struct rt_ctx {
     int n_materials = 0, n_textures = 0;
     int block_chunks = 0;               // RT_OPT_BLOCK_CHUNKS: chunks per item-pool work block (0: auto)
     int block_samples = 0;              // RT_OPT_BLOCK_SAMPLES: samples per per-sample-pool work block (0: auto)
-    int64_t wf_paths = 0;               // RT_OPT_WF_PATHS: wavefront schedule path slots (0: auto)
-    int wf_refill = 0;                  // RT_OPT_WF_REFILL: idle lanes before a wf_trace wave refills (0: auto)
     int opt_ring = 1;                   // RT_OPT_POOL_RING: POOL reduces finished blocks in the kernel (0 never,
                                         // 1 when its per-sample buffer would not fit the bound, 2 always)
     double* ring = nullptr;             // its per-wave record ring (kPoolRing blocks per wave)
@@ -132,14 +130,6 @@ struct rt_ctx {
     int n_tlas_nodes = 0;
     int n_nodes = 0;                    // BVH nodes of the uploaded scene (TLAS + BLASes)
     int n_cus = 256;
-    // RT_SCHED_WAVEFRONT: the path pool (one allocation, WfPaths views into it), the host's poll of
-    // the live flag (pinned) and the scene's fitness for the schedule (upload)
-    rtk::WfPaths wf{};
-    void* wf_buf = nullptr;
-    size_t wf_cap = 0;
-    int32_t* wf_flag_host = nullptr;
-    hipEvent_t wf_ev[2] = {nullptr, nullptr};
-    bool wf_scene_ok = false;
     size_t lds_per_cu = 160 * 1024;     // the device's LDS per CU and per workgroup (read at creation)
     size_t lds_per_block = 160 * 1024;
 };
@@ -211,8 +201,6 @@ int rt_ctx_create(int device, rt_ctx** out)
     for (int i = 0; i < 2 && e == hipSuccess; ++i) e = hipEventCreateWithFlags(&c->ev_tr[i], hipEventDisableTiming);
     for (int i = 0; i < 2 && e == hipSuccess; ++i) e = hipEventCreateWithFlags(&c->ev_rd[i], hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_in, hipEventDisableTiming);
-    for (int i = 0; i < 2 && e == hipSuccess; ++i) e = hipEventCreateWithFlags(&c->wf_ev[i], hipEventDisableTiming);
-    if (e == hipSuccess) e = hipHostMalloc((void**)&c->wf_flag_host, 2 * sizeof(int32_t), hipHostMallocDefault);
     if (e != hipSuccess) {
         rt_ctx_destroy(c);
         return hip_fail(e, "rt_ctx_create");
@@ -237,10 +225,6 @@ void rt_ctx_destroy(rt_ctx* c)
     (void)hipFree(c->params);
     (void)hipFree(c->work);
     (void)hipFree(c->acc_tmp);
-    (void)hipFree(c->wf_buf);
-    if (c->wf_flag_host) (void)hipHostFree(c->wf_flag_host);
-    for (auto& e : c->wf_ev)
-        if (e) (void)hipEventDestroy(e);
     for (auto& e : c->ev)
         if (e) (void)hipEventDestroy(e);
     if (c->ev_done) (void)hipEventDestroy(c->ev_done);
@@ -964,7 +948,6 @@ int rt_ctx_upload_soa(rt_ctx* c, const rt_scene_soa* s)
     // level holds one instance over a BVH and none of the others (the final scene) needs the
     // larger of the two walks, not their sum: 13 entries instead of 25 per lane, 12 KB less LDS
     // per block.
-    c->S.defer_inst = -1;
     if (RT_DEFER_INST && blas_depth > 0) {
         int n_inst = 0;
         bool inst_boundary = false;
@@ -982,25 +965,14 @@ int rt_ctx_upload_soa(rt_ctx* c, const rt_scene_soa* s)
                 const rt_prim& p = s->prims[s->prim_refs[j]];
                 if (p.kind == RT_PRIM_INSTANCE) {   // an instance that may walk a BLAS
                     const rt_instance& in = s->instances[p.a];
-                    if (in.child_kind == RT_CHILD_BVH) {
-                        ++n_inst;
-                        c->S.defer_inst = p.a;
-                    }
+                    if (in.child_kind == RT_CHILD_BVH) ++n_inst;
                     else if (s->prims[in.child].kind == RT_PRIM_MEDIUM) inst_boundary = true;   // never deferred
                 }
                 if (p.kind == RT_PRIM_MEDIUM && s->prims[p.a].kind == RT_PRIM_INSTANCE) inst_boundary = true;
             }
         }
         if (n_inst <= 1 && !inst_boundary) c->S.stack_entries = std::max(tlas_depth + 1, blas_depth + 1);
-        // the wavefront schedule walks the top level and the deferred BLAS in one region of one
-        // stack, every node staged in LDS: at most one instance over a BVH, that BVH the BFS-
-        // ordered one right after the TLAS, nothing else (wf_trace)
-        c->wf_scene_ok = n_inst <= 1 && !inst_boundary && n_tlas_nodes + n_blas_bfs == s->n_nodes;
-        if (n_inst != 1) c->S.defer_inst = -1;
-    } else {
-        c->wf_scene_ok = blas_depth == 0 && n_tlas_nodes == s->n_nodes;
     }
-    if (s->tlas_root < 0 && s->n_nodes == 0) c->wf_scene_ok = false;   // (no node: the Cornell scenes)
     c->n_tlas_nodes = n_tlas_nodes;
     c->n_nodes = s->n_nodes;
     c->n_materials = s->n_materials;
@@ -1236,58 +1208,6 @@ static int grow(rt_ctx* c, hipStream_t stream, double*& buf, size_t& cap, size_t
     return RT_OK;
 }
 
-// The wavefront schedule's path pool for a batch of `units` (pixel, sample) units: RT_OPT_WF_PATHS
-// slots (default kWfDefaultPaths), at most the units rounded up, a multiple of 2048 (whole logic
-// blocks of 256 per shard). One allocation carved into the WfPaths arrays, grown on demand.
-constexpr long long kWfDefaultPaths = 2LL << 20;
-constexpr int kWfDefaultRefill = 16;
-static int wf_pool(rt_ctx* c, hipStream_t stream, long long units)
-{
-    long long n = c->wf_paths > 0 ? c->wf_paths : kWfDefaultPaths;
-    n = std::max<long long>(2048, std::min(n, (units + 2047) / 2048 * 2048));
-    n = (n + 2047) / 2048 * 2048;
-    const size_t seg = (size_t)n / 64;
-    const size_t a = 256;
-    const size_t N1 = (size_t)n;
-    const size_t bytes[] = {3 * 8 * N1, 16 * N1, 8 * N1, 4 * N1, 4 * N1,                  // T rng xk st qpos
-                            2 * 3 * 8 * N1, 2 * 3 * 8 * N1, 2 * 8 * N1, 2 * 16 * N1,     // qo qd qtime qkey
-                            2 * 8 * N1, 2 * 8 * N1,                                      // ht hp
-                            4 * seg, 16 * seg, 4 * rtk::kWfShards, 4 * rtk::kWfFlags};
-    constexpr int N = (int)(sizeof(bytes) / sizeof(bytes[0]));
-    size_t off[N], total = 0;
-    for (int i = 0; i < N; ++i) {
-        off[i] = total;
-        total = align_up(total + bytes[i], a);
-    }
-    if (total > c->wf_cap) {
-        HIP_TRY(hipStreamSynchronize(stream));
-        (void)hipFree(c->wf_buf);
-        c->wf_buf = nullptr;
-        c->wf_cap = 0;
-        HIP_TRY(hipMalloc(&c->wf_buf, total));
-        c->wf_cap = total;
-    }
-    char* b = (char*)c->wf_buf;
-    rtk::WfPaths& W = c->wf;
-    W.n = (int32_t)n;
-    W.T = (double*)(b + off[0]);
-    W.rng = (uint4*)(b + off[1]);
-    W.xk = (int2*)(b + off[2]);
-    W.st = (int32_t*)(b + off[3]);
-    W.qpos = (uint32_t*)(b + off[4]);
-    W.qo = (double*)(b + off[5]);
-    W.qd = (double*)(b + off[6]);
-    W.qtime = (double*)(b + off[7]);
-    W.qkey = (uint4*)(b + off[8]);
-    W.ht = (double*)(b + off[9]);
-    W.hp = (int2*)(b + off[10]);
-    W.qn = (uint32_t*)(b + off[11]);
-    W.wblk = (int4*)(b + off[12]);
-    W.tctr = (unsigned*)(b + off[13]);
-    W.flag = (int32_t*)(b + off[14]);
-    return RT_OK;
-}
-
 // Where a sample range's per-pixel sums go: added to acc (n_px x 3 f64), or (acc null)
 // written as sum * scale to out (f32 / f64).
 struct Sink {
@@ -1359,7 +1279,6 @@ static int run_range(rt_ctx* c, const rt_camera* cam, const rt_render_params* p,
         K.tile_order = c->tile_order;
         K.tile_major = 1;   // the order's first tiles done first and entirely (rt_abi.h rt_ctx_set_tile_order)
     }
-    K.wf_refill = c->wf_refill > 0 ? c->wf_refill : kWfDefaultRefill;
     K.n_rows = n_rows;
     K.tiles_x = (lay.w + 7) / 8;
     K.tiles_y = (n_rows + 7) / 8;
@@ -1426,12 +1345,6 @@ static int run_range(rt_ctx* c, const rt_camera* cam, const rt_render_params* p,
     // two (C2 kernel ms, pool 1/2/4 chunks: 99.8/100.2/103.2; items 1/2/4: 106.8/104.1/105.0;
     // profiles/r02f_*, r02g_*)
     K.block_chunks = c->block_chunks > 0 ? c->block_chunks : 2;
-    // RT_SCHED_WAVEFRONT: the final-scene feature set (wf_logic / wf_trace are its kernels), f64,
-    // f32 slabs, the stack and every node in LDS; otherwise AUTO's choice runs
-    const bool wavefront = c->opt_pool == RT_SCHED_WAVEFRONT && c->wf_scene_ok && !o.f32 && o.slab32 && o.lds_stack &&
-                           rtk::variant_features(o.features) == rtk::FEAT_SET_FINAL &&
-                           S.n_lds_nodes == c->n_tlas_nodes && rtk::wavefront_fits(c->S, c->lds_per_block);
-
     // Schedule and buffer batches, from the context's trace-output bound (sample_buf_cap). The
     // bound is sized from the free HBM when the context is created; if the device has less by
     // now (another context, torch or RCCL allocated since), the allocation below fails and the
@@ -1482,11 +1395,9 @@ static int run_range(rt_ctx* c, const rt_camera* cam, const rt_render_params* p,
         // (the media variant, Cornell smoke 600x600x200: items 31.72 ms, per-sample buffer 30.28: pool)
         const bool cornell = variant == rtk::FEAT_SET_RECTINST;
         const bool fits_one = (size_t)total * sample_bytes <= buf_cap;
-        o.pool = wavefront ? RT_SCHED_WAVEFRONT
-                 : c->opt_pool != RT_SCHED_AUTO && c->opt_pool != RT_SCHED_WAVEFRONT
-                     ? c->opt_pool
-                     : cornell && !o.f32 ? RT_SCHED_ITEMS
-                     : (ring_ok || (size_t)total * sample_bytes <= 4 * buf_cap ? RT_SCHED_POOL : RT_SCHED_ITEMS);
+        o.pool = c->opt_pool != RT_SCHED_AUTO ? c->opt_pool
+                 : cornell && !o.f32 ? RT_SCHED_ITEMS
+                 : (ring_ok || (size_t)total * sample_bytes <= 4 * buf_cap ? RT_SCHED_POOL : RT_SCHED_ITEMS);
         // POOL with the in-kernel reduction: chunk partials like ITEMS (the ring takes its share of
         // the bound first, the partials at least one chunk)
         ring = o.pool == RT_SCHED_POOL && ring_ok && (c->opt_ring == 2 || !fits_one);
@@ -1504,12 +1415,11 @@ static int run_range(rt_ctx* c, const rt_camera* cam, const rt_render_params* p,
         // does not fit in one batch takes two buffers of half the bound: batch k traces into half
         // k & 1 on stream tstream[k & 1] while the caller's stream reduces batch k - 1, so the
         // next trace fills the CUs its predecessor's last waves leave (no tail per batch).
-        per_sample = (o.pool == RT_SCHED_POOL && !ring) || o.pool == RT_SCHED_WAVEFRONT;
+        per_sample = o.pool == RT_SCHED_POOL && !ring;
         const size_t unit = per_sample ? sample_bytes : px_bytes;
         long long fit = (long long)std::max<size_t>(1, out_cap / unit);
         batch = std::min<long long>(total, per_sample ? fit : fit * chunk);
-        // (the wavefront schedule's host loop enqueues one batch after the other)
-        overlap = c->opt_overlap && batch < total && o.pool != RT_SCHED_CHUNKS && o.pool != RT_SCHED_WAVEFRONT;
+        overlap = c->opt_overlap && batch < total && o.pool != RT_SCHED_CHUNKS;
         if (overlap) {
             fit = (long long)std::max<size_t>(1, out_cap / 2 / unit);
             batch = std::min<long long>(total, per_sample ? fit : fit * chunk);
@@ -1565,14 +1475,9 @@ static int run_range(rt_ctx* c, const rt_camera* cam, const rt_render_params* p,
         }
         HIP_TRY(hipMemsetAsync(c->tile_cost, 0, (size_t)img_tiles * sizeof(unsigned long long), stream));
         K.tile_cost = c->tile_cost;
-        // (the pool kernels count them; the chunk and wavefront schedules do not)
+        // (the pool kernels count them; the chunk schedule does not)
         c->tile_cost_n = o.pool == RT_SCHED_POOL || o.pool == RT_SCHED_ITEMS ? img_tiles : 0;
     }
-    if (wavefront) {
-        const int rc = wf_pool(c, stream, (long long)K.tiles_x * K.tiles_y * 64 * std::min<long long>(total, batch));
-        if (rc) return rc;
-    }
-    int wf_iterations = 0;
     int waves_per_simd = 0;
     o.waves_per_simd = &waves_per_simd;
     HIP_TRY(hipEventRecord(c->ev[0], stream));
@@ -1591,7 +1496,7 @@ static int run_range(rt_ctx* c, const rt_camera* cam, const rt_render_params* p,
         K.spp = b1;
         K.n_chunks = (b1 - b0 + chunk - 1) / chunk;
         {
-            const unsigned g = o.pool == RT_SCHED_ITEMS ? (unsigned)K.block_chunks : (unsigned)K.block_samples;   // (POOL, WAVEFRONT: samples)
+            const unsigned g = o.pool == RT_SCHED_ITEMS ? (unsigned)K.block_chunks : (unsigned)K.block_samples;   // (POOL: samples)
             const unsigned n = o.pool == RT_SCHED_ITEMS ? (unsigned)K.n_chunks : (unsigned)(K.spp - K.sample_begin);
             const unsigned n_groups = (n + g - 1) / std::max(g, 1u);
             K.n_work_blocks = (unsigned)K.tiles_x * (unsigned)K.tiles_y * n_groups;
@@ -1606,14 +1511,7 @@ static int run_range(rt_ctx* c, const rt_camera* cam, const rt_render_params* p,
         rtk::KParams* dK = c->params + c->param_slot;
         c->param_slot = (c->param_slot + 1) % kParamSlots;
         HIP_TRY(hipMemcpyAsync(dK, &K, sizeof K, hipMemcpyHostToDevice, ts));
-        if (o.pool == RT_SCHED_WAVEFRONT) {
-            rtk::WfHost host{c->wf_flag_host, {c->wf_ev[0], c->wf_ev[1]}, 0, 0};
-            HIP_TRY(rtk::launch_wavefront(S, K, dK, buf, c->work + h, c->wf, c->counters, count, host, ts));
-            wf_iterations += host.iterations;
-            waves_per_simd = host.waves_per_simd;
-        } else {
-            HIP_TRY(rtk::launch_trace(S, K, dK, buf, c->counters, c->work + h, o, ts));
-        }
+        HIP_TRY(rtk::launch_trace(S, K, dK, buf, c->counters, c->work + h, o, ts));
         if (bi == n_batches - 1) HIP_TRY(hipEventRecord(c->ev[1], ts));
         if (overlap) {   // reduce in batch order on `stream`, after this batch's trace
             HIP_TRY(hipEventRecord(c->ev_tr[h], ts));
@@ -1649,7 +1547,6 @@ static int run_range(rt_ctx* c, const rt_camera* cam, const rt_render_params* p,
                                                                : (size_t)((batch + chunk - 1) / chunk) * px_bytes)) +
                                c->stats.ring_bytes;
     c->stats.overlapped = overlap ? 1 : 0;
-    c->stats.wf_iterations = wf_iterations;
     c->stats.samples = (uint64_t)n_px * (uint64_t)total;
     c->stats.n_chunks = (int32_t)((total + chunk - 1) / chunk);
     c->stats.n_items = (uint64_t)n_px * (uint64_t)c->stats.n_chunks;
@@ -2101,14 +1998,6 @@ int rt_ctx_set_option(rt_ctx* c, int key, int64_t v)
         c->extra_features = (uint32_t)v;
         return RT_OK;
     case RT_OPT_HOIST: c->opt_hoist = v != 0; return RT_OK;
-    case RT_OPT_WF_PATHS:
-        if (v < 0 || v > ((int64_t)1 << 26)) return fail(RT_ERR_INVALID, "path slots out of range");
-        c->wf_paths = v;
-        return RT_OK;
-    case RT_OPT_WF_REFILL:
-        if (v < 0 || v > 64) return fail(RT_ERR_INVALID, "refill lanes out of range (0..64)");
-        c->wf_refill = (int)v;
-        return RT_OK;
     case RT_OPT_POOL_RING:
         if (v < 0 || v > 2) return fail(RT_ERR_INVALID, "pool ring mode out of range (0 never, 1 when needed, 2 always)");
         c->opt_ring = (int)v;
@@ -2127,8 +2016,6 @@ int rt_ctx_get_option(rt_ctx* c, int key, int64_t* v)
     case RT_OPT_BLOCK_CHUNKS: *v = c->block_chunks; return RT_OK;
     case RT_OPT_EXTRA_FEATURES: *v = c->extra_features; return RT_OK;
     case RT_OPT_HOIST: *v = c->opt_hoist; return RT_OK;
-    case RT_OPT_WF_PATHS: *v = c->wf_paths; return RT_OK;
-    case RT_OPT_WF_REFILL: *v = c->wf_refill; return RT_OK;
     case RT_OPT_POOL_RING: *v = c->opt_ring; return RT_OK;
     default: return fail(RT_ERR_INVALID, "unknown option");
     }
@@ -2136,7 +2023,9 @@ int rt_ctx_get_option(rt_ctx* c, int key, int64_t* v)
 
 int rt_ctx_set_schedule(rt_ctx* c, int schedule)
 {
-    if (!c || schedule < RT_SCHED_CHUNKS || schedule > RT_SCHED_WAVEFRONT) return fail(RT_ERR_INVALID, "bad schedule");
+    if (c && schedule == 4)   // the wavefront schedule of ABI v4 (rejected, scripts/experiments/r05_wavefront.patch)
+        return fail(RT_ERR_UNSUPPORTED, "schedule 4 (wavefront) was removed: 2.3x slower than the pool on C4 (DESIGN.md 5.7)");
+    if (!c || schedule < RT_SCHED_CHUNKS || schedule > RT_SCHED_AUTO) return fail(RT_ERR_INVALID, "bad schedule");
     c->opt_pool = schedule;
     return RT_OK;
 }

@@ -1183,7 +1183,7 @@ __device__ __forceinline__ void medium_finish(const rt_prim& m, const RayT<R>& r
 // The HitRecord of the closest hit (t, leaf slot, sub-primitive, box side) of a world-space ray:
 // the arithmetic of the winning primitive's hit (hittable.rs:254-384, 417-473) and of the
 // instance chain back to world space (hittable.rs:232-244, 386-415). Traversal keeps only the
-// reference; the record is built once per cast (trace_world; the wavefront schedule's logic step).
+// reference; the record is built once per cast (trace_world).
 template <class C, class R = typename C::Real>
 __device__ __forceinline__ void finish_hit(const SceneDev& S, const RayT<R>& r, const HitRefT<R>& best, HitT<R>& h)
 {

@@ -70,9 +70,7 @@ struct SceneDev {
     // nodes[n_tlas_nodes, n_tlas_nodes + n_blas_bfs) (abi.cpp), and a launch stages the first
     // n_lds_blas of them (its LDS budget): the nested walk's top levels then read LDS
     int32_t n_blas_bfs, n_lds_blas;
-    // the wavefront schedule's scenes (abi.cpp wf_scene_ok): the one instance over a BVH that a
-    // top-level walk can defer (its record is staged in LDS by wf_trace), or -1
-    int32_t defer_inst;
+    int32_t pad0;           // (unused: keeps the kernel-argument layout the kernels were timed with)
 };
 
 struct KParams {
@@ -97,7 +95,7 @@ struct KParams {
     int32_t tile_shard;         // rt_render_params.tile_shard: grid tile m = the frame's tile at position
                                 // row_begin + m*row_stride of tile_order (raster order if null)
     int32_t img_tiles_x;        // tiles per tile row of the image
-    int32_t wf_refill;          // wavefront schedule: a wf_trace wave refills once this many lanes are idle
+    int32_t pad0;               // (unused: keeps the fields below at the offsets the kernels were timed with)
     int32_t ring_waves;         // per-sample pool, in-kernel reduction: waves the ring holds (0: off)
     double* ring;               // per-sample pool, in-kernel reduction: kPoolRing blocks of records per wave
     // tile shards: the frame's tile order (rt_ctx_set_tile_order), position -> raster tile; null: raster
@@ -182,63 +180,12 @@ __host__ __device__ inline size_t tiled_pixels(int width, int n_rows)   // recor
     return (size_t)((width + 7) / 8) * (size_t)((n_rows + 7) / 8) * 64;
 }
 
-// ---- the wavefront schedule (RT_SCHED_WAVEFRONT, trace_wavefront.hip) ------------------------
-// A pool of P path slots in HBM, structure of arrays (component-major: x[0..P) y[..] z[..]), and
-// per iteration two launches: wf_logic (one thread per slot: the hit record of the slot's last
-// cast, emission / background, the material's draws and scattered ray, or a new (pixel, sample)
-// unit's camera ray; each wave appends its live slots to its 64-entry segment of the ray queue)
-// and wf_trace (a persistent grid whose lanes take rays from the queue segments and, when their
-// walk ends, the next ray at once: closest hit over the TLAS and the deferred instance BLAS in
-// one step loop). The per-(pixel, sample) arithmetic is the megakernel's, in the same order.
-constexpr int kWfShards = 8;         // trace-side segment counters (one per XCD of round-robin placement)
-constexpr int kWfFlags = 64;         // ring of per-iteration "any path live" flags the host polls
-struct WfPaths {
-    int32_t n;              // slots (a multiple of 2048: whole logic blocks per shard)
-    // per slot: the path's state between its casts
-    double* T;              // [3][n] path throughput
-    uint4* rng;             // [n] the path stream (rt_pstream)
-    int2* xk;               // [n] the unit's pixel on the shard grid
-    int32_t* st;            // [n] -1: no path; else the remaining depth (the slot's ray is queued)
-    uint32_t* qpos;         // [n] the slot's entry in the last iteration's queue
-    // the ray queue, two buffers (iteration parity): wave w of wf_logic writes its live rays to
-    // entries [64 w, 64 w + qn[w]) of this iteration's buffer, wf_trace reads them there and writes
-    // the hits beside them, and the next wf_logic reads both back (one dependent load per slot)
-    double* qo;             // [2][3][n] ray origin (world)
-    double* qd;             // [2][3][n] ray direction
-    double* qtime;          // [2][n] the path's shutter time (Ray::time, set by the camera)
-    uint4* qkey;            // [2][n] image pixel key, sample, bounce (the medium draws' key), -
-    double* ht;             // [2][n] closest hit t
-    int2* hp;               // [2][n] (leaf slot, sub << 3 | box side); x = -1: a miss
-    uint32_t* qn;           // [n / 64] live entries per segment
-    int4* wblk;             // [n / 64] per logic wave: current work block (b, next, units, exhausted)
-    unsigned* tctr;         // [kWfShards] trace segment counters (reset by every wf_logic)
-    int32_t* flag;          // [kWfFlags] iteration i: any slot live after its wf_logic
-};
-// bytes of one slot's arrays
-constexpr size_t kWfSlotBytes = 3 * 8 + 16 + 8 + 4 + 4 + 2 * (3 * 8 + 3 * 8 + 8 + 16 + 8 + 8);
-
 uint32_t variant_features(uint32_t scene_features);
 // Ph: host copy of the params (grid size); P: the same params in device memory
 // chunk schedule: out = chunk partials [n_chunks][n_px][3]; pool schedule: out = per-sample
 // radiance, tiled_record order over spp - sample_begin samples; work = one device counter
 hipError_t launch_trace(const SceneDev& S, const KParams& Ph, const KParams* P, double* out,
                         unsigned long long* counters, unsigned* work, const LaunchOpts& o, hipStream_t stream);
-// The wavefront schedule of one batch (samples [Ph.sample_begin, Ph.spp) of the shard) into the
-// per-sample buffer `out` (tiled_record order, as the per-sample pool): wf_logic / wf_trace
-// iterations enqueued on `stream` in chunks until an iteration leaves no path live (polled through
-// `flag_host`, pinned memory, and `ev`). S: the scene as uploaded; the launcher builds the two
-// kernels' LDS views. Returns hipErrorNotSupported if the scene does not fit the schedule.
-struct WfHost {
-    volatile int32_t* flag_host;   // pinned, 2 entries
-    hipEvent_t ev[2];
-    int iterations;                // out: iterations enqueued
-    int waves_per_simd;            // out: of the trace kernel
-};
-bool wavefront_fits(const SceneDev& S, size_t lds_per_block);
-hipError_t launch_wavefront(const SceneDev& S, const KParams& Ph, const KParams* P, double* out, unsigned* work,
-                            const WfPaths& W, unsigned long long* counters, bool count, WfHost& host,
-                            hipStream_t stream);
-
 // pool schedule: per pixel, chunk sums of its samples (sample order) added to 0.0, scaled to out
 // (out and the carried sums are in pixel order k * width + x)
 hipError_t launch_reduce_samples(const double* samples, void* out, bool f64, SampleTiles g, int n_samples,

@@ -36,7 +36,6 @@ RT_SCHED_CHUNKS = 0
 RT_SCHED_POOL = 1
 RT_SCHED_ITEMS = 2
 RT_SCHED_AUTO = 3
-RT_SCHED_WAVEFRONT = 4
 RT_PREC_F64 = 0
 RT_PREC_F32 = 1
 RT_ACCEL_SAH = 0
@@ -49,8 +48,6 @@ RT_OPT_BLOCK_SAMPLES = 3
 RT_OPT_BLOCK_CHUNKS = 4
 RT_OPT_EXTRA_FEATURES = 5
 RT_OPT_HOIST = 6
-RT_OPT_WF_PATHS = 7
-RT_OPT_WF_REFILL = 8
 RT_OPT_POOL_RING = 9
 # SAH builder options (rt_world_set_build_option)
 RT_BUILD_C_ISECT = 1
@@ -145,7 +142,7 @@ class Stats(ctypes.Structure):
                 ("wave_leaf_steps", ctypes.c_uint64), ("camera_lanes", ctypes.c_uint64),
                 ("camera_steps", ctypes.c_uint64), ("shade_lanes", ctypes.c_uint64),
                 ("shade_steps", ctypes.c_uint64), ("precision", ctypes.c_int32), ("waves_per_simd", ctypes.c_int32),
-                ("trace_buf_bytes", ctypes.c_int64), ("overlapped", ctypes.c_int32), ("wf_iterations", ctypes.c_int32),
+                ("trace_buf_bytes", ctypes.c_int64), ("overlapped", ctypes.c_int32), ("reserved0", ctypes.c_int32),
                 ("ring_bytes", ctypes.c_int64)]
 
     def as_dict(self):

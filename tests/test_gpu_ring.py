@@ -175,15 +175,20 @@ def test_context_options_round_trip_and_reject_bad_values(rt):
         assert r.get_option(rt.RT_OPT_POOL_RING) == 1          # default: the ring when needed
         assert r.get_option(rt.RT_OPT_TRACE_BUF_BYTES) <= 4 * GIB
         for key, val in ((rt.RT_OPT_POOL_RING, 2), (rt.RT_OPT_POOL_RING, 0), (rt.RT_OPT_BLOCK_SAMPLES, 8),
-                         (rt.RT_OPT_BLOCK_CHUNKS, 3), (rt.RT_OPT_BATCH_OVERLAP, 0), (rt.RT_OPT_WF_REFILL, 48),
-                         (rt.RT_OPT_WF_PATHS, 1 << 20), (rt.RT_OPT_TRACE_BUF_BYTES, 64 << 20)):
+                         (rt.RT_OPT_BLOCK_CHUNKS, 3), (rt.RT_OPT_BATCH_OVERLAP, 0),
+                         (rt.RT_OPT_TRACE_BUF_BYTES, 64 << 20)):
             r.set_option(key, val)
             assert r.get_option(key) == val, key
-        for key, val in ((rt.RT_OPT_POOL_RING, 3), (rt.RT_OPT_POOL_RING, -1), (rt.RT_OPT_WF_REFILL, 65), (999, 1)):
+        for key, val in ((rt.RT_OPT_POOL_RING, 3), (rt.RT_OPT_POOL_RING, -1), (7, 0), (8, 0), (999, 1)):
             with pytest.raises(rt.RTError):
                 r.set_option(key, val)
         with pytest.raises(rt.RTError):
             r.get_option(999)
+        # the removed wavefront schedule (ABI v4's 4) is refused as unsupported, not run as AUTO
+        with pytest.raises(rt.RTError, match="RT_ERR_UNSUPPORTED"):
+            r.set_schedule(4)
+        with pytest.raises(rt.RTError, match="RT_ERR_INVALID"):
+            r.set_schedule(5)
         r.set_option(rt.RT_OPT_TRACE_BUF_BYTES, 0)               # 0 restores the default
         assert 0 < r.get_option(rt.RT_OPT_TRACE_BUF_BYTES) <= 4 * GIB
     finally:
