@@ -2,11 +2,14 @@
 """Headline benchmark: Msamples/s (pixels x spp per second) on the 1200x800 random-spheres
 scene, 500 spp, max depth 50 (BASELINE.json configs[1] = SURVEY C2), at N GPUs.
 
-One step = one full render of the frame: every rank traces its shard through the HIP
-megakernel (C ABI, librtiow_amd.so) — at N > 1 the frame's 8x8 tiles t = rank + k*N
-(rt_render_params.tile_shard; --shard rows: rows y = rank + k*N) — and the shards are
-gathered to rank 0 over RCCL (torch.distributed "nccl") and put back in image order —
-inside the timed region. The scene is built and uploaded before timing.
+One step = one full render of the frame through the library's multi-GPU entry point,
+rt_render_gather (C ABI, librtiow_amd.so): every rank traces its 8x8 tile shard (the tiles at
+positions rank + k*N of the frame's tile order) through the HIP megakernel, the library's own
+RCCL communicator gathers the slabs to rank 0 and a reorder kernel writes the frame there —
+inside the timed region; at N = 1 the same call over a world-1 communicator. torch.distributed
+(gloo, on the host) only hands out the RCCL unique id and runs the barriers and the MAX
+all-reduce of the step time. The scene is built and uploaded, and the tile order's cost pass
+run, before timing; the cost pass's time is amortised into `value` (value_steady without).
 
 Prints ONE JSON line (rank 0). Besides the contract fields it carries
   roofline:     the binding resource, VALU issue: the issue cycles the launch's VALU
@@ -75,24 +78,29 @@ def parse():
     ap.add_argument("--no-count", action="store_true", help="skip the count_work pass (profiling runs)")
     ap.add_argument("--ppm", default="", help="write the rendered frame (rank 0) as a P3 PPM")
     ap.add_argument("--frame-npy", default="", help="save the rendered f64 frame (rank 0) as .npy")
+    ap.add_argument("--transport", default="rccl", choices=["rccl", "gloo", "none"],
+                    help="rccl (default, every N): the library's multi-GPU render, rt_render_gather — the rank's "
+                         "8x8 tile shard, one RCCL gather to rank 0 over the library's own communicator, the "
+                         "on-device reorder kernel (at N = 1 a world-1 communicator: the same code path); gloo: "
+                         "tile (or row) slabs staged through the host and gathered by torch.distributed gloo, so "
+                         "several ranks can share one GPU (tests of the N > 1 path on a 1-GPU box); none: N = 1 "
+                         "only, rt_render straight into the frame")
     ap.add_argument("--shard", default="tiles", choices=["tiles", "rows"],
-                    help="N > 1 partition: the frame's 8x8 tiles round-robin (rt_render_params.tile_shard) or "
-                         "single rows round-robin")
-    ap.add_argument("--tile-order", default="cost", choices=["raster", "cost"],
-                    help="N > 1 tile shards: cost (default: rank 0 times a count_work pass of --cost-spp "
-                         "samples per pixel before the timed steps, like the scene upload, and broadcasts "
-                         "the tiles sorted by cost; rt_ctx_set_tile_order, whose shards then deal their "
-                         "blocks tile-major: expensive tiles first and entirely) or raster")
+                    help="partition: the frame's 8x8 tiles round-robin (rt_render_params.tile_shard) or, with "
+                         "--transport gloo only, single rows round-robin")
+    ap.add_argument("--tile-order", default="auto", choices=["auto", "raster", "cost"],
+                    help="tile shards: cost (every rank counts its raster shard at --cost-spp samples per "
+                         "pixel, one all-reduce of the per-tile lane-cycles, the tiles sorted by cost: "
+                         "rt_comm_tile_order; shards then deal their blocks tile-major), raster, or auto "
+                         "(default: cost at N > 1, raster at N = 1). The pass runs before the timed steps and "
+                         "its time is amortised into the headline value (value_steady leaves it out)")
     ap.add_argument("--cost-spp", type=int, default=8, help="spp of the --tile-order cost pass")
-    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
-                    help="N > 1: nccl (RCCL over xGMI, the product) or gloo (host-staged slabs; lets several "
-                         "ranks share one GPU, for tests of this N > 1 path on a 1-GPU box)")
     ap.add_argument("--device", type=int, default=None,
-                    help="GPU index for every rank (default: LOCAL_RANK); with --dist-backend gloo, ranks may share one")
+                    help="GPU index for every rank (default: LOCAL_RANK); with --transport gloo, ranks may share one")
     ap.add_argument("--force-dist", action="store_true",
-                    help="take the distributed branch (process group, device gather of the shard slab, "
-                         "reassembly, barrier, MAX all-reduce) even at world size 1, so the RCCL path runs on a "
-                         "1-GPU box: launch as torch.distributed.run --nproc-per-node 1 ... --gpus 1 --force-dist")
+                    help="take the distributed branch (torch.distributed control plane, unique-id broadcast, "
+                         "barriers, MAX all-reduce) even at world size 1: launch as torch.distributed.run "
+                         "--nproc-per-node 1 ... --gpus 1 --force-dist")
     ap.add_argument("--precision", default="f64", choices=["f64", "f32"],
                     help="f64: the reference's arithmetic (the headline); f32: the fast mode (SURVEY §8 f3)")
     ap.add_argument("--schedule", default="auto", choices=sorted(SCHEDULES),
@@ -210,21 +218,28 @@ def main():
     if world != args.gpus:
         if world == 1 and args.gpus > 1:
             raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run (one rank per GPU)")
-    # the distributed branch: N > 1, or N = 1 under --force-dist (the RCCL code path on one GPU)
+    # the distributed branch: N > 1, or N = 1 under --force-dist
     dist_on = world > 1 or args.force_dist
     if args.force_dist and "MASTER_ADDR" not in os.environ:
         raise SystemExit("--force-dist needs torch.distributed.run (MASTER_ADDR / RANK / WORLD_SIZE in the env)")
-    gloo = dist_on and args.dist_backend == "gloo"
+    transport = args.transport
+    gloo = transport == "gloo"
+    if transport == "none" and world > 1:
+        raise SystemExit("--transport none is the one-GPU path")
+    if gloo and not dist_on:
+        raise SystemExit("--transport gloo needs torch.distributed.run")
+    if args.shard == "rows" and not gloo:
+        raise SystemExit("--shard rows needs --transport gloo (rt_render_gather deals 8x8 tiles)")
     if args.device is not None:
         if world > 1 and not gloo:
-            raise SystemExit("--device with N > 1 needs --dist-backend gloo (RCCL needs one GPU per rank)")
+            raise SystemExit("--device with N > 1 needs --transport gloo (RCCL needs one GPU per rank)")
         local = args.device
     torch.cuda.set_device(local)
     if dist_on:
-        if gloo:
-            dist.init_process_group("gloo")
-        else:
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        # torch.distributed is the control plane only (the unique-id broadcast, barriers, the MAX
+        # all-reduce of the step time), on the host; with --transport rccl every frame byte moves
+        # through the library's own RCCL communicator (rt_render_gather)
+        dist.init_process_group("gloo")
     device = torch.device("cuda", local)
 
     import __graft_entry__ as ge
@@ -244,99 +259,137 @@ def main():
         renderer.set_option(rt.RT_OPT_TRACE_BUF_BYTES, args.buf_mb << 20)
     if args.no_overlap:
         renderer.set_option(rt.RT_OPT_BATCH_OVERLAP, 0)
+    comm = None
+    if transport == "rccl":   # rank 0 makes the RCCL unique id, torch (gloo) hands it to the others
+        uid = [rt.Comm.unique_id() if rank == 0 else None]
+        if dist_on:
+            dist.broadcast_object_list(uid, src=0)
+        comm = rt.Comm(renderer, rank, world, uid[0])
     t_build = time.perf_counter() - t_build
 
-    # N > 1: ranks take the frame's 8x8 tiles round-robin (tile shards: every work tile stays a
-    # compact 8x8 block of the image and every rank gets the same tile count to within one).
-    # Rank 0's C2 shard at N = 8 runs at 6,202 Msamples/s in 8x8 tiles against 5,993 as single
-    # rows 8 apart (8-row bands, the other compact layout, leave 13 vs 12 bands per rank;
-    # scripts/shard_coherence.py, profiles/r03u_shard.log). --shard rows keeps the row partition.
-    tiles = dist_on and args.shard == "tiles"
+    def progress(msg):   # stderr, one line per step: long configs (C5) keep the run visibly alive
+        if rank == 0:
+            print(f"bench: {msg}", file=sys.stderr, flush=True)
+
+    def max_over_ranks(x):
+        if not dist_on:
+            return x
+        t = torch.tensor([x], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    # Ranks take the frame's 8x8 tiles round-robin (tile shards: every work tile stays a compact
+    # 8x8 block of the image and every rank gets the same tile count to within one). Rank 0's C2
+    # shard at N = 8 runs at 6,202 Msamples/s in 8x8 tiles against 5,993 as single rows 8 apart
+    # (scripts/shard_coherence.py, profiles/r03u_shard.log). --shard rows keeps the row partition.
+    tiles = transport != "none" and args.shard == "tiles"
     if tiles:
         n_mine = rt.tiles_in_shard(W, H, rank, world)
         n_max = max(rt.tiles_in_shard(W, H, r, world) for r in range(world))
         px_mine, slab_shape = 64 * n_mine, (8, 8 * n_max, 3)
-    else:
+    elif gloo:
         rows = rt.rows_in_shard(H, rank, world, ROW_BLOCK)
         rows_max = max(rt.rows_in_shard(H, r, world, ROW_BLOCK) for r in range(world))
         px_mine, slab_shape = rows * W, (rows_max, W, 3)
-    # --tile-order cost: the tiles sorted by the lane-cycles of a count_work pass, most expensive
-    # first, dealt round-robin. Rank 0 measures (lane-cycles differ from run to
-    # run, so one rank decides) and broadcasts the order before the timed steps, like the upload.
-    tile_order, t_order = None, 0.0
-    if tiles and args.tile_order == "cost":
+    else:
+        px_mine, slab_shape = W * H, None
+    frame_params = rt.Renderer.params(W, H, spp, depth, bg, args.seed, spp_chunk=args.spp_chunk,
+                                      out_format=rt.RT_OUT_F64)
+    # Tile order: cost = the tiles sorted by the lane-cycles of a count_work pass, most
+    # expensive first, dealt round-robin. Every rank counts its own raster shard (1/N of a cost_spp
+    # frame), one all-reduce sums the per-tile costs, and every rank sorts the same vector
+    # (rt_comm_tile_order: RCCL, in the library; --transport gloo: the same steps over gloo here).
+    # The pass is setup like the upload but not free: its time is amortised into `value`.
+    order_mode = args.tile_order if args.tile_order != "auto" else ("cost" if world > 1 else "raster")
+    tile_order, t_order, gloo_order = None, 0.0, None
+    if tiles and order_mode == "cost":
         t0 = time.perf_counter()
-        n_img_tiles = ((W + 7) // 8) * ((H + 7) // 8)
-        obuf = torch.zeros(n_img_tiles, dtype=torch.int64, device="cpu" if gloo else device)
-        if rank == 0:
-            renderer.render(cam, rt.Renderer.params(W, H, args.cost_spp, depth, bg, args.seed, out_format=rt.RT_OUT_F32,
-                                                    count_work=1))
-            obuf.copy_(torch.from_numpy(rt.cost_tile_order(renderer.tile_costs()).astype(np.int64)))
-        dist.broadcast(obuf, src=0)
-        tile_order = obuf.cpu().numpy()
-        renderer.set_tile_order(tile_order)
-        t_order = time.perf_counter() - t0
-    # the render writes its shard contiguously at the start of the slab (a tile shard's 8 x 8n
-    # layout is then a prefix of the padded 8 x 8n_max buffer, read back with the same view)
-    # f64 output (sum * (1/spp), the reference's `self.x * scale`, math.rs:120-125): the frame the
-    # PPM writer turns into the reference's bytes (rt_write_ppm_f64); 23 MB for C2
-    slab = torch.zeros(slab_shape, dtype=torch.float64, device=device)
-    # gloo gathers host copies of the slabs (staged through pinned memory), RCCL device slabs
-    stage = torch.empty(slab.shape, dtype=slab.dtype, pin_memory=True) if gloo else None
-    gathered = ([torch.empty_like(stage if gloo else slab) for _ in range(world)]
-                if (dist_on and rank == 0) else None)
+        if comm is not None:
+            try:   # a failed pass leaves every rank in raster order (RT_ERR_PEER on the others)
+                comm.tile_order(cam, rt.Renderer.params(W, H, spp, depth, bg, args.seed), args.cost_spp)
+            except rt.RTError as e:
+                progress(f"tile-order cost pass failed, raster order: {e}")
+        else:   # gloo: f64 and a pool schedule for the count (the chunk schedule counts no tile costs)
+            n_img_tiles = ((W + 7) // 8) * ((H + 7) // 8)
+            costs, ok = np.zeros(n_img_tiles, dtype=np.int64), 1
+            try:
+                renderer.set_tile_order(None)
+                renderer.set_precision(rt.RT_PREC_F64)
+                renderer.set_schedule(rt.RT_SCHED_POOL if args.schedule == "chunks" else SCHEDULES[args.schedule])
+                renderer.render(cam, rt.Renderer.params(W, H, args.cost_spp, depth, bg, args.seed, row_begin=rank,
+                                                        row_stride=world, tile_shard=1, count_work=1))
+                c = renderer.tile_costs()
+                if len(c) == n_img_tiles:
+                    costs[:] = c.astype(np.int64)
+                else:
+                    ok = 0
+            except rt.RTError:
+                ok = 0
+            finally:
+                renderer.set_precision(rt.RT_PREC_F32 if f32 else rt.RT_PREC_F64)
+                renderer.set_schedule(SCHEDULES[args.schedule])
+            v = torch.from_numpy(np.concatenate([costs if ok else np.zeros_like(costs), [1 - ok]]))
+            dist.all_reduce(v)   # every rank takes part, failed or not: no rank waits forever
+            if int(v[-1]) == 0:
+                gloo_order = rt.cost_tile_order(v[:-1].numpy().astype(np.uint64))
+                renderer.set_tile_order(gloo_order)
+            else:
+                order_mode = "raster (cost pass failed on %d rank(s))" % int(v[-1])
+        st = comm.stats() if comm is not None else None
+        if st is not None and not st.tile_order:
+            order_mode = "raster (cost pass failed)"
+        tile_order = order_mode
+        t_order = max_over_ranks(time.perf_counter() - t0)
     frame = torch.empty((H, W, 3), dtype=torch.float64, device=device) if rank == 0 else None
-    # A stream of our own: torch's default stream has the null handle, which the C ABI reads
-    # as "the context's stream" (a non-blocking stream the default stream does not wait
-    # for), so the frame copy / RCCL gather would not be ordered after the render. Every
-    # op of a step runs under this stream; NCCL orders its gather after it.
+    # gloo: the render writes its shard contiguously at the start of a slab padded to the largest
+    # shard (a tile shard's 8 x 8n layout is then a prefix of the 8 x 8n_max buffer), staged through
+    # pinned host memory and gathered by gloo; rank 0 puts the slabs back in image order
+    slab = torch.zeros(slab_shape, dtype=torch.float64, device=device) if gloo else None
+    stage = torch.empty(slab.shape, dtype=slab.dtype, pin_memory=True) if gloo else None
+    gathered = [torch.empty_like(stage) for _ in range(world)] if (gloo and rank == 0) else None
+    # A stream of our own: torch's default stream has the null handle, which the C ABI reads as
+    # "the context's stream" (a non-blocking stream the default stream does not wait for), so a
+    # torch op on the frame would not be ordered after the render. Every op of a step runs on it.
     stream = torch.cuda.Stream(device)
-    params = rt.Renderer.params(W, H, spp, depth, bg, args.seed, row_begin=rank, row_stride=world,
-                                spp_chunk=args.spp_chunk, out_format=rt.RT_OUT_F64,
-                                row_block=1 if tiles else ROW_BLOCK, tile_shard=int(tiles))
+    shard_params = rt.Renderer.params(W, H, spp, depth, bg, args.seed, row_begin=rank, row_stride=world,
+                                      spp_chunk=args.spp_chunk, out_format=rt.RT_OUT_F64,
+                                      row_block=1 if tiles else ROW_BLOCK, tile_shard=int(tiles))
 
     def assemble(slabs):
         if tiles:
             views = [g.reshape(-1)[: 3 * 64 * rt.tiles_in_shard(W, H, r, world)].view(8, -1, 3)
                      for r, g in enumerate(slabs)]
-            rt.assemble_tiles(views, W, H, world, out=frame, order=tile_order)
+            rt.assemble_tiles(views, W, H, world, out=frame, order=gloo_order)
         else:
             rt.assemble_rows(slabs, H, world, out=frame, row_block=ROW_BLOCK)
-    kernel_ms = []
-    gather_ev = []    # (before, after) events on `stream` around the RCCL gather of each timed step
-    gather_host_ms = []
+    kernel_ms, gather_ms, render_ms = [], [], []
 
     def step(timed=False):
         with torch.cuda.stream(stream):
-            renderer.render_device(cam, params, slab.data_ptr(), stream.cuda_stream)
-            if gloo:
+            if comm is not None:   # the product path at every N: rt_render_gather
+                comm.render_gather_device(cam, frame_params, frame.data_ptr() if rank == 0 else None,
+                                          stream.cuda_stream)
+            elif gloo:
+                renderer.render_device(cam, shard_params, slab.data_ptr(), stream.cuda_stream)
                 stage.copy_(slab, non_blocking=True)
                 stream.synchronize()
                 tg = time.perf_counter()
                 dist.gather(stage, gathered if rank == 0 else None, dst=0)
                 if timed:
-                    gather_host_ms.append((time.perf_counter() - tg) * 1e3)
+                    gather_ms.append((time.perf_counter() - tg) * 1e3)
                 if rank == 0:
                     assemble([g.to(device, non_blocking=True) for g in gathered])
-            elif dist_on:
-                # the events bracket the gather on the render's stream: from the end of this rank's
-                # render to the gather's completion (the wait for slower ranks included)
-                e0 = torch.cuda.Event(enable_timing=True) if timed else None
-                e1 = torch.cuda.Event(enable_timing=True) if timed else None
-                if timed:
-                    e0.record(stream)
-                dist.gather(slab, gathered if rank == 0 else None, dst=0)
-                if timed:
-                    e1.record(stream)
-                    gather_ev.append((e0, e1))
-                if rank == 0:
-                    assemble(gathered)
             else:
-                frame[:] = slab[:H]
+                renderer.render_device(cam, frame_params, frame.data_ptr(), stream.cuda_stream)
 
-    def progress(msg):   # stderr, one line per step: long configs (C5) keep the run visibly alive
-        if rank == 0:
-            print(f"bench: {msg}", file=sys.stderr, flush=True)
+    def record():   # after the step's synchronize: HIP-event times of this rank's step
+        if comm is not None:
+            cs = comm.stats()
+            kernel_ms.append(cs.kernel_ms)
+            gather_ms.append(cs.gather_ms)
+            render_ms.append(cs.render_ms)
+        else:
+            kernel_ms.append(renderer.stats().kernel_ms)   # HIP events around the trace kernel on `stream`
 
     for i in range(args.warmup):
         step()
@@ -350,28 +403,26 @@ def main():
     step_ends = []
     for i in range(args.steps):
         step(timed=True)
-        kernel_ms.append(renderer.stats().kernel_ms)   # HIP events around the trace kernel on `stream`
         torch.cuda.synchronize(device)
         step_ends.append(time.perf_counter())
+        record()
         progress(f"step {i + 1}/{args.steps}: kernel {kernel_ms[-1]:.1f} ms")
     torch.cuda.synchronize(device)
     if dist_on:
         dist.barrier()
     torch.cuda.synchronize(device)
-    elapsed = time.perf_counter() - t0
+    elapsed = max_over_ranks(time.perf_counter() - t0)
     per_rank = None
     if dist_on:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if gloo else device)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        # per-rank kernel and gather times, so a multi-GPU line says where its time went
-        g_ms = ([a.elapsed_time(b) for a, b in gather_ev] if not gloo else gather_host_ms) or [float("nan")]
-        mine = torch.tensor([float(np.mean(kernel_ms)) if kernel_ms else float("nan"), float(np.mean(g_ms)),
-                             float(px_mine * spp)], dtype=torch.float64, device="cpu" if gloo else device)
+        # per-rank kernel, render and gather times, so a multi-GPU line says where its time went
+        mine = torch.tensor([float(np.mean(kernel_ms)) if kernel_ms else float("nan"),
+                             float(np.mean(gather_ms)) if gather_ms else float("nan"),
+                             float(np.mean(render_ms)) if render_ms else float("nan"),
+                             float(px_mine * spp)], dtype=torch.float64)
         allr = [torch.empty_like(mine) for _ in range(world)]
         dist.all_gather(allr, mine)
         per_rank = [{"rank": r, "kernel_ms": round(float(v[0]), 3), "gather_ms": round(float(v[1]), 3),
-                     "samples": int(v[2])} for r, v in enumerate(a.cpu() for a in allr)]
+                     "render_ms": round(float(v[2]), 3), "samples": int(v[3])} for r, v in enumerate(allr)]
     last = renderer.stats()
 
     samples_per_step = W * H * spp
@@ -541,14 +592,20 @@ def main():
             "vs_baseline": None,
             "dtype": args.precision,
             "data": "synthetic (seeded scene builders, scene_seed=render_seed=%d)" % args.seed,
+            "value_steady": round(value_steady, 3),
+            "value_basis": ("timed steps + the tile-order cost pass (%.3f s) amortised over them; value_steady: "
+                            "the timed steps alone" % t_order) if t_order > 0 else "timed steps (no cost pass)",
             "config": {"workload": "%s %s %dx%d, %d spp, max depth %d, %s-sharded over %d GPU"
                                    % (args.config, SCENE_NAMES.get(args.scene, "scene %d" % args.scene), W, H, spp,
-                                      depth, "tile" if tiles else "row", world),
+                                      depth, "tile" if tiles else "row" if gloo else "not", world),
                        "scene": args.scene, "width": W, "height": H, "spp": spp, "max_depth": depth,
-                       "tile_order": args.tile_order if tiles else None,
-                       "parallelism": "%s interleaved over %d rank(s), %s gather"
-                                      % (("8x8 tiles (%s order)" % args.tile_order) if tiles else "rows", world,
-                                         "gloo (host-staged)" if gloo else "RCCL" if dist_on else "no")},
+                       "tile_order": order_mode if tiles else None,
+                       "parallelism": "%s interleaved over %d rank(s), %s"
+                                      % (("8x8 tiles (%s order)" % order_mode) if tiles else
+                                         "rows" if gloo else "whole frame", world,
+                                         "gloo gather (host-staged)" if gloo else
+                                         "RCCL gather (library communicator, rt_render_gather)" if comm is not None
+                                         else "no gather")},
             "roofline": roofline,
             "cpu_baseline": cpu,
             "parity": parity,
@@ -562,11 +619,14 @@ def main():
                        "trace_buf_bytes": int(last.trace_buf_bytes), "batches_overlapped": bool(last.overlapped),
                        "scene_bytes": int(last.scene_bytes), "scene_build_upload_s": round(t_build, 3),
                        "tile_order_pass_s": round(t_order, 3) if tile_order is not None else None,
+                       "render_ms_mean": round(float(np.mean(render_ms)), 3) if render_ms else None,
+                       "gather_ms_mean": round(float(np.mean(gather_ms)), 3) if gather_ms else None,
                        "algorithmic_bytes_survey_8d": alg},
         }
         if per_rank is not None:
             out["per_rank"] = per_rank
-            out["distributed"] = {"backend": "gloo" if gloo else "nccl (RCCL)", "world_size": world,
+            out["distributed"] = {"transport": "gloo (host-staged)" if gloo else "RCCL (library communicator)",
+                                  "control_plane": "torch.distributed gloo", "world_size": world,
                                   "forced_at_world_1": bool(args.force_dist and world == 1)}
         print(json.dumps(out), flush=True)
     if dist_on:

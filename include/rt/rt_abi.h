@@ -23,6 +23,9 @@
  *   rt_accum_* /              the per-thread partial sums, their merge into the shared
  *   rt_render_progressive     buffer and the progress channel (main.rs:504-582), as
  *                             resumable sample batches with a progress callback
+ *   rt_comm_* /               the partition of one frame over workers (main.rs:497-551)
+ *   rt_render_gather          and the merge of their buffers (main.rs:542-547), over GPUs:
+ *                             8x8 tile shards, one RCCL gather to rank 0, a reorder kernel
  *
  * Threading: a context is bound to one device and is used by one host thread at
  * a time. Worlds are plain host objects.
@@ -39,7 +42,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 4
+#define RT_ABI_VERSION 5
 
 enum {
     RT_OK = 0,
@@ -48,7 +51,9 @@ enum {
     RT_ERR_UNSUPPORTED = -3,  /* a Hittable nesting the flattener does not lower */
     RT_ERR_OOM = -4,
     RT_ERR_NO_DEVICE = -5,
-    RT_ERR_NO_SCENE = -6      /* render before upload */
+    RT_ERR_NO_SCENE = -6,     /* render before upload */
+    RT_ERR_COMM = -7,         /* an RCCL call failed, or RCCL could not be loaded (see rt_last_error) */
+    RT_ERR_PEER = -8          /* a collective call failed on another rank; this rank's state is consistent */
 };
 
 typedef struct rt_ctx rt_ctx;
@@ -270,6 +275,88 @@ int rt_last_tile_costs(rt_ctx* ctx, uint64_t* out, int64_t n);
  * expensive tiles). Only which pixels a shard renders, and when, changes, not their bits.
  * n = 0: raster order again (the default). Waits for the device. */
 int rt_ctx_set_tile_order(rt_ctx* ctx, const uint32_t* order, int64_t n);
+
+/* ---- multi-GPU render: tile shards, one RCCL gather, on-device reassembly (ABI v5) ------------
+ * The reference splits one frame over 10 threads (main.rs:497-551: every thread all pixels,
+ * spp/10 samples) and merges their buffers under a mutex (main.rs:542-547). Here a frame is split
+ * over GPUs by 8x8 tiles: rank r of `world` renders the tiles at positions r, r + world, ... of the
+ * frame's tile order (rt_render_params.tile_shard), RCCL gathers every rank's slab to rank 0 over
+ * xGMI in one collective, and a reorder kernel on rank 0 writes the frame. Every draw is keyed by
+ * (pixel, sample), so the frame is bit-identical to rt_render's at any world size and tile order.
+ *
+ * A communicator binds one context (one device) to one rank. Two ways to make them:
+ *   one process per GPU:     rank 0 calls rt_comm_unique_id and sends the 128 bytes to the other
+ *                            ranks (any channel: MPI, a socket, torch.distributed); every rank then
+ *                            calls rt_comm_init_rank with its own context (ncclCommInitRank);
+ *   one process, N GPUs:     rt_comm_init_all over N contexts on N distinct devices
+ *                            (ncclCommInitAll), then the *_all calls drive every rank from one
+ *                            host thread (RCCL group calls).
+ * RCCL (librccl.so.1) is loaded when the first communicator is made; the rest of the library does
+ * not need it. Collective calls (rt_comm_tile_order, rt_render_gather) must be made by every rank
+ * of the communicator with the same camera and frame parameters. */
+typedef struct rt_comm rt_comm;
+enum { RT_COMM_ID_BYTES = 128 };   /* ncclUniqueId */
+int rt_comm_unique_id(uint8_t id[RT_COMM_ID_BYTES]);
+int rt_comm_init_rank(rt_ctx* ctx, int rank, int world, const uint8_t id[RT_COMM_ID_BYTES], rt_comm** out);
+int rt_comm_init_all(rt_ctx* const* ctxs, int n, rt_comm** comms_out);
+/* Destroys the RCCL communicator (after the rank's enqueued work is done); the context stays. */
+void rt_comm_destroy(rt_comm* comm);
+int rt_comm_rank(const rt_comm* comm, int* rank, int* world);
+
+/* Collective: the cost-ordered tile deal (rt_ctx_set_tile_order) on every rank. Each rank renders
+ * its raster-order tile shard of the frame p describes (its shard fields are ignored) at cost_spp
+ * samples per pixel with count_work — f64 and a pool schedule, whatever the context is set to —
+ * one RCCL all-reduce sums the per-tile lane-cycles (each tile counted by one rank), and every
+ * rank sets the same order, rt_cost_tile_order's, on its context. A rank whose pass fails (and,
+ * with RT_ERR_PEER, every other rank) falls back to raster order. The cost pass is 1/world of a
+ * cost_spp frame per rank. */
+int rt_comm_tile_order(rt_comm* comm, const rt_camera* cam, const rt_render_params* p, int cost_spp);
+int rt_comm_tile_order_all(rt_comm* const* comms, int n, const rt_camera* cam, const rt_render_params* p,
+                           int cost_spp);
+
+/* Collective: one frame over the communicator's ranks. p describes the whole frame (its shard
+ * fields row_begin / row_stride / row_block / tile_shard are ignored: rank r renders the tile
+ * shard r of `world` in the context's tile order). Rank 0 receives the frame (height x width x 3
+ * of p->out_format, row 0 = bottom), as rt_render's: on the device if p->out_on_device (the work
+ * is then only enqueued on p->stream or the context's stream), else in host memory (synchronous).
+ * Other ranks ignore `frame` (may be NULL) and, without out_on_device, return once their slab
+ * has been sent. */
+int rt_render_gather(rt_comm* comm, const rt_camera* cam, const rt_render_params* p, void* frame);
+/* The same for the n ranks of one process (rt_comm_init_all; comms[i] is rank i): every rank's
+ * render is enqueued on its context's stream, then the n gathers as one RCCL group. p->stream must
+ * be NULL; with out_on_device, frame is a device pointer on comms[0]'s device. */
+int rt_render_gather_all(rt_comm* const* comms, int n, const rt_camera* cam, const rt_render_params* p,
+                         void* frame);
+
+typedef struct rt_comm_stats {
+    double render_ms;     /* last rt_render_gather: this rank's shard render (HIP events on its stream) */
+    double gather_ms;     /* its RCCL gather: from the end of its render to the gather's end (includes the
+                             wait for slower ranks) */
+    double assemble_ms;   /* rank 0: the reorder kernel */
+    double kernel_ms;     /* the trace kernel's part of render_ms (rt_stats.kernel_ms) */
+    int64_t slab_bytes;   /* bytes each rank sent (its slab, padded to the largest shard) */
+    int32_t tiles;        /* this rank's tiles */
+    int32_t tile_order;   /* 1: a cost order was set by the last rt_comm_tile_order; 0: raster */
+    double cost_pass_ms;  /* last rt_comm_tile_order on this rank: wall time of the count pass + all-reduce */
+    int32_t peer_failed;  /* rank 0: ranks whose shard render failed in the last gather (their status words,
+                             sent with the slabs; a host-bound rt_render_gather returns RT_ERR_PEER then) */
+} rt_comm_stats;
+int rt_comm_last_stats(rt_comm* comm, rt_comm_stats* out);
+
+/* The reorder kernel alone, for callers with their own transport: `world` tile slabs at
+ * `slabs` (device memory of ctx's device, rank r's at r * slab_elems elements; slab_elems >=
+ * 8 * 8 * rt_tiles_in_shard(width, height, 0, world) * 3) -> frame (device, height x width x 3) of
+ * p->out_format for the frame p describes, in ctx's tile order. Enqueued on p->stream (or the
+ * context's stream). */
+int rt_tiles_assemble(rt_ctx* ctx, const void* slabs, int64_t slab_elems, int world, const rt_render_params* p,
+                      void* frame);
+/* The same on the host (no device): elem_bytes 4 (f32) or 8 (f64), order NULL (raster) or the
+ * n-tile permutation rt_ctx_set_tile_order takes. */
+int rt_tiles_assemble_host(const void* slabs, int64_t slab_elems, int world, int width, int height, int elem_bytes,
+                           const uint32_t* order, void* frame);
+/* The cost order from per-tile costs (rt_last_tile_costs): raster tiles sorted by cost, most
+ * expensive first, ties in raster order. Host only. */
+int rt_cost_tile_order(const uint64_t* costs, int64_t n, uint32_t* order);
 
 /* ---- progressive / resumable accumulation ------------------------------------ */
 /* A device f64 running sum per pixel of one row shard. Batches render consecutive sample

@@ -17,6 +17,7 @@
 #include <vector>
 
 #include "rt/rt_abi.h"
+#include "ctx_internal.hpp"
 #include "scene_model.hpp"
 #include "trace_kernel.hpp"
 
@@ -2050,3 +2051,18 @@ int rt_device_eval(rt_ctx* c, int fn, const double* x, const double* y, const do
 }
 
 }  // extern "C"
+
+// ---- what comm.cpp reads of a context (ctx_internal.hpp) ---------------------------------------
+namespace rtx {
+int fail(int code, const std::string& msg) { return ::fail(code, msg); }
+int hip_fail(hipError_t e, const char* what) { return ::hip_fail(e, what); }
+int ctx_device(const rt_ctx* c) { return c->device; }
+hipStream_t ctx_stream(const rt_ctx* c) { return c->stream; }
+const uint32_t* ctx_tile_order(const rt_ctx* c, int64_t* n)
+{
+    *n = c->tile_order_n;
+    return c->tile_order;
+}
+int ctx_schedule(const rt_ctx* c) { return c->opt_pool; }
+int ctx_precision(const rt_ctx* c) { return c->opt_precision; }
+}  // namespace rtx

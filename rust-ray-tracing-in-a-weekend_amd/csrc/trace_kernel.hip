@@ -134,6 +134,39 @@ __global__ void __launch_bounds__(256) accumulate_chunks(const double* __restric
     acc[3 * i + 2] = b;
 }
 
+// Multi-GPU reassembly (rt_tiles_assemble, rt_render_gather; the merge of main.rs:542-547): the
+// gathered tile slabs of `world` ranks, rank r's at r * slab_elems (8 rows x 8 * n_r tiles x 3,
+// its tiles m at positions r + m * world of the tile order), written into the frame (row 0 =
+// bottom). One thread per slab pixel: 8 consecutive threads read one tile row's 24 contiguous
+// elements and write them to one frame row; pixels of an edge tile outside the image are dropped.
+template <typename T>
+__global__ void __launch_bounds__(256) assemble_tiles(const T* __restrict__ gathered, T* __restrict__ frame,
+                                                      int world, long long slab_elems, int n_max, int width,
+                                                      int height, int tiles_x, long long n_tiles,
+                                                      const uint32_t* __restrict__ order)
+{
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;   // (rank, row k, column)
+    const long long per_rank = 64LL * n_max;
+    if (i >= per_rank * world) return;
+    const int r = (int)(i / per_rank);
+    const long long j = i - (long long)r * per_rank;
+    const int n_r = (int)((n_tiles - r + world - 1) / world);   // rt_tiles_in_shard
+    const int k = (int)(j / (8LL * n_max));
+    const int col = (int)(j - (long long)k * 8 * n_max);
+    const int m = col >> 3;
+    if (m >= n_r) return;
+    const long long pos = r + (long long)m * world;
+    const long long t = order ? (long long)order[pos] : pos;
+    const int x = (int)(t % tiles_x) * 8 + (col & 7);
+    const int y = (int)(t / tiles_x) * 8 + k;
+    if (x >= width || y >= height) return;
+    const T* src = gathered + (long long)r * slab_elems + ((long long)k * 8 * n_r + col) * 3;
+    T* dst = frame + ((long long)y * width + x) * 3;
+    dst[0] = src[0];
+    dst[1] = src[1];
+    dst[2] = src[2];
+}
+
 struct StoredUV {   // hit_uv's config for the eval kernel: uv inputs held in the record
     static constexpr uint32_t F = FEAT_ALL;
 };
@@ -279,6 +312,25 @@ hipError_t launch_accumulate(const double* partial, double* acc, long long n_px,
     const long long blocks = (n_px + 255) / 256;
     if (blocks <= 0) return hipSuccess;
     hipLaunchKernelGGL(accumulate_chunks, dim3((unsigned)blocks), dim3(256), 0, stream, partial, acc, n_px, n_chunks);
+    return hipGetLastError();
+}
+
+hipError_t launch_assemble_tiles(const void* gathered, void* frame, bool f64, int world, long long slab_elems,
+                                 int width, int height, const uint32_t* order, hipStream_t stream)
+{
+    const int tiles_x = (width + 7) / 8;
+    const long long n_tiles = (long long)tiles_x * ((height + 7) / 8);
+    const int n_max = (int)((n_tiles + world - 1) / world);
+    const long long n = 64LL * n_max * world;
+    const long long blocks = (n + 255) / 256;
+    if (blocks <= 0) return hipSuccess;
+    if (blocks > 0x7fffffffLL || slab_elems < 192LL * n_max) return hipErrorInvalidValue;
+    if (f64)
+        hipLaunchKernelGGL(assemble_tiles<double>, dim3((unsigned)blocks), dim3(256), 0, stream, (const double*)gathered,
+                           (double*)frame, world, slab_elems, n_max, width, height, tiles_x, n_tiles, order);
+    else
+        hipLaunchKernelGGL(assemble_tiles<float>, dim3((unsigned)blocks), dim3(256), 0, stream, (const float*)gathered,
+                           (float*)frame, world, slab_elems, n_max, width, height, tiles_x, n_tiles, order);
     return hipGetLastError();
 }
 

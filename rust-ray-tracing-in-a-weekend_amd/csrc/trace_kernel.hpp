@@ -198,6 +198,10 @@ hipError_t launch_reduce(const double* partial, void* out, bool f64, long long n
                          hipStream_t stream);
 // acc[i] += chunk partials in chunk order (progressive accumulation, rt_accum_add)
 hipError_t launch_accumulate(const double* partial, double* acc, long long n_px, int n_chunks, hipStream_t stream);
+// tile shards gathered from `world` ranks (rank r's slab at r * slab_elems elements) -> the frame
+// (height x width x 3, row 0 = bottom) in the tile order `order` (null: raster); rt_tiles_assemble
+hipError_t launch_assemble_tiles(const void* gathered, void* frame, bool f64, int world, long long slab_elems,
+                                 int width, int height, const uint32_t* order, hipStream_t stream);
 hipError_t launch_eval(int fn, const double* x, const double* y, const double* z, double* out, int n,
                        hipStream_t stream);
 

@@ -25,7 +25,8 @@ EARTH_JPG = os.path.join(REPO, "assets", "earthmap.jpg")
 
 RT_OK = 0
 ERRORS = {-1: "RT_ERR_INVALID", -2: "RT_ERR_HIP", -3: "RT_ERR_UNSUPPORTED", -4: "RT_ERR_OOM",
-          -5: "RT_ERR_NO_DEVICE", -6: "RT_ERR_NO_SCENE"}
+          -5: "RT_ERR_NO_DEVICE", -6: "RT_ERR_NO_SCENE", -7: "RT_ERR_COMM", -8: "RT_ERR_PEER"}
+RT_COMM_ID_BYTES = 128
 
 SCENES = {"random": 0, "two_spheres": 1, "two_perlin": 2, "earth": 3, "simple_light": 4,
           "cornell": 5, "cornell_smoke": 6, "final": 7}
@@ -73,6 +74,9 @@ EXPORTED = [
     "rt_accum_get", "rt_accum_set", "rt_accum_resolve", "rt_render_progressive", "rt_ctx_set_schedule", "rt_ctx_set_precision",
     "rt_scene_validate", "rt_build_info", "rt_ctx_set_option", "rt_ctx_get_option", "rt_world_set_build_option",
     "rt_last_tile_costs", "rt_ctx_set_tile_order",
+    "rt_comm_unique_id", "rt_comm_init_rank", "rt_comm_init_all", "rt_comm_destroy", "rt_comm_rank",
+    "rt_comm_tile_order", "rt_comm_tile_order_all", "rt_render_gather", "rt_render_gather_all",
+    "rt_comm_last_stats", "rt_tiles_assemble", "rt_tiles_assemble_host", "rt_cost_tile_order",
 ]
 
 # int (*rt_progress_fn)(void* user, int64_t samples_done, int64_t samples_total)
@@ -149,6 +153,16 @@ class Stats(ctypes.Structure):
         return {k: getattr(self, k) for k, _ in self._fields_}
 
 
+class CommStats(ctypes.Structure):
+    """rt_comm_stats: the last rt_render_gather / rt_comm_tile_order of one rank."""
+    _fields_ = [("render_ms", ctypes.c_double), ("gather_ms", ctypes.c_double), ("assemble_ms", ctypes.c_double),
+                ("kernel_ms", ctypes.c_double), ("slab_bytes", ctypes.c_int64), ("tiles", ctypes.c_int32),
+                ("tile_order", ctypes.c_int32), ("cost_pass_ms", ctypes.c_double), ("peer_failed", ctypes.c_int32)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
 _lib = None
 
 
@@ -208,6 +222,16 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "rt_accum_resolve": ([P, P, D, I, I, P], I),
         "rt_render_progressive": ([P, ctypes.POINTER(Camera), ctypes.POINTER(RenderParams), I, PROGRESS_FN, P,
                                    P], I),
+        "rt_comm_unique_id": ([P], I), "rt_comm_init_rank": ([P, I, I, P, ctypes.POINTER(P)], I),
+        "rt_comm_init_all": ([P, I, P], I), "rt_comm_destroy": ([P], None), "rt_comm_rank": ([P, PI, PI], I),
+        "rt_comm_tile_order": ([P, ctypes.POINTER(Camera), ctypes.POINTER(RenderParams), I], I),
+        "rt_comm_tile_order_all": ([P, I, ctypes.POINTER(Camera), ctypes.POINTER(RenderParams), I], I),
+        "rt_render_gather": ([P, ctypes.POINTER(Camera), ctypes.POINTER(RenderParams), P], I),
+        "rt_render_gather_all": ([P, I, ctypes.POINTER(Camera), ctypes.POINTER(RenderParams), P], I),
+        "rt_comm_last_stats": ([P, ctypes.POINTER(CommStats)], I),
+        "rt_tiles_assemble": ([P, P, ctypes.c_int64, I, ctypes.POINTER(RenderParams), P], I),
+        "rt_tiles_assemble_host": ([P, ctypes.c_int64, I, I, I, I, P, P], I),
+        "rt_cost_tile_order": ([P, ctypes.c_int64, P], I),
     }
     for name, (args, res) in sigs.items():
         fn = getattr(lib, name, None)
@@ -403,9 +427,30 @@ def cost_tile_order(costs) -> np.ndarray:
     """rt_ctx_set_tile_order's order from per-tile costs (rt_last_tile_costs): the raster tiles
     by cost, most expensive first (ties in raster order). Dealt round-robin, every shard gets
     every N-th tile of the sorted list, so the shards' costs differ by at most about one
-    tile's, and each shard renders its expensive tiles first."""
-    c = np.asarray(costs, dtype=np.float64)
-    return np.argsort(-c, kind="stable").astype(np.uint32)
+    tile's, and each shard renders its expensive tiles first. Integer costs go through the
+    library's rt_cost_tile_order (what rt_comm_tile_order sets); others are sorted here."""
+    c = np.asarray(costs)
+    if c.dtype.kind in "ui" and (c.size == 0 or c.min() >= 0):
+        c = np.ascontiguousarray(c, dtype=np.uint64)
+        out = np.empty(c.size, dtype=np.uint32)
+        _check(load_library().rt_cost_tile_order(c.ctypes.data, c.size, out.ctypes.data), "rt_cost_tile_order")
+        return out
+    return np.argsort(-np.asarray(c, dtype=np.float64), kind="stable").astype(np.uint32)
+
+
+def assemble_tiles_host(slabs: np.ndarray, width: int, height: int, world: int, order=None) -> np.ndarray:
+    """rt_tiles_assemble_host: slabs is world x slab_elems (f32 or f64; rank r's tile slab, padded
+    to the largest shard's, at row r) -> the height x width x 3 frame."""
+    a = np.ascontiguousarray(slabs)
+    if a.dtype not in (np.float32, np.float64) or a.ndim < 2 or a.shape[0] != world:
+        raise RTError("slabs: world x slab_elems of f32 / f64")
+    a = a.reshape(world, -1)
+    o = None if order is None else np.ascontiguousarray(order, dtype=np.uint32)
+    out = np.zeros((height, width, 3), dtype=a.dtype)
+    _check(load_library().rt_tiles_assemble_host(a.ctypes.data, a.shape[1], world, width, height, a.dtype.itemsize,
+                                                 None if o is None else o.ctypes.data, out.ctypes.data),
+           "rt_tiles_assemble_host")
+    return out
 
 
 def scattered_tile_order(n_tiles: int, stride: int) -> np.ndarray:
@@ -640,6 +685,13 @@ class Renderer:
         _check(self.lib.rt_last_stats(self.h, ctypes.byref(s)), "rt_last_stats")
         return s
 
+    def assemble_device(self, slabs_ptr: int, slab_elems: int, world: int, params: RenderParams, frame_ptr: int,
+                        stream: Optional[int] = None):
+        """rt_tiles_assemble: gathered tile slabs (device) -> frame (device), in this context's tile order."""
+        params.stream = stream
+        _check(self.lib.rt_tiles_assemble(self.h, ctypes.c_void_p(slabs_ptr), slab_elems, world, ctypes.byref(params),
+                                          ctypes.c_void_p(frame_ptr)), "rt_tiles_assemble")
+
     def device_eval(self, fn: int, x, y=None, z=None) -> np.ndarray:
         x = np.ascontiguousarray(x, dtype=np.float64)
         y = np.ascontiguousarray(x if y is None else y, dtype=np.float64)
@@ -648,6 +700,110 @@ class Renderer:
         _check(self.lib.rt_device_eval(self.h, fn, x.ctypes.data, y.ctypes.data, z.ctypes.data, out.ctypes.data,
                                        x.size), "rt_device_eval")
         return out
+
+
+class Comm:
+    """One rank of a multi-GPU render (rt_comm_*): binds a Renderer (its device) to rank `rank` of
+    `world`. One process per GPU: rank 0 makes the id (Comm.unique_id()) and sends it to the others
+    (any channel), every rank then builds Comm(renderer, rank, world, uid). One process over several
+    GPUs: Comm.init_all(renderers)."""
+
+    def __init__(self, renderer: Renderer, rank: int, world: int, uid: bytes, _handle=None):
+        self.r, self.lib = renderer, renderer.lib
+        self.rank, self.world = rank, world
+        if _handle is not None:
+            self.h = _handle
+            return
+        if len(uid) != RT_COMM_ID_BYTES:
+            raise RTError("unique id must be %d bytes" % RT_COMM_ID_BYTES)
+        h = ctypes.c_void_p()
+        buf = (ctypes.c_uint8 * RT_COMM_ID_BYTES).from_buffer_copy(uid)
+        _check(self.lib.rt_comm_init_rank(renderer.h, rank, world, buf, ctypes.byref(h)), "rt_comm_init_rank")
+        self.h = h
+
+    @staticmethod
+    def unique_id() -> bytes:
+        buf = (ctypes.c_uint8 * RT_COMM_ID_BYTES)()
+        _check(load_library().rt_comm_unique_id(buf), "rt_comm_unique_id")
+        return bytes(buf)
+
+    @staticmethod
+    def init_all(renderers) -> list:
+        n = len(renderers)
+        ctxs = (ctypes.c_void_p * n)(*[r.h.value if isinstance(r.h, ctypes.c_void_p) else r.h for r in renderers])
+        hs = (ctypes.c_void_p * n)()
+        _check(load_library().rt_comm_init_all(ctxs, n, hs), "rt_comm_init_all")
+        return [Comm(r, i, n, b"", _handle=ctypes.c_void_p(hs[i])) for i, r in enumerate(renderers)]
+
+    def close(self):
+        if self.h:
+            self.lib.rt_comm_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def tile_order(self, camera: Camera, params: RenderParams, cost_spp: int = 8):
+        """Collective rt_comm_tile_order: every rank counts its raster shard, one all-reduce, the
+        cost order set on every rank's context."""
+        params.stream = params.stream if params.stream else None
+        _check(self.lib.rt_comm_tile_order(self.h, ctypes.byref(camera), ctypes.byref(params), cost_spp),
+               "rt_comm_tile_order")
+
+    def render_gather(self, camera: Camera, params: RenderParams, out=None):
+        """Collective rt_render_gather into host memory: rank 0 returns the height x width x 3 frame
+        (or fills `out`), the other ranks None."""
+        params.out_on_device = 0
+        if self.rank != 0:
+            _check(self.lib.rt_render_gather(self.h, ctypes.byref(camera), ctypes.byref(params), None),
+                   "rt_render_gather")
+            return None
+        dt = np.float64 if params.out_format == RT_OUT_F64 else np.float32
+        if out is None:
+            out = np.empty((params.height, params.width, 3), dtype=dt)
+        if out.dtype != dt or out.size != params.height * params.width * 3 or not out.flags.c_contiguous:
+            raise RTError("frame buffer of the wrong shape or type")
+        _check(self.lib.rt_render_gather(self.h, ctypes.byref(camera), ctypes.byref(params), out.ctypes.data),
+               "rt_render_gather")
+        return out
+
+    def render_gather_device(self, camera: Camera, params: RenderParams, dev_ptr: Optional[int],
+                             stream: Optional[int] = None):
+        """Collective rt_render_gather, enqueued on `stream`: rank 0's frame into a device buffer."""
+        params.out_on_device = 1
+        params.stream = stream
+        _check(self.lib.rt_render_gather(self.h, ctypes.byref(camera), ctypes.byref(params),
+                                         ctypes.c_void_p(dev_ptr) if dev_ptr else None), "rt_render_gather")
+
+    def stats(self) -> CommStats:
+        s = CommStats()
+        _check(self.lib.rt_comm_last_stats(self.h, ctypes.byref(s)), "rt_comm_last_stats")
+        return s
+
+
+def _comm_array(comms):
+    return (ctypes.c_void_p * len(comms))(*[c.h.value for c in comms])
+
+
+def tile_order_all(comms, camera: Camera, params: RenderParams, cost_spp: int = 8):
+    """rt_comm_tile_order_all over the ranks of one process (Comm.init_all)."""
+    params.stream = None
+    _check(load_library().rt_comm_tile_order_all(_comm_array(comms), len(comms), ctypes.byref(camera),
+                                                 ctypes.byref(params), cost_spp), "rt_comm_tile_order_all")
+
+
+def render_gather_all(comms, camera: Camera, params: RenderParams) -> np.ndarray:
+    """rt_render_gather_all over the ranks of one process: the frame in host memory."""
+    params.out_on_device = 0
+    params.stream = None
+    dt = np.float64 if params.out_format == RT_OUT_F64 else np.float32
+    out = np.empty((params.height, params.width, 3), dtype=dt)
+    _check(load_library().rt_render_gather_all(_comm_array(comms), len(comms), ctypes.byref(camera),
+                                               ctypes.byref(params), out.ctypes.data), "rt_render_gather_all")
+    return out
 
 
 class Accumulator:

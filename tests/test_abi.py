@@ -27,7 +27,7 @@ def test_library_exports_every_header_symbol(rt):
     missing = [s for s in declared if not hasattr(lib, s)]
     assert not missing, missing
     assert sorted(declared) == sorted(rt.EXPORTED)
-    assert lib.rt_abi_version() == 4
+    assert lib.rt_abi_version() == 5
 
 
 @pytest.mark.parametrize("scene_id", range(8))
@@ -210,6 +210,16 @@ def test_errors_do_not_abort(rt):
     assert lib.rt_accum_resolve(None, None, 0.0, 0, 0, None) == -1
     assert lib.rt_render_progressive(None, None, None, 1, rt.PROGRESS_FN(), None, None) == -1
     lib.rt_accum_destroy(None)
+    # multi-GPU entry points (ABI v5) check their arguments before loading RCCL or touching a device
+    assert lib.rt_comm_init_rank(None, 0, 1, None, None) == -1
+    assert lib.rt_comm_init_all(None, 0, None) == -1
+    assert lib.rt_comm_tile_order(None, None, None, 8) == -1
+    assert lib.rt_render_gather(None, None, None, None) == -1
+    assert lib.rt_render_gather_all(None, 0, None, None, None) == -1
+    assert lib.rt_comm_last_stats(None, None) == -1
+    assert lib.rt_tiles_assemble(None, None, 0, 1, None, None) == -1
+    assert lib.rt_comm_rank(None, None, None) == -1
+    lib.rt_comm_destroy(None)
     with pytest.raises(rt.RTError):
         w.flatten(7)                         # unknown accel mode
 
@@ -437,7 +447,8 @@ def test_ctypes_structs_match_the_c_header(rt, tmp_path):
     import subprocess
     import ctypes
     structs = {"rt_stats": rt.Stats, "rt_render_params": rt.RenderParams, "rt_camera": rt.Camera,
-               "rt_scene_preset": rt.ScenePreset, "rt_world_info": rt.WorldInfo, "rt_scene_soa": rt.SceneSoA}
+               "rt_scene_preset": rt.ScenePreset, "rt_world_info": rt.WorldInfo, "rt_scene_soa": rt.SceneSoA,
+               "rt_comm_stats": rt.CommStats}
     src = ['#include <stdio.h>', '#include <stddef.h>', '#include "rt/rt_abi.h"', "int main(void) {"]
     for cname, py in structs.items():
         src.append(f'printf("{cname} size %zu\\n", sizeof({cname}));')

@@ -152,6 +152,47 @@ def test_tile_order_assemble_and_cost_order():
     assert max(sums) - min(sums) <= heavy.max()
 
 
+def _gathered(slabs, world):
+    """Slabs padded to the largest shard's, one row per rank (what the RCCL gather lands on rank 0)."""
+    flat = [s.reshape(-1) for s in slabs]
+    n = max(f.size for f in flat)
+    out = np.zeros((world, n), flat[0].dtype)
+    for r, f in enumerate(flat):
+        out[r, : f.size] = f
+    return out
+
+
+def test_library_tile_assembly_and_cost_order_match_python():
+    """The library's host restatements (ABI v5), which rt_render_gather's reorder kernel and
+    rt_comm_tile_order are checked against on the GPU, equal the Python ones: rt_tiles_assemble_host
+    inverts every rank's tile slab (raster and permuted orders, f32 and f64, cut edge tiles, more
+    ranks than tiles), and rt_cost_tile_order is a stable descending sort (ties in raster order)."""
+    import __graft_entry__ as ge
+    rt = ge.import_binding()
+    rng = np.random.default_rng(11)
+    for (h, w) in ((19, 24), (9, 17), (8, 8), (90, 160), (53, 96)):
+        tiles = ((w + 7) // 8) * ((h + 7) // 8)
+        for dt in (np.float64, np.float32):
+            img = rng.standard_normal((h, w, 3)).astype(dt)
+            for order in (None, rng.permutation(tiles).astype(np.uint32)):
+                for world in (1, 2, 3, 8, tiles + 2):
+                    slabs = [tile_slab(img, r, world, order) for r in range(world)]
+                    g = _gathered(slabs, world)
+                    got = rt.assemble_tiles_host(g, w, h, world, order=order)
+                    assert got.dtype == dt and np.array_equal(got, img), (h, w, world, dt)
+    with pytest.raises(rt.RTError):   # a slab narrower than the largest shard's
+        rt.assemble_tiles_host(np.zeros((2, 10)), 24, 19, 2)
+    with pytest.raises(rt.RTError):   # not a permutation
+        rt.assemble_tiles_host(np.zeros((1, 9 * 192)), 24, 19, 1, order=np.zeros(9, np.uint32))
+    costs = np.array([5, 9, 9, 1, 7, 3, 0, 9], dtype=np.uint64)
+    assert rt.cost_tile_order(costs).tolist() == [1, 2, 7, 4, 0, 5, 3, 6]
+    for _ in range(5):
+        c = rng.integers(0, 50, 4000).astype(np.uint64)   # many ties
+        assert np.array_equal(rt.cost_tile_order(c), np.argsort(-c.astype(np.float64), kind="stable"))
+    big = np.array([2**62, 2**62 + 1, 7], dtype=np.uint64)   # beyond f64's integers: exact in the library
+    assert rt.cost_tile_order(big).tolist() == [1, 0, 2]
+
+
 @pytest.mark.parametrize("world", [2, 3])
 def test_row_sharded_gather_equals_single_render(tmp_path, world):
     out = str(tmp_path / "frame.npy")
