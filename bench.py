@@ -523,27 +523,28 @@ def main():
     if rank == 0 and not dist_on and not args.no_cpu_baseline:
         from tests import oracle_binding as ob
         cores, n_aff, quota = usable_cores()
-        # calibrate on `cores` interleaved rows at low spp, then take an interleaved row
-        # subset of the real workload worth ~cpu_seconds (a multiple of `cores` rows)
+        # calibrate on `cores` interleaved rows at low spp, then take an interleaved subset of the
+        # real workload's rows worth ~cpu_seconds, at full spp: the oracle deals pixels round-robin
+        # over its threads, so even one row keeps every core busy, and the timed frame's own rows
+        # are then compared at full spp on every config
         cal_stride = max(1, H // cores)
         _, st1 = ob.render(args.scene, W, H, min(spp, 16), depth, args.seed, args.seed, row_begin=0,
                            row_stride=cal_stride, threads=cores, return_stats=True)
         rate = st1.samples / max(st1.seconds, 1e-9)
         target = args.cpu_seconds * rate            # samples worth ~cpu_seconds
-        n_rows = int(target / (W * spp))
-        n_rows = max(cores, min(H, n_rows // cores * cores))
+        n_rows = max(1, min(H, int(target / (W * spp))))
         stride = max(1, H // n_rows)
-        n_rows = len(range(0, H, stride))
-        # a frame too large for even `cores` full rows (C5) takes the first spp_cpu samples
-        # of every pixel of those rows: the per-sample work is the same
-        spp_cpu = int(min(spp, max(1, target // (n_rows * W))))
-        ref_img, st = ob.render(args.scene, W, H, spp_cpu, depth, args.seed, args.seed, row_begin=0,
+        row0 = stride // 2                          # rows y = row0 + k * stride, centred in their bands
+        n_rows = len(range(row0, H, stride))
+        # a row worth more than ~3 budgets takes the first spp_cpu samples of every pixel instead
+        spp_cpu = spp if W * spp <= 3 * target else int(max(1, target // (n_rows * W)))
+        ref_img, st = ob.render(args.scene, W, H, spp_cpu, depth, args.seed, args.seed, row_begin=row0,
                                 row_stride=stride, threads=cores, return_stats=True)
         spp_note = "" if spp_cpu == spp else f", samples 0..{spp_cpu - 1} of each pixel"
         cpu = {"value": st.samples / st.seconds / 1e6, "unit": "Msamples/s", "cores": cores, "kind": "port",
-               "sample": f"oracle (C, f64, recursive ray_color, linear hit_hittables scan) on rows y % {stride} == 0 "
-                         f"of the same {W}x{H}x{spp} depth-{depth} frame{spp_note}: {st.samples} samples in "
-                         f"{st.seconds:.1f} s on {cores} threads (interleaved rows)",
+               "sample": f"oracle (C, f64, recursive ray_color, linear hit_hittables scan) on rows y % {stride} == "
+                         f"{row0} of the same {W}x{H}x{spp} depth-{depth} frame{spp_note}: {st.samples} samples in "
+                         f"{st.seconds:.1f} s on {cores} threads (pixels round-robin)",
                "cpu_model": cpu_model(), "nproc": os.cpu_count(), "affinity": n_aff, "cgroup_quota": quota}
         # the reference's own decomposition: 10 threads, each all pixels x spp/10 samples
         # (main.rs:497-551, spp/thread_count at :516), the figure comparable to README.md:6
@@ -559,12 +560,12 @@ def main():
                              "older book-1 scene revision, unknown CPU)"}
         # parity: the GPU renders exactly those rows and samples (f64 output) and the timed
         # frame's same rows (full spp only) are compared as well
-        gp = rt.Renderer.params(W, H, spp_cpu, depth, bg, args.seed, row_begin=0, row_stride=stride,
+        gp = rt.Renderer.params(W, H, spp_cpu, depth, bg, args.seed, row_begin=row0, row_stride=stride,
                                 out_format=rt.RT_OUT_F64)
         gimg = renderer.render(cam, gp)
         d = np.abs(gimg - ref_img)
         parity = {"linf": float(d.max()), "max_rel": float((d / np.maximum(np.abs(ref_img), 1e-300)).max()),
-                  "rows": n_rows, "row_stride": stride, "spp": spp_cpu, "max_depth": depth,
+                  "rows": n_rows, "row_begin": row0, "row_stride": stride, "spp": spp_cpu, "max_depth": depth,
                   "samples": int(st.samples), "tolerance": 1e-3, "pass": bool(d.max() <= 1e-3),
                   "vs": "oracle image of the cpu_baseline sample (same rows, samples, seeds)"}
         if f32:   # the f32 mode's paths are its own: statistical parity (tests/test_gpu_f32.py)
@@ -572,9 +573,9 @@ def main():
             parity.update({"mode": "statistical (f32)", "mean_rel": mean_rel, "tolerance": 0.01,
                            "pass": bool(mean_rel < 0.01)})
         if spp_cpu == spp and not f32:
-            parity["linf_timed_frame"] = float(np.abs(frame_np[0::stride] - ref_img).max())
+            parity["linf_timed_frame"] = float(np.abs(frame_np[row0::stride] - ref_img).max())
             # the timed frame's PPM bytes (rt_write_color) against the oracle's write_color of its image
-            parity["ppm_bytes_equal_on_rows"] = bool(np.array_equal(rt.write_color(frame_np[0::stride]),
+            parity["ppm_bytes_equal_on_rows"] = bool(np.array_equal(rt.write_color(frame_np[row0::stride]),
                                                                     ob.write_color(ref_img)))
 
     if rank == 0:

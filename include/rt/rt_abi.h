@@ -254,7 +254,11 @@ int rt_last_stats(rt_ctx* ctx, rt_stats* out);
  * generation, 4 trace, 5 shading, 8 node loops, 9 leaf tests (both of the top-level walk),
  * 15 ray set-up, 16 walk prologue (pre-leaf test), 17 hit record, 18 media and 19 instances
  * (inside the leaf tests), 20 refill, 21 kernel total (summed over waves), 22 deferred instance
- * walks (after the top-level walk). */
+ * walks (after the top-level walk), 23 / 24 ray generation's seeding + jitter / rejection loop, 25
+ * the longest wave lifetime, 26 waves. Bounce-loop lane slots that cast nothing (with casts they
+ * add up to 64 x wave_steps): 27 idle, no unit left (the tail), 28 idle, every ring slot holding
+ * an unfinished block, 29 the path ended in its scatter, 30 the depth cap, 31 a rejection loop
+ * carried to the next iteration. */
 int rt_last_counters(rt_ctx* ctx, uint64_t* out, int n);
 
 /* ---- tile order: balancing tile shards (ABI v4; main.rs:497-551's partition, rebalanced) ------ */

@@ -91,6 +91,11 @@ struct Count {
     uint64_t t_setup, t_pre, t_rec, t_med, t_inst, t_refill, t_defer;
     // ray generation split (pool kernels): path seeding + camera jitter, the rejection loop
     uint64_t t_seed, t_tries;
+    // pool kernels, why a lane of a bounce-loop iteration casts no ray (with casts they add up to
+    // 64 x wave_steps): no unit left to take (the launch's tail), every ring slot holding an
+    // unfinished block (RING), a path that ended in its scatter (the material absorbed it), the
+    // depth cap, a rejection loop left for the next iteration (RT_TRY_LEFT)
+    uint32_t idle_tail, idle_ring, no_scatter, depth_cap, try_wait;
 };
 // COUNT phase stamps: tp is the lane's last stamp; the first active lane adds the interval
 #define RT_STAMP(acc, tp)                                                   \
@@ -2277,6 +2282,13 @@ __global__ void __launch_bounds__(BlockThreads<C>(), min_waves<C>()) trace_pool(
         }
         if (!__any(active)) break;
         if (C::COUNT && first_active_lane()) cnt.wave_steps++;
+        if (C::COUNT) {   // lanes the refill left idle: nothing left to take, or (RING) no free slot
+            const uint64_t idle = __ballot(!active);
+            if (first_active_lane()) {
+                if (exhausted) cnt.idle_tail += (uint32_t)__popcll(idle);
+                else cnt.idle_ring += (uint32_t)__popcll(idle);
+            }
+        }
         if (!active) continue;
         // (COUNT) refill and loop overhead since the last iteration's end stamp: lanes refilled this
         // iteration were idle, so their stamp is old — take the wave's latest (max over lanes)
@@ -2357,6 +2369,11 @@ __global__ void __launch_bounds__(BlockThreads<C>(), min_waves<C>()) trace_pool(
             }
         }
         RT_STAMP(t_cam, t_prev);
+        if (C::COUNT) {
+            cnt.try_wait += gen_wait ? 1u : 0u;
+            cnt.no_scatter += (!go && !gen_wait) ? 1u : 0u;
+            cnt.depth_cap += (go && depth <= 0) ? 1u : 0u;
+        }
         if (go && depth > 0) {  // main.rs:21-23: depth 0 is black
             key.bounce = (uint32_t)(P.max_depth - depth);
             if (C::COUNT) cnt.casts++;
@@ -2435,6 +2452,11 @@ __global__ void __launch_bounds__(BlockThreads<C>(), min_waves<C>()) trace_pool(
         atomicAdd(&counters[19], (unsigned long long)cnt.t_inst);
         atomicAdd(&counters[20], (unsigned long long)cnt.t_refill);
         atomicAdd(&counters[22], (unsigned long long)cnt.t_defer);
+        atomicAdd(&counters[27], (unsigned long long)cnt.idle_tail);
+        atomicAdd(&counters[28], (unsigned long long)cnt.idle_ring);
+        atomicAdd(&counters[29], (unsigned long long)cnt.no_scatter);
+        atomicAdd(&counters[30], (unsigned long long)cnt.depth_cap);
+        atomicAdd(&counters[31], (unsigned long long)cnt.try_wait);
         if (lane == 0) {   // the wave's lifetime; the longest, and the wave count (the launch's tail: 25, 26)
             const unsigned long long life = __builtin_amdgcn_s_memtime() - t_start;
             atomicAdd(&counters[21], life);
