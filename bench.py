@@ -630,6 +630,9 @@ def main():
                                   "control_plane": "torch.distributed gloo", "world_size": world,
                                   "forced_at_world_1": bool(args.force_dist and world == 1)}
         print(json.dumps(out), flush=True)
+    if comm is not None:   # the RCCL communicator before the process group and the context
+        comm.close()
+    renderer.close()
     if dist_on:
         dist.destroy_process_group()
 

@@ -1368,7 +1368,8 @@ static int run_range(rt_ctx* c, const rt_camera* cam, const rt_render_params* p,
     // its grid to ring_waves)
     bool ring_ok = c->opt_ring && K.block_samples == chunk && chunk <= (int)(rtk::kRingSlot / 64) &&
                    s_end <= (int)rtk::kRingSampleMask;
-    const int ring_waves = c->n_cus * 20;
+    // (the f32 mode's spheres variant runs 6 waves per SIMD: RT_BLOCK_F32_SPHERES)
+    const int ring_waves = c->n_cus * (o.f32 && rtk::variant_features(o.features) == rtk::FEAT_SET_SPHERES ? 24 : 20);
     const size_t ring_bytes = (size_t)ring_waves * rtk::kRingWaveDoubles * sizeof(double);
     bool ring = false;
     bool per_sample = false;

@@ -241,7 +241,7 @@ struct Stack16 {   // node records at LDS addresses < 32 KB, leaf codes > -32768
 template <class C>
 constexpr bool Stack16Cfg()
 {
-    return RT_STACK16 && C::LDS && C::NALL && C::S32 && C::F == FEAT_SET_SPHERES && !C::F32;
+    return RT_STACK16 && C::LDS && C::NALL && C::S32 && C::F == FEAT_SET_SPHERES;
 }
 template <class C>
 using StackT = typename std::conditional<Stack16Cfg<C>(), Stack16<BlockThreads<C>()>,
@@ -1860,6 +1860,9 @@ __device__ __forceinline__ bool lane_work(const KParams& P, LaneWork& w)
     return true;
 }
 
+#ifndef RT_MIN_WAVES_F32_SPHERES
+#define RT_MIN_WAVES_F32_SPHERES 6   // 76 VGPRs (<= 80 for 6), 512-thread blocks (RT_BLOCK_F32_SPHERES)
+#endif
 #ifndef RT_MIN_WAVES_SPHERES
 #define RT_MIN_WAVES_SPHERES 1
 #endif
@@ -1888,7 +1891,8 @@ __device__ __forceinline__ bool lane_work(const KParams& P, LaneWork& w)
 template <class C>
 constexpr int min_waves()
 {
-    return Stack16Cfg<C>() && C::F == FEAT_SET_SPHERES ? 5
+    return Stack16Cfg<C>() && C::F32 ? RT_MIN_WAVES_F32_SPHERES   // (the f32 mode's spheres variant)
+           : Stack16Cfg<C>() && C::F == FEAT_SET_SPHERES ? 5
            : C::F == FEAT_SET_SPHERES ? RT_MIN_WAVES_SPHERES
            : C::F == FEAT_SET_RECTINST ? RT_MIN_WAVES_RECTINST
            : C::F == FEAT_SET_MEDIA    ? RT_MIN_WAVES_MEDIA
@@ -2508,7 +2512,7 @@ template <uint32_t F, bool S32, bool LDS, bool COUNT, bool F32>
 static void launch_one(const Launch& L, hipStream_t stream, bool nall)
 {
     const SceneDev& S = *L.S;
-    const bool s16 = RT_STACK16 && LDS && nall && S32 && F == FEAT_SET_SPHERES && !F32;   // Stack16Cfg
+    const bool s16 = RT_STACK16 && LDS && nall && S32 && F == FEAT_SET_SPHERES;   // Stack16Cfg
     const int node_bytes = nall && S32 ? (int)sizeof(LdsNode) : (int)sizeof(rt_bvh_node);   // lds_node_bytes
     const bool stage = F != FEAT_SET_SPHERES;                   // StageShade
     const bool blas = RT_STAGE_BLAS && (F & FEAT_INST_BLAS) != 0 && !F32;   // StageBlas
@@ -2591,10 +2595,17 @@ hipError_t launch_variant(const Launch& L, const LaunchOpts& o, hipStream_t stre
 
 // The f32 fast mode's kernels of one feature set (trace_f32_*.hip): f32 slab tests always
 // (an f32 path gains nothing from f64 boxes), no count variant.
+// The whole-TLAS spheres instantiation keeps 16-bit stack entries (Stack16Cfg), as launch_f's: a
+// scene whose node addresses or leaf codes do not fit takes the partial-TLAS instantiation.
+inline bool f32_nall(const SceneDev& S, uint32_t F, bool lds)
+{
+    const bool nall = S.n_lds_nodes > 0 && S.n_lds_nodes == S.n_tlas_nodes;
+    return nall && !(RT_STACK16 && F == FEAT_SET_SPHERES && lds && !S.stack16_ok);
+}
 template <uint32_t F>
 hipError_t launch_variant_f32(const Launch& L, const LaunchOpts& o, hipStream_t stream)
 {
-    const bool nall = L.S->n_lds_nodes > 0 && L.S->n_lds_nodes == L.S->n_tlas_nodes;
+    const bool nall = f32_nall(*L.S, F, o.lds_stack);
     if (o.lds_stack) launch_one<F, true, true, false, true>(L, stream, nall);
     else launch_one<F, true, false, false, true>(L, stream, nall);
     return hipGetLastError();
@@ -2605,7 +2616,7 @@ hipError_t launch_variant_f32(const Launch& L, const LaunchOpts& o, hipStream_t 
 template <uint32_t F>
 hipError_t launch_variant_f32_count(const Launch& L, const LaunchOpts& o, hipStream_t stream)
 {
-    const bool nall = L.S->n_lds_nodes > 0 && L.S->n_lds_nodes == L.S->n_tlas_nodes;
+    const bool nall = f32_nall(*L.S, F, o.lds_stack);
     if (o.lds_stack) launch_one<F, true, true, true, true>(L, stream, nall);
     else launch_one<F, true, false, true, true>(L, stream, nall);
     return hipGetLastError();

@@ -24,10 +24,20 @@
 
 namespace rtk {
 
-// workgroup threads of a kernel variant (host and device): see RT_BLOCK_FINAL
+// Threads per workgroup of the f32 mode's spheres variant: its 76 VGPRs allow 6 waves per SIMD,
+// which 256-thread blocks cannot reach (each holds its own 22.7 KB copy of the random scene's
+// TLAS, 6 x 28.8 KB > 160 KB per CU); 512-thread blocks share one copy among 8 waves (3 blocks,
+// 105 KB).
+#ifndef RT_BLOCK_F32_SPHERES
+#define RT_BLOCK_F32_SPHERES 512
+#endif
+
+// workgroup threads of a kernel variant (host and device): see RT_BLOCK_FINAL, RT_BLOCK_F32_SPHERES
 __host__ __device__ constexpr int block_threads_of(uint32_t variant_features, bool f32)
 {
-    return variant_features == 287u /* FEAT_SET_FINAL */ && !f32 ? RT_BLOCK_FINAL : 256;
+    return variant_features == 287u /* FEAT_SET_FINAL */ && !f32  ? RT_BLOCK_FINAL
+           : variant_features == 0u /* FEAT_SET_SPHERES */ && f32 ? RT_BLOCK_F32_SPHERES
+                                                                 : 256;
 }
 
 // Device view of the uploaded rt_scene_soa tables.
