@@ -419,7 +419,7 @@ int rt_ctx_set_variant(rt_ctx* ctx, int slab32, int lds_stack, int lds_nodes);
 /* Context options (rt_ctx_set_option / rt_ctx_get_option). The library reads no environment
  * variable: every behaviour switch is one of these or a setter above. Images do not depend on
  * any of them (the tests check this); they trade speed and memory.
- *   RT_OPT_TRACE_BUF_BYTES  bound of the trace-output buffer (below); 0 restores the default
+ *   RT_OPT_TRACE_BUF_BYTES  bound of the trace-output buffer (below, default 64 GiB); 0 restores the default
  *   RT_OPT_BATCH_OVERLAP    1 (default): buffer batches overlap on two streams; 0: one buffer, in order
  *   RT_OPT_BLOCK_SAMPLES    per-sample pool: samples per work block (0: auto, 16 down to 4 for small shards)
  *   RT_OPT_BLOCK_CHUNKS     item pool: chunks per work block (0: auto = 2)
@@ -449,13 +449,13 @@ int rt_ctx_get_option(rt_ctx* ctx, int key, int64_t* value);
  *   CHUNKS: a wave owns an 8x8 tile x one chunk of samples, each lane one pixel's chunk,
  *           written as one partial per (pixel, chunk); the wave waits for its slowest lane.
  *   POOL:   persistent waves take (tile, chunk) blocks from a device counter and a lane
- *           whose path ended takes the block's next (pixel, sample) at once. A block belongs
- *           to one wave: its samples' radiance waits in that wave's ring of 4 blocks, and when
- *           the block's last sample ends the wave sums every pixel's samples in order into the
- *           chunk partial (1/chunk of the per-sample bytes, as ITEMS). Small shards, whose
- *           blocks are cut below one chunk (RT_OPT_BLOCK_SAMPLES), and RT_OPT_POOL_RING 0 write
- *           every sample to a per-sample buffer ([8x8 tile][sample][pixel of the tile]) summed
- *           per pixel in sample order by a second kernel.
+ *           whose path ended takes the block's next (pixel, sample) at once. Every sample's
+ *           radiance goes to a per-sample buffer ([8x8 tile][sample][pixel of the tile]) summed
+ *           per pixel in sample order by a second kernel. When that buffer does not fit the bound
+ *           in one batch (RT_OPT_POOL_RING), a block belongs to one wave instead: its samples wait
+ *           in that wave's ring of 4 blocks, and when the block's last sample ends the wave sums
+ *           every pixel's samples in order into the chunk partial (1/chunk of the per-sample
+ *           bytes, as ITEMS). Same bits either way.
  *   ITEMS:  persistent waves as POOL, but a lane takes a whole (pixel, chunk) item, traces
  *           its samples in order and writes one partial, as CHUNKS does (1/chunk of POOL's
  *           buffer bytes); a lane whose item ended takes the next item at once.
@@ -467,12 +467,13 @@ int rt_ctx_get_option(rt_ctx* ctx, int key, int64_t* value);
  * measured 2.3x slower than POOL on the final scene and removed; rt_ctx_set_schedule(4) returns
  * RT_ERR_UNSUPPORTED (the code: scripts/experiments/r05_wavefront.patch).
  * The trace-output buffer (POOL's ring included) is bounded by RT_OPT_TRACE_BUF_BYTES (default
- * 4 GiB, or half the device's free memory if that is less; allocated lazily, as large as a
+ * 64 GiB, or half the device's free memory if that is less; allocated lazily, as large as a
  * render needs). A larger render runs in buffer
  * batches whose sums are carried across, in two halves of the bound: batch k traces into half
  * k & 1 on one of two context streams while the render's stream reduces batch k - 1, so
  * consecutive traces overlap (RT_OPT_BATCH_OVERLAP 0: one buffer, in order). Under the default
- * bound C2 (1.2 GB with the ring) and C4 (3.4 GB) render in one batch, C5 in 64. */
+ * bound C2 (11.5 GB) and C4 (49.8 GB) render through the per-sample buffer in one batch, C5
+ * (1.6 TB of records) through the ring's chunk partials in a few. */
 enum { RT_SCHED_CHUNKS = 0, RT_SCHED_POOL = 1, RT_SCHED_ITEMS = 2, RT_SCHED_AUTO = 3 };
 int rt_ctx_set_schedule(rt_ctx* ctx, int schedule);
 

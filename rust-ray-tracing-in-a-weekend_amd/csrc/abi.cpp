@@ -135,14 +135,17 @@ struct rt_ctx {
     size_t lds_per_block = 160 * 1024;
 };
 
-// The trace-output buffer's default bound: 4 GiB, or half the device's free
-// memory if that is less. The per-sample pool reduces each finished block inside the kernel
-// (kPoolRing), so its output is chunk partials — C2 0.74 GB, C4 3.1 GB, one launch each — plus a
-// ring of ~0.5 GB; the per-sample buffer (small shards, RT_OPT_POOL_RING 0) is what the bound batches.
+// The trace-output buffer's default bound: 64 GiB, or half the device's free memory if that is
+// less (round 6). The per-sample buffer is as fast as the in-kernel ring reduction on the random
+// scene and 1.4 % faster on the final scene, whose ring reductions stall a wave holding 4 waves'
+// worth of path state per SIMD (interleaved medians, kernel + reduce ms: C2 74.47 vs 74.41, C2 f32
+// 64.46 vs 64.38, C4 982.1 vs 996.2; profiles/r06c_ab_*.log), and a 288 GB device holds C4's
+// 49.8 GB of records in one batch. The ring stays for renders the bound does not hold in one
+// batch (C5: 1.6 TB of records), where its chunk partials are 1/16 of the bytes.
 static size_t default_buf_cap()
 {
     size_t fr = 0, tot = 0;
-    size_t cap = (size_t)4 << 30;
+    size_t cap = (size_t)64 << 30;
     if (hipMemGetInfo(&fr, &tot) == hipSuccess && fr > 0) cap = std::min(cap, fr / 2);
     return std::max(cap >> 20, (size_t)1) << 20;
 }
