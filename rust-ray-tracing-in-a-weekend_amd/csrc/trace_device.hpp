@@ -373,6 +373,7 @@ __device__ __forceinline__ void set_face_normal(HitT<R>& h, R dx, R dy, R dz, R 
 // ---------------------------------------------------------------------------
 
 // hittable.rs:254-273: the root in [t_min, t_max]
+template <bool SMALL = false>
 __device__ __forceinline__ bool sphere_t(double cx, double cy, double cz, double radius, const RayT<double>& r,
                                          double t_min, double t_max, double& t)
 {
@@ -421,14 +422,38 @@ __device__ __forceinline__ bool sphere_t2(double cx, double cy, double cz, doubl
     return true;
 }
 
+// f32 mode: c = |oc|^2 - r^2 and b/2 = oc . d of a sphere test. c of a large sphere is taken in
+// f64 (an f32 c loses everything to cancellation on the r = 1000 ground sphere, whose surface
+// every bounce starts on: |oc|^2 ~ 1e6, one f32 ulp 0.06); a small one's in f32, where the
+// cancellation costs at most ~r^2 2^-24 (3e-6 at r <= 8), far below the t_min = 0.001 it must
+// stay under. The random scene's BVH holds only r <= 1 spheres (its ground is the pre-leaf).
+// SMALL: the spheres variant only (in the final-scene variant the second path costs spills).
+#ifndef RT_F32_SMALL_SPHERE
+#define RT_F32_SMALL_SPHERE 8.0
+#endif
+template <bool SMALL = false>
+__device__ __forceinline__ void sphere_cb(double cx, double cy, double cz, double radius, const RayT<float>& r,
+                                          float& c, float& half_b)
+{
+    if (SMALL && radius <= RT_F32_SMALL_SPHERE) {
+        const float ox = r.ox - (float)cx, oy = r.oy - (float)cy, oz = r.oz - (float)cz;
+        const float rf = (float)radius;
+        c = (ox * ox + oy * oy + oz * oz) - rf * rf;
+        half_b = ox * r.dx + oy * r.dy + oz * r.dz;
+        return;
+    }
+    const double ocx = (double)r.ox - cx, ocy = (double)r.oy - cy, ocz = (double)r.oz - cz;
+    c = (float)((ocx * ocx + ocy * ocy + ocz * ocz) - radius * radius);
+    half_b = (float)ocx * r.dx + (float)ocy * r.dy + (float)ocz * r.dz;
+}
+
 // f32 mode: sphere_t's f32 roots, the same selection (its second query starts at
 // t1 + max(1e-4, |t1| 2^-19), medium_t)
 __device__ __forceinline__ bool sphere_t2(double cx, double cy, double cz, double radius, const RayT<float>& r,
                                           float& t1, float& t2)
 {
-    const double ocx = (double)r.ox - cx, ocy = (double)r.oy - cy, ocz = (double)r.oz - cz;
-    const float c = (float)((ocx * ocx + ocy * ocy + ocz * ocz) - radius * radius);
-    const float half_b = (float)ocx * r.dx + (float)ocy * r.dy + (float)ocz * r.dz;
+    float c, half_b;
+    sphere_cb(cx, cy, cz, radius, r, c, half_b);
     const float disc = half_b * half_b - r.a * c;
     if (disc < 0.0f) return false;
     const float q = -(half_b + __builtin_copysignf(__builtin_sqrtf(disc), half_b));
@@ -445,16 +470,14 @@ __device__ __forceinline__ bool sphere_t2(double cx, double cy, double cz, doubl
     return true;
 }
 
-// f32 mode: the same roots, robust in f32 (Haines et al., Ray Tracing Gems ch. 7): c = |oc|^2
-// - r^2 is taken in f64 (an f32 c loses everything to cancellation on the r = 1000 ground
-// sphere, whose surface every bounce starts on), the near root as c / q (Vieta) instead of
-// the cancelling -b - sqrt(disc).
+// f32 mode: the same roots, robust in f32 (Haines et al., Ray Tracing Gems ch. 7): c as
+// sphere_cb takes it, the near root as c / q (Vieta) instead of the cancelling -b - sqrt(disc).
+template <bool SMALL = false>
 __device__ __forceinline__ bool sphere_t(double cx, double cy, double cz, double radius, const RayT<float>& r,
                                          float t_min, float t_max, float& t)
 {
-    const double ocx = (double)r.ox - cx, ocy = (double)r.oy - cy, ocz = (double)r.oz - cz;
-    const float c = (float)((ocx * ocx + ocy * ocy + ocz * ocz) - radius * radius);
-    const float half_b = (float)ocx * r.dx + (float)ocy * r.dy + (float)ocz * r.dz;
+    float c, half_b;
+    sphere_cb<SMALL>(cx, cy, cz, radius, r, c, half_b);
     const float disc = half_b * half_b - r.a * c;
     if (disc < 0.0f) return false;
     const float q = -(half_b + __builtin_copysignf(__builtin_sqrtf(disc), half_b));
@@ -703,7 +726,7 @@ __device__ __forceinline__ bool simple_t(const rt_prim& p, const RayT<R>& r, R t
     if (!(C::F & FEAT_RECT) || p.kind <= RT_PRIM_MOVING_SPHERE) {
         double cx, cy, cz;
         sphere_center(p, r, gs, cx, cy, cz, (C::F & FEAT_STATIC) != 0);
-        return sphere_t(cx, cy, cz, p.p[3], r, t_min, t_max, t);
+        return sphere_t<C::F == FEAT_SET_SPHERES>(cx, cy, cz, p.p[3], r, t_min, t_max, t);
     } else {
         const R q0 = (R)p.p[0], q1 = (R)p.p[1], q2 = (R)p.p[2], q3 = (R)p.p[3], q4 = (R)p.p[4];
         switch (p.kind) {

@@ -28,7 +28,7 @@ def snapshot(out: str, csrc: str = ge.CSRC, jobs: int = 8) -> None:
 
     def one(tu):
         dst = os.path.join(out, tu[:-4] + ".s")
-        subprocess.run([ge.HIPCC, *ge.CXXFLAGS, "--cuda-device-only", "-S", os.path.join(csrc, tu), "-o", dst],
+        subprocess.run([ge.HIPCC, *ge.tu_flags(tu), "--cuda-device-only", "-S", os.path.join(csrc, tu), "-o", dst],
                        check=True, capture_output=True)
         return tu
 
