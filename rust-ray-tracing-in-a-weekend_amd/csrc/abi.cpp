@@ -1276,6 +1276,13 @@ static int run_range(rt_ctx* c, const rt_camera* cam, const rt_render_params* p,
     K.tile_shard = p->tile_shard;
     K.img_tiles_x = (p->width + 7) / 8;
     const int64_t img_tiles = (int64_t)K.img_tiles_x * ((p->height + 7) / 8);
+    {   // t / img_tiles_x by multiply-high: m = floor(2^32 / d) + 1 gives floor(t * m / 2^32) =
+        // floor(t / d) whenever t * (m d - 2^32) < 2^32 (the excess stays under one step of t / d)
+        const uint64_t d = (uint64_t)K.img_tiles_x, m = ((uint64_t)1 << 32) / std::max<uint64_t>(d, 1) + 1;
+        const uint64_t e = m * d - ((uint64_t)1 << 32);
+        K.tile_div_magic = (d >= 2 && m < ((uint64_t)1 << 32) && (uint64_t)img_tiles * e < ((uint64_t)1 << 32))
+                               ? (uint32_t)m : 0u;
+    }
     if (p->tile_shard && c->tile_order_n > 0) {   // the context's tile order: every tile shard takes it
         if (c->tile_order_n != img_tiles)
             return fail(RT_ERR_INVALID, "the tile order has " + std::to_string(c->tile_order_n) + " tiles, the frame " +

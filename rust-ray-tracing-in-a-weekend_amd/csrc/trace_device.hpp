@@ -1848,7 +1848,9 @@ __device__ __forceinline__ void image_xy(const KParams& P, int x, int k, int& X,
     if (P.tile_shard) {   // wave-uniform
         unsigned t = (unsigned)P.row_begin + (unsigned)(x >> 3) * (unsigned)P.row_stride;
         if (__builtin_expect(P.tile_order != nullptr, 0)) t = P.tile_order[t];
-        const unsigned ty = t / (unsigned)P.img_tiles_x;
+        // (the division by a runtime value was ~25 VALU instructions in every bounce-loop iteration
+        // that starts a sample: 0.7 % of C2's kernel as a world-1 tile shard, profiles/r06d_*)
+        const unsigned ty = P.tile_div_magic ? __umulhi(t, P.tile_div_magic) : t / (unsigned)P.img_tiles_x;
         X = (int)(t - ty * (unsigned)P.img_tiles_x) * 8 + (x & 7);
         Y = (int)ty * 8 + k;
     } else {

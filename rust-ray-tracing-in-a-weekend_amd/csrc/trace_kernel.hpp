@@ -105,7 +105,9 @@ struct KParams {
     int32_t tile_shard;         // rt_render_params.tile_shard: grid tile m = the frame's tile at position
                                 // row_begin + m*row_stride of tile_order (raster order if null)
     int32_t img_tiles_x;        // tiles per tile row of the image
-    int32_t pad0;               // (unused: keeps the fields below at the offsets the kernels were timed with)
+    // tile shards: ty = t / img_tiles_x as umulhi(t, tile_div_magic), exact for every tile t of the
+    // frame (host-checked: t * (magic * img_tiles_x - 2^32) < 2^32); 0: a plain division
+    uint32_t tile_div_magic;
     int32_t ring_waves;         // per-sample pool, in-kernel reduction: waves the ring holds (0: off)
     double* ring;               // per-sample pool, in-kernel reduction: kPoolRing blocks of records per wave
     // tile shards: the frame's tile order (rt_ctx_set_tile_order), position -> raster tile; null: raster

@@ -50,8 +50,10 @@ def test_f32_mode_agrees_statistically(rt, renderer, scene_id, W, H, spp, mean_t
 
 def test_f32_mode_all_scenes_and_schedules(rt, renderer):
     """Every reference scene renders in f32 (finite, non-negative, within a few % of the f64
-    image mean), and the f32 mode gives the same bits under every schedule and row shard
-    (its draws are keyed per (pixel, sample) like the f64 mode's)."""
+    image mean). The f32 mode's draws are keyed per (pixel, sample) like the f64 mode's, so a
+    row shard gives the bits of the whole frame; its translation units contract FMAs (round 6,
+    DESIGN.md §5.6), so the kernels of different schedules (CHUNKS / POOL / ITEMS: each compiles
+    the path code on its own) round differently in the last bits and agree statistically."""
     for scene_id in range(8):
         a = _render(rt, renderer, scene_id, 32, 24, 32, 3, rt.RT_PREC_F32)
         b = _render(rt, renderer, scene_id, 32, 24, 32, 3, rt.RT_PREC_F64)
@@ -82,5 +84,5 @@ def test_f32_mode_all_scenes_and_schedules(rt, renderer):
         renderer.set_precision(rt.RT_PREC_F64)
         renderer.set_schedule(rt.RT_SCHED_AUTO)
     for im in imgs[1:]:
-        assert np.array_equal(im, imgs[0])
-    assert np.array_equal(shard, imgs[0][1::3])
+        assert abs(float(im.mean()) / float(imgs[0].mean()) - 1.0) < 0.03
+    assert np.array_equal(shard, imgs[2][1::3])   # ITEMS, the last schedule set: the same kernel
