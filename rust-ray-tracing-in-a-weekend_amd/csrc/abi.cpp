@@ -1331,11 +1331,10 @@ static int run_range(rt_ctx* c, const rt_camera* cam, const rt_render_params* p,
     // the top levels of the BFS-ordered instance BLAS in LDS too (variants with nested walks),
     // as many as the LDS left over at the block count the rest of the layout allows
     S.n_lds_blas = 0;
-    if (c->S.n_blas_bfs > 0 && c->opt_lds_nodes && !o.f32 &&
-        (rtk::variant_features(o.features) & rtk::FEAT_INST_BLAS) != 0) {
+    if (c->S.n_blas_bfs > 0 && c->opt_lds_nodes && (rtk::variant_features(o.features) & rtk::FEAT_INST_BLAS) != 0) {
         const bool oct = o.slab32 && S.n_lds_nodes == c->n_tlas_nodes && S.n_lds_nodes > 0;
         const uint32_t variant = rtk::variant_features(o.features);
-        const int bt = rtk::block_threads_of(variant, false);   // workgroup threads (RT_BLOCK_FINAL)
+        const int bt = rtk::block_threads_of(variant, o.f32 != 0);   // workgroup threads (RT_BLOCK_FINAL)
         const size_t base = (size_t)S.n_lds_nodes * (oct ? 80 : 64) +
                             (o.lds_stack ? (size_t)c->S.stack_entries * (size_t)bt * 4 : 0) +
                             (size_t)S.n_lds_materials * 64 + (size_t)S.n_lds_textures * 96;

@@ -853,7 +853,7 @@ __host__ __device__ constexpr LdsLayout lds_layout(int n_nodes, int node_bytes, 
 #define RT_STAGE_BLAS 1
 #endif
 template <class C>
-constexpr bool StageBlas() { return RT_STAGE_BLAS && (C::F & FEAT_INST_BLAS) != 0 && !C::F32; }
+constexpr bool StageBlas() { return RT_STAGE_BLAS && (C::F & FEAT_INST_BLAS) != 0; }
 template <class C>
 __device__ __forceinline__ LdsLayout lds_layout_of(const SceneDev& S)
 {
@@ -2540,7 +2540,7 @@ static void launch_one(const Launch& L, hipStream_t stream, bool nall)
     const bool s16 = RT_STACK16 && LDS && nall && S32 && F == FEAT_SET_SPHERES;   // Stack16Cfg
     const int node_bytes = nall && S32 ? (int)sizeof(LdsNode) : (int)sizeof(rt_bvh_node);   // lds_node_bytes
     const bool stage = F != FEAT_SET_SPHERES;                   // StageShade
-    const bool blas = RT_STAGE_BLAS && (F & FEAT_INST_BLAS) != 0 && !F32;   // StageBlas
+    const bool blas = RT_STAGE_BLAS && (F & FEAT_INST_BLAS) != 0;   // StageBlas
     constexpr int bt = block_threads_of(F, F32), wpb = bt / 64;   // BlockThreads
     const size_t lds = lds_layout(S.n_lds_nodes, node_bytes, blas ? S.n_lds_blas : 0, LDS ? S.stack_entries : 0,
                                   s16 ? 2 : 4, stage ? S.n_lds_materials : 0, stage ? S.n_lds_textures : 0, bt).total;

@@ -35,7 +35,7 @@ namespace rtk {
 // workgroup threads of a kernel variant (host and device): see RT_BLOCK_FINAL, RT_BLOCK_F32_SPHERES
 __host__ __device__ constexpr int block_threads_of(uint32_t variant_features, bool f32)
 {
-    return variant_features == 287u /* FEAT_SET_FINAL */ && !f32  ? RT_BLOCK_FINAL
+    return variant_features == 287u /* FEAT_SET_FINAL */          ? RT_BLOCK_FINAL
            : variant_features == 0u /* FEAT_SET_SPHERES */ && f32 ? RT_BLOCK_F32_SPHERES
                                                                  : 256;
 }
