@@ -8,7 +8,7 @@ Prints per-build median kernel ms and whether the f64 test image equals the firs
 
 usage: python scripts/ab_builds.py lib/a.so lib/b.so [--scene 0 --width 1200 --height 800 --spp 500]
        (a build given as lib/a.so@opt9=0,opt1=4294967296 runs with those rt_ctx_set_option
-       keys and values, @optsched=2 with that rt_ctx_set_schedule; any other NAME=V pair is set
+       keys and values, @optsched=2 with that rt_ctx_set_schedule, @optprec=1 the f32 mode; any other NAME=V pair is set
        in the child's environment)
        Times are kernel + reduce ms (the frame's trace launches and their reductions).
 """
@@ -34,6 +34,8 @@ r = rt.Renderer(0)
 for k, v in a["opts"].items():
     if k == "sched":
         r.set_schedule(int(v))
+    elif k == "prec":
+        r.set_precision(int(v))
     else:
         r.set_option(int(k), int(v))
 r.upload(world)
