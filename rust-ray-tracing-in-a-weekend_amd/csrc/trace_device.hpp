@@ -2113,14 +2113,6 @@ __device__ __forceinline__ void ring_reduce(const KParams& P, const double* __re
     }
 }
 
-// Work-block prefetch: a wave takes its next block's id from the counter when it takes the current
-// one, so the atomic's round trip overlaps the current block's tracing instead of stalling the
-// refill (a block is ~6-20 bounce-loop iterations of the wave). The order in which blocks are
-// dealt changes, not which units exist, so the image does not.
-#ifndef RT_BLOCK_PREFETCH
-#define RT_BLOCK_PREFETCH 1
-#endif
-
 // ITEMS (the item pool, default): a unit is a (pixel, chunk) item instead of one sample.
 // The lane that takes it traces the chunk's samples in order, summing their radiance in
 // registers exactly as trace_chunks does, and writes one partial per (pixel, chunk) when
@@ -2184,10 +2176,6 @@ __global__ void __launch_bounds__(BlockThreads<C>(), min_waves<C>()) trace_pool(
     // as else-branches the spheres variant's kernel compiled to other code, 1.4 % slower on C2)
     int ringv = 0;                       // !RingSgpr: lane q slot q's block, kRingCur, kRingOcc
     unsigned occ = 0, cur_slot = 0;      // RingSgpr (the other form: read from ringv where used)
-    unsigned pre_b = 0;                  // RT_BLOCK_PREFETCH: lane 0, the next block's id (in flight)
-    bool have_pre = false;               //   (wave-uniform) pre_b holds one
-    (void)pre_b;
-    (void)have_pre;
     for (;;) {
         if constexpr (ring && !RingSgpr<C>()) {   // (final variant) the same, the state in ringv's lanes
             unsigned occv = (unsigned)__builtin_amdgcn_readlane(ringv, kRingOcc);
@@ -2237,21 +2225,8 @@ __global__ void __launch_bounds__(BlockThreads<C>(), min_waves<C>()) trace_pool(
                     free_slot = __builtin_ctz(~occ);
                 }
                 unsigned b = 0;
-                if constexpr (RT_BLOCK_PREFETCH) {
-                    // the block taken one fetch ago (lane 0's pre_b): its id arrived while the wave
-                    // traced the previous block, so this fetch does not wait on the atomic
-                    if (have_pre) {
-                        b = __builtin_amdgcn_readfirstlane(pre_b);
-                    } else {
-                        if (lane == 0) b = atomicAdd(work, 1u);
-                        b = __builtin_amdgcn_readfirstlane(b);
-                    }
-                    have_pre = b < n_blocks;
-                    if (have_pre && lane == 0) pre_b = atomicAdd(work, 1u);   // the next one, in flight
-                } else {
-                    if (lane == 0) b = atomicAdd(work, 1u);
-                    b = __builtin_amdgcn_readfirstlane(b);
-                }
+                if (lane == 0) b = atomicAdd(work, 1u);
+                b = __builtin_amdgcn_readfirstlane(b);
                 if (b >= n_blocks) {
                     exhausted = true;
                     break;
