@@ -1318,8 +1318,9 @@ static int run_range(rt_ctx* c, const rt_camera* cam, const rt_render_params* p,
     const long long total = s_end - s_begin;
     const size_t px_bytes = px * 3 * sizeof(double);
     // one sample's records in the per-sample buffer: whole 8x8 tiles (trace_kernel.hpp, tiled_record)
-    const rtk::SampleTiles tiles{lay.w, n_rows, (lay.w + 7) / 8};
-    const size_t sample_bytes = rtk::tiled_pixels(lay.w, n_rows) * 3 * sizeof(double);
+    // (the f32 mode's records are f32: SampleTiles.f32_records; trace_pool writes them so)
+    const rtk::SampleTiles tiles{lay.w, n_rows, (lay.w + 7) / 8, o.f32 ? 1 : 0};
+    const size_t sample_bytes = rtk::tiled_pixels(lay.w, n_rows) * 3 * (o.f32 ? sizeof(float) : sizeof(double));
     // the TLAS in LDS (read-only, shared by the block) when it fits the per-block budget
     rtk::SceneDev S = c->S;
     S.n_lds_nodes = c->opt_lds_nodes ? std::min(c->n_tlas_nodes, kMaxLdsNodes) : 0;

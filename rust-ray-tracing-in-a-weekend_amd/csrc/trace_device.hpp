@@ -2447,9 +2447,19 @@ __global__ void __launch_bounds__(BlockThreads<C>(), min_waves<C>()) trace_pool(
             } else {
                 o = samples + tiled_record(P.tiles_x, P.spp - P.sample_begin, x, k, s - P.sample_begin) * 3;
             }
-            o[0] = cr;
-            o[1] = cg;
-            o[2] = cb;
+            if constexpr (C::F32 && !ITEMS && !ring) {
+                // the f32 mode's per-sample records are f32 (SampleTiles.f32_records): half the bytes
+                float* of = reinterpret_cast<float*>(samples) +
+                            tiled_record(P.tiles_x, P.spp - P.sample_begin, x, k, s - P.sample_begin) * 3;
+                of[0] = (float)cr;
+                of[1] = (float)cg;
+                of[2] = (float)cb;
+                (void)o;
+            } else {
+                o[0] = cr;
+                o[1] = cg;
+                o[2] = cb;
+            }
             active = false;
         }
     }

@@ -23,8 +23,8 @@ __device__ __forceinline__ bool tile_slot(SampleTiles g, int n_samples, long lon
 // Per pixel: chunk sums of consecutive samples (chunk order, each from 0.0), added in
 // chunk order to 0.0 and scaled into out: the same additions, in the same order, as the
 // chunk schedule's lane sums + reduce_chunks.
-template <typename T>
-__global__ void __launch_bounds__(256) reduce_samples(const double* __restrict__ samples, T* __restrict__ out,
+template <typename T, typename Rec = double>
+__global__ void __launch_bounds__(256) reduce_samples(const Rec* __restrict__ samples, T* __restrict__ out,
                                                       SampleTiles g, long long n_slots, int n_samples, int chunk,
                                                       double scale)
 {
@@ -37,10 +37,10 @@ __global__ void __launch_bounds__(256) reduce_samples(const double* __restrict__
         const int c1 = min(n_samples, c0 + chunk);
         double cr = 0.0, cg = 0.0, cb = 0.0;
         for (int j = c0; j < c1; ++j) {
-            const double* p = samples + (rec + (size_t)j * 64) * 3;
-            cr = cr + p[0];
-            cg = cg + p[1];
-            cb = cb + p[2];
+            const Rec* p = samples + (rec + (size_t)j * 64) * 3;
+            cr = cr + (double)p[0];
+            cg = cg + (double)p[1];
+            cb = cb + (double)p[2];
         }
         r = r + cr;
         g_ = g_ + cg;
@@ -54,7 +54,8 @@ __global__ void __launch_bounds__(256) reduce_samples(const double* __restrict__
 // The same sums over a render split into buffer batches that need not end on a chunk
 // boundary: acc holds the closed chunks' total, open the chunk in progress (pos samples
 // in at batch start, uniform); `close` ends the render's last chunk.
-__global__ void __launch_bounds__(256) reduce_samples_carry(const double* __restrict__ samples,
+template <typename Rec = double>
+__global__ void __launch_bounds__(256) reduce_samples_carry(const Rec* __restrict__ samples,
                                                             double* __restrict__ acc, double* __restrict__ open,
                                                             SampleTiles g, long long n_slots, int n_samples,
                                                             int chunk, int pos, int close)
@@ -71,10 +72,10 @@ __global__ void __launch_bounds__(256) reduce_samples_carry(const double* __rest
         cb = open[3 * px + 2];
     }
     for (int j = 0; j < n_samples; ++j) {
-        const double* p = samples + (rec + (size_t)j * 64) * 3;
-        cr = cr + p[0];
-        cg = cg + p[1];
-        cb = cb + p[2];
+        const Rec* p = samples + (rec + (size_t)j * 64) * 3;
+        cr = cr + (double)p[0];
+        cg = cg + (double)p[1];
+        cb = cb + (double)p[2];
         if (++pos == chunk) {
             r = r + cr;
             g_ = g_ + cg;
@@ -273,7 +274,14 @@ hipError_t launch_reduce_samples(const double* samples, void* out, bool f64, Sam
     const long long n_slots = (long long)tiled_pixels(g.width, g.n_rows);
     const long long blocks = (n_slots + 255) / 256;
     if (blocks <= 0) return hipSuccess;
-    if (f64)
+    const float* rec32 = reinterpret_cast<const float*>(samples);
+    if (g.f32_records && f64)
+        hipLaunchKernelGGL((reduce_samples<double, float>), dim3((unsigned)blocks), dim3(256), 0, stream, rec32,
+                           (double*)out, g, n_slots, n_samples, chunk, scale);
+    else if (g.f32_records)
+        hipLaunchKernelGGL((reduce_samples<float, float>), dim3((unsigned)blocks), dim3(256), 0, stream, rec32,
+                           (float*)out, g, n_slots, n_samples, chunk, scale);
+    else if (f64)
         hipLaunchKernelGGL(reduce_samples<double>, dim3((unsigned)blocks), dim3(256), 0, stream, samples, (double*)out,
                            g, n_slots, n_samples, chunk, scale);
     else
@@ -288,8 +296,13 @@ hipError_t launch_reduce_samples_carry(const double* samples, double* acc, doubl
     const long long n_slots = (long long)tiled_pixels(g.width, g.n_rows);
     const long long blocks = (n_slots + 255) / 256;
     if (blocks <= 0) return hipSuccess;
-    hipLaunchKernelGGL(reduce_samples_carry, dim3((unsigned)blocks), dim3(256), 0, stream, samples, acc, open, g,
-                       n_slots, n_samples, chunk, pos, (int)close);
+    if (g.f32_records)
+        hipLaunchKernelGGL(reduce_samples_carry<float>, dim3((unsigned)blocks), dim3(256), 0, stream,
+                           reinterpret_cast<const float*>(samples), acc, open, g, n_slots, n_samples, chunk, pos,
+                           (int)close);
+    else
+        hipLaunchKernelGGL(reduce_samples_carry<double>, dim3((unsigned)blocks), dim3(256), 0, stream, samples, acc,
+                           open, g, n_slots, n_samples, chunk, pos, (int)close);
     return hipGetLastError();
 }
 

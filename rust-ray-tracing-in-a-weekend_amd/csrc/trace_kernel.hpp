@@ -181,6 +181,7 @@ struct LaunchOpts {
 // Edge tiles keep all 64 slots (unused ones are never written or read).
 struct SampleTiles {
     int32_t width, n_rows, tiles_x;
+    int32_t f32_records;   // the f32 mode's records: f32 x 3 (12 B) instead of f64 x 3 (24 B)
 };
 __host__ __device__ inline size_t tiled_record(int tiles_x, int n_samples, int x, int k, int s)
 {
