@@ -1456,9 +1456,14 @@ __device__ void hit_uv(const HitT<R>& h, R& u, R& v)
 
 // texture.rs:35-41: sin(10x)*sin(10y)*sin(10z) < 0 from the three signs (rt_sin_sign);
 // the full product only when a factor may be tiny enough to underflow it
-__device__ __forceinline__ bool checker_odd(const HitT<float>& h)   // f32 mode: the product itself
+// f32 mode: the same sign test without the three sinf: sin(10a) < 0 exactly when floor(10a / pi)
+// is odd, so the product is negative when the three floors sum to an odd number (the zeros of a
+// factor, where the reference's product is 0 and not < 0, are a measure-zero set)
+__device__ __forceinline__ bool checker_odd(const HitT<float>& h)
 {
-    return sinf(10.0f * h.px) * sinf(10.0f * h.py) * sinf(10.0f * h.pz) < 0.0f;
+    constexpr float k = (float)(10.0 / 3.14159265358979323846);
+    const int n = (int)__builtin_floorf(h.px * k) + (int)__builtin_floorf(h.py * k) + (int)__builtin_floorf(h.pz * k);
+    return (n & 1) != 0;
 }
 __device__ __forceinline__ bool checker_odd(const HitT<double>& h)
 {
