@@ -29,7 +29,7 @@ for s in "$@"; do
     bench_c5) specs+=("600:${P}bench_c5:python bench.py --config C5 --steps 3 --warmup 1") ;;
     f32_c2) specs+=("300:${P}f32_c2:python bench.py --steps 10 --warmup 2 --precision f32 $NB") ;;
     f32_c3) specs+=("300:${P}f32_c3:python bench.py --config C3 --steps 5 --warmup 1 --precision f32 $NB") ;;
-    f32_c4) specs+=("300:${P}f32_c4:python bench.py --config C4 --steps 2 --warmup 1 --precision f32 $NB") ;;
+    f32_c4) specs+=("300:${P}f32_c4:python bench.py --config C4 --steps 3 --warmup 1 --precision f32 $NB") ;;
     prof_c1) specs+=("500:${P}prof_c1:PROF_DIR=${P}prof_c1 BENCH_ARGS='--config C1 --steps 2 --warmup 1 $NB' scripts/profile_r02.sh") ;;
     prof_c2) specs+=("700:${P}prof_c2:PROF_DIR=${P}prof_c2 scripts/profile_r02.sh") ;;
     prof_c3) specs+=("700:${P}prof_c3:PROF_DIR=${P}prof_c3 BENCH_ARGS='--config C3 --steps 1 --warmup 0 $NB' scripts/profile_r02.sh") ;;
