@@ -648,6 +648,8 @@ def main():
                                   "control_plane": "torch.distributed gloo", "world_size": world,
                                   "forced_at_world_1": bool(args.force_dist and world == 1)}
         print(json.dumps(out), flush=True)
+    if dist_on:   # every rank done with the communicator before any destroys it
+        dist.barrier()
     if comm is not None:   # the RCCL communicator before the process group and the context
         comm.close()
     renderer.close()
