@@ -1842,9 +1842,15 @@ __device__ __forceinline__ bool shade_end(const SceneDev& S, const HitT<R>& h, R
         // cover at grazing angles on the final scene's |p| ~ 1000 boxes (the next ray would hit
         // its own surface again); move the origin off the surface, to the side the new ray
         // leaves on (Wachter & Binder, Ray Tracing Gems ch. 6). Media (uvkind 0) have no surface.
+        // The scale is measured (round 6, C4 geometry at 16 spp, count variant; f64 paths: 3.690
+        // casts per sample, 9.75 node visits per cast): |p| 2^-23 4.44 / 11.88, 2^-21 4.33 /
+        // 11.85, 2^-19 (rounds 3-5) 4.14 / 11.64, 2^-17 3.93 / 10.85, 2^-15 3.696 / 9.72, 2^-13
+        // 3.693 / 9.53 (profiles/r06m_*, r06n_*, r06o_*). Below 2^-15 the f32 paths re-hit their
+        // own surfaces and run longer than the reference's; 2^-15 gives its path lengths (and
+        // the statistical parity of tests/test_gpu_f32.py), 2^-13 starts to skip geometry.
         if (h.uvkind != 0) {
             const float m = fmaxf(fmaxf(__builtin_fabsf(h.px), __builtin_fabsf(h.py)), __builtin_fabsf(h.pz));
-            float eps = m * 0x1.0p-19f + 1e-5f;
+            float eps = m * 0x1.0p-15f + 1e-5f;
             if (sdx * h.nx + sdy * h.ny + sdz * h.nz < 0.0f) eps = -eps;
             r.ox = h.px + h.nx * eps;
             r.oy = h.py + h.ny * eps;

@@ -5,8 +5,8 @@
 #   pmc    (here, afterwards) profiles/pmc.json entries + r06_final_c*_pmc.md from them
 #   lines  the bench lines of C1-C5 (>= 3 timed steps each), the default line and the f32 lines
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-PROF="${PROF:-r06k_}"
-LINES="${LINES:-r06l_}"
+PROF="${PROF:-r06p_}"
+LINES="${LINES:-r06q_}"
 case "${1:-}" in
 prof1) PREFIX=$PROF scripts/gpu_session.sh tests smoke prof_c1 prof_c2 prof_c3 ;;
 prof2) PREFIX=$PROF scripts/gpu_session.sh prof_c4 prof_c5 ;;
