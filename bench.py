@@ -95,6 +95,9 @@ def parse():
                          "(default: cost at N > 1, raster at N = 1). The pass runs before the timed steps and "
                          "its time is amortised into the headline value (value_steady leaves it out)")
     ap.add_argument("--cost-spp", type=int, default=8, help="spp of the --tile-order cost pass")
+    ap.add_argument("--comm-direct", type=int, default=1, choices=[0, 1],
+                    help="RT_OPT_COMM_DIRECT: 1 (default) a world of one in raster order renders straight into "
+                         "the frame inside rt_render_gather; 0 the tile shard + RCCL gather + reorder as at N > 1")
     ap.add_argument("--device", type=int, default=None,
                     help="GPU index for every rank (default: LOCAL_RANK); with --transport gloo, ranks may share one")
     ap.add_argument("--force-dist", action="store_true",
@@ -273,6 +276,7 @@ def main():
         renderer.set_option(rt.RT_OPT_TRACE_BUF_BYTES, args.buf_mb << 20)
     if args.no_overlap:
         renderer.set_option(rt.RT_OPT_BATCH_OVERLAP, 0)
+    renderer.set_option(rt.RT_OPT_COMM_DIRECT, args.comm_direct)
     comm = None
     if transport == "rccl":   # rank 0 makes the RCCL unique id, torch (gloo) hands it to the others
         with stdout_to_stderr():   # RCCL's version banner: stdout carries the one JSON line alone
@@ -439,6 +443,7 @@ def main():
         per_rank = [{"rank": r, "kernel_ms": round(float(v[0]), 3), "gather_ms": round(float(v[1]), 3),
                      "render_ms": round(float(v[2]), 3), "samples": int(v[3])} for r, v in enumerate(allr)]
     last = renderer.stats()
+    direct = comm is not None and comm.stats().slab_bytes == 0   # the world-1 direct render (RT_OPT_COMM_DIRECT)
 
     samples_per_step = W * H * spp
     # the headline: the timed steps plus the tile-order cost pass amortised over them (the pass is
@@ -616,13 +621,15 @@ def main():
                             "the timed steps alone" % t_order) if t_order > 0 else "timed steps (no cost pass)",
             "config": {"workload": "%s %s %dx%d, %d spp, max depth %d, %s-sharded over %d GPU"
                                    % (args.config, SCENE_NAMES.get(args.scene, "scene %d" % args.scene), W, H, spp,
-                                      depth, "tile" if tiles else "row" if gloo else "not", world),
+                                      depth, "tile" if tiles and not direct else "row" if gloo else "not", world),
                        "scene": args.scene, "width": W, "height": H, "spp": spp, "max_depth": depth,
                        "tile_order": order_mode if tiles else None,
                        "parallelism": "%s interleaved over %d rank(s), %s"
-                                      % (("8x8 tiles (%s order)" % order_mode) if tiles else
+                                      % (("8x8 tiles (%s order)" % order_mode) if tiles and not direct else
                                          "rows" if gloo else "whole frame", world,
                                          "gloo gather (host-staged)" if gloo else
+                                         "rt_render_gather of a world of one: straight into the frame, no gather "
+                                         "(RT_OPT_COMM_DIRECT)" if direct else
                                          "RCCL gather (library communicator, rt_render_gather)" if comm is not None
                                          else "no gather")},
             "roofline": roofline,

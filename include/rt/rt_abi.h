@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 5
+#define RT_ABI_VERSION 6   /* v6: RT_OPT_COMM_DIRECT */
 
 enum {
     RT_OK = 0,
@@ -430,7 +430,11 @@ int rt_ctx_set_variant(rt_ctx* ctx, int slab32, int lds_stack, int lds_nodes);
  *   RT_OPT_POOL_RING        1 (default): POOL reduces each finished (tile, chunk) block inside the
  *                           trace kernel into chunk partials when its per-sample buffer would not
  *                           fit the bound in one batch; 2: whenever its blocks allow; 0: never (the
- *                           per-sample buffer and reduce_samples; see RT_SCHED_POOL) */
+ *                           per-sample buffer and reduce_samples; see RT_SCHED_POOL)
+ *   RT_OPT_COMM_DIRECT      1 (default): rt_render_gather on a communicator of one rank, with the
+ *                           context in raster tile order, is rt_render straight into the frame (a
+ *                           world of one has nothing to gather); 0: the tile shard, the RCCL gather
+ *                           and the reorder kernel as at any other world size (tests) */
 enum {
     RT_OPT_TRACE_BUF_BYTES = 1,
     RT_OPT_BATCH_OVERLAP = 2,
@@ -439,7 +443,8 @@ enum {
     RT_OPT_EXTRA_FEATURES = 5,
     RT_OPT_HOIST = 6,
     /* 7, 8: ABI v4's wavefront-schedule options, removed with it (RT_ERR_INVALID) */
-    RT_OPT_POOL_RING = 9
+    RT_OPT_POOL_RING = 9,
+    RT_OPT_COMM_DIRECT = 10
 };
 int rt_ctx_set_option(rt_ctx* ctx, int key, int64_t value);
 int rt_ctx_get_option(rt_ctx* ctx, int key, int64_t* value);

@@ -103,6 +103,7 @@ struct rt_ctx {
     int block_samples = 0;              // RT_OPT_BLOCK_SAMPLES: samples per per-sample-pool work block (0: auto)
     int opt_ring = 1;                   // RT_OPT_POOL_RING: POOL reduces finished blocks in the kernel (0 never,
                                         // 1 when its per-sample buffer would not fit the bound, 2 always)
+    int opt_comm_direct = 1;            // RT_OPT_COMM_DIRECT: a world-1 rt_render_gather renders straight into the frame
     double* ring = nullptr;             // its per-wave record ring (kPoolRing blocks per wave)
     size_t ring_cap = 0;
     unsigned long long raw_counters[kCounters] = {};   // the last count_work render's counters (rt_last_counters)
@@ -2014,6 +2015,7 @@ int rt_ctx_set_option(rt_ctx* c, int key, int64_t v)
         if (v < 0 || v > 2) return fail(RT_ERR_INVALID, "pool ring mode out of range (0 never, 1 when needed, 2 always)");
         c->opt_ring = (int)v;
         return RT_OK;
+    case RT_OPT_COMM_DIRECT: c->opt_comm_direct = v != 0; return RT_OK;
     default: return fail(RT_ERR_INVALID, "unknown option");
     }
 }
@@ -2029,6 +2031,7 @@ int rt_ctx_get_option(rt_ctx* c, int key, int64_t* v)
     case RT_OPT_EXTRA_FEATURES: *v = c->extra_features; return RT_OK;
     case RT_OPT_HOIST: *v = c->opt_hoist; return RT_OK;
     case RT_OPT_POOL_RING: *v = c->opt_ring; return RT_OK;
+    case RT_OPT_COMM_DIRECT: *v = c->opt_comm_direct; return RT_OK;
     default: return fail(RT_ERR_INVALID, "unknown option");
     }
 }
@@ -2076,4 +2079,5 @@ const uint32_t* ctx_tile_order(const rt_ctx* c, int64_t* n)
 }
 int ctx_schedule(const rt_ctx* c) { return c->opt_pool; }
 int ctx_precision(const rt_ctx* c) { return c->opt_precision; }
+bool ctx_comm_direct(const rt_ctx* c) { return c->opt_comm_direct != 0; }
 }  // namespace rtx

@@ -125,6 +125,7 @@ struct rt_comm {
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};   // render start / end, gathered, assembled
     rt_comm_stats stats{};
     bool pending = false;       // a gather's events not yet read into stats
+    bool direct = false;        // the last frame was a world-1 direct render (no slabs gathered)
     size_t status_off = 0;      // byte offset of the status trailer in a slab (rank 0: to check the peers')
     size_t slab_stride = 0;     // bytes per rank in recv
 };
@@ -250,8 +251,41 @@ int peer_status(rt_comm* m)
 void note_gather(rt_comm* m, const Shard& f)
 {
     m->pending = true;
+    m->direct = false;
     m->stats.slab_bytes = (int64_t)f.slab_bytes;
     m->stats.tiles = f.n_mine;
+}
+
+// A world of one (RT_OPT_COMM_DIRECT, raster tile order): rt_render straight into the frame.
+// The frame is the tile path's bit for bit (every draw keyed by (pixel, sample)); it skips the
+// slab, the one-rank gather and the reorder pass (C2 at N = 1: 75.09 -> 74.70-74.92 ms per step,
+// profiles/r06e_c2_*.log). The stats' gather and assemble times are 0.
+bool direct_ok(const rt_comm* m)
+{
+    int64_t n_order = 0;
+    (void)rtx::ctx_tile_order(m->ctx, &n_order);
+    return m->world == 1 && n_order == 0 && rtx::ctx_comm_direct(m->ctx);
+}
+
+int render_direct(rt_comm* m, const rt_camera* cam, const rt_render_params* p, hipStream_t s, void* frame)
+{
+    if (bad_frame(p)) return fail(RT_ERR_INVALID, "bad render params");
+    rt_render_params q = *p;
+    q.row_begin = 0;
+    q.row_stride = 1;
+    q.row_block = 0;
+    q.tile_shard = 0;
+    q.stream = s;
+    HIP_TRY(hipSetDevice(m->device));
+    HIP_TRY(hipEventRecord(m->ev[0], s));
+    const int rc = rt_render(m->ctx, cam, &q, frame);
+    HIP_TRY(hipSetDevice(m->device));
+    for (int i = 1; i < 4; ++i) HIP_TRY(hipEventRecord(m->ev[i], s));
+    m->pending = true;
+    m->direct = true;
+    m->stats.slab_bytes = 0;
+    m->stats.tiles = rt_tiles_in_shard(p->width, p->height, 0, 1);
+    return rc;
 }
 
 int check_comms(rt_comm* const* comms, int n)
@@ -505,6 +539,7 @@ int rt_render_gather(rt_comm* m, const rt_camera* cam, const rt_render_params* p
 {
     if (!m || !cam || !p) return fail(RT_ERR_INVALID, "null argument");
     if (m->rank == 0 && !frame) return fail(RT_ERR_INVALID, "rank 0 needs a frame");
+    if (direct_ok(m)) return render_direct(m, cam, p, stream_of(m, p), frame);
     const Rccl* R;
     int rc = load_rccl(R);
     if (rc) return rc;
@@ -537,6 +572,7 @@ int rt_render_gather_all(rt_comm* const* comms, int n, const rt_camera* cam, con
     const Rccl* R;
     rc = load_rccl(R);
     if (rc) return rc;
+    if (n == 1 && direct_ok(comms[0])) return render_direct(comms[0], cam, p, rtx::ctx_stream(comms[0]->ctx), frame);
     std::vector<Shard> f((size_t)n);
     for (int i = 0; i < n; ++i) {
         rc = shard_of(comms[i], p, rtx::ctx_stream(comms[i]->ctx), f[(size_t)i]);
@@ -598,7 +634,7 @@ int rt_comm_last_stats(rt_comm* m, rt_comm_stats* out)
         rt_stats st;
         if (rt_last_stats(m->ctx, &st) == RT_OK) m->stats.kernel_ms = st.kernel_ms;
         m->stats.peer_failed = 0;
-        for (int r = 0; m->rank == 0 && r < m->world; ++r) {
+        for (int r = 0; m->rank == 0 && !m->direct && r < m->world; ++r) {
             int32_t v = 0;
             HIP_TRY(hipMemcpy(&v, (char*)m->recv + (size_t)r * m->slab_stride + m->status_off, 4, hipMemcpyDeviceToHost));
             m->stats.peer_failed += v != 0;

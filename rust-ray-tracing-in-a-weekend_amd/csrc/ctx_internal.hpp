@@ -24,5 +24,7 @@ const uint32_t* ctx_tile_order(const rt_ctx* c, int64_t* n);
 // rt_ctx_set_schedule / rt_ctx_set_precision as set (RT_SCHED_*, RT_PREC_*)
 int ctx_schedule(const rt_ctx* c);
 int ctx_precision(const rt_ctx* c);
+// RT_OPT_COMM_DIRECT as set
+bool ctx_comm_direct(const rt_ctx* c);
 
 }  // namespace rtx

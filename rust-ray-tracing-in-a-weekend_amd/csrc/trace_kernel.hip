@@ -51,6 +51,82 @@ __global__ void __launch_bounds__(256) reduce_samples(const Rec* __restrict__ sa
     out[3 * px + 2] = (T)(b * scale);
 }
 
+// reduce_samples with one block per 8x8 tile: wave w of kReduceWaves sums chunks w, w + W, ... of
+// the tile's 64 pixels (each chunk from 0.0, its samples in order, four samples' loads in flight),
+// parks the chunk sums in LDS, and wave 0 adds a round's W chunk sums in chunk order to the running
+// total: reduce_samples' additions in reduce_samples' order (bit-identical), with W waves' loads
+// in flight per tile instead of one lane's walk over every sample, and no tail of long per-pixel
+// loops at the end of the launch.
+#ifndef RT_REDUCE_TILED
+#define RT_REDUCE_TILED 1
+#endif
+constexpr int kReduceWaves = 8;
+template <typename T, typename Rec = double>
+__global__ void __launch_bounds__(64 * kReduceWaves) reduce_samples_tiled(const Rec* __restrict__ samples,
+                                                                          T* __restrict__ out, SampleTiles g,
+                                                                          int n_samples, int chunk, double scale)
+{
+    __shared__ double part[kReduceWaves][3][64];
+    const unsigned tile = blockIdx.x;
+    const int lane = (int)(threadIdx.x & 63u), w = (int)(threadIdx.x >> 6);
+    const Rec* base = samples + ((size_t)tile * (size_t)n_samples * 64 + (size_t)lane) * 3;
+    const int n_chunks = (n_samples + chunk - 1) / chunk;
+    double r = 0.0, g_ = 0.0, b = 0.0;
+    for (int c0 = 0; c0 < n_chunks; c0 += kReduceWaves) {
+        const int c = c0 + w;
+        if (c < n_chunks) {
+            const int j0 = c * chunk, j1 = min(n_samples, j0 + chunk);
+            double cr = 0.0, cg = 0.0, cb = 0.0;
+            int j = j0;
+            for (; j + 4 <= j1; j += 4) {
+                Rec v[4][3];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const Rec* p = base + (size_t)(j + q) * 192;
+                    v[q][0] = p[0];
+                    v[q][1] = p[1];
+                    v[q][2] = p[2];
+                }
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    cr = cr + (double)v[q][0];
+                    cg = cg + (double)v[q][1];
+                    cb = cb + (double)v[q][2];
+                }
+            }
+            for (; j < j1; ++j) {
+                const Rec* p = base + (size_t)j * 192;
+                cr = cr + (double)p[0];
+                cg = cg + (double)p[1];
+                cb = cb + (double)p[2];
+            }
+            part[w][0][lane] = cr;
+            part[w][1][lane] = cg;
+            part[w][2][lane] = cb;
+        }
+        __syncthreads();
+        if (w == 0) {
+            const int nc = min(kReduceWaves, n_chunks - c0);
+            for (int q = 0; q < nc; ++q) {
+                r = r + part[q][0][lane];
+                g_ = g_ + part[q][1][lane];
+                b = b + part[q][2][lane];
+            }
+        }
+        __syncthreads();
+    }
+    if (w == 0) {
+        const int x = (int)(tile % (unsigned)g.tiles_x) * 8 + (lane & 7);
+        const int k = (int)(tile / (unsigned)g.tiles_x) * 8 + (lane >> 3);
+        if (x < g.width && k < g.n_rows) {
+            const size_t px = (size_t)k * (size_t)g.width + (size_t)x;
+            out[3 * px + 0] = (T)(r * scale);
+            out[3 * px + 1] = (T)(g_ * scale);
+            out[3 * px + 2] = (T)(b * scale);
+        }
+    }
+}
+
 // The same sums over a render split into buffer batches that need not end on a chunk
 // boundary: acc holds the closed chunks' total, open the chunk in progress (pos samples
 // in at batch start, uniform); `close` ends the render's last chunk.
@@ -272,9 +348,27 @@ hipError_t launch_reduce_samples(const double* samples, void* out, bool f64, Sam
                                  int chunk, double scale, hipStream_t stream)
 {
     const long long n_slots = (long long)tiled_pixels(g.width, g.n_rows);
+    const float* rec32 = reinterpret_cast<const float*>(samples);
+    if (RT_REDUCE_TILED) {   // one block per tile
+        const long long tiles = n_slots / 64;
+        if (tiles <= 0 || chunk < 1) return tiles <= 0 ? hipSuccess : hipErrorInvalidValue;
+        const dim3 grid((unsigned)tiles), block(64 * kReduceWaves);
+        if (g.f32_records && f64)
+            hipLaunchKernelGGL((reduce_samples_tiled<double, float>), grid, block, 0, stream, rec32, (double*)out, g,
+                               n_samples, chunk, scale);
+        else if (g.f32_records)
+            hipLaunchKernelGGL((reduce_samples_tiled<float, float>), grid, block, 0, stream, rec32, (float*)out, g,
+                               n_samples, chunk, scale);
+        else if (f64)
+            hipLaunchKernelGGL(reduce_samples_tiled<double>, grid, block, 0, stream, samples, (double*)out, g, n_samples,
+                               chunk, scale);
+        else
+            hipLaunchKernelGGL(reduce_samples_tiled<float>, grid, block, 0, stream, samples, (float*)out, g, n_samples,
+                               chunk, scale);
+        return hipGetLastError();
+    }
     const long long blocks = (n_slots + 255) / 256;
     if (blocks <= 0) return hipSuccess;
-    const float* rec32 = reinterpret_cast<const float*>(samples);
     if (g.f32_records && f64)
         hipLaunchKernelGGL((reduce_samples<double, float>), dim3((unsigned)blocks), dim3(256), 0, stream, rec32,
                            (double*)out, g, n_slots, n_samples, chunk, scale);

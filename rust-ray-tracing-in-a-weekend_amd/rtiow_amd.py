@@ -50,6 +50,7 @@ RT_OPT_BLOCK_CHUNKS = 4
 RT_OPT_EXTRA_FEATURES = 5
 RT_OPT_HOIST = 6
 RT_OPT_POOL_RING = 9
+RT_OPT_COMM_DIRECT = 10
 # SAH builder options (rt_world_set_build_option)
 RT_BUILD_C_ISECT = 1
 RT_BUILD_MAX_LEAF = 2

@@ -44,13 +44,14 @@ img = r.render(cam, rt.Renderer.params(a["width"], a["height"], 2, a["depth"], b
 p = rt.Renderer.params(a["width"], a["height"], a["spp"], a["depth"], bg, 1, out_format=rt.RT_OUT_F32)
 out = np.empty((a["height"], a["width"], 3), np.float32)
 r.render(cam, p, out)
-ms = []
+ms, red = [], []
 for _ in range(a["reps"]):
     r.render(cam, p, out)
     st = r.stats()
     ms.append(st.kernel_ms + st.reduce_ms)
+    red.append(st.reduce_ms)
 import hashlib
-print("RESULT", json.dumps({{"ms": ms, "trace_buf_bytes": st.trace_buf_bytes, "n_batches": st.n_batches,
+print("RESULT", json.dumps({{"ms": ms, "reduce_ms": red, "trace_buf_bytes": st.trace_buf_bytes, "n_batches": st.n_batches,
                             "ring_bytes": getattr(st, "ring_bytes", 0), "img": hashlib.sha1(img.tobytes()).hexdigest(),
                             "frame": hashlib.sha1(out.tobytes()).hexdigest()}}))
 """
@@ -69,6 +70,7 @@ def main():
     a = ap.parse_args()
     base_args = dict(scene=a.scene, width=a.width, height=a.height, spp=a.spp, depth=a.depth, reps=a.reps)
     res = {lib: [] for lib in a.libs}
+    red = {lib: [] for lib in a.libs}
     imgs = {}
     for _ in range(a.rounds):
         for lib in a.libs:
@@ -84,6 +86,7 @@ def main():
             line = [x for x in out.stdout.splitlines() if x.startswith("RESULT ")][-1]
             d = json.loads(line[7:])
             res[lib] += d["ms"]
+            red[lib] += d.get("reduce_ms", [])
             imgs[lib] = (d["img"], d.get("frame"))
             print(f"  {lib}: {['%.2f' % m for m in d['ms']]}  buf {d['trace_buf_bytes'] / 2**30:.2f} GiB "
                   f"(ring {d['ring_bytes'] / 2**30:.2f}) batches {d['n_batches']}", flush=True)
@@ -93,7 +96,8 @@ def main():
         ms = sorted(res[lib])[len(res[lib]) // 2]
         print(f"{lib}: median {ms:.2f} ms  min {min(res[lib]):.2f}  -> {n / ms / 1e3:.1f} Msamples/s  "
               f"image == {a.libs[0]}: {imgs[lib][0] == base[0]}  whole timed frame == {a.libs[0]}: "
-              f"{imgs[lib][1] == base[1]}")
+              f"{imgs[lib][1] == base[1]}"
+              + (f"  reduce median {sorted(red[lib])[len(red[lib]) // 2]:.3f} ms" if red[lib] else ""))
 
 
 if __name__ == "__main__":

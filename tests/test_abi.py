@@ -27,7 +27,7 @@ def test_library_exports_every_header_symbol(rt):
     missing = [s for s in declared if not hasattr(lib, s)]
     assert not missing, missing
     assert sorted(declared) == sorted(rt.EXPORTED)
-    assert lib.rt_abi_version() == 5
+    assert lib.rt_abi_version() == 6
 
 
 @pytest.mark.parametrize("scene_id", range(8))

@@ -98,9 +98,10 @@ def test_bench_py_n2_branch_equals_n1(tmp_path):
     samples = 160 * 90 * 8 * 2
     assert abs(j2["value"] - samples / (j2["ms_per_step"] * 2e-3) / 1e6) <= 1e-3 * j2["value"] + 1e-3
     assert abs(samples / (j2["value_steady"] * 1e6) + pass_s - samples / (j2["value"] * 1e6)) < 1e-3
-    # N = 1: no cost pass, one value; its path is rt_render_gather over a world-1 communicator
+    # N = 1: no cost pass, one value; its path is rt_render_gather over a world-1 communicator,
+    # which renders straight into the frame (RT_OPT_COMM_DIRECT)
     assert j1["value"] == j1["value_steady"] and j1["detail"]["tile_order_pass_s"] is None
-    assert "RCCL gather (library communicator" in j1["config"]["parallelism"]
+    assert "rt_render_gather of a world of one" in j1["config"]["parallelism"]
 
 
 @pytest.mark.timeout(900)
@@ -123,10 +124,12 @@ def test_bench_py_rccl_branch_at_world_size_1(tmp_path):
     control plane broadcasts the RCCL unique id, rt_comm_init_rank, rt_comm_tile_order (the count
     pass of the rank's shard, the RCCL all-reduce of the tile costs, the cost order set),
     rt_render_gather per step (the shard, the RCCL gather, the reorder kernel), the barriers and the
-    MAX all-reduce. Its frame and PPM equal the plain N = 1 run (rt_render_gather, raster order)
-    and the --transport none run (rt_render straight into the frame) bit for bit."""
+    MAX all-reduce. Its frame and PPM equal the plain N = 1 run (rt_render_gather of a world of one:
+    straight into the frame), the same with --comm-direct 0 (the raster tile shard, the RCCL
+    gather, the reorder kernel) and the --transport none run (rt_render) bit for bit."""
     jd, fd, pd = _bench(tmp_path, 1, "rccl1", extra=("--tile-order", "cost"), rccl=True)
     j1, f1, p1 = _bench(tmp_path, 1, "plain1")
+    js, fs, ps = _bench(tmp_path, 1, "shard1", extra=("--comm-direct", "0"))
     jn, fn, pn = _bench(tmp_path, 1, "none1", extra=("--transport", "none"))
     assert jd["n_gpus"] == 1 and "RCCL gather (library communicator" in jd["config"]["parallelism"]
     assert "8x8 tiles (cost order)" in jd["config"]["parallelism"] and jd["config"]["tile_order"] == "cost"
@@ -136,11 +139,13 @@ def test_bench_py_rccl_branch_at_world_size_1(tmp_path):
     pr = jd["per_rank"]
     assert len(pr) == 1 and pr[0]["kernel_ms"] > 0 and pr[0]["gather_ms"] >= 0 and pr[0]["samples"] >= 160 * 90 * 8
     assert pr[0]["render_ms"] >= pr[0]["kernel_ms"]
-    assert "per_rank" not in j1 and "8x8 tiles (raster order)" in j1["config"]["parallelism"]
+    assert "per_rank" not in j1 and "rt_render_gather of a world of one" in j1["config"]["parallelism"]
+    assert j1["detail"]["gather_ms_mean"] <= js["detail"]["gather_ms_mean"]
+    assert "8x8 tiles (raster order)" in js["config"]["parallelism"] and "RCCL gather" in js["config"]["parallelism"]
     assert "no gather" in jn["config"]["parallelism"] and jn["detail"]["gather_ms_mean"] is None
-    assert fd.dtype == np.float64 and fd.shape == f1.shape == fn.shape == (90, 160, 3)
-    assert np.array_equal(fd, f1) and np.array_equal(fn, f1)
-    assert pd == p1 == pn
+    assert fd.dtype == np.float64 and fd.shape == f1.shape == fs.shape == fn.shape == (90, 160, 3)
+    assert np.array_equal(fd, f1) and np.array_equal(fs, f1) and np.array_equal(fn, f1)
+    assert pd == p1 == ps == pn
 
 
 @pytest.mark.timeout(900)

@@ -4,8 +4,9 @@ the merge of their buffers (main.rs:542-547) — on the box's one GPU.
 
 - World size 1 through the library's own RCCL communicator, both constructors
   (rt_comm_init_rank with a unique id, rt_comm_init_all): the tile shard, the RCCL gather, the
-  reorder kernel; frames bit-identical to rt_render's, raster and cost tile order, f64 and f32,
-  host and device output.
+  reorder kernel (RT_OPT_COMM_DIRECT 0, or a cost tile order), and the direct render of a world
+  of one (the default); frames bit-identical to rt_render's, raster and cost tile order, f64 and
+  f32, host and device output.
 - The reorder kernel alone (rt_tiles_assemble) with N = 2, 3, 8 shard slabs rendered one after
   the other on the one GPU, in the padded layout the gather lands on rank 0: bit-identical to
   the one-launch frame in raster and cost order, and equal to the host restatement
@@ -35,12 +36,18 @@ def _params(rt, bg, fmt, spp=SPP, **kw):
 
 
 @pytest.mark.timeout(300)
-def test_render_gather_world1_equals_render(rt, scene_renderer):
+@pytest.mark.parametrize("direct", [0, 1])
+def test_render_gather_world1_equals_render(rt, scene_renderer, direct):
+    """direct 0: the tile shard, the RCCL gather and the reorder kernel, as at any world size;
+    direct 1 (RT_OPT_COMM_DIRECT, the default): a world of one in raster order renders straight
+    into the frame (no slab, no gather). Under a cost order both take the shard path."""
     cam, bg = rt.scene_camera(0, W, H)
     r = scene_renderer
     comm = rt.Comm(r, 0, 1, rt.Comm.unique_id())
     try:
-        assert r.lib.rt_abi_version() == 5
+        assert r.lib.rt_abi_version() == 6
+        r.set_option(rt.RT_OPT_COMM_DIRECT, direct)
+        assert r.get_option(rt.RT_OPT_COMM_DIRECT) == direct
         for fmt in (rt.RT_OUT_F64, rt.RT_OUT_F32):
             r.set_tile_order(None)
             ref = r.render(cam, _params(rt, bg, fmt))
@@ -48,7 +55,8 @@ def test_render_gather_world1_equals_render(rt, scene_renderer):
             assert got.dtype == ref.dtype and np.array_equal(got, ref), fmt
             st = comm.stats()
             n_tiles = 20 * 12
-            assert st.tiles == n_tiles and st.slab_bytes == 192 * n_tiles * (8 if fmt == rt.RT_OUT_F64 else 4) + 8
+            slab = 192 * n_tiles * (8 if fmt == rt.RT_OUT_F64 else 4) + 8
+            assert st.tiles == n_tiles and st.slab_bytes == (0 if direct else slab)
             assert st.render_ms >= st.kernel_ms > 0 and st.gather_ms >= 0 and st.assemble_ms >= 0
             assert st.peer_failed == 0
             # the cost order (count pass, RCCL all-reduce, the order set): same bits, tiles dealt anew
@@ -57,10 +65,12 @@ def test_render_gather_world1_equals_render(rt, scene_renderer):
             assert st.tile_order == 1 and st.cost_pass_ms > 0
             again = comm.render_gather(cam, _params(rt, bg, fmt))
             assert np.array_equal(again, ref), fmt
+            assert comm.stats().slab_bytes == slab   # a tile order: the shard path
         r.set_tile_order(None)
     finally:
         comm.close()
         r.set_tile_order(None)
+        r.set_option(rt.RT_OPT_COMM_DIRECT, 1)
 
 
 @pytest.mark.timeout(300)
