@@ -53,6 +53,11 @@ constexpr int kMaxLdsStack = 48;
 // TLAS nodes kept in LDS (32 KB per block): the first kMaxLdsNodes in BFS order, i.e.
 // the top levels; deeper ones are read from L1/L2
 constexpr int kMaxLdsNodes = 512;
+// waves per SIMD of the final-scene variant (trace_device.hpp min_waves: its LDS budget is per
+// workgroup of the workgroups those waves make)
+#ifndef RT_MIN_WAVES_FINAL
+#define RT_MIN_WAVES_FINAL 4
+#endif
 // instance BLAS nodes staged in LDS at most (64 B each)
 #ifndef RT_LDS_BLAS_MAX
 #define RT_LDS_BLAS_MAX 1024   // the LDS budget decides (512-thread final variant: 512 of the final scene's 548
@@ -1346,7 +1351,8 @@ static int run_range(rt_ctx* c, const rt_camera* cam, const rt_render_params* p,
         // workgroups than the variant's registers allow (final scene 4 waves per SIMD, the
         // all-features variant 3: 16 or 12 waves per CU)
         const size_t lds_cu = c->lds_per_cu, granule = 1024;
-        const size_t wave_blocks = std::max<size_t>(1, (size_t)(variant == rtk::FEAT_SET_FINAL ? 16 : 12) / (size_t)(bt / 64));
+        const size_t wave_blocks = std::max<size_t>(1, (size_t)(variant == rtk::FEAT_SET_FINAL ? 4 * RT_MIN_WAVES_FINAL : 12) /
+                                                           (size_t)(bt / 64));
         const size_t blocks = std::max<size_t>(1, std::min(wave_blocks,
             lds_cu / (((std::max<size_t>(base, 1) + granule - 1) / granule) * granule)));
         const size_t budget = std::min(lds_cu / blocks, c->lds_per_block) / granule * granule;
@@ -1375,12 +1381,12 @@ static int run_range(rt_ctx* c, const rt_camera* cam, const rt_render_params* p,
     }
     // the pool's in-kernel reduction needs blocks of exactly one chunk (a block's sum is the
     // chunk's) and batches on chunk boundaries; its ring: kPoolRing blocks for each wave of the
-    // persistent grid (at most 20 per CU: the spheres variant's 5 per SIMD; the launch clamps
-    // its grid to ring_waves)
+    // persistent grid (at most 24 per CU: the spheres variant's 6 per SIMD, f64 and f32; the
+    // launch clamps its grid to ring_waves)
     bool ring_ok = c->opt_ring && K.block_samples == chunk && chunk <= (int)(rtk::kRingSlot / 64) &&
                    s_end <= (int)rtk::kRingSampleMask;
-    // (the f32 mode's spheres variant runs 6 waves per SIMD: RT_BLOCK_F32_SPHERES)
-    const int ring_waves = c->n_cus * (o.f32 && rtk::variant_features(o.features) == rtk::FEAT_SET_SPHERES ? 24 : 20);
+    // (the spheres variant runs 6 waves per SIMD: RT_BLOCK_SPHERES, RT_BLOCK_F32_SPHERES)
+    const int ring_waves = c->n_cus * (rtk::variant_features(o.features) == rtk::FEAT_SET_SPHERES ? 24 : 20);
     const size_t ring_bytes = (size_t)ring_waves * rtk::kRingWaveDoubles * sizeof(double);
     bool ring = false;
     bool per_sample = false;

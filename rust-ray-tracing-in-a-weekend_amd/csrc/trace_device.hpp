@@ -159,7 +159,7 @@ struct Cfg {
     static constexpr bool F32 = F32_;
     // threads per workgroup (RT_BLOCK_FINAL): a property of the launched kernel, inherited by the
     // reduced configurations of nested code (CfgDrop), which share its LDS stack
-    static constexpr int BT = block_threads_of(F_, F32_);
+    static constexpr int BT = block_threads_of(F_, F32_, RT_STACK16 && LDS_ && NALL_ && S32_);
     using Real = typename std::conditional<F32_, float, double>::type;
 };
 
@@ -430,6 +430,12 @@ __device__ __forceinline__ bool sphere_t2(double cx, double cy, double cz, doubl
 // SMALL: the spheres variant only (in the final-scene variant the second path costs spills).
 #ifndef RT_F32_SMALL_SPHERE
 #define RT_F32_SMALL_SPHERE 8.0
+#endif
+// 1: the small-sphere path in every f32 variant. Off: in the final-scene variant it was no faster
+// (C4 1920x1080x100 f32 89.82 ms against 89.50 without; with the fast division 87.89 against
+// 86.36; profiles/r06t_ab_f32final_c4.log)
+#ifndef RT_F32_SMALL_ALL
+#define RT_F32_SMALL_ALL 0
 #endif
 template <bool SMALL = false>
 __device__ __forceinline__ void sphere_cb(double cx, double cy, double cz, double radius, const RayT<float>& r,
@@ -726,7 +732,7 @@ __device__ __forceinline__ bool simple_t(const rt_prim& p, const RayT<R>& r, R t
     if (!(C::F & FEAT_RECT) || p.kind <= RT_PRIM_MOVING_SPHERE) {
         double cx, cy, cz;
         sphere_center(p, r, gs, cx, cy, cz, (C::F & FEAT_STATIC) != 0);
-        return sphere_t<C::F == FEAT_SET_SPHERES>(cx, cy, cz, p.p[3], r, t_min, t_max, t);
+        return sphere_t<C::F == FEAT_SET_SPHERES || (RT_F32_SMALL_ALL && C::F32)>(cx, cy, cz, p.p[3], r, t_min, t_max, t);
     } else {
         const R q0 = (R)p.p[0], q1 = (R)p.p[1], q2 = (R)p.p[2], q3 = (R)p.p[3], q4 = (R)p.p[4];
         switch (p.kind) {
@@ -1930,6 +1936,11 @@ __device__ __forceinline__ bool lane_work(const KParams& P, LaneWork& w)
 #ifndef RT_MIN_WAVES_SPHERES
 #define RT_MIN_WAVES_SPHERES 1
 #endif
+// the f64 spheres variant with its 16-bit LDS stack (C1, C2, C5): 6 waves per SIMD at 80 VGPRs
+// (94 at 5, spill-free) with 768-thread workgroups (RT_BLOCK_SPHERES)
+#ifndef RT_MIN_WAVES_SPHERES_S16
+#define RT_MIN_WAVES_SPHERES_S16 6
+#endif
 #ifndef RT_MIN_WAVES_RECTINST
 // measured (Cornell 800x800x200): chunk schedule 4 waves 190 vs 202 ms; pool schedule 4: 80.7,
 // 3: 81.0; after the reciprocal divisions (more live state, 4 waves spilled to scratch):
@@ -1951,12 +1962,19 @@ __device__ __forceinline__ bool lane_work(const KParams& P, LaneWork& w)
 // (4: 112.0 ms with 0.7 TB of scratch writes per launch, 3: 102.8, 2: 131.5 at 960x540x200)
 #define RT_MIN_WAVES_FINAL 4
 #endif
+// the f32 final-scene variant: 4 like the f64 one (3 waves, 136-142 VGPRs and no spills even with
+// the small-sphere test, is slower: C4 1920x1080x100 f32 101.9 ms with 768-thread blocks, 107.0
+// with 256, against 89.4 at 4; profiles/r06s_ab_f32final_c4.log)
+#ifndef RT_MIN_WAVES_F32_FINAL
+#define RT_MIN_WAVES_F32_FINAL RT_MIN_WAVES_FINAL
+#endif
 // minimum waves per SIMD requested from the register allocator, per feature set
 template <class C>
 constexpr int min_waves()
 {
     return Stack16Cfg<C>() && C::F32 ? RT_MIN_WAVES_F32_SPHERES   // (the f32 mode's spheres variant)
-           : Stack16Cfg<C>() && C::F == FEAT_SET_SPHERES ? 5
+           : C::F32 && C::F == FEAT_SET_FINAL ? RT_MIN_WAVES_F32_FINAL
+           : Stack16Cfg<C>() && C::F == FEAT_SET_SPHERES ? RT_MIN_WAVES_SPHERES_S16
            : C::F == FEAT_SET_SPHERES ? RT_MIN_WAVES_SPHERES
            : C::F == FEAT_SET_RECTINST ? RT_MIN_WAVES_RECTINST
            : C::F == FEAT_SET_MEDIA    ? RT_MIN_WAVES_MEDIA
@@ -2592,7 +2610,7 @@ static void launch_one(const Launch& L, hipStream_t stream, bool nall)
     const int node_bytes = nall && S32 ? (int)sizeof(LdsNode) : (int)sizeof(rt_bvh_node);   // lds_node_bytes
     const bool stage = F != FEAT_SET_SPHERES;                   // StageShade
     const bool blas = RT_STAGE_BLAS && (F & FEAT_INST_BLAS) != 0;   // StageBlas
-    constexpr int bt = block_threads_of(F, F32), wpb = bt / 64;   // BlockThreads
+    const int bt = block_threads_of(F, F32, RT_STACK16 && LDS && nall && S32), wpb = bt / 64;   // BlockThreads
     const size_t lds = lds_layout(S.n_lds_nodes, node_bytes, blas ? S.n_lds_blas : 0, LDS ? S.stack_entries : 0,
                                   s16 ? 2 : 4, stage ? S.n_lds_materials : 0, stage ? S.n_lds_textures : 0, bt).total;
     if (L.pool) {

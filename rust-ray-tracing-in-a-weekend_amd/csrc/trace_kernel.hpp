@@ -18,8 +18,12 @@
 // the instanced BLAS in LDS (SceneDev.n_lds_blas; the host sizes that budget with it): the
 // final scene's 1000-sphere BLAS 512 of 548 nodes staged instead of 64, C4 1920x1080x100
 // 110.95 -> 108.23 ms; 512 threads with 64 staged 111.27 (profiles/r03r_ab_c4.log)
+// Round 6: 1024 (16 waves, one workgroup per CU at 4 waves per SIMD) stages the whole BLAS and
+// shares one copy of everything among the CU's waves: C4 1920x1080x1000 979.1 -> 976.4 ms, f32 mode
+// at 100 spp 86.33 -> 84.98, images bit-identical (profiles/r06u_ab_b1024_c4*.log; at 100 spp
+// 105.15 -> 104.71, r06t_ab_b1024_c4.log)
 #ifndef RT_BLOCK_FINAL
-#define RT_BLOCK_FINAL 512
+#define RT_BLOCK_FINAL 1024
 #endif
 
 namespace rtk {
@@ -28,16 +32,33 @@ namespace rtk {
 // which 256-thread blocks cannot reach (each holds its own 22.7 KB copy of the random scene's
 // TLAS, 6 x 28.8 KB > 160 KB per CU); 512-thread blocks share one copy among 8 waves (3 blocks,
 // 105 KB).
+#ifndef RT_BLOCK_F32_FINAL
+#define RT_BLOCK_F32_FINAL RT_BLOCK_FINAL
+#endif
+// Threads per workgroup of the f64 spheres variant (C1, C2, C5): 768 (12 waves, two workgroups per
+// CU) at 6 waves per SIMD (RT_MIN_WAVES_SPHERES_S16: 80 VGPRs, 32-40 B of scratch), two LDS copies
+// of the TLAS per CU instead of five. C2 1200x800x500 74.55 -> 72.00 ms, images identical; 512
+// threads at 6 waves 72.24, 384 at 6 81.12, 448 at 7 (96 B of scratch) 89.86, 512 at 5 (two
+// workgroups: 4 waves per SIMD) 82.42 (profiles/r06w_ab_sph_c2.log, r06x_ab_sph_c2.log)
+#ifndef RT_BLOCK_SPHERES
+#define RT_BLOCK_SPHERES 768
+#endif
 #ifndef RT_BLOCK_F32_SPHERES
 #define RT_BLOCK_F32_SPHERES 512
 #endif
 
-// workgroup threads of a kernel variant (host and device): see RT_BLOCK_FINAL, RT_BLOCK_F32_SPHERES
-__host__ __device__ constexpr int block_threads_of(uint32_t variant_features, bool f32)
+// workgroup threads of a kernel variant (host and device): see RT_BLOCK_FINAL, RT_BLOCK_SPHERES,
+// RT_BLOCK_F32_SPHERES. s16: the spheres variant's 16-bit-stack configuration (slab32, LDS stack,
+// whole TLAS in LDS: Stack16Cfg), the one those workgroup sizes and their wave counts are for;
+// its other configurations keep 256-thread workgroups
+#ifndef RT_STACK16
+#define RT_STACK16 1
+#endif
+__host__ __device__ constexpr int block_threads_of(uint32_t variant_features, bool f32, bool s16 = false)
 {
-    return variant_features == 287u /* FEAT_SET_FINAL */          ? RT_BLOCK_FINAL
-           : variant_features == 0u /* FEAT_SET_SPHERES */ && f32 ? RT_BLOCK_F32_SPHERES
-                                                                 : 256;
+    return variant_features == 287u /* FEAT_SET_FINAL */            ? (f32 ? RT_BLOCK_F32_FINAL : RT_BLOCK_FINAL)
+           : variant_features == 0u /* FEAT_SET_SPHERES */ && s16 ? (f32 ? RT_BLOCK_F32_SPHERES : RT_BLOCK_SPHERES)
+                                                                   : 256;
 }
 
 // Device view of the uploaded rt_scene_soa tables.
