@@ -1438,7 +1438,14 @@ static int run_range(rt_ctx* c, const rt_camera* cam, const rt_render_params* p,
         const size_t unit = per_sample ? sample_bytes : px_bytes;
         long long fit = (long long)std::max<size_t>(1, out_cap / unit);
         batch = std::min<long long>(total, per_sample ? fit : fit * chunk);
-        overlap = c->opt_overlap && batch < total && o.pool != RT_SCHED_CHUNKS;
+        // (only with 256-thread workgroups: a batch's launch of the large-workgroup variants —
+        // the spheres variant's 768 threads, the final scene's 1024 — takes a CU only when a whole
+        // workgroup of its predecessor has left, and the two persistent grids then contend instead:
+        // C5 4096x4096x4096 overlapped 11,471 ms per frame, in order 10,474, profiles/r06zz_c5_*)
+        const bool big_wg = rtk::block_threads_of(variant, o.f32 != 0,
+                                                  o.slab32 && o.lds_stack && S.n_lds_nodes > 0 &&
+                                                      S.n_lds_nodes == c->n_tlas_nodes && S.stack16_ok) > 256;
+        overlap = c->opt_overlap && !big_wg && batch < total && o.pool != RT_SCHED_CHUNKS;
         if (overlap) {
             fit = (long long)std::max<size_t>(1, out_cap / 2 / unit);
             batch = std::min<long long>(total, per_sample ? fit : fit * chunk);
