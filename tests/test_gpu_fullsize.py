@@ -283,7 +283,10 @@ def test_overlapped_buffer_batches_at_c2_size(rt, renderer, sched):
     render's stream reduces the previous batch. The whole C2 frame at 48 spp under a 256 MB bound
     (per-sample pool: 5 samples per half, 10 batches; item pool: chunks of 3, 5 chunks per half,
     4 batches) equals the one-batch render bit for bit, and so does the same bound without
-    overlap (RT_OPT_BATCH_OVERLAP 0: 11 samples or chunks per batch, 5 and 2 batches)."""
+    overlap (RT_OPT_BATCH_OVERLAP 0: 11 samples or chunks per batch, 5 and 2 batches). Batches
+    overlap only for kernels of 256-thread workgroups (abi.cpp): the overlapped runs take the
+    random scene's partial-TLAS instantiation (lds_nodes 0: 256 threads); the default one (768-
+    thread workgroups, 6 waves per SIMD) runs its batches in order, as with the option at 0."""
     W, H, spp = 1200, 800, 48
     world = rt.World(1).build_scene(0)
     cam, bg = rt.scene_camera(0, W, H)
@@ -295,11 +298,12 @@ def test_overlapped_buffer_batches_at_c2_size(rt, renderer, sched):
         assert renderer.stats().n_batches == 1
     finally:
         renderer.set_schedule(rt.RT_SCHED_AUTO)
-    for overlap in ("1", "0"):
+    for overlap, lds_nodes in (("1", 0), ("0", 0), ("1", 1)):
         r = rt.Renderer(0)
         r.set_option(rt.RT_OPT_TRACE_BUF_BYTES, 256 << 20)
         r.set_option(rt.RT_OPT_BATCH_OVERLAP, int(overlap))
         r.set_option(rt.RT_OPT_POOL_RING, 2 if sched == "RING" else 0)
+        r.set_variant(1, 1, lds_nodes)
         try:
             r.set_schedule(rt.RT_SCHED_ITEMS if sched == "ITEMS" else rt.RT_SCHED_POOL)
             r.upload(world)
@@ -309,8 +313,8 @@ def test_overlapped_buffer_batches_at_c2_size(rt, renderer, sched):
             r.close()
         # RING: the ring (two when overlapped) leaves the 256 MB bound less than one 23 MB chunk of
         # partials per batch, so batches of one chunk (the bound's floor)
-        expect = {("POOL", "1"): 10, ("POOL", "0"): 5, ("ITEMS", "1"): 4, ("ITEMS", "0"): 2,
-                  ("RING", "1"): 16, ("RING", "0"): 16}[(sched, overlap)]
-        assert st.n_batches == expect, (overlap, st.n_batches)
+        expect = {("POOL", "1", 0): 10, ("POOL", "0", 0): 5, ("POOL", "1", 1): 5, ("ITEMS", "1", 0): 4,
+                  ("ITEMS", "0", 0): 2, ("ITEMS", "1", 1): 2}.get((sched, overlap, lds_nodes), 16)
+        assert st.n_batches == expect, (overlap, lds_nodes, st.n_batches)
         same = img == one
-        assert same.all(), f"overlap {overlap}: {int((~same.all(axis=2)).sum())} px differ"
+        assert same.all(), f"overlap {overlap} lds_nodes {lds_nodes}: {int((~same.all(axis=2)).sum())} px differ"
